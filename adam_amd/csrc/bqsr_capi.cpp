@@ -1,0 +1,1047 @@
+// bqsr_capi.cpp -- host side of the C ABI declared in include/adam_bqsr.h.
+//
+// Owns HIP resources, packs ADAMRecord columns into the device layout
+// (bqsr_internal.h), launches the kernels of bqsr_kernels.hip and maps device
+// error words back to the reference's exception classes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bqsr_internal.h"
+
+using namespace bqsr;
+
+// the kernels are compiled in this translation unit (one HIP module)
+#include "bqsr_kernels.hip"
+
+// ------------------------------------------------------------- errors -----
+
+namespace {
+thread_local std::string g_err;
+thread_local int64_t g_err_read = -1;
+
+bqsr_status fail(bqsr_status s, const std::string& msg, int64_t read = -1) {
+  g_err = msg;
+  g_err_read = read;
+  return s;
+}
+bqsr_status ok() {
+  g_err.clear();
+  g_err_read = -1;
+  return BQSR_OK;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return fail(BQSR_ERR_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_));    \
+  } while (0)
+
+hipStream_t S(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
+
+const char* kStatusNames[] = {"OK",          "NULL_RG",      "MD_PARSE",       "CIGAR_SHORT", "BAD_REVCOMP_BASE",
+                              "EMPTY_TABLE", "MISSING_KEY",  "QUAL_RANGE",     "NULL_FIELD",  "SEQ_SHORT",
+                              "CIGAR_INVALID", "INVALID_ARG", "DEVICE",        "UNSUPPORTED"};
+
+// map a device error key to (status, read) and record the message
+bqsr_status from_err_key(unsigned long long k, int64_t read_base) {
+  if (k == kNoError) return ok();
+  const int code = (int)(k & 0xF);
+  const int64_t read = (int64_t)(k >> 28) + read_base;
+  const uint32_t o = (uint32_t)((k >> 8) & 0xFFFFF);
+  char buf[160];
+  snprintf(buf, sizeof buf, "%s at read %lld, read offset %u", kStatusNames[code], (long long)read, o);
+  return fail((bqsr_status)code, buf, read);
+}
+
+// ------------------------------------------------- static numeric tables ---
+
+// PhredUtils.phredToErrorProbabilityCache (PhredUtils.scala:22-24)
+struct Pow10 {
+  double v[256];
+  Pow10() {
+    for (int p = 0; p < 256; ++p) v[p] = std::pow(10.0, (double)(-p) / 10.0);
+  }
+};
+const Pow10& pow10tab() {
+  static Pow10 t;
+  return t;
+}
+
+// log10 correctly rounded to double (one rounding of the long double result)
+double cr_log10(double x) { return (double)log10l((long double)x); }
+int32_t java_d2i(double d) {
+  if (std::isnan(d)) return 0;
+  if (d >= 2147483647.0) return INT32_MAX;
+  if (d <= -2147483648.0) return INT32_MIN;
+  return (int32_t)d;
+}
+int32_t phred_of(double p) { return java_d2i(-10.0 * cr_log10(p)); }  // PhredUtils.scala:34-38
+
+// errorProbabilityToPhred is a non-increasing step function of p; its breaks:
+// thr[n - qmin] = the largest positive double p with phred_of(p) >= n.
+struct PhredThresholds {
+  std::vector<double> thr;
+  PhredThresholds() {
+    thr.resize(kThrN);
+    const uint64_t lo_bits = 1, hi_bits = 0x7FEFFFFFFFFFFFFFull;
+    auto val = [](uint64_t b) {
+      double d;
+      memcpy(&d, &b, 8);
+      return d;
+    };
+    for (int i = 0; i < kThrN; ++i) {
+      const int n = kThrQmin + i;
+      if (phred_of(val(hi_bits)) >= n) {
+        thr[i] = val(hi_bits);
+        continue;
+      }
+      if (phred_of(val(lo_bits)) < n) {
+        thr[i] = 0.0;
+        continue;
+      }
+      uint64_t a = lo_bits, b = hi_bits;  // phred(a) >= n > phred(b)
+      while (b - a > 1) {
+        const uint64_t m = a + (b - a) / 2;
+        if (phred_of(val(m)) >= n) a = m; else b = m;
+      }
+      thr[i] = val(a);
+    }
+  }
+};
+const PhredThresholds& thresholds() {
+  static PhredThresholds t;
+  return t;
+}
+
+int64_t table_words(const bqsr_dims& d) {
+  const int64_t K = 60LL * (d.n_rg - 1) + 128, cells = 2LL * d.max_len + 1 + kCtxSlots;
+  return K + 2 * K * cells;
+}
+TableGeom geom(const bqsr_dims& d) {
+  TableGeom g;
+  g.K = 60 * (d.n_rg - 1) + 128;
+  g.L = d.max_len;
+  g.C = 2 * d.max_len + 1;
+  g.cells = g.C + kCtxSlots;
+  return g;
+}
+
+constexpr size_t kLdsMax = 163840;
+size_t stage_bytes() {
+  // mirrors the device WaveStage layout (bqsr_kernels.hip)
+  struct WaveStageHost {
+    uint8_t bases[kTileSlots / 2 + 16];
+    uint32_t mmbits[kTileSlots / 32 + 1];
+    uint32_t maskbits[kTileSlots / 32 + 1];
+    uint16_t rslot[kMaxTileReads + 1];
+    uint16_t rows[kMaxTileReads * 5];
+    uint32_t hist[kQBins];
+    uint8_t md[kMdStage];
+    uint32_t cigar[kCigarStage];
+  };
+  return sizeof(WaveStageHost) * kWaves;
+}
+size_t observe_lds(int qw, int cells) {
+  size_t head = (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4 + 16;
+  head = (head + 15) & ~(size_t)15;
+  return head + stage_bytes();
+}
+size_t apply_lds(int qw, int C) {
+  size_t head = (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + kThrLdsN * 8 + ((qw + 15) & ~15) + 16;
+  head = (head + 15) & ~(size_t)15;
+  return head + stage_bytes();
+}
+int observe_qw(int cells) {
+  int qw = 64;
+  while (qw > 1 && observe_lds(qw, cells) > kLdsMax) --qw;
+  return qw;
+}
+int apply_qw(int C) {
+  int qw = 64;
+  while (qw > 1 && apply_lds(qw, C) > kLdsMax) --qw;
+  return qw;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ handles -----
+
+struct bqsr_context {
+  int device = 0;
+  int n_cu = 256;
+  double* d_pow10 = nullptr;  // 256 doubles
+  double* d_thr = nullptr;    // kThrN doubles
+};
+
+struct bqsr_sites {
+  bqsr_context* ctx = nullptr;
+  std::vector<std::string> names;
+  int64_t* pos = nullptr;
+  uint64_t* off = nullptr;
+  uint32_t* bucket = nullptr;
+  uint64_t* bucket_off = nullptr;
+  int64_t* bucket_base = nullptr;
+  int32_t n = 0;
+  int32_t shift = 8;
+  SitesDev dev() const { return SitesDev{pos, off, bucket, bucket_off, bucket_base, n, shift}; }
+};
+
+struct bqsr_batch {
+  bqsr_context* ctx = nullptr;
+  bool owned = false;
+  ReadsDev rd{};
+  bqsr_dims dims{1, 1};
+  int64_t n_slots = 0;
+  int64_t n_bases = 0;
+  int32_t q_lo = 0, rg_lo = 0;  // LDS window choice
+  std::vector<void*> allocs;
+  // per-call scratch
+  uint16_t* d_h2 = nullptr;
+  uint32_t* d_hq = nullptr;
+  unsigned long long* d_err = nullptr;  // [4]: err, n_exc, status, pad
+  double* d_em = nullptr;
+  int32_t n_blocks = 0;
+  ~bqsr_batch() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+struct bqsr_table {
+  bqsr_context* ctx = nullptr;
+  bqsr_dims dims{1, 1};
+  int64_t* words = nullptr;
+  bool owned = false;
+  ~bqsr_table() {
+    if (owned && words) (void)hipFree(words);
+  }
+  TableGeom g() const { return geom(dims); }
+  int64_t* touched() const { return words; }
+  int64_t* obs() const { return words + g().K; }
+  int64_t* mm() const { return words + g().K + (int64_t)g().K * g().cells; }
+};
+
+struct bqsr_lut {
+  bqsr_context* ctx = nullptr;
+  bqsr_dims dims{1, 1};
+  int32_t n_groups = 0;
+  std::vector<void*> allocs;
+  int64_t *qk_obs = nullptr, *qk_mm = nullptr, *grp_obs = nullptr, *grp_mm = nullptr;
+  uint8_t *grp_ok = nullptr, *key_ok = nullptr, *rq_ok = nullptr;
+  double *a2 = nullptr, *s1 = nullptr, *d2 = nullptr;
+  FinalOut* d_out = nullptr;
+  FinalOut out{};
+  // host mirror for stats / shifts queries (filled lazily)
+  bool host_ready = false;
+  std::vector<int64_t> h_words, h_qk_obs, h_qk_mm, h_grp_obs, h_grp_mm;
+  std::vector<uint8_t> h_grp_ok;
+  const bqsr_table* src = nullptr;
+  ~bqsr_lut() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+namespace {
+template <class T>
+bqsr_status dalloc(std::vector<void*>& v, T** p, size_t n) {
+  void* q = nullptr;
+  HIP_TRY(hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)));
+  v.push_back(q);
+  *p = (T*)q;
+  return BQSR_OK;
+}
+}  // namespace
+
+// ------------------------------------------------------------- library ----
+
+extern "C" {
+
+int bqsr_abi_version(void) { return BQSR_ABI_VERSION; }
+const char* bqsr_last_error(void) { return g_err.c_str(); }
+int64_t bqsr_last_error_read(void) { return g_err_read; }
+const char* bqsr_status_name(bqsr_status s) {
+  if ((int)s < 0 || (int)s > 13) return "UNKNOWN";
+  return kStatusNames[(int)s];
+}
+
+bqsr_status bqsr_context_create(int device, bqsr_context** out) {
+  if (!out) return fail(BQSR_ERR_INVALID_ARG, "null out");
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  bqsr_context* c = new bqsr_context;
+  c->device = device;
+  c->n_cu = prop.multiProcessorCount;
+  hipError_t e = hipMalloc(&c->d_pow10, 256 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&c->d_thr, kThrN * sizeof(double));
+  if (e == hipSuccess) e = hipMemcpy(c->d_pow10, pow10tab().v, 256 * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_thr, thresholds().thr.data(), kThrN * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  if (e != hipSuccess) {
+    bqsr_context_destroy(c);
+    return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return ok();
+}
+
+void bqsr_context_destroy(bqsr_context* c) {
+  if (!c) return;
+  if (c->d_pow10) (void)hipFree(c->d_pow10);
+  if (c->d_thr) (void)hipFree(c->d_thr);
+  delete c;
+}
+
+// ---------------------------------------------------------------- sites ----
+
+bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, const int64_t* const* pos,
+                              const uint64_t* n, int32_t n_contigs, bqsr_sites** out) {
+  if (!ctx || !out || n_contigs < 0 || (n_contigs > 0 && (!contigs || !pos || !n)))
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_sites_create: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  bqsr_sites* s = new bqsr_sites;
+  s->ctx = ctx;
+  s->n = n_contigs;
+  std::vector<int64_t> all;
+  std::vector<uint64_t> off(1, 0);
+  std::vector<uint32_t> bucket;
+  std::vector<uint64_t> boff(1, 0);
+  std::vector<int64_t> bbase;
+  for (int32_t c = 0; c < n_contigs; ++c) {
+    s->names.emplace_back(contigs[c] ? contigs[c] : "");
+    std::vector<int64_t> v(pos[c], pos[c] + n[c]);  // SnpTable: Set[Long] per contig
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    const int64_t base = v.empty() ? 0 : v.front();
+    const int64_t nb = v.empty() ? 0 : ((v.back() - base) >> s->shift) + 1;
+    size_t j = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t lo = base + (b << s->shift);
+      while (j < v.size() && v[j] < lo) ++j;
+      bucket.push_back((uint32_t)j);
+    }
+    bbase.push_back(base);
+    boff.push_back(bucket.size());
+    all.insert(all.end(), v.begin(), v.end());
+    off.push_back(all.size());
+  }
+  std::vector<void*> keep;
+  auto up = [&](auto** dst, const auto& src) -> hipError_t {
+    using T = typename std::remove_reference<decltype(src[0])>::type;
+    hipError_t e = hipMalloc((void**)dst, std::max<size_t>(src.size(), 1) * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (!src.empty()) e = hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+  };
+  hipError_t e = up(&s->pos, all);
+  if (e == hipSuccess) e = up(&s->off, off);
+  if (e == hipSuccess) e = up(&s->bucket, bucket);
+  if (e == hipSuccess) e = up(&s->bucket_off, boff);
+  if (e == hipSuccess) e = up(&s->bucket_base, bbase);
+  if (e != hipSuccess) {
+    bqsr_sites_destroy(s);
+    return fail(BQSR_ERR_DEVICE, std::string("sites upload: ") + hipGetErrorString(e));
+  }
+  *out = s;
+  return ok();
+}
+
+void bqsr_sites_destroy(bqsr_sites* s) {
+  if (!s) return;
+  for (void* p : {(void*)s->pos, (void*)s->off, (void*)s->bucket, (void*)s->bucket_off, (void*)s->bucket_base})
+    if (p) (void)hipFree(p);
+  delete s;
+}
+
+// ---------------------------------------------------------------- batch ----
+
+namespace {
+
+inline uint8_t code_of(uint8_t c) {
+  switch (c) {
+    case 'A': return kCodeA;
+    case 'C': return kCodeC;
+    case 'G': return kCodeG;
+    case 'T': return kCodeT;
+    case 'N': return kCodeN;
+    default: return kCodeOther;
+  }
+}
+
+bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
+  if (max_slot_len > kTileSlots)
+    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kTileSlots) + " bases are not supported");
+  const int64_t n = b->rd.n_reads;
+  b->rd.reads_per_tile = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kMaxTileReads, kTileSlots / std::max<int64_t>(1, max_slot_len)));
+  b->rd.n_tiles = (n + b->rd.reads_per_tile - 1) / b->rd.reads_per_tile;
+  b->n_blocks = b->ctx->n_cu;
+  bqsr_status st;
+  if ((st = dalloc(b->allocs, &b->d_h2, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kQBins)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_hq, (size_t)b->n_blocks * kQBins)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_err, 4)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
+  return BQSR_OK;
+}
+
+// host pack of one record partition (bqsr_records -> device layout)
+struct Packed {
+  std::vector<ReadMeta> meta;
+  std::vector<ReadAlign> align;
+  std::vector<uint8_t> qual, bases, md;
+  std::vector<uint32_t> cigar;
+  int64_t n_slots = 0, n_bases = 0, max_slot = 0;
+  int32_t n_rg = 1, max_len = 1;
+  int64_t qhist[256] = {0};
+  std::vector<int64_t> rghist;
+};
+
+bqsr_status pack(const bqsr_records* R, Packed& P) {
+  const int64_t n = R->n_reads;
+  P.meta.resize((size_t)n);
+  P.align.resize((size_t)n);
+  uint64_t slot = 0, md_tot = 0, cig_tot = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    const uint32_t f = R->flags[r];
+    const uint64_t lq = (f & BQSR_F_HAS_QUAL) ? R->qual_offset[r + 1] - R->qual_offset[r] : 0;
+    const uint64_t ls = (f & BQSR_F_HAS_SEQ) ? R->seq_offset[r + 1] - R->seq_offset[r] : 0;
+    const uint64_t nmd = (f & BQSR_F_HAS_MD) ? R->md_offset[r + 1] - R->md_offset[r] : 0;
+    const uint64_t ncig = (f & BQSR_F_HAS_CIGAR) ? R->cigar_offset[r + 1] - R->cigar_offset[r] : 0;
+    if (lq > 65535 || ls > 65535 || nmd > 65535 || ncig > 65535)
+      return fail(BQSR_ERR_UNSUPPORTED, "read field longer than 65535", r);
+    if ((f & BQSR_F_HAS_RG) && (R->rg_id[r] < 0 || R->rg_id[r] > 65535))
+      return fail(BQSR_ERR_UNSUPPORTED, "recordGroupId outside [0, 65535]", r);
+    ReadMeta& m = P.meta[(size_t)r];
+    m.slot = slot;
+    m.lq = (uint16_t)lq;
+    m.ls = (uint16_t)ls;
+    m.flags = (uint16_t)(f & 0x7FFF);
+    m.rg = (f & BQSR_F_HAS_RG) ? (uint16_t)R->rg_id[r] : 0;
+    ReadAlign& a = P.align[(size_t)r];
+    a.start = R->start[r];
+    a.cigar_off = (uint32_t)cig_tot;
+    a.md_off = (uint32_t)md_tot;
+    a.contig = R->contig_id[r];
+    a.n_cigar = (uint16_t)ncig;
+    a.md_len = (uint16_t)nmd;
+    const uint64_t sl = std::max(lq, ls);
+    slot += sl;
+    P.max_slot = std::max<int64_t>(P.max_slot, (int64_t)sl);
+    md_tot += nmd;
+    cig_tot += ncig;
+    P.n_bases += (int64_t)(R->seq_offset[r + 1] - R->seq_offset[r]);
+    if (f & BQSR_F_HAS_RG) P.n_rg = std::max<int32_t>(P.n_rg, R->rg_id[r] + 1);
+    P.max_len = std::max<int32_t>(P.max_len, (int32_t)ls);
+  }
+  if (md_tot > 0xFFFFFFFFull || cig_tot > 0xFFFFFFFFull)
+    return fail(BQSR_ERR_UNSUPPORTED, "partition MD / CIGAR columns exceed 4 GiB");
+  P.n_slots = (int64_t)slot;
+  P.qual.assign(((size_t)slot + 15) / 16 * 16 + 16, 0);
+  P.bases.assign((size_t)slot / 2 + 16, 0);
+  P.md.resize(std::max<uint64_t>(md_tot, 1));
+  P.cigar.resize(std::max<uint64_t>(cig_tot, 1));
+  P.rghist.assign((size_t)P.n_rg, 0);
+  // per-base columns, parallel over read ranges
+  const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(16, n / 65536));
+  std::vector<std::thread> th;
+  std::vector<std::array<int64_t, 256>> qh((size_t)nth);
+  for (auto& h : qh) h.fill(0);
+  auto work = [&](int t) {
+    const int64_t r0 = n * t / nth, r1 = n * (t + 1) / nth;
+    for (int64_t r = r0; r < r1; ++r) {
+      const ReadMeta& m = P.meta[(size_t)r];
+      const ReadAlign& a = P.align[(size_t)r];
+      const uint8_t* q = R->qual + R->qual_offset[r];
+      for (uint32_t i = 0; i < m.lq; ++i) {
+        const uint8_t v = (uint8_t)(q[i] - 33);  // (char - 33).toByte
+        P.qual[m.slot + i] = v;
+        qh[(size_t)t][v]++;
+      }
+      const uint8_t* s = R->seq + R->seq_offset[r];
+      bool other = false;
+      for (uint32_t i = 0; i < m.ls; ++i) {
+        const uint8_t c = code_of(s[i]);
+        other |= c == kCodeOther;
+        const uint64_t k = m.slot + i;
+        // two reads can share a byte only at odd boundaries: threads own whole reads,
+        // so write nibbles with a CAS-free scheme: even nibble by value, odd by or
+        if (k & 1) __atomic_fetch_or(&P.bases[k >> 1], (uint8_t)(c << 4), __ATOMIC_RELAXED);
+        else __atomic_fetch_or(&P.bases[k >> 1], c, __ATOMIC_RELAXED);
+      }
+      if (other) P.meta[(size_t)r].flags |= kSeqOther;
+      if (m.flags & BQSR_F_HAS_MD) memcpy(&P.md[a.md_off], R->md + R->md_offset[r], a.md_len);
+      if (m.flags & BQSR_F_HAS_CIGAR) memcpy(&P.cigar[a.cigar_off], R->cigar + R->cigar_offset[r], a.n_cigar * 4u);
+    }
+  };
+  for (int t = 0; t < nth; ++t) th.emplace_back(work, t);
+  for (auto& x : th) x.join();
+  for (auto& h : qh)
+    for (int i = 0; i < 256; ++i) P.qhist[i] += h[(size_t)i];
+  for (int64_t r = 0; r < n; ++r)
+    if (P.meta[(size_t)r].flags & BQSR_F_HAS_RG) P.rghist[P.meta[(size_t)r].rg]++;
+  return BQSR_OK;
+}
+
+// LDS window start: the 64-wide qual range holding the most bases
+int32_t best_q_lo(const int64_t* qhist, int qw) {
+  int best = 0;
+  int64_t bestv = -1;
+  for (int lo = 0; lo + 1 <= kQBins; ++lo) {
+    int64_t v = 0;
+    for (int q = lo; q < std::min(kQBins, lo + qw); ++q) v += qhist[q];
+    if (v > bestv) {
+      bestv = v;
+      best = lo;
+    }
+    if (lo + qw >= kQBins) break;
+  }
+  return best;
+}
+
+}  // namespace
+
+bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* stream, bqsr_batch** out) {
+  if (!ctx || !R || !out || R->n_reads < 0) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_create: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  Packed P;
+  bqsr_status st = pack(R, P);
+  if (st != BQSR_OK) return st;
+  bqsr_batch* b = new bqsr_batch;
+  b->ctx = ctx;
+  b->owned = true;
+  b->rd.n_reads = R->n_reads;
+  b->n_slots = P.n_slots;
+  b->n_bases = P.n_bases;
+  b->dims = bqsr_dims{P.n_rg, P.max_len};
+  // window: most frequent read group, densest qual range (the window width is
+  // decided per launch from the table geometry; 40 is a typical width)
+  int32_t rg_lo = 0;
+  for (int32_t i = 0; i < (int32_t)P.rghist.size(); ++i)
+    if (P.rghist[(size_t)i] > P.rghist[(size_t)rg_lo]) rg_lo = i;
+  b->rg_lo = rg_lo;
+  b->q_lo = best_q_lo(P.qhist, 40);
+  ReadMeta* meta;
+  ReadAlign* align;
+  uint8_t *qual, *bases, *md;
+  uint32_t* cigar;
+  hipStream_t s = S(stream);
+  auto up = [&](auto** dst, const auto& v) -> bqsr_status {
+    using T = typename std::remove_reference<decltype(v[0])>::type;
+    bqsr_status x = dalloc(b->allocs, dst, v.size());
+    if (x != BQSR_OK) return x;
+    if (!v.empty()) HIP_TRY(hipMemcpyAsync(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    return BQSR_OK;
+  };
+  if ((st = up(&meta, P.meta)) != BQSR_OK || (st = up(&align, P.align)) != BQSR_OK || (st = up(&qual, P.qual)) != BQSR_OK ||
+      (st = up(&bases, P.bases)) != BQSR_OK || (st = up(&md, P.md)) != BQSR_OK || (st = up(&cigar, P.cigar)) != BQSR_OK) {
+    delete b;
+    return st;
+  }
+  b->rd.meta = meta;
+  b->rd.align = align;
+  b->rd.qual = qual;
+  b->rd.bases = bases;
+  b->rd.md = md;
+  b->rd.cigar = cigar;
+  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK) {
+    delete b;
+    return st;
+  }
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    delete b;
+    return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
+  }
+  *out = b;
+  return ok();
+}
+
+bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* dev, bqsr_batch** out) {
+  if (!ctx || !dev || !out || dev->n_reads < 0 || dev->dims.n_rg < 1 || dev->dims.max_len < 1)
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_wrap_device: bad arguments");
+  if (dev->dims.max_len > kTileSlots)
+    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kTileSlots) + " bases are not supported");
+  HIP_TRY(hipSetDevice(ctx->device));
+  bqsr_batch* b = new bqsr_batch;
+  b->ctx = ctx;
+  b->rd.n_reads = dev->n_reads;
+  b->rd.meta = (const ReadMeta*)dev->meta;
+  b->rd.align = (const ReadAlign*)dev->align;
+  b->rd.qual = dev->qual;
+  b->rd.bases = dev->bases;
+  b->rd.cigar = dev->cigar;
+  b->rd.md = dev->md;
+  b->n_slots = dev->n_slots;
+  b->n_bases = -1;
+  b->dims = dev->dims;
+  b->q_lo = 0;
+  b->rg_lo = 0;
+  bqsr_status st = finish_batch(b, dev->dims.max_len);
+  if (st != BQSR_OK) {
+    delete b;
+    return st;
+  }
+  *out = b;
+  return ok();
+}
+
+void bqsr_batch_destroy(bqsr_batch* b) { delete b; }
+int64_t bqsr_batch_reads(const bqsr_batch* b) { return b ? b->rd.n_reads : -1; }
+int64_t bqsr_batch_bases(const bqsr_batch* b) { return b ? b->n_bases : -1; }
+bqsr_dims bqsr_batch_dims(const bqsr_batch* b) { return b ? b->dims : bqsr_dims{0, 0}; }
+
+// window override (exported for device batches whose quals the host never saw)
+bqsr_status bqsr_batch_set_window(bqsr_batch* b, int32_t q_lo, int32_t rg_lo) {
+  if (!b || q_lo < 0 || q_lo >= kQBins || rg_lo < 0) return fail(BQSR_ERR_INVALID_ARG, "bad window");
+  b->q_lo = q_lo;
+  b->rg_lo = rg_lo;
+  return ok();
+}
+int32_t bqsr_batch_reads_per_tile(const bqsr_batch* b) { return b ? b->rd.reads_per_tile : -1; }
+
+// ---------------------------------------------------------------- table ----
+
+int64_t bqsr_table_words(bqsr_dims d) { return (d.n_rg < 1 || d.max_len < 1) ? -1 : table_words(d); }
+
+bqsr_status bqsr_table_create(bqsr_context* ctx, bqsr_dims d, void* device_words, bqsr_table** out) {
+  if (!ctx || !out || d.n_rg < 1 || d.max_len < 1 || d.max_len > 65535)
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_table_create: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  bqsr_table* t = new bqsr_table;
+  t->ctx = ctx;
+  t->dims = d;
+  const size_t bytes = (size_t)table_words(d) * 8;
+  if (device_words) {
+    t->words = (int64_t*)device_words;
+  } else {
+    hipError_t e = hipMalloc((void**)&t->words, bytes);
+    if (e != hipSuccess) {
+      delete t;
+      return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
+    }
+    t->owned = true;
+  }
+  hipError_t e = hipMemset(t->words, 0, bytes);
+  if (e != hipSuccess) {
+    delete t;
+    return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
+  }
+  *out = t;
+  return ok();
+}
+void bqsr_table_destroy(bqsr_table* t) { delete t; }
+bqsr_dims bqsr_table_dims(const bqsr_table* t) { return t ? t->dims : bqsr_dims{0, 0}; }
+void* bqsr_table_device_ptr(bqsr_table* t) { return t ? t->words : nullptr; }
+
+bqsr_status bqsr_table_download(const bqsr_table* t, int64_t* host) {
+  if (!t || !host) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(t->ctx->device));
+  HIP_TRY(hipMemcpy(host, t->words, (size_t)table_words(t->dims) * 8, hipMemcpyDeviceToHost));
+  return ok();
+}
+bqsr_status bqsr_table_upload(bqsr_table* t, const int64_t* host) {
+  if (!t || !host) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(t->ctx->device));
+  HIP_TRY(hipMemcpy(t->words, host, (size_t)table_words(t->dims) * 8, hipMemcpyHostToDevice));
+  return ok();
+}
+
+bqsr_status bqsr_table_merge(bqsr_table* acc, const bqsr_table* part, double* acc_em, double part_em) {
+  if (!acc || !part || !acc_em) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (acc->dims.n_rg != part->dims.n_rg || acc->dims.max_len != part->dims.max_len)
+    return fail(BQSR_ERR_INVALID_ARG, "table dims differ");
+  HIP_TRY(hipSetDevice(acc->ctx->device));
+  const int64_t n = table_words(acc->dims);
+  hipLaunchKernelGGL(bqsr_table_add, dim3((unsigned)std::min<int64_t>(4096, (n + 255) / 256)), dim3(256), 0,
+                     hipStreamPerThread, acc->words, part->words, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(hipStreamPerThread));
+  *acc_em = *acc_em + part_em;  // RecalTable.++: this.expectedMismatch + other.expectedMismatch
+  return ok();
+}
+
+// -------------------------------------------------------------- observe ----
+
+namespace {
+bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
+  if (b->dims.n_rg > t->dims.n_rg || b->dims.max_len > t->dims.max_len)
+    return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's (n_rg / max_len)");
+  return BQSR_OK;
+}
+}  // namespace
+
+// launch observe + fold; does not synchronise (results land in b->d_err / d_em)
+bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t, void* stream) {
+  if (!ctx || !b || !t) return fail(BQSR_ERR_INVALID_ARG, "null");
+  bqsr_status st = check_dims(b, t);
+  if (st != BQSR_OK) return st;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = S(stream);
+  HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
+  if (b->rd.n_reads == 0) {
+    HIP_TRY(hipMemsetAsync(b->d_em, 0, 8, s));
+    return ok();
+  }
+  ObserveParams P{};
+  P.rd = b->rd;
+  if (sites) P.sites = sites->dev();
+  P.g = geom(t->dims);
+  P.w.qw = observe_qw(P.g.cells);
+  P.w.q_lo = std::min(b->q_lo, kQBins - 1);
+  P.w.rg_lo = b->rg_lo;
+  P.touched = t->touched();
+  P.obs = t->obs();
+  P.mm = t->mm();
+  P.hq_block = b->d_hq;
+  P.h2 = b->d_h2;
+  P.err = b->d_err;
+  P.n_blocks = b->n_blocks;
+  const size_t lds = observe_lds(P.w.qw, P.g.cells);
+  hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  HIP_TRY(hipGetLastError());
+  FoldParams F{};
+  F.rd = b->rd;
+  F.hq_block = b->d_hq;
+  F.h2 = b->d_h2;
+  F.pow10 = ctx->d_pow10;
+  F.n_blocks = b->n_blocks;
+  F.em_out = b->d_em;
+  F.status = b->d_err + 2;
+  hipLaunchKernelGGL(bqsr_fold_kernel, dim3(1), dim3(256), 0, s, F);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+bqsr_status bqsr_observe_result(bqsr_batch* b, double* em, void* stream) {
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t s = S(stream);
+  unsigned long long err = 0;
+  double e = 0;
+  HIP_TRY(hipMemcpyAsync(&err, b->d_err, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&e, b->d_em, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (em) *em = e;
+  return from_err_key(err, 0);
+}
+
+bqsr_status bqsr_observe(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
+                         double* expected_mismatch, void* stream) {
+  bqsr_status st = bqsr_observe_async(ctx, b, sites, t, stream);
+  if (st != BQSR_OK) return st;
+  return bqsr_observe_result(b, expected_mismatch, stream);
+}
+
+bqsr_status bqsr_observe_records(bqsr_context* ctx, const bqsr_records* recs, const bqsr_sites* sites, bqsr_dims dims,
+                                 bqsr_table** out_partial, double* out_em) {
+  if (!out_partial || !out_em) return fail(BQSR_ERR_INVALID_ARG, "null out");
+  bqsr_batch* b = nullptr;
+  bqsr_status st = bqsr_batch_create(ctx, recs, nullptr, &b);
+  if (st != BQSR_OK) return st;
+  bqsr_table* t = nullptr;
+  st = bqsr_table_create(ctx, dims, nullptr, &t);
+  if (st == BQSR_OK) st = bqsr_observe(ctx, b, sites, t, out_em, nullptr);
+  bqsr_batch_destroy(b);
+  if (st != BQSR_OK) {
+    bqsr_table_destroy(t);
+    return st;
+  }
+  *out_partial = t;
+  return ok();
+}
+
+// ------------------------------------------------------------- finalize ----
+
+bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double em, bqsr_lut** out, void* stream) {
+  if (!ctx || !t || !out) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = S(stream);
+  bqsr_lut* L = new bqsr_lut;
+  L->ctx = ctx;
+  L->dims = t->dims;
+  L->src = t;
+  const TableGeom g = geom(t->dims);
+  const int n_rg = t->dims.n_rg;
+  L->n_groups = (g.K - 1) / kMaxQ + 2;
+  bqsr_status st;
+  if ((st = dalloc(L->allocs, &L->qk_obs, g.K)) != BQSR_OK || (st = dalloc(L->allocs, &L->qk_mm, g.K)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->grp_obs, L->n_groups)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->grp_mm, L->n_groups)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->grp_ok, L->n_groups)) != BQSR_OK || (st = dalloc(L->allocs, &L->key_ok, g.K)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->rq_ok, (size_t)n_rg * kQBins)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->a2, (size_t)n_rg * kQBins)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->s1, (size_t)n_rg * kQBins * g.C)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->d2, (size_t)n_rg * kQBins * kCtxSlots)) != BQSR_OK ||
+      (st = dalloc(L->allocs, &L->d_out, 1)) != BQSR_OK) {
+    delete L;
+    return st;
+  }
+  hipLaunchKernelGGL(bqsr_final_keys, dim3((g.K + 3) / 4), dim3(256), 0, s, t->touched(), t->obs(), t->mm(), g, L->qk_obs,
+                     L->qk_mm);
+  hipLaunchKernelGGL(bqsr_final_groups, dim3(1), dim3(256), 0, s, t->touched(), L->qk_obs, L->qk_mm, g, n_rg, em,
+                     ctx->d_pow10, L->n_groups, L->grp_obs, L->grp_mm, L->grp_ok, L->key_ok, L->a2, L->rq_ok, L->d_out);
+  const int64_t ncell = (int64_t)n_rg * kQBins * (g.C + kCtxSlots);
+  hipLaunchKernelGGL(bqsr_final_tables, dim3((unsigned)std::min<int64_t>(8192, (ncell + 255) / 256)), dim3(256), 0, s,
+                     t->obs(), t->mm(), g, n_rg, L->a2, L->rq_ok, pow10tab().v[kMaxQ], L->s1, L->d2);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) {
+    delete L;
+    return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
+  }
+  *out = L;
+  return ok();
+}
+
+bqsr_status bqsr_finalize_result(bqsr_lut* L, void* stream) {
+  HIP_TRY(hipSetDevice(L->ctx->device));
+  HIP_TRY(hipStreamSynchronize(S(stream)));
+  if (!L->out.any_key)  // readGroupCounts.values.reduce on an empty map (RecalTable.scala:123)
+    return fail(BQSR_ERR_EMPTY_TABLE, "empty.reduceLeft: no usable base was observed");
+  return ok();
+}
+
+bqsr_status bqsr_finalize(bqsr_context* ctx, const bqsr_table* t, double em, bqsr_lut** out) {
+  bqsr_lut* L = nullptr;
+  bqsr_status st = bqsr_finalize_async(ctx, t, em, &L, nullptr);
+  if (st != BQSR_OK) return st;
+  st = bqsr_finalize_result(L, nullptr);
+  if (st != BQSR_OK) {
+    delete L;
+    return st;
+  }
+  *out = L;
+  return ok();
+}
+
+void bqsr_lut_destroy(bqsr_lut* l) { delete l; }
+
+namespace {
+bqsr_status lut_host(bqsr_lut* L) {
+  if (L->host_ready) return BQSR_OK;
+  HIP_TRY(hipSetDevice(L->ctx->device));
+  const TableGeom g = geom(L->dims);
+  L->h_words.resize((size_t)table_words(L->dims));
+  L->h_qk_obs.resize((size_t)g.K);
+  L->h_qk_mm.resize((size_t)g.K);
+  L->h_grp_obs.resize((size_t)L->n_groups);
+  L->h_grp_mm.resize((size_t)L->n_groups);
+  L->h_grp_ok.resize((size_t)L->n_groups);
+  HIP_TRY(hipMemcpy(L->h_words.data(), L->src->words, L->h_words.size() * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(L->h_qk_obs.data(), L->qk_obs, (size_t)g.K * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(L->h_qk_mm.data(), L->qk_mm, (size_t)g.K * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(L->h_grp_obs.data(), L->grp_obs, (size_t)L->n_groups * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(L->h_grp_mm.data(), L->grp_mm, (size_t)L->n_groups * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(L->h_grp_ok.data(), L->grp_ok, (size_t)L->n_groups, hipMemcpyDeviceToHost));
+  L->host_ready = true;
+  return BQSR_OK;
+}
+bool eprob(int64_t obs, int64_t mm, double* v) {
+  if (obs == 0) return false;
+  const double x = (double)mm / (double)obs;
+  *v = std::max(pow10tab().v[kMaxQ], x);
+  return true;
+}
+}  // namespace
+
+bqsr_status bqsr_lut_stats(const bqsr_lut* lc, bqsr_final_stats* out) {
+  bqsr_lut* L = const_cast<bqsr_lut*>(lc);
+  if (!L || !out) return fail(BQSR_ERR_INVALID_ARG, "null");
+  out->average_reported_error = L->out.avg;
+  out->global_error = L->out.global_error;
+  out->global_obs = L->out.g_obs;
+  out->global_mm = L->out.g_mm;
+  out->n_groups = L->n_groups;
+  return ok();
+}
+
+// per-group counts (index r + 1); returns 0 when the group does not exist
+int bqsr_lut_group(const bqsr_lut* lc, int32_t r, int64_t* obs, int64_t* mm) {
+  bqsr_lut* L = const_cast<bqsr_lut*>(lc);
+  if (!L || lut_host(L) != BQSR_OK) return -1;
+  if (r + 1 < 0 || r + 1 >= L->n_groups || !L->h_grp_ok[(size_t)(r + 1)]) return 0;
+  *obs = L->h_grp_obs[(size_t)(r + 1)];
+  *mm = L->h_grp_mm[(size_t)(r + 1)];
+  return 1;
+}
+
+bqsr_status bqsr_lut_shifts(const bqsr_lut* lc, int32_t key, int32_t qual, int32_t cyc, int32_t ctx, double sh[4],
+                            int32_t* new_q) {
+  bqsr_lut* L = const_cast<bqsr_lut*>(lc);
+  if (!L || !sh || !new_q) return fail(BQSR_ERR_INVALID_ARG, "null");
+  bqsr_status st = lut_host(L);
+  if (st != BQSR_OK) return st;
+  const TableGeom g = geom(L->dims);
+  if (cyc < -g.L || cyc > g.L || ctx < -4 || ctx > 16) return fail(BQSR_ERR_INVALID_ARG, "covariate out of range");
+  const int64_t r = ((int64_t)key - 1) / kMaxQ;
+  if (r + 1 < 0 || r + 1 >= L->n_groups || !L->h_grp_ok[(size_t)(r + 1)])
+    return fail(BQSR_ERR_MISSING_KEY, "read group missing");
+  const double avg = L->out.avg;
+  double v;
+  const double rgd = (eprob(L->h_grp_obs[(size_t)(r + 1)], L->h_grp_mm[(size_t)(r + 1)], &v) ? v : avg) - avg;
+  if (key < 0 || key >= g.K || L->h_words[(size_t)key] == 0) return fail(BQSR_ERR_MISSING_KEY, "key missing");
+  if (qual < 0 || qual > 255) return fail(BQSR_ERR_QUAL_RANGE, "qual out of range");
+  const double e = pow10tab().v[qual];
+  const double a1 = e + rgd;
+  const double qd = (eprob(L->h_qk_obs[(size_t)key], L->h_qk_mm[(size_t)key], &v) ? v : a1) - a1;
+  const double a2 = a1 + qd;
+  const int64_t* obs = L->h_words.data() + g.K;
+  const int64_t* mm = obs + (int64_t)g.K * g.cells;
+  const int64_t c1 = (int64_t)key * g.cells + cyc + g.L, c2 = (int64_t)key * g.cells + g.C + ctx + 4;
+  const double cd = (eprob(obs[c1], mm[c1], &v) ? v : a2) - a2;
+  const double xd = (eprob(obs[c2], mm[c2], &v) ? v : a2) - a2;
+  sh[0] = rgd;
+  sh[1] = qd;
+  sh[2] = cd;
+  sh[3] = xd;
+  double p = e;
+  for (int i = 0; i < 4; ++i) p = p + sh[i];
+  *new_q = phred_of(p);
+  return ok();
+}
+
+// the threshold form of errorProbabilityToPhred, as the apply kernel uses it
+int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin) {
+  const auto& t = thresholds().thr;
+  if (qmin) *qmin = kThrQmin;
+  if (out) memcpy(out, t.data(), sizeof(double) * (size_t)std::min<int32_t>(cap, (int32_t)t.size()));
+  return (int32_t)t.size();
+}
+
+// ---------------------------------------------------------------- apply ----
+
+bqsr_status bqsr_apply_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
+                             uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
+                             void* stream) {
+  if (!ctx || !b || !L || !out_qual || !out_start || !out_len) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (b->dims.n_rg > L->dims.n_rg || b->dims.max_len > L->dims.max_len)
+    return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = S(stream);
+  HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
+  HIP_TRY(hipMemsetAsync(b->d_err + 1, 0, 8, s));
+  if (b->rd.n_reads == 0) return ok();
+  ApplyParams P{};
+  P.rd = b->rd;
+  P.g = geom(L->dims);
+  P.w.qw = apply_qw(P.g.C);
+  P.w.q_lo = std::min(b->q_lo, kQBins - 1);
+  P.w.rg_lo = b->rg_lo;
+  P.n_rg = L->dims.n_rg;
+  P.s1 = L->s1;
+  P.d2 = L->d2;
+  P.rq_ok = L->rq_ok;
+  P.key_ok = L->key_ok;
+  P.grp_ok = L->grp_ok;
+  P.n_groups = L->n_groups;
+  P.thr = ctx->d_thr;
+  P.thr_qmin = kThrQmin;
+  P.thr_n = kThrN;
+  P.out_qual = out_qual;
+  P.out_start = out_start;
+  P.out_len = out_len;
+  P.exc = (unsigned long long*)exceptions;
+  P.max_exc = exceptions ? max_exceptions : 0;
+  P.n_exc = b->d_err + 1;
+  P.err = b->d_err;
+  const size_t lds = apply_lds(P.w.qw, P.g.C);
+  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+bqsr_status bqsr_apply_result(bqsr_batch* b, int64_t* n_exceptions, void* stream) {
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t s = S(stream);
+  unsigned long long w[2];
+  HIP_TRY(hipMemcpyAsync(w, b->d_err, 16, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (n_exceptions) *n_exceptions = (int64_t)w[1];
+  return from_err_key(w[0], 0);
+}
+
+bqsr_status bqsr_apply(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint8_t* out_qual, uint32_t* out_start,
+                       uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions, int64_t* n_exceptions,
+                       void* stream) {
+  bqsr_status st = bqsr_apply_async(ctx, b, l, out_qual, out_start, out_len, exceptions, max_exceptions, stream);
+  if (st != BQSR_OK) return st;
+  return bqsr_apply_result(b, n_exceptions, stream);
+}
+
+bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* R, const bqsr_lut* l, uint16_t* out_qual,
+                               uint32_t* out_len) {
+  if (!ctx || !R || !l || !out_qual || !out_len) return fail(BQSR_ERR_INVALID_ARG, "null");
+  bqsr_batch* b = nullptr;
+  bqsr_status st = bqsr_batch_create(ctx, R, nullptr, &b);
+  if (st != BQSR_OK) return st;
+  const int64_t n = R->n_reads;
+  uint8_t* d_out = nullptr;
+  uint32_t *d_start = nullptr, *d_len = nullptr;
+  uint64_t* d_exc = nullptr;
+  const int64_t max_exc = 1 << 16;
+  std::vector<void*> tmp;
+  if ((st = dalloc(tmp, &d_out, (size_t)b->n_slots + 16)) != BQSR_OK || (st = dalloc(tmp, &d_start, (size_t)n)) != BQSR_OK ||
+      (st = dalloc(tmp, &d_len, (size_t)n)) != BQSR_OK || (st = dalloc(tmp, &d_exc, (size_t)max_exc)) != BQSR_OK) {
+    for (void* p : tmp) (void)hipFree(p);
+    bqsr_batch_destroy(b);
+    return st;
+  }
+  int64_t n_exc = 0;
+  st = bqsr_apply(ctx, b, l, d_out, d_start, d_len, d_exc, max_exc, &n_exc, nullptr);
+  if (st == BQSR_OK && n_exc > max_exc) st = fail(BQSR_ERR_UNSUPPORTED, "too many non-byte quality chars");
+  if (st == BQSR_OK) {
+    std::vector<uint8_t> h_out((size_t)b->n_slots + 16);
+    std::vector<uint32_t> h_start((size_t)std::max<int64_t>(n, 1)), h_len((size_t)std::max<int64_t>(n, 1));
+    std::vector<uint64_t> h_exc((size_t)std::max<int64_t>(n_exc, 1));
+    hipError_t e = hipMemcpy(h_out.data(), d_out, h_out.size(), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && n) e = hipMemcpy(h_start.data(), d_start, (size_t)n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && n) e = hipMemcpy(h_len.data(), d_len, (size_t)n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && n_exc) e = hipMemcpy(h_exc.data(), d_exc, (size_t)n_exc * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      st = fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
+    } else {
+      // slots of read r start at the packed offsets; rebuild them on the host
+      std::vector<uint64_t> slot((size_t)n + 1, 0);
+      for (int64_t r = 0; r < n; ++r) {
+        const uint32_t f = R->flags[r];
+        const uint64_t lq = (f & BQSR_F_HAS_QUAL) ? R->qual_offset[r + 1] - R->qual_offset[r] : 0;
+        const uint64_t ls = (f & BQSR_F_HAS_SEQ) ? R->seq_offset[r + 1] - R->seq_offset[r] : 0;
+        slot[(size_t)r + 1] = slot[(size_t)r] + std::max(lq, ls);
+      }
+      std::vector<uint16_t> wide;  // exceptions keyed by slot
+      std::vector<std::pair<uint64_t, uint16_t>> ex;
+      for (int64_t i = 0; i < n_exc; ++i) ex.push_back({h_exc[(size_t)i] >> 16, (uint16_t)(h_exc[(size_t)i] & 0xFFFF)});
+      std::sort(ex.begin(), ex.end());
+      for (int64_t r = 0; r < n; ++r) {
+        uint16_t* dst = out_qual + R->qual_offset[r];
+        const uint64_t s0 = slot[(size_t)r] + h_start[(size_t)r];
+        for (uint32_t k = 0; k < h_len[(size_t)r]; ++k) {
+          uint16_t v = h_out[s0 + k];
+          if (!ex.empty()) {
+            auto it = std::lower_bound(ex.begin(), ex.end(), std::make_pair(s0 + k, (uint16_t)0));
+            if (it != ex.end() && it->first == s0 + k) v = it->second;
+          }
+          dst[k] = v;
+        }
+        out_len[r] = h_len[(size_t)r];
+      }
+    }
+  }
+  for (void* p : tmp) (void)hipFree(p);
+  bqsr_batch_destroy(b);
+  return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,174 @@
+// bqsr_internal.h -- device data layout and kernel parameter blocks shared by
+// the HIP kernels (bqsr_kernels.hip) and the host side (bqsr_capi.cpp).
+// Layout rationale: DESIGN.md "Data layout in HBM".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/adam_bqsr.h"
+
+namespace bqsr {
+
+// ---- per-read records (SoA of two fixed-size records) -----------------------
+// 16 B: everything the per-base passes need.
+struct ReadMeta {
+  uint64_t slot;   // first base slot of the read in qual[] / bases[]
+  uint16_t lq;     // quality length (Lq)
+  uint16_t ls;     // sequence length (Ls)
+  uint16_t flags;  // BQSR_F_* (bits 0-5, 8-14) | kSeqOther
+  uint16_t rg;     // recordGroupId
+};
+static_assert(sizeof(ReadMeta) == 16, "ReadMeta must be 16 B");
+
+// 24 B: alignment fields, read by the per-read prep only.
+struct ReadAlign {
+  int64_t start;       // 0-based alignment start
+  uint32_t cigar_off;  // into cigar[]
+  uint32_t md_off;     // into md[]
+  int32_t contig;      // index into the known-site contigs, <0 unknown
+  uint16_t n_cigar;
+  uint16_t md_len;
+};
+static_assert(sizeof(ReadAlign) == 24, "ReadAlign must be 24 B");
+
+// packer-derived flag: the sequence holds a byte outside "ACGTN"
+// (BaseContext.simpleReverseComplement throws on it for reverse reads,
+// StandardCovariate.scala:55-57,70).
+constexpr uint16_t kSeqOther = 1u << 15;
+
+// 4-bit base codes
+constexpr uint8_t kCodeA = 0, kCodeC = 1, kCodeG = 2, kCodeT = 3, kCodeN = 4, kCodeOther = 5;
+
+constexpr int kMaxQ = 60;      // RecalUtil.Constants.MAX_REASONABLE_QSCORE
+constexpr int kCtxSlots = 21;  // contexts -4..16
+constexpr int kQBins = 128;    // qual values 0..127 (Java byte >= 0)
+
+// Tile geometry: a tile is `reads_per_tile` consecutive reads whose slots fit
+// in kTileSlots; one wavefront processes one tile at a time.
+constexpr int kTileSlots = 2048;
+constexpr int kMaxTileReads = 64;
+constexpr int kWaves = 8;  // waves per block (512 threads)
+constexpr int kBlockThreads = 64 * kWaves;
+constexpr int kMdStage = 1024;    // MD bytes staged per tile (larger tiles read MD from HBM)
+constexpr int kCigarStage = 192;  // CIGAR elements staged per tile
+
+// Error reporting: one u64 per launch, atomicMin of
+//   read << 28 | read_offset << 8 | rank << 4 | code
+// so the first failing read (read order), and within it the first failing
+// base / step, wins -- the exception the JVM would raise first.
+constexpr uint64_t kNoError = ~0ull;
+__host__ __device__ inline uint64_t err_key(uint64_t read, uint32_t o, uint32_t rank, uint32_t code) {
+  return (read << 28) | ((uint64_t)(o & 0xFFFFF) << 8) | ((uint64_t)(rank & 0xF) << 4) | (code & 0xF);
+}
+// ranks at one read offset, in the order ReadCovariates.next evaluates them
+enum : uint32_t {
+  kRankCtor = 0,   // constructor: qual / RG / sequence / reverse complement
+  kRankCigar = 1,  // referencePositions (null cigar/start, empty range, index past the end)
+  kRankMd = 2,     // mdEvent parse
+  kRankSnp = 3,    // SnpTable: null referenceName
+  kRankCov = 4,    // BaseCovariates: covariate arrays shorter than the quals
+  kRankTable = 5   // RecalTable += / getErrorRateShifts
+};
+
+// ---- known sites -------------------------------------------------------------
+struct SitesDev {
+  const int64_t* pos;          // all contigs' sorted unique positions
+  const uint64_t* off;         // [n_contigs + 1]
+  const uint32_t* bucket;      // per contig: first site index (relative) with pos >= b << shift
+  const uint64_t* bucket_off;  // [n_contigs + 1] into bucket
+  const int64_t* bucket_base;  // [n_contigs] position of bucket 0 (min pos)
+  int32_t n_contigs;
+  int32_t shift;
+};
+
+// ---- table geometry ----------------------------------------------------------
+struct TableGeom {
+  int32_t K;      // 60*(n_rg-1) + 128
+  int32_t C;      // 2*L + 1
+  int32_t L;      // max_len
+  int32_t cells;  // C + 21
+};
+
+// LDS window of the covariate table: rows (rg_lo, q_lo .. q_lo+qw-1).
+struct Window {
+  int32_t qw;
+  int32_t q_lo;
+  int32_t rg_lo;
+};
+
+struct ReadsDev {
+  const ReadMeta* meta;
+  const ReadAlign* align;
+  const uint8_t* qual;
+  const uint8_t* bases;
+  const uint32_t* cigar;
+  const uint8_t* md;
+  int64_t n_reads;
+  int32_t reads_per_tile;
+  int64_t n_tiles;
+};
+
+struct ObserveParams {
+  ReadsDev rd;
+  SitesDev sites;  // n_contigs == 0: SnpTable()
+  TableGeom g;
+  Window w;
+  int64_t* touched;  // [K]
+  int64_t* obs;      // [K*cells]
+  int64_t* mm;       // [K*cells]
+  uint32_t* hq_block;  // [n_blocks][128] per-block qual histogram of folded bases
+  uint16_t* h2;        // [n_tiles][128]   per-tile qual histogram of folded bases
+  unsigned long long* err;
+  int32_t n_blocks;
+};
+
+struct FoldParams {
+  ReadsDev rd;
+  const uint32_t* hq_block;
+  const uint16_t* h2;
+  const double* pow10;  // phredToErrorProbabilityCache[0..127]
+  int32_t n_blocks;
+  double* em_out;      // [1]
+  unsigned long long* status;  // [1] 0 = ok
+};
+
+struct ApplyParams {
+  ReadsDev rd;
+  TableGeom g;
+  Window w;
+  int32_t n_rg;
+  const double* s1;       // [n_rg*128][C]  a2 + cycleDelta
+  const double* d2;       // [n_rg*128][21] contextDelta
+  const uint8_t* rq_ok;   // [n_rg*128]     key touched && read group present
+  const uint8_t* key_ok;  // [K]  touched
+  const uint8_t* grp_ok;  // [n_groups] group r exists at index r+1
+  int32_t n_groups;
+  const double* thr;      // phred thresholds, see PhredThresholds
+  int32_t thr_qmin;       // Q value of thr[0]
+  int32_t thr_n;
+  uint8_t* out_qual;
+  uint32_t* out_start;
+  uint32_t* out_len;
+  unsigned long long* exc;  // (slot << 16 | code16)
+  int64_t max_exc;
+  unsigned long long* n_exc;
+  unsigned long long* err;
+};
+
+// finalize results read back by the host
+struct FinalOut {
+  int64_t g_obs, g_mm;
+  double avg, global_error;
+  int32_t any_key;
+  int32_t pad;
+};
+
+// errorProbabilityToPhred step function: thr[i] = the largest p > 0 whose
+// javaD2I(-10*log10(p)) >= thr_qmin + i.  Q(p) = max{n : p <= thr[n - qmin]}.
+constexpr int kThrQmin = -3100;
+constexpr int kThrQmax = 3300;
+constexpr int kThrN = kThrQmax - kThrQmin + 1;
+constexpr int kThrLdsLo = -64;  // LDS copy covers Q in [-64, 191]
+constexpr int kThrLdsN = 256;
+
+}  // namespace bqsr

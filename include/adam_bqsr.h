@@ -1,0 +1,245 @@
+/*
+ * adam_bqsr.h -- C ABI of the MI355X-native BQSR (base quality score
+ * recalibration) path.  This is the drop-in boundary that replaces the two
+ * JVM function bodies of ADAM's RecalibrateBaseQualities:
+ *
+ *   observe : RecalibrateBaseQualities.computeTable  (the per-partition
+ *             `aggregate` fold)      adam-core/.../rdd/RecalibrateBaseQualities.scala:52-64
+ *   apply   : RecalibrateBaseQualities.applyTable    (the per-partition
+ *             `map(recalibrate)`)    adam-core/.../rdd/RecalibrateBaseQualities.scala:66-76
+ *
+ * The driver-side pieces stay host-side and are exported separately:
+ *   merge    : RecalTable.++          adam-core/.../rdd/recalibration/RecalTable.scala:90-108
+ *   finalize : RecalTable.finalizeTable                  RecalTable.scala:117-126
+ *   sites    : SnpTable (known-site mask)   adam-core/.../models/SnpTable.scala:12-47
+ *
+ * The public Scala API in front of these bodies is unchanged:
+ *   AdamRecordRDDFunctions.adamBQSR(dbSNP: SnpTable)  core/rdd/AdamRDDFunctions.scala:104-107
+ *   `adam transform -recalibrate_base_qualities [-dbsnp_sites f]` cli/Transform.scala:47-50
+ * (INTEGRATION.md shows the JNI stubs a maintainer adds to those closures.)
+ *
+ * Conventions
+ *  - plain C, POD structs, no torch / HIP types in any signature; `stream`
+ *    arguments are a hipStream_t passed as void* (NULL = the library's own
+ *    per-thread stream);
+ *  - the library owns every handle and the device memory behind it; every
+ *    handle has a *_destroy;
+ *  - every function returns a bqsr_status; on failure bqsr_last_error()
+ *    returns a thread-local message and, for data errors, the index of the
+ *    first offending read (in read order) is reported through
+ *    bqsr_last_error_read();
+ *  - all exports are re-entrant: Spark local[N] calls observe/apply from N
+ *    task threads at once.  merge/finalize are single-threaded driver calls.
+ */
+#ifndef ADAM_BQSR_H
+#define ADAM_BQSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BQSR_ABI_VERSION 1
+
+/* Status codes.  Data errors mirror the JVM exception the reference throws
+ * on the same input (it fails the whole Spark job). */
+typedef enum bqsr_status {
+  BQSR_OK = 0,
+  BQSR_ERR_NULL_RG = 1,          /* NullPointerException, QualByRG: StandardCovariate.scala:28            */
+  BQSR_ERR_MD_PARSE = 2,         /* IllegalArgumentException, MdTag.apply: MdTag.scala:52,75              */
+  BQSR_ERR_CIGAR_SHORT = 3,      /* IndexOutOfBoundsException, referencePositions(o): RichADAMRecord.scala:191 */
+  BQSR_ERR_BAD_REVCOMP_BASE = 4, /* NoSuchElementException, COMPL_MP(b): StandardCovariate.scala:70       */
+  BQSR_ERR_EMPTY_TABLE = 5,      /* UnsupportedOperationException("empty.reduceLeft"): RecalTable.scala:123 */
+  BQSR_ERR_MISSING_KEY = 6,      /* NoSuchElementException, readGroupCounts/qualByRGCounts: RecalTable.scala:129,135 */
+  BQSR_ERR_QUAL_RANGE = 7,       /* ArrayIndexOutOfBoundsException, phredToErrorProbability: PhredUtils.scala:32 */
+  BQSR_ERR_NULL_FIELD = 8,       /* NullPointerException on a null qual/sequence/cigar/start/referenceName */
+  BQSR_ERR_SEQ_SHORT = 9,        /* ArrayIndexOutOfBoundsException: covariate arrays shorter than the quals */
+  BQSR_ERR_CIGAR_INVALID = 10,   /* NoSuchElementException: zero-length M/X/=/S element (Range.last)     */
+  BQSR_ERR_INVALID_ARG = 11,     /* bad call: null pointer, inconsistent sizes, dims mismatch            */
+  BQSR_ERR_DEVICE = 12,          /* HIP runtime failure                                                  */
+  BQSR_ERR_UNSUPPORTED = 13      /* input outside what the device path handles          */
+} bqsr_status;
+
+/* ADAMRecord boolean fields (adam-format/.../adam.avdl:28-38) and null-ness
+ * of the optional fields BQSR dereferences.  A field absent in the record is
+ * a 0 bit. */
+enum {
+  BQSR_F_PAIRED = 1u << 0,         /* readPaired          */
+  BQSR_F_MAPPED = 1u << 1,         /* readMapped          */
+  BQSR_F_NEG_STRAND = 1u << 2,     /* readNegativeStrand  */
+  BQSR_F_SECOND_OF_PAIR = 1u << 3, /* secondOfPair        */
+  BQSR_F_PRIMARY = 1u << 4,        /* primaryAlignment    */
+  BQSR_F_DUPLICATE = 1u << 5,      /* duplicateRead       */
+  BQSR_F_HAS_RG = 1u << 8,         /* recordGroupId != null        */
+  BQSR_F_HAS_MD = 1u << 9,         /* mismatchingPositions != null */
+  BQSR_F_HAS_QUAL = 1u << 10,      /* qual != null                 */
+  BQSR_F_HAS_SEQ = 1u << 11,       /* sequence != null             */
+  BQSR_F_HAS_CIGAR = 1u << 12,     /* cigar != null                */
+  BQSR_F_HAS_START = 1u << 13,     /* start != null                */
+  BQSR_F_HAS_REFNAME = 1u << 14    /* referenceName != null        */
+};
+
+/* BAM CIGAR op codes (len << 4 | op), the samtools CigarOperator order. */
+enum { BQSR_CIGAR_M = 0, BQSR_CIGAR_I = 1, BQSR_CIGAR_D = 2, BQSR_CIGAR_N = 3, BQSR_CIGAR_S = 4,
+       BQSR_CIGAR_H = 5, BQSR_CIGAR_P = 6, BQSR_CIGAR_EQ = 7, BQSR_CIGAR_X = 8 };
+
+/* Contig id meaning "referenceName is not a SnpTable contig" (not masked,
+ * SnpTable.scala:21-22 catches the lookup failure). */
+#define BQSR_CONTIG_UNKNOWN (-1)
+
+/* One partition of ADAMRecords flattened to columns: what the JNI shim fills
+ * from the Spark partition iterator.  Strings are byte columns addressed by
+ * [n_reads+1] offset arrays (Arrow layout). */
+typedef struct bqsr_records {
+  int64_t n_reads;
+  const uint32_t* flags;        /* [n] BQSR_F_* bits                                   */
+  const int32_t* rg_id;         /* [n] recordGroupId (RecordGroupDictionary index)    */
+  const int32_t* contig_id;     /* [n] index into the bqsr_sites contig list, or BQSR_CONTIG_UNKNOWN */
+  const int64_t* start;         /* [n] 0-based alignment start                         */
+  const uint64_t* seq_offset;   /* [n+1] into seq                                      */
+  const uint8_t* seq;           /* sequence bytes (ASCII)                              */
+  const uint64_t* qual_offset;  /* [n+1] into qual                                     */
+  const uint8_t* qual;          /* quality chars, phred+33 (ASCII)                     */
+  const uint64_t* cigar_offset; /* [n+1] into cigar                                    */
+  const uint32_t* cigar;        /* BAM-encoded CIGAR elements (len<<4 | op)            */
+  const uint64_t* md_offset;    /* [n+1] into md                                       */
+  const uint8_t* md;            /* MD:Z strings                                        */
+} bqsr_records;
+
+/* Dense covariate-table dimensions.  The reference's RecalTable is a
+ * HashMap[qualByRG key -> Array(cycle map, context map)]; the dense form has
+ *   K = 60*(n_rg-1) + 128 keys (q + 60*rg, RecalTable key aliasing kept),
+ *   C = 2*max_len + 1 cycle slots (cycle c -> c + max_len),
+ *   X = 21 context slots (ctx x -> x + 4, x in [-4, 16]). */
+typedef struct bqsr_dims {
+  int32_t n_rg;    /* read groups (max recordGroupId + 1) */
+  int32_t max_len; /* longest sequence                   */
+} bqsr_dims;
+
+typedef struct bqsr_context bqsr_context; /* device, streams, static tables  */
+typedef struct bqsr_sites bqsr_sites;     /* known sites (SnpTable)          */
+typedef struct bqsr_batch bqsr_batch;     /* device-resident packed reads    */
+typedef struct bqsr_table bqsr_table;     /* device-resident count table     */
+typedef struct bqsr_lut bqsr_lut;         /* finalized table / apply tables  */
+
+/* ---- library / errors ---------------------------------------------------- */
+int bqsr_abi_version(void);
+const char* bqsr_last_error(void);
+int64_t bqsr_last_error_read(void);
+const char* bqsr_status_name(bqsr_status s);
+
+/* Open the library on a HIP device (one context per device / rank). */
+bqsr_status bqsr_context_create(int device, bqsr_context** out);
+void bqsr_context_destroy(bqsr_context* ctx);
+
+/* ---- known sites (SnpTable.apply(File) + broadcast, SnpTable.scala:32-47,
+ *      AdamRDDFunctions.scala:105) ------------------------------------------ */
+/* positions are the VCF POS values exactly as stored (no -1: quirk Q7).  Each
+ * contig's list may be unsorted / contain duplicates. */
+bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, const int64_t* const* pos,
+                              const uint64_t* n, int32_t n_contigs, bqsr_sites** out);
+void bqsr_sites_destroy(bqsr_sites* s);
+
+/* ---- reads --------------------------------------------------------------- */
+/* Pack a record partition into the device layout (4-bit base codes, phred
+ * bytes, 16+24 B per-read metadata, CIGAR, MD) and upload it. */
+bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* recs, void* stream, bqsr_batch** out);
+void bqsr_batch_destroy(bqsr_batch* b);
+int64_t bqsr_batch_reads(const bqsr_batch* b);
+int64_t bqsr_batch_bases(const bqsr_batch* b);
+bqsr_dims bqsr_batch_dims(const bqsr_batch* b);
+
+/* Caller-owned device buffers already in the packed layout (used by the
+ * benchmark, which synthesises reads directly in HBM).  Layout documented in
+ * DESIGN.md §"Data layout in HBM".  No copy; buffers must outlive the batch. */
+typedef struct bqsr_device_reads {
+  int64_t n_reads;
+  int64_t n_slots;        /* total base slots (sum of max(Ls, Lq) per read)           */
+  const void* meta;       /* [n] 16-B records {u64 slot; u16 lq; u16 ls; u16 flags; u16 rg} */
+  const void* align;      /* [n] 24-B records {i64 start; u32 cigar_off; u32 md_off; i32 contig; u16 n_cigar; u16 md_len} */
+  const uint8_t* qual;    /* [n_slots] phred bytes (qual char - 33, as Java byte)    */
+  const uint8_t* bases;   /* [(n_slots+1)/2] 4-bit codes A0 C1 G2 T3 N4 other5         */
+  const uint32_t* cigar;  /* BAM elements                                             */
+  const uint8_t* md;      /* MD bytes                                                 */
+  bqsr_dims dims;
+} bqsr_device_reads;
+bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* dev, bqsr_batch** out);
+
+/* ---- table --------------------------------------------------------------- */
+/* int64 words of a dense table: [touched K][obs K*(C+X)][mm K*(C+X)]. */
+int64_t bqsr_table_words(bqsr_dims d);
+/* Zeroed table in library memory, or over caller device memory (e.g. a torch
+ * tensor that takes part in an RCCL all-reduce) when `device_words` != NULL. */
+bqsr_status bqsr_table_create(bqsr_context* ctx, bqsr_dims d, void* device_words, bqsr_table** out);
+void bqsr_table_destroy(bqsr_table* t);
+bqsr_dims bqsr_table_dims(const bqsr_table* t);
+void* bqsr_table_device_ptr(bqsr_table* t);
+/* Copy to / from host int64 arrays in the word layout above. */
+bqsr_status bqsr_table_download(const bqsr_table* t, int64_t* host_words);
+bqsr_status bqsr_table_upload(bqsr_table* t, const int64_t* host_words);
+
+/* ---- observe: computeTable's per-partition fold ------------------------- */
+/* Folds every usable read (readMapped && primaryAlignment && !duplicateRead &&
+ * mismatchingPositions != null, RecalibrateBaseQualities.scala:29-32) of the
+ * batch into `table` (added to its counts) and returns the partition's
+ * expectedMismatch, folded from 0.0 in read/base order exactly as Spark's
+ * per-partition foldLeft does (RecalTable.scala:61).  `sites` may be NULL
+ * (SnpTable()). */
+bqsr_status bqsr_observe(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* table,
+                         double* expected_mismatch, void* stream);
+
+/* Host-records convenience form of the survey's `bqsr_observe(soa, sites,
+ * out_partial, out_em)`: packs, uploads, observes into a fresh table. */
+bqsr_status bqsr_observe_records(bqsr_context* ctx, const bqsr_records* recs, const bqsr_sites* sites,
+                                 bqsr_dims dims, bqsr_table** out_partial, double* out_expected_mismatch);
+
+/* ---- merge: RecalTable.++ on the driver ---------------------------------- */
+/* acc += part (int64, exact); *acc_em = *acc_em + part_em (the caller owns
+ * the merge order, H1 in SURVEY.md).  Dims must match. */
+bqsr_status bqsr_table_merge(bqsr_table* acc, const bqsr_table* part, double* acc_em, double part_em);
+
+/* ---- finalize: RecalTable.finalizeTable ---------------------------------- */
+/* Returns BQSR_ERR_EMPTY_TABLE where the reference throws
+ * UnsupportedOperationException("empty.reduceLeft"). */
+bqsr_status bqsr_finalize(bqsr_context* ctx, const bqsr_table* t, double expected_mismatch, bqsr_lut** out);
+void bqsr_lut_destroy(bqsr_lut* l);
+/* Finalized statistics (RecalTable fields): average reported error, global
+ * counts, and per-read-group counts ((key-1)/60 grouping). */
+typedef struct bqsr_final_stats {
+  double average_reported_error;
+  double global_error;
+  int64_t global_obs, global_mm;
+  int32_t n_groups; /* group slots reported in rg_obs/rg_mm (index r + 1; slot 0 = group -1 unused) */
+} bqsr_final_stats;
+bqsr_status bqsr_lut_stats(const bqsr_lut* l, bqsr_final_stats* out);
+/* getErrorRateShifts for one base covariate (RecalTable.scala:128-152):
+ * shifts[0..3] = readGroupDelta, qualScoreDelta, cycleDelta, contextDelta;
+ * *new_q = errorProbabilityToPhred(fold).  qual_by_rg = q + 60*rg. */
+bqsr_status bqsr_lut_shifts(const bqsr_lut* l, int32_t qual_by_rg, int32_t qual, int32_t cycle, int32_t context,
+                            double shifts[4], int32_t* new_q);
+
+/* ---- apply: applyTable's per-partition map -------------------------------- */
+/* Device form.  For every read: eligible reads (mapped && primary && !dup,
+ * RecalibrateBaseQualities.scala:69) get new quality chars
+ * (char)(Q+33) for read offsets [st, end) written at out_qual[slot+st ..
+ * slot+end) (low byte), with out_start[r] = st, out_len[r] = end-st;
+ * ineligible reads are passed through (out_start 0, out_len Lq, chars copied).
+ * Codes that do not fit a byte (Q+33 > 255 after Java's (char) narrowing) are
+ * reported through the exception list: (slot index, 16-bit code) pairs;
+ * *n_exceptions counts them (the list holds at most max_exceptions).
+ * All output pointers are device pointers. */
+bqsr_status bqsr_apply(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint8_t* out_qual,
+                       uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
+                       int64_t* n_exceptions, void* stream);
+
+/* Host-records form: out_qual is host uint16_t[qual_offset[n]] (Java chars),
+ * read r's new qual string is out_qual[qual_offset[r] .. + out_len[r]). */
+bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* recs, const bqsr_lut* l,
+                               uint16_t* out_qual, uint32_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADAM_BQSR_H */

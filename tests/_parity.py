@@ -1,0 +1,106 @@
+"""Shared helpers: run one BQSR job through the HIP C ABI and through the CPU
+oracle on the same partitions, and compare bit for bit."""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+import oracle as O
+from adam_amd import _capi, bqsr
+from adam_amd.records import RecordBatch
+
+
+class Result:
+    def __init__(self, words=None, em=None, outs=None, error=None, error_read=-1, parts_em=None):
+        self.words, self.em, self.outs = words, em, outs
+        self.error, self.error_read = error, error_read
+        self.parts_em = parts_em or []
+
+
+def run_gpu(parts: Sequence[RecordBatch], sites: Optional[Dict] = None, dims=None, stage="all") -> Result:
+    """observe each partition (fresh table, em from 0.0) -> merge in order -> finalize -> apply."""
+    ctx = bqsr.Context.get(0)
+    snp = bqsr.SnpTable(sites) if sites else None
+    d = dims or bqsr.dims_of(parts)
+    L = _capi.lib()
+    acc = bqsr.RecalTable(d, ctx)
+    parts_em = []
+    try:
+        for p in parts:
+            s, keep = p.c_struct(p.contig_ids_for(snp.contigs if snp else None))
+            h = ctypes.c_void_p()
+            em = ctypes.c_double(0.0)
+            _capi.check(L.bqsr_observe_records(ctx.handle, ctypes.byref(s), snp.handle(ctx) if snp else None, d,
+                                               ctypes.byref(h), ctypes.byref(em)))
+            part = bqsr.RecalTable.__new__(bqsr.RecalTable)
+            part.ctx, part.dims, part.handle, part.expected_mismatch = ctx, d, h, em.value
+            parts_em.append(em.value)
+            acc.merge_into(part)
+        words = acc.words()
+        if stage == "observe":
+            return Result(words, acc.expected_mismatch, None, parts_em=parts_em)
+        fin = acc.finalize_table()
+        outs = []
+        for p in parts:
+            s, keep = p.c_struct()
+            chars = np.zeros(max(1, int(p.qual_offset[-1])), dtype=np.uint16)
+            out_len = np.zeros(max(1, p.n_reads), dtype=np.uint32)
+            _capi.check(L.bqsr_apply_records(ctx.handle, ctypes.byref(s), fin.handle, chars.ctypes.data,
+                                             out_len.ctypes.data))
+            outs.append((chars, out_len))
+        return Result(words, acc.expected_mismatch, outs, parts_em=parts_em)
+    except _capi.BQSRError as e:
+        return Result(error=e.name, error_read=e.read)
+
+
+def run_oracle(parts: Sequence[RecordBatch], sites: Optional[Dict] = None, dims=None, stage="all") -> Result:
+    d = dims or bqsr.dims_of(parts)
+    od = O.Dims(d.n_rg, d.max_len)
+    osites = O.Sites(sites) if sites else None
+    words = np.zeros(O.table_words(od), dtype=np.int64)
+    em = 0.0
+    parts_em = []
+    try:
+        for p in parts:
+            w, e = O.observe(p, osites, od)
+            words += w
+            em = em + e
+            parts_em.append(e)
+        if stage == "observe":
+            return Result(words, em, None, parts_em=parts_em)
+        fin = O.Final(od, words, em)
+        outs = [O.apply(p, fin) for p in parts]
+        return Result(words, em, outs, parts_em=parts_em)
+    except O.OracleError as e:
+        return Result(error=_capi.STATUS_NAMES[e.code], error_read=e.read)
+
+
+def assert_same(parts, g: Result, o: Result):
+    assert g.error == o.error, "error: gpu %s@%d oracle %s@%d" % (g.error, g.error_read, o.error, o.error_read)
+    if o.error is not None:
+        assert g.error_read == o.error_read, "error read: gpu %d oracle %d" % (g.error_read, o.error_read)
+        return
+    assert np.array_equal(g.words, o.words), "covariate table differs at %s" % np.nonzero(g.words != o.words)[0][:10]
+    assert g.parts_em == o.parts_em, "per-partition expectedMismatch differs: %r vs %r" % (g.parts_em, o.parts_em)
+    assert g.em == o.em
+    if o.outs is None:
+        return
+    for p, (gc, gl), (oc, ol) in zip(parts, g.outs, o.outs):
+        n = p.n_reads
+        bad = np.nonzero(gl[:n] != ol[:n])[0]
+        assert bad.size == 0, "out_len differs at reads %s" % bad[:10]
+        m = int(p.qual_offset[-1])
+        bad = np.nonzero(gc[:m] != oc[:m])[0]
+        assert bad.size == 0, "qualities differ at chars %s: gpu %s oracle %s" % (bad[:10], gc[bad[:10]], oc[bad[:10]])
+
+
+def check(parts, sites=None, dims=None, expect_error=None):
+    parts = list(parts)
+    o = run_oracle(parts, sites, dims)
+    g = run_gpu(parts, sites, dims)
+    if expect_error is not None:
+        assert o.error == expect_error, "oracle gave %s, expected %s" % (o.error, expect_error)
+    assert_same(parts, g, o)
+    return g, o
