@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libadam_bqsr.so")
 
 BQSR_OK = 0
+STAGE_RESET, STAGE_KERNEL, STAGE_FOLD = 1, 2, 4
 STATUS_NAMES = ["OK", "NULL_RG", "MD_PARSE", "CIGAR_SHORT", "BAD_REVCOMP_BASE", "EMPTY_TABLE", "MISSING_KEY",
                 "QUAL_RANGE", "NULL_FIELD", "SEQ_SHORT", "CIGAR_INVALID", "INVALID_ARG", "DEVICE", "UNSUPPORTED"]
 (NULL_RG, MD_PARSE, CIGAR_SHORT, BAD_REVCOMP_BASE, EMPTY_TABLE, MISSING_KEY, QUAL_RANGE, NULL_FIELD, SEQ_SHORT,
@@ -89,6 +90,7 @@ def lib():
             "bqsr_batch_destroy": (None, [vp]),
             "bqsr_batch_reads": (i64, [vp]),
             "bqsr_batch_bases": (i64, [vp]),
+            "bqsr_batch_slots": (i64, [vp]),
             "bqsr_batch_dims": (Dims, [vp]),
             "bqsr_batch_wrap_device": (ctypes.c_int, [vp, ctypes.POINTER(DeviceReads), pp]),
             "bqsr_batch_set_window": (ctypes.c_int, [vp, i32, i32]),
@@ -103,6 +105,10 @@ def lib():
             "bqsr_observe": (ctypes.c_int, [vp, vp, vp, vp, ctypes.POINTER(dbl), vp]),
             "bqsr_observe_async": (ctypes.c_int, [vp, vp, vp, vp, vp]),
             "bqsr_observe_result": (ctypes.c_int, [vp, ctypes.POINTER(dbl), vp]),
+            "bqsr_observe_stage": (ctypes.c_int, [vp, vp, vp, vp, i32, vp]),
+            "bqsr_table_zero_async": (ctypes.c_int, [vp, vp]),
+            "bqsr_batch_em_device_ptr": (vp, [vp]),
+            "bqsr_apply_stage": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
             "bqsr_observe_records": (ctypes.c_int, [vp, vp, vp, Dims, pp, ctypes.POINTER(dbl)]),
             "bqsr_table_merge": (ctypes.c_int, [vp, vp, ctypes.POINTER(dbl), dbl]),
             "bqsr_finalize": (ctypes.c_int, [vp, vp, dbl, pp]),

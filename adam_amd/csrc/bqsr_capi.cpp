@@ -601,6 +601,7 @@ bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* d
 void bqsr_batch_destroy(bqsr_batch* b) { delete b; }
 int64_t bqsr_batch_reads(const bqsr_batch* b) { return b ? b->rd.n_reads : -1; }
 int64_t bqsr_batch_bases(const bqsr_batch* b) { return b ? b->n_bases : -1; }
+int64_t bqsr_batch_slots(const bqsr_batch* b) { return b ? b->n_slots : -1; }
 bqsr_dims bqsr_batch_dims(const bqsr_batch* b) { return b ? b->dims : bqsr_dims{0, 0}; }
 
 // window override (exported for device batches whose quals the host never saw)
@@ -683,18 +684,25 @@ bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
 }
 }  // namespace
 
-// launch observe + fold; does not synchronise (results land in b->d_err / d_em)
-bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t, void* stream) {
+// Stages of observe, launched on `stream` without synchronising (results land
+// in the batch's error word / expectedMismatch slot):
+//   BQSR_STAGE_RESET   clear the error word
+//   BQSR_STAGE_KERNEL  the observe kernel (counts into `t`)
+//   BQSR_STAGE_FOLD    the expectedMismatch fold kernel
+// Exposed separately so a caller can bracket one kernel with HIP events.
+bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
+                               int32_t stages, void* stream) {
   if (!ctx || !b || !t) return fail(BQSR_ERR_INVALID_ARG, "null");
   bqsr_status st = check_dims(b, t);
   if (st != BQSR_OK) return st;
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
-  HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
+  if (stages & BQSR_STAGE_RESET) HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
   if (b->rd.n_reads == 0) {
-    HIP_TRY(hipMemsetAsync(b->d_em, 0, 8, s));
+    if (stages & BQSR_STAGE_FOLD) HIP_TRY(hipMemsetAsync(b->d_em, 0, 8, s));
     return ok();
   }
+  if (stages & BQSR_STAGE_KERNEL) {
   ObserveParams P{};
   P.rd = b->rd;
   if (sites) P.sites = sites->dev();
@@ -712,6 +720,8 @@ bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   const size_t lds = observe_lds(P.w.qw, P.g.cells);
   hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
+  }
+  if (stages & BQSR_STAGE_FOLD) {
   FoldParams F{};
   F.rd = b->rd;
   F.hq_block = b->d_hq;
@@ -722,8 +732,25 @@ bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   F.status = b->d_err + 2;
   hipLaunchKernelGGL(bqsr_fold_kernel, dim3(1), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
+  }
   return ok();
 }
+
+// launch observe + fold; does not synchronise
+bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t, void* stream) {
+  return bqsr_observe_stage(ctx, b, sites, t, BQSR_STAGE_RESET | BQSR_STAGE_KERNEL | BQSR_STAGE_FOLD, stream);
+}
+
+// zero a table on a stream (a fresh `new RecalTable` for the next job)
+bqsr_status bqsr_table_zero_async(bqsr_table* t, void* stream) {
+  if (!t) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(t->ctx->device));
+  HIP_TRY(hipMemsetAsync(t->words, 0, (size_t)table_words(t->dims) * 8, S(stream)));
+  return ok();
+}
+
+// device pointer of the batch's expectedMismatch result (one double)
+void* bqsr_batch_em_device_ptr(bqsr_batch* b) { return b ? (void*)b->d_em : nullptr; }
 
 bqsr_status bqsr_observe_result(bqsr_batch* b, double* em, void* stream) {
   HIP_TRY(hipSetDevice(b->ctx->device));
@@ -768,15 +795,19 @@ bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double e
   if (!ctx || !t || !out) return fail(BQSR_ERR_INVALID_ARG, "null");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
-  bqsr_lut* L = new bqsr_lut;
+  const TableGeom g = geom(t->dims);
+  const int n_rg = t->dims.n_rg;
+  // *out may hold a LUT of the same dims from an earlier job: its buffers are reused
+  bqsr_lut* L = *out;
+  const bool reuse = L && L->ctx == ctx && L->dims.n_rg == t->dims.n_rg && L->dims.max_len == t->dims.max_len;
+  if (!reuse) L = new bqsr_lut;
   L->ctx = ctx;
   L->dims = t->dims;
   L->src = t;
-  const TableGeom g = geom(t->dims);
-  const int n_rg = t->dims.n_rg;
+  L->host_ready = false;
   L->n_groups = (g.K - 1) / kMaxQ + 2;
   bqsr_status st;
-  if ((st = dalloc(L->allocs, &L->qk_obs, g.K)) != BQSR_OK || (st = dalloc(L->allocs, &L->qk_mm, g.K)) != BQSR_OK ||
+  if (!reuse && ((st = dalloc(L->allocs, &L->qk_obs, g.K)) != BQSR_OK || (st = dalloc(L->allocs, &L->qk_mm, g.K)) != BQSR_OK ||
       (st = dalloc(L->allocs, &L->grp_obs, L->n_groups)) != BQSR_OK ||
       (st = dalloc(L->allocs, &L->grp_mm, L->n_groups)) != BQSR_OK ||
       (st = dalloc(L->allocs, &L->grp_ok, L->n_groups)) != BQSR_OK || (st = dalloc(L->allocs, &L->key_ok, g.K)) != BQSR_OK ||
@@ -784,7 +815,7 @@ bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double e
       (st = dalloc(L->allocs, &L->a2, (size_t)n_rg * kQBins)) != BQSR_OK ||
       (st = dalloc(L->allocs, &L->s1, (size_t)n_rg * kQBins * g.C)) != BQSR_OK ||
       (st = dalloc(L->allocs, &L->d2, (size_t)n_rg * kQBins * kCtxSlots)) != BQSR_OK ||
-      (st = dalloc(L->allocs, &L->d_out, 1)) != BQSR_OK) {
+      (st = dalloc(L->allocs, &L->d_out, 1)) != BQSR_OK)) {
     delete L;
     return st;
   }
@@ -798,7 +829,7 @@ bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double e
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost, s);
   if (e != hipSuccess) {
-    delete L;
+    if (!reuse) delete L;
     return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
   }
   *out = L;
@@ -814,6 +845,7 @@ bqsr_status bqsr_finalize_result(bqsr_lut* L, void* stream) {
 }
 
 bqsr_status bqsr_finalize(bqsr_context* ctx, const bqsr_table* t, double em, bqsr_lut** out) {
+  if (!out) return fail(BQSR_ERR_INVALID_ARG, "null out");
   bqsr_lut* L = nullptr;
   bqsr_status st = bqsr_finalize_async(ctx, t, em, &L, nullptr);
   if (st != BQSR_OK) return st;
@@ -922,17 +954,20 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin) {
 
 // ---------------------------------------------------------------- apply ----
 
-bqsr_status bqsr_apply_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
+// stages: BQSR_STAGE_RESET (error word, exception count), BQSR_STAGE_KERNEL (apply kernel)
+bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
                              uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
-                             void* stream) {
+                             int32_t stages, void* stream) {
   if (!ctx || !b || !L || !out_qual || !out_start || !out_len) return fail(BQSR_ERR_INVALID_ARG, "null");
   if (b->dims.n_rg > L->dims.n_rg || b->dims.max_len > L->dims.max_len)
     return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
-  HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
-  HIP_TRY(hipMemsetAsync(b->d_err + 1, 0, 8, s));
-  if (b->rd.n_reads == 0) return ok();
+  if (stages & BQSR_STAGE_RESET) {
+    HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
+    HIP_TRY(hipMemsetAsync(b->d_err + 1, 0, 8, s));
+  }
+  if (b->rd.n_reads == 0 || !(stages & BQSR_STAGE_KERNEL)) return ok();
   ApplyParams P{};
   P.rd = b->rd;
   P.g = geom(L->dims);
@@ -960,6 +995,13 @@ bqsr_status bqsr_apply_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
   return ok();
+}
+
+bqsr_status bqsr_apply_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
+                             uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
+                             void* stream) {
+  return bqsr_apply_stage(ctx, b, L, out_qual, out_start, out_len, exceptions, max_exceptions,
+                          BQSR_STAGE_RESET | BQSR_STAGE_KERNEL, stream);
 }
 
 bqsr_status bqsr_apply_result(bqsr_batch* b, int64_t* n_exceptions, void* stream) {

@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""BQSR (observe + apply) throughput on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+
+One step = one whole BQSR job over the GPU's read shard, inputs resident in
+HBM: zero the covariate table, observe (+ the exact expectedMismatch fold),
+[N > 1: RCCL int64 all-reduce of the table, all-gather of the per-shard
+expectedMismatch folded in rank order], finalize, apply.  `bases` = sum of the
+sequence lengths of ALL reads (filtered ones included).  Reads shard across
+ranks (each rank its own synthetic shard: weak scaling); rank 0 prints one
+JSON line.  See DESIGN.md "Measurement".
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "BQSR bases/sec (observe+apply) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E peak (spec)
+
+WORKLOADS = {
+    "cfg2": "cfg2: synthetic 10M x 100 bp reads, 1 read group, no known sites (per GPU)",
+    "cfg3": "cfg3: synthetic 60M x 101 bp reads on a 64.4 Mbp contig, ~1.3M known sites (sharded)",
+    "cfg4": "cfg4: synthetic 20M reads 150/250 bp, 96 read groups (per GPU)",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the config's)")
+    ap.add_argument("--cpu-reads", type=int, default=1_000_000, help="oracle baseline sample (reads)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from adam_amd import _capi, bqsr, synth
+    from adam_amd._capi import Dims, check
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    L = _capi.lib()
+    ctx = bqsr.Context.get(local)
+
+    cfg = dict(synth.CONFIGS[args.config])
+    n_reads = args.reads or cfg["n_reads"]
+    if args.config == "cfg3":
+        n_reads = args.reads or (cfg["n_reads"] // max(1, world))  # cfg3 is one dataset sharded over the GPUs
+    t_gen = time.time()
+    batch = synth.generate(n_reads, cfg["lens"], cfg["n_rg"], cfg["seed"] + 1_000_003 * rank)
+    sites = synth.known_sites(cfg["sites"]) if cfg["sites"] else None
+    snp = bqsr.SnpTable(sites) if sites else None
+    t_gen = time.time() - t_gen
+    n_bases = batch.n_bases
+
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    s, keep = batch.c_struct(batch.contig_ids_for(snp.contigs if snp else None))
+    bh = ctypes.c_void_p()
+    check(L.bqsr_batch_create(ctx.handle, ctypes.byref(s), sp, ctypes.byref(bh)))
+    del keep
+    n_slots = int(L.bqsr_batch_slots(bh))
+    dims = Dims(cfg["n_rg"], max(cfg["lens"]))
+    words = int(L.bqsr_table_words(dims))
+    table_t = torch.zeros(words, dtype=torch.int64, device=dev)
+    th = ctypes.c_void_p()
+    check(L.bqsr_table_create(ctx.handle, dims, ctypes.c_void_p(table_t.data_ptr()), ctypes.byref(th)))
+    sites_h = snp.handle(ctx) if snp else None
+    out_qual = torch.empty(n_slots + 64, dtype=torch.uint8, device=dev)
+    out_start = torch.empty(max(1, batch.n_reads), dtype=torch.int32, device=dev)
+    out_len = torch.empty(max(1, batch.n_reads), dtype=torch.int32, device=dev)
+    max_exc = 1 << 16
+    exc = torch.empty(max_exc, dtype=torch.int64, device=dev)
+    lut = ctypes.c_void_p()
+    torch.cuda.synchronize()
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    kt = {"observe": [], "fold": [], "apply": []}
+
+    def step(record: bool):
+        check(L.bqsr_table_zero_async(th, sp))
+        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_RESET, sp))
+        ev[0].record(stream)
+        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_KERNEL, sp))
+        ev[1].record(stream)
+        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_FOLD, sp))
+        ev[2].record(stream)
+        em = ctypes.c_double()
+        check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
+        if world > 1:
+            dist.all_reduce(table_t)  # exact int64 sum over xGMI (RCCL)
+            ems = torch.zeros(world, dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(ems, torch.tensor([em.value], dtype=torch.float64, device=dev))
+            total = 0.0
+            for v in ems.tolist():  # RecalTable.++ in rank order
+                total = total + v
+        else:
+            total = 0.0 + em.value
+        check(L.bqsr_finalize_async(ctx.handle, th, total, ctypes.byref(lut), sp))
+        check(L.bqsr_finalize_result(lut, sp))
+        check(L.bqsr_apply_stage(ctx.handle, bh, lut, ctypes.c_void_p(out_qual.data_ptr()),
+                                 ctypes.c_void_p(out_start.data_ptr()), ctypes.c_void_p(out_len.data_ptr()),
+                                 ctypes.c_void_p(exc.data_ptr()), max_exc, _capi.STAGE_RESET, sp))
+        ev[3].record(stream)
+        check(L.bqsr_apply_stage(ctx.handle, bh, lut, ctypes.c_void_p(out_qual.data_ptr()),
+                                 ctypes.c_void_p(out_start.data_ptr()), ctypes.c_void_p(out_len.data_ptr()),
+                                 ctypes.c_void_p(exc.data_ptr()), max_exc, _capi.STAGE_KERNEL, sp))
+        ev[4].record(stream)
+        nexc = ctypes.c_int64()
+        check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
+        if record:
+            kt["observe"].append(ev[0].elapsed_time(ev[1]))
+            kt["fold"].append(ev[1].elapsed_time(ev[2]))
+            kt["apply"].append(ev[3].elapsed_time(ev[4]))
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nb = torch.tensor([n_bases], dtype=torch.int64, device=dev)
+        dist.all_reduce(nb)
+        total_bases = int(nb.item())
+    else:
+        total_bases = n_bases
+
+    if rank == 0:
+        ms = {k: float(np.mean(v)) for k, v in kt.items()}
+        R = batch.n_reads
+        # algorithmic bytes: observe 1.75 B/base + 16 B/read, apply 2.5 B/base + 16 B/read
+        alg = {"observe": 1.75 * n_bases + 16 * R, "apply": 2.5 * n_bases + 16 * R}
+        dom = "observe" if ms["observe"] >= ms["apply"] else "apply"
+        achieved = alg[dom] / (ms[dom] * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic) as fh:
+                tr = json.load(fh)
+            if tr.get("config") == args.config and tr.get("reads_per_gpu") == R:
+                traffic = tr["kernels"].get(dom, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError, KeyError):
+            traffic = None
+        value = args.steps * total_bases / elapsed
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "bases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8 in, int64 counts, f64 recalibration",
+            "data": "synthetic (deterministic generator, SURVEY.md 8d spec), resident in HBM",
+            "config": {
+                "workload": WORKLOADS[args.config],
+                "reads_per_gpu": R,
+                "bases_per_gpu": n_bases,
+                "read_len": list(cfg["lens"]),
+                "read_groups": cfg["n_rg"],
+                "known_sites": int(sum(len(v) for v in sites.values())) if sites else 0,
+                "parallelism": "dp%d: read shards per GPU, RCCL int64 table all-reduce" % world,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "bqsr_%s_kernel" % dom,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg[dom],
+                "kernel_ms": ms,
+            },
+            "hbm_roofline_frac_step": (total_bases / world) * (4.25 + 32.0 / max(cfg["lens"])) /
+                                      (elapsed / args.steps) / (HBM_PEAK_GBS * 1e9),
+            "gen_s": t_gen,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, cfg)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cfg):
+    """The oracle (C++ restatement of ADAM BQSR, oracle/) on a bounded sample of
+    the same workload, std::thread x cores; partitions = threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from adam_amd import synth
+    cores = min(16, len(os.sched_getaffinity(0)))
+    n = args.cpu_reads
+    sample = synth.generate(n, cfg["lens"], cfg["n_rg"], cfg["seed"])
+    sites = synth.known_sites(cfg["sites"]) if cfg["sites"] else None
+    osites = O.Sites(sites) if sites else None
+    d = O.Dims(cfg["n_rg"], max(cfg["lens"]))
+    t = time.perf_counter()
+    O.bqsr(sample, osites, d, n_parts=cores, nthreads=cores)
+    dt = time.perf_counter() - t
+    one = sample.slice(0, max(1, n // 8))
+    t1 = time.perf_counter()
+    O.bqsr(one, osites, d, n_parts=1, nthreads=1)
+    dt1 = time.perf_counter() - t1
+    return {"value": sample.n_bases / dt, "unit": "bases/s", "cores": cores, "kind": "port",
+            "sample": "%d reads (%d bases) of %s, observe+merge+finalize+apply, %d partitions" %
+                      (n, sample.n_bases, args.config, cores),
+            "value_1thread": one.n_bases / dt1, "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

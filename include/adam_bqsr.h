@@ -239,6 +239,47 @@ bqsr_status bqsr_apply(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint
 bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* recs, const bqsr_lut* l,
                                uint16_t* out_qual, uint32_t* out_len);
 
+/* ---- asynchronous / staged device API -------------------------------------
+ * The calls above synchronise.  These enqueue on `stream` and return at once,
+ * so a driver can keep a whole BQSR job on the device (the benchmark and the
+ * multi-GPU path use them; RCCL collectives go between the stages). */
+enum { BQSR_STAGE_RESET = 1, BQSR_STAGE_KERNEL = 2, BQSR_STAGE_FOLD = 4 };
+/* observe stages: RESET clears the error word, KERNEL is the observe kernel,
+ * FOLD the expectedMismatch fold (result at bqsr_batch_em_device_ptr). */
+bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
+                               int32_t stages, void* stream);
+bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
+                               void* stream);
+/* waits for the stream, returns the data error (if any) and the partition's expectedMismatch */
+bqsr_status bqsr_observe_result(bqsr_batch* b, double* expected_mismatch, void* stream);
+void* bqsr_batch_em_device_ptr(bqsr_batch* b);
+bqsr_status bqsr_table_zero_async(bqsr_table* t, void* stream);
+/* finalize into *out; a non-NULL *out of the same dims is reused (no allocation) */
+bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double expected_mismatch, bqsr_lut** out,
+                                void* stream);
+bqsr_status bqsr_finalize_result(bqsr_lut* l, void* stream);
+/* apply stages: RESET clears the error word and exception count, KERNEL the apply kernel */
+bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint8_t* out_qual,
+                             uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
+                             int32_t stages, void* stream);
+bqsr_status bqsr_apply_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint8_t* out_qual,
+                             uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
+                             void* stream);
+bqsr_status bqsr_apply_result(bqsr_batch* b, int64_t* n_exceptions, void* stream);
+
+/* ---- introspection --------------------------------------------------------- */
+/* LDS window of the covariate table a batch's launches privatise: read group
+ * rg_lo, quals q_lo.. (chosen from the packed quals; settable for device batches). */
+bqsr_status bqsr_batch_set_window(bqsr_batch* b, int32_t q_lo, int32_t rg_lo);
+int32_t bqsr_batch_reads_per_tile(const bqsr_batch* b);
+/* base slots of the packed layout (sum over reads of max(Ls, Lq)): the size of apply's out_qual */
+int64_t bqsr_batch_slots(const bqsr_batch* b);
+/* read-group counts of a finalized table, group r at (r >= -1): 1 found, 0 absent, -1 error */
+int bqsr_lut_group(const bqsr_lut* l, int32_t r, int64_t* obs, int64_t* mm);
+/* the errorProbabilityToPhred threshold table the apply kernel uses:
+ * out[i] = largest p with phred(p) >= qmin + i; returns the entry count */
+int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin);
+
 #ifdef __cplusplus
 }
 #endif
