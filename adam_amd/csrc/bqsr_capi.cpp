@@ -125,6 +125,36 @@ const PhredThresholds& thresholds() {
   return t;
 }
 
+// Buckets of p by binade and top kQbBits mantissa bits (bqsr_internal.h):
+// each holds at most one threshold, so Q = p <= thr_b ? q_b : q_b - 1.
+struct PhredBuckets {
+  std::vector<double> thr;
+  std::vector<int16_t> q;
+  PhredBuckets() {
+    thr.resize(kQbN);
+    q.resize(kQbN);
+    const auto& T = thresholds().thr;
+    for (int i = 0; i < kQbN; ++i) {
+      const int e = kQbElo + (i >> kQbBits), m = i & ((1 << kQbBits) - 1);
+      const double lo = std::ldexp(1.0 + (double)m / (1 << kQbBits), e);
+      const double hi = std::ldexp(1.0 + (double)(m + 1) / (1 << kQbBits), e);
+      const double last = std::nextafter(hi, 0.0);
+      const int qhi = phred_of(lo), qlo = phred_of(last);
+      if (qhi - qlo > 1 || qhi - kThrQmin < 0 || qhi - kThrQmin >= kThrN || qhi > 32767 || qhi < -32767) {
+        q[(size_t)i] = -32768;  // not representable: full table
+        thr[(size_t)i] = 0.0;
+      } else {
+        q[(size_t)i] = (int16_t)qhi;
+        thr[(size_t)i] = T[(size_t)(qhi - kThrQmin)];
+      }
+    }
+  }
+};
+const PhredBuckets& buckets() {
+  static PhredBuckets b;
+  return b;
+}
+
 int64_t table_words(const bqsr_dims& d) {
   const int64_t K = 60LL * (d.n_rg - 1) + 128, cells = 2LL * d.max_len + 1 + kCtxSlots;
   return K + 2 * K * cells;
@@ -139,29 +169,16 @@ TableGeom geom(const bqsr_dims& d) {
 }
 
 constexpr size_t kLdsMax = 163840;
-size_t stage_bytes() {
-  // mirrors the device WaveStage layout (bqsr_kernels.hip)
-  struct WaveStageHost {
-    uint8_t bases[kTileSlots / 2 + 16];
-    uint32_t mmbits[kTileSlots / 32 + 1];
-    uint32_t maskbits[kTileSlots / 32 + 1];
-    uint16_t rslot[kMaxTileReads + 1];
-    uint16_t rows[kMaxTileReads * 5];
-    uint32_t hist[kQBins];
-    uint8_t md[kMdStage];
-    uint32_t cigar[kCigarStage];
-  };
-  return sizeof(WaveStageHost) * kWaves;
-}
+size_t tiles_bytes() { return sizeof(WaveTile) * kWaves; }
 size_t observe_lds(int qw, int cells) {
   size_t head = (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4 + 16;
   head = (head + 15) & ~(size_t)15;
-  return head + stage_bytes();
+  return head + tiles_bytes();
 }
 size_t apply_lds(int qw, int C) {
-  size_t head = (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + kThrLdsN * 8 + ((qw + 15) & ~15) + 16;
+  size_t head = (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2) + ((qw + 15) & ~15) + 16;
   head = (head + 15) & ~(size_t)15;
-  return head + stage_bytes();
+  return head + tiles_bytes();
 }
 int observe_qw(int cells) {
   int qw = 64;
@@ -183,6 +200,8 @@ struct bqsr_context {
   int n_cu = 256;
   double* d_pow10 = nullptr;  // 256 doubles
   double* d_thr = nullptr;    // kThrN doubles
+  double* d_qbt = nullptr;    // kQbN bucket thresholds
+  int16_t* d_qbq = nullptr;   // kQbN bucket phred values
 };
 
 struct bqsr_sites {
@@ -207,10 +226,16 @@ struct bqsr_batch {
   int64_t n_bases = 0;
   int32_t q_lo = 0, rg_lo = 0;  // LDS window choice
   std::vector<void*> allocs;
+  // per-read prep results (valid once `prepped`)
+  ReadInfo* d_info = nullptr;
+  uint64_t* d_bits = nullptr;
+  int32_t W = 1;  // bitmap words per read
+  bool prepped = false;
+  const bqsr_sites* prep_sites = nullptr;
   // per-call scratch
   uint16_t* d_h2 = nullptr;
   uint32_t* d_hq = nullptr;
-  unsigned long long* d_err = nullptr;  // [4]: err, n_exc, status, pad
+  unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
   int32_t n_blocks = 0;
   ~bqsr_batch() {
@@ -287,6 +312,10 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_thr, kThrN * sizeof(double));
   if (e == hipSuccess) e = hipMemcpy(c->d_pow10, pow10tab().v, 256 * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_thr, thresholds().thr.data(), kThrN * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&c->d_qbt, kQbN * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
+  if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
@@ -303,6 +332,8 @@ void bqsr_context_destroy(bqsr_context* c) {
   if (!c) return;
   if (c->d_pow10) (void)hipFree(c->d_pow10);
   if (c->d_thr) (void)hipFree(c->d_thr);
+  if (c->d_qbt) (void)hipFree(c->d_qbt);
+  if (c->d_qbq) (void)hipFree(c->d_qbq);
   delete c;
 }
 
@@ -383,8 +414,8 @@ inline uint8_t code_of(uint8_t c) {
 }
 
 bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
-  if (max_slot_len > kTileSlots)
-    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kTileSlots) + " bases are not supported");
+  if (max_slot_len > kMaxReadLen)
+    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
   const int64_t n = b->rd.n_reads;
   b->rd.reads_per_tile = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kMaxTileReads, kTileSlots / std::max<int64_t>(1, max_slot_len)));
   b->rd.n_tiles = (n + b->rd.reads_per_tile - 1) / b->rd.reads_per_tile;
@@ -392,7 +423,10 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   bqsr_status st;
   if ((st = dalloc(b->allocs, &b->d_h2, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kQBins)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_hq, (size_t)b->n_blocks * kQBins)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_err, 4)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_err, kErrWords)) != BQSR_OK) return st;
+  b->W = (int32_t)((std::max<int64_t>(1, max_slot_len) + 31) / 32);
+  if ((st = dalloc(b->allocs, &b->d_info, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_bits, (size_t)std::max<int64_t>(1, n) * b->W)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
   return BQSR_OK;
 }
@@ -572,8 +606,8 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
 bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* dev, bqsr_batch** out) {
   if (!ctx || !dev || !out || dev->n_reads < 0 || dev->dims.n_rg < 1 || dev->dims.max_len < 1)
     return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_wrap_device: bad arguments");
-  if (dev->dims.max_len > kTileSlots)
-    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kTileSlots) + " bases are not supported");
+  if (dev->dims.max_len > kMaxReadLen)
+    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
   HIP_TRY(hipSetDevice(ctx->device));
   bqsr_batch* b = new bqsr_batch;
   b->ctx = ctx;
@@ -685,11 +719,33 @@ bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
 }  // namespace
 
 // Stages of observe, launched on `stream` without synchronising (results land
-// in the batch's error word / expectedMismatch slot):
-//   BQSR_STAGE_RESET   clear the error word
+// in the batch's error words / expectedMismatch slot):
+//   BQSR_STAGE_RESET   clear the observe error word
+//   BQSR_STAGE_PREP    the per-read prep kernel (also validates for apply)
 //   BQSR_STAGE_KERNEL  the observe kernel (counts into `t`)
 //   BQSR_STAGE_FOLD    the expectedMismatch fold kernel
 // Exposed separately so a caller can bracket one kernel with HIP events.
+namespace {
+bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
+  HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
+  if (b->rd.n_reads > 0) {
+    PrepParams P{};
+    P.rd = b->rd;
+    if (sites) P.sites = sites->dev();
+    P.info = b->d_info;
+    P.bits = b->d_bits;
+    P.W = b->W;
+    P.err = b->d_err;
+    const int64_t blocks = std::min<int64_t>((b->rd.n_reads + 255) / 256, (int64_t)ctx->n_cu * 32);
+    hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P);
+    HIP_TRY(hipGetLastError());
+  }
+  b->prepped = true;
+  b->prep_sites = sites;
+  return BQSR_OK;
+}
+}  // namespace
+
 bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
                                int32_t stages, void* stream) {
   if (!ctx || !b || !t) return fail(BQSR_ERR_INVALID_ARG, "null");
@@ -697,48 +753,56 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   if (st != BQSR_OK) return st;
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
-  if (stages & BQSR_STAGE_RESET) HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
+  if (stages & BQSR_STAGE_RESET) HIP_TRY(hipMemsetAsync(b->d_err + kErrObs, 0xFF, 8, s));
+  if (stages & BQSR_STAGE_PREP) {
+    if ((st = launch_prep(ctx, b, sites, s)) != BQSR_OK) return st;
+  }
   if (b->rd.n_reads == 0) {
     if (stages & BQSR_STAGE_FOLD) HIP_TRY(hipMemsetAsync(b->d_em, 0, 8, s));
     return ok();
   }
+  if ((stages & BQSR_STAGE_KERNEL) && (!b->prepped || b->prep_sites != sites))
+    return fail(BQSR_ERR_INVALID_ARG, "observe kernel before the prep stage (or with other known sites)");
   if (stages & BQSR_STAGE_KERNEL) {
-  ObserveParams P{};
-  P.rd = b->rd;
-  if (sites) P.sites = sites->dev();
-  P.g = geom(t->dims);
-  P.w.qw = observe_qw(P.g.cells);
-  P.w.q_lo = std::min(b->q_lo, kQBins - 1);
-  P.w.rg_lo = b->rg_lo;
-  P.touched = t->touched();
-  P.obs = t->obs();
-  P.mm = t->mm();
-  P.hq_block = b->d_hq;
-  P.h2 = b->d_h2;
-  P.err = b->d_err;
-  P.n_blocks = b->n_blocks;
-  const size_t lds = observe_lds(P.w.qw, P.g.cells);
-  hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
-  HIP_TRY(hipGetLastError());
+    ObserveParams P{};
+    P.rd = b->rd;
+    P.info = b->d_info;
+    P.bits = b->d_bits;
+    P.W = b->W;
+    P.g = geom(t->dims);
+    P.w.qw = observe_qw(P.g.cells);
+    P.w.q_lo = std::min(b->q_lo, kQBins - 1);
+    P.w.rg_lo = b->rg_lo;
+    P.touched = t->touched();
+    P.obs = t->obs();
+    P.mm = t->mm();
+    P.hq_block = b->d_hq;
+    P.h2 = b->d_h2;
+    P.err = b->d_err + kErrObs;
+    P.n_blocks = b->n_blocks;
+    const size_t lds = observe_lds(P.w.qw, P.g.cells);
+    hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-  FoldParams F{};
-  F.rd = b->rd;
-  F.hq_block = b->d_hq;
-  F.h2 = b->d_h2;
-  F.pow10 = ctx->d_pow10;
-  F.n_blocks = b->n_blocks;
-  F.em_out = b->d_em;
-  F.status = b->d_err + 2;
-  hipLaunchKernelGGL(bqsr_fold_kernel, dim3(1), dim3(256), 0, s, F);
-  HIP_TRY(hipGetLastError());
+    FoldParams F{};
+    F.rd = b->rd;
+    F.info = b->d_info;
+    F.hq_block = b->d_hq;
+    F.h2 = b->d_h2;
+    F.pow10 = ctx->d_pow10;
+    F.n_blocks = b->n_blocks;
+    F.em_out = b->d_em;
+    hipLaunchKernelGGL(bqsr_fold_kernel, dim3(1), dim3(1024), 0, s, F);
+    HIP_TRY(hipGetLastError());
   }
   return ok();
 }
 
 // launch observe + fold; does not synchronise
 bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t, void* stream) {
-  return bqsr_observe_stage(ctx, b, sites, t, BQSR_STAGE_RESET | BQSR_STAGE_KERNEL | BQSR_STAGE_FOLD, stream);
+  return bqsr_observe_stage(ctx, b, sites, t, BQSR_STAGE_RESET | BQSR_STAGE_PREP | BQSR_STAGE_KERNEL | BQSR_STAGE_FOLD,
+                            stream);
 }
 
 // zero a table on a stream (a fresh `new RecalTable` for the next job)
@@ -757,7 +821,7 @@ bqsr_status bqsr_observe_result(bqsr_batch* b, double* em, void* stream) {
   hipStream_t s = S(stream);
   unsigned long long err = 0;
   double e = 0;
-  HIP_TRY(hipMemcpyAsync(&err, b->d_err, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&err, b->d_err + kErrObs, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(&e, b->d_em, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (em) *em = e;
@@ -954,7 +1018,9 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin) {
 
 // ---------------------------------------------------------------- apply ----
 
-// stages: BQSR_STAGE_RESET (error word, exception count), BQSR_STAGE_KERNEL (apply kernel)
+// stages: BQSR_STAGE_RESET (apply-kernel error word, exception count),
+// BQSR_STAGE_KERNEL (apply kernel).  The prep kernel runs first when observe
+// has not run it on this batch.
 bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
                              uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
                              int32_t stages, void* stream) {
@@ -964,12 +1030,17 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
   if (stages & BQSR_STAGE_RESET) {
-    HIP_TRY(hipMemsetAsync(b->d_err, 0xFF, 8, s));
-    HIP_TRY(hipMemsetAsync(b->d_err + 1, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(b->d_err + kErrAppKern, 0xFF, 8, s));
+    HIP_TRY(hipMemsetAsync(b->d_err + kNExc, 0, 8, s));
+  }
+  if (!b->prepped || (stages & BQSR_STAGE_PREP)) {
+    bqsr_status st = launch_prep(ctx, b, nullptr, s);
+    if (st != BQSR_OK) return st;
   }
   if (b->rd.n_reads == 0 || !(stages & BQSR_STAGE_KERNEL)) return ok();
   ApplyParams P{};
   P.rd = b->rd;
+  P.info = b->d_info;
   P.g = geom(L->dims);
   P.w.qw = apply_qw(P.g.C);
   P.w.q_lo = std::min(b->q_lo, kQBins - 1);
@@ -984,13 +1055,15 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.thr = ctx->d_thr;
   P.thr_qmin = kThrQmin;
   P.thr_n = kThrN;
+  P.qb_thr = ctx->d_qbt;
+  P.qb_q = ctx->d_qbq;
   P.out_qual = out_qual;
   P.out_start = out_start;
   P.out_len = out_len;
   P.exc = (unsigned long long*)exceptions;
   P.max_exc = exceptions ? max_exceptions : 0;
-  P.n_exc = b->d_err + 1;
-  P.err = b->d_err;
+  P.n_exc = b->d_err + kNExc;
+  P.err = b->d_err + kErrAppKern;
   const size_t lds = apply_lds(P.w.qw, P.g.C);
   hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
@@ -1007,11 +1080,11 @@ bqsr_status bqsr_apply_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
 bqsr_status bqsr_apply_result(bqsr_batch* b, int64_t* n_exceptions, void* stream) {
   HIP_TRY(hipSetDevice(b->ctx->device));
   hipStream_t s = S(stream);
-  unsigned long long w[2];
-  HIP_TRY(hipMemcpyAsync(w, b->d_err, 16, hipMemcpyDeviceToHost, s));
+  unsigned long long w[kErrWords];
+  HIP_TRY(hipMemcpyAsync(w, b->d_err, sizeof w, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (n_exceptions) *n_exceptions = (int64_t)w[1];
-  return from_err_key(w[0], 0);
+  if (n_exceptions) *n_exceptions = (int64_t)w[kNExc];
+  return from_err_key(std::min(w[kErrAppPrep], w[kErrAppKern]), 0);
 }
 
 bqsr_status bqsr_apply(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint8_t* out_qual, uint32_t* out_start,

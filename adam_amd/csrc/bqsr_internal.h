@@ -9,8 +9,8 @@
 
 namespace bqsr {
 
-// ---- per-read records (SoA of two fixed-size records) -----------------------
-// 16 B: everything the per-base passes need.
+// ---- per-read records (SoA of fixed-size records) --------------------------
+// 16 B: what the per-base passes need.
 struct ReadMeta {
   uint64_t slot;   // first base slot of the read in qual[] / bases[]
   uint16_t lq;     // quality length (Lq)
@@ -20,7 +20,7 @@ struct ReadMeta {
 };
 static_assert(sizeof(ReadMeta) == 16, "ReadMeta must be 16 B");
 
-// 24 B: alignment fields, read by the per-read prep only.
+// 24 B: alignment fields, read by the prep kernel only.
 struct ReadAlign {
   int64_t start;       // 0-based alignment start
   uint32_t cigar_off;  // into cigar[]
@@ -30,6 +30,23 @@ struct ReadAlign {
   uint16_t md_len;
 };
 static_assert(sizeof(ReadAlign) == 24, "ReadAlign must be 24 B");
+
+// 8 B per read, written by the prep kernel for the observe / apply passes.
+struct ReadInfo {
+  uint16_t st;  // qualityStartOffset
+  uint16_t en;  // qualityEndOffset, or the offset of the read's first error
+  uint16_t fl;  // kInfo* bits
+  uint16_t pad;
+};
+static_assert(sizeof(ReadInfo) == 8, "ReadInfo must be 8 B");
+constexpr uint16_t kInfoObs = 1;        // usable, valid: its bases go into the table
+constexpr uint16_t kInfoObsCheck = 2;   // usable, fails at `en`: bases before it are only qual-checked
+constexpr uint16_t kInfoApp = 4;        // eligible for recalibration, valid
+constexpr uint16_t kInfoAppCheck = 8;   // eligible, fails at `en`: bases before it only checked
+constexpr uint16_t kInfoNeg = 16;       // readNegativeStrand
+constexpr uint16_t kInfoSecond = 32;    // readPaired && secondOfPair (DiscreteCycle negates)
+constexpr uint16_t kInfoPass = 64;      // not eligible: quality string passed through
+constexpr uint16_t kInfoCycNeg = 128;   // (tile record only) cycle cell decreases with the slot
 
 // packer-derived flag: the sequence holds a byte outside "ACGTN"
 // (BaseContext.simpleReverseComplement throws on it for reverse reads,
@@ -43,16 +60,16 @@ constexpr int kMaxQ = 60;      // RecalUtil.Constants.MAX_REASONABLE_QSCORE
 constexpr int kCtxSlots = 21;  // contexts -4..16
 constexpr int kQBins = 128;    // qual values 0..127 (Java byte >= 0)
 
-// Tile geometry: a tile is `reads_per_tile` consecutive reads whose slots fit
-// in kTileSlots; one wavefront processes one tile at a time.
-constexpr int kTileSlots = 2048;
+// Tile geometry of the per-base passes: a tile is `reads_per_tile`
+// consecutive reads (<= 64) whose base slots fit in kTileSlots; one wavefront
+// processes one tile at a time, one base per lane per step.
+constexpr int kTileSlots = 4096;
 constexpr int kMaxTileReads = 64;
-constexpr int kWaves = 8;  // waves per block (512 threads)
+constexpr int kWaves = 16;  // waves per block of the per-base passes (1024 threads)
 constexpr int kBlockThreads = 64 * kWaves;
-constexpr int kMdStage = 1024;    // MD bytes staged per tile (larger tiles read MD from HBM)
-constexpr int kCigarStage = 192;  // CIGAR elements staged per tile
+constexpr int kMaxReadLen = 4096;  // longest read the device path takes
 
-// Error reporting: one u64 per launch, atomicMin of
+// Error reporting: u64 words, atomicMin of
 //   read << 28 | read_offset << 8 | rank << 4 | code
 // so the first failing read (read order), and within it the first failing
 // base / step, wins -- the exception the JVM would raise first.
@@ -69,12 +86,14 @@ enum : uint32_t {
   kRankCov = 4,    // BaseCovariates: covariate arrays shorter than the quals
   kRankTable = 5   // RecalTable += / getErrorRateShifts
 };
+// error words of a batch
+enum { kErrObs = 0, kErrAppPrep = 1, kErrAppKern = 2, kNExc = 3, kErrWords = 4 };
 
 // ---- known sites -------------------------------------------------------------
 struct SitesDev {
   const int64_t* pos;          // all contigs' sorted unique positions
   const uint64_t* off;         // [n_contigs + 1]
-  const uint32_t* bucket;      // per contig: first site index (relative) with pos >= b << shift
+  const uint32_t* bucket;      // per contig: first site index (relative) with pos >= base + (b << shift)
   const uint64_t* bucket_off;  // [n_contigs + 1] into bucket
   const int64_t* bucket_base;  // [n_contigs] position of bucket 0 (min pos)
   int32_t n_contigs;
@@ -108,9 +127,20 @@ struct ReadsDev {
   int64_t n_tiles;
 };
 
+struct PrepParams {
+  ReadsDev rd;
+  SitesDev sites;
+  ReadInfo* info;      // [n_reads]
+  uint64_t* bits;      // [n_reads][W]: per 32 read offsets, masked bits | mismatch bits << 32
+  int32_t W;           // words per read
+  unsigned long long* err;  // error words
+};
+
 struct ObserveParams {
   ReadsDev rd;
-  SitesDev sites;  // n_contigs == 0: SnpTable()
+  const ReadInfo* info;
+  const uint64_t* bits;  // PrepParams::bits
+  int32_t W;
   TableGeom g;
   Window w;
   int64_t* touched;  // [K]
@@ -124,16 +154,26 @@ struct ObserveParams {
 
 struct FoldParams {
   ReadsDev rd;
+  const ReadInfo* info;
   const uint32_t* hq_block;
   const uint16_t* h2;
   const double* pow10;  // phredToErrorProbabilityCache[0..127]
   int32_t n_blocks;
   double* em_out;      // [1]
-  unsigned long long* status;  // [1] 0 = ok
 };
+
+// errorProbabilityToPhred by buckets: p's binade (unbiased exponent
+// kQbElo..kQbEhi) and top 5 mantissa bits select a bucket holding at most one
+// phred threshold: Q = p <= qb_thr[b] ? qb_q[b] : qb_q[b] - 1.  Other p take
+// the full threshold table (thr).
+constexpr int kQbElo = -48;
+constexpr int kQbEhi = 3;
+constexpr int kQbBits = 5;
+constexpr int kQbN = (kQbEhi - kQbElo + 1) << kQbBits;
 
 struct ApplyParams {
   ReadsDev rd;
+  const ReadInfo* info;
   TableGeom g;
   Window w;
   int32_t n_rg;
@@ -146,6 +186,8 @@ struct ApplyParams {
   const double* thr;      // phred thresholds, see PhredThresholds
   int32_t thr_qmin;       // Q value of thr[0]
   int32_t thr_n;
+  const double* qb_thr;   // [kQbN]
+  const int16_t* qb_q;    // [kQbN]
   uint8_t* out_qual;
   uint32_t* out_start;
   uint32_t* out_len;
@@ -154,6 +196,25 @@ struct ApplyParams {
   unsigned long long* n_exc;
   unsigned long long* err;
 };
+
+// Per-wave tile state of the per-base passes (LDS).  Reads of the tile that
+// own at least one slot are listed in slot order ("compact" index c), one
+// 16-B record each (one ds_read_b128), all positions tile-relative slots:
+//   x = st | en << 16       trimmed read offsets (pass-through reads: 0, Lq)
+//   y = fl | cb << 16       cycle cell of slot s = cb + s (kInfoCycNeg: cb - s)
+//   z = rslot | cm << 16    first slot; context operands of slot s are the
+//                           codes at s - 1, s (reverse strand: cm - s, cm - s - 1)
+//   w = rg | rtile << 16    read group, read index within the tile
+//   sb = one bit per slot marking compact read starts, pre = popcount prefix
+//   of sb per word: the compact index of slot s is
+//   pre[s >> 5] + popc(sb[s >> 5] & ones(s & 31)) - 1.
+struct WaveTile {
+  uint4 rec[kMaxTileReads];
+  uint32_t sb[kTileSlots / 32];
+  uint32_t hist[kQBins];
+  uint16_t pre[kTileSlots / 32];
+};
+static_assert(sizeof(WaveTile) % 16 == 0, "WaveTile must keep 16-B alignment");
 
 // finalize results read back by the host
 struct FinalOut {
@@ -168,7 +229,5 @@ struct FinalOut {
 constexpr int kThrQmin = -3100;
 constexpr int kThrQmax = 3300;
 constexpr int kThrN = kThrQmax - kThrQmin + 1;
-constexpr int kThrLdsLo = -64;  // LDS copy covers Q in [-64, 191]
-constexpr int kThrLdsN = 256;
 
 }  // namespace bqsr

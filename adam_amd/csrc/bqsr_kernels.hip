@@ -1,22 +1,28 @@
 // bqsr_kernels.hip -- gfx950 kernels of the BQSR path.
 //
+//   bqsr_prep_kernel      per read: ReadCovariates' constructor + the per-read
+//                         parts of next() (trimming, CIGAR, MD, known sites)
 //   bqsr_observe_kernel   RecalibrateBaseQualities.computeTable, one partition
 //   bqsr_fold_kernel      expectedMismatch: the partition's sequential fold
 //   bqsr_final_*          RecalTable.finalizeTable + the apply tables
 //   bqsr_apply_kernel     RecalUtil.recalibrate over every eligible read
 //   bqsr_table_add        RecalTable.++ (int64 counts)
 //
-// Structure (DESIGN.md has the full account): one 512-thread workgroup per CU,
-// each owning a contiguous range of read tiles; each wavefront processes one
-// tile (<= 64 reads, <= 2048 base slots) at a time:
-//   1. stage the tile's packed bases / MD / CIGAR into LDS (coalesced),
-//   2. per-read prep, one lane per read: quality trimming, CIGAR walk, MD
-//      parse, known-site lookup -> two LDS bitmasks {masked, mismatch} over
-//      the tile's slots (the "2-bit structural mask" of SURVEY.md 8d),
-//   3. per-base pass, 16 slots per lane per step (one 16-B qual load):
-//      covariates -> LDS-privatised u32 histogram of the workgroup's window
-//      of the table; bases outside the window go to global int64 atomics,
-//   4. at the end the workgroup flushes its window with int64 atomics.
+// Structure (DESIGN.md has the full account):
+//  * prep: one thread per read, full occupancy.  The serial, branchy work
+//    (quality trimming, CIGAR walk, MD parse, known-site lookup, the JVM's
+//    exception order) happens once per read and leaves an 8-B ReadInfo plus
+//    two per-read bitmaps {masked, mismatch} over read offsets -- the "2-bit
+//    structural mask" of SURVEY.md 8d.
+//  * observe / apply: one 1024-thread workgroup per CU owning a contiguous
+//    range of read tiles; a wavefront takes one tile (<= 64 reads, <= 4096
+//    base slots) at a time and its lanes walk the slots one base per lane per
+//    step.  A lane finds its read by a popcount over a per-tile read-start
+//    bitmap, so there is no per-lane serial loop and no divergence beyond the
+//    trimmed ends.  observe accumulates a u32 LDS-privatised window of the
+//    covariate table (flushed with int64 atomics at the end); apply reads the
+//    window's double tables from LDS and turns p into a phred score with two
+//    LDS loads (bucketed threshold table).
 // Compiled with -ffp-contract=off: the double arithmetic must round exactly
 // as the JVM's.
 #include <hip/hip_runtime.h>
@@ -40,17 +46,6 @@ __device__ __forceinline__ bool eligible_read(uint16_t f) {  // RecalibrateBaseQ
 }
 
 __device__ __forceinline__ void report(unsigned long long* err, uint64_t key) { atomicMin(err, (unsigned long long)key); }
-
-// set bits [lo, hi) of an LDS bitmap (ranges of different reads may share a word)
-__device__ void lds_set_bits(uint32_t* bits, int lo, int hi) {
-  while (lo < hi) {
-    int w = lo >> 5, b = lo & 31;
-    int n = min(32 - b, hi - lo);
-    uint32_t m = (n == 32) ? 0xFFFFFFFFu : (((1u << n) - 1u) << b);
-    atomicOr(&bits[w], m);
-    lo += n;
-  }
-}
 
 __device__ __forceinline__ uint32_t cig_op(uint32_t e) { return e & 0xFu; }
 __device__ __forceinline__ uint32_t cig_len(uint32_t e) { return e >> 4; }
@@ -131,69 +126,89 @@ __device__ int refpos_to_offset(const uint32_t* cig, int ncig, int64_t unclipped
   return -1;
 }
 
-__device__ __forceinline__ int64_t lower_bound_i64(const int64_t* a, int64_t n, int64_t v) {
-  int64_t lo = 0, hi = n;
+// set bits [lo, hi) of a read-private bitmap in global memory (single
+// writer): word i holds offsets 32i..32i+31 at bit `half` (0 masked, 32 mismatch)
+__device__ void set_bits(uint64_t* w, int lo, int hi, int half) {
   while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1; else hi = mid;
+    const int i = lo >> 5, b = lo & 31;
+    const int n = min(32 - b, hi - lo);
+    const uint32_t m = (n == 32) ? 0xFFFFFFFFu : (((1u << n) - 1u) << b);
+    w[i] |= (uint64_t)m << half;
+    lo += n;
   }
-  return lo;
 }
 
-// per-read results of the prep step, kept in LDS for the per-base pass
-struct ReadRow {
-  uint16_t st, en, ls, fl, rg;
-};
-constexpr uint16_t kRowActive = 1, kRowNeg = 2, kRowSecond = 4, kRowQualCheck = 8;
-
-// Per-read prep, one lane per read (ReadCovariates' constructor plus the
-// per-read parts of next(), ReadCovariates.scala:30-60):
-//   quality trimming, the error checks in the order the JVM would hit them,
-//   and (observe) the masked / mismatch bits of every trimmed base:
+// ---------------------------------------------------------------- prep -----
+//
+// One thread per read.  Eligible reads (mapped, primary, not duplicate) get
+// trimmed and validated in the order ReadCovariates would throw; usable reads
+// (eligible + MD) also get their masked / mismatch bitmaps:
 //   masked   = refPos None, refPos outside [start, end), or a known site
 //              (ReadCovariates.scala:56: snp(o) || mismatch(o).isEmpty);
 //   mismatch = !MdTag.isMatch(refPos)  (RichADAMRecord.scala:138-154).
-template <bool kObserve>
-__device__ ReadRow prep_read(const ReadsDev& rd, const SitesDev& sites, uint64_t r, const ReadMeta& m,
-                             const ReadAlign& a, int rslot, const uint32_t* cig, const uint8_t* md, uint32_t* mmbits,
-                             uint32_t* maskbits, unsigned long long* err) {
-  ReadRow row{0, 0, m.ls, 0, m.rg};
+// Errors of usable reads are errors of observe; those of every eligible read
+// are errors of apply (observe runs first).
+__device__ void prep_one(const PrepParams& P, int64_t r) {
+  const ReadMeta m = P.rd.meta[r];
+  ReadInfo inf{0, 0, 0, 0};
   const uint16_t f = m.flags;
-  if (!(kObserve ? usable_read(f) : eligible_read(f))) return row;
-  if (!(f & BQSR_F_HAS_QUAL)) {  // qualityScores: getQual.toString
-    report(err, err_key(r, 0, kRankCtor, BQSR_ERR_NULL_FIELD));
-    return row;
+  if (!eligible_read(f)) {
+    inf.fl = kInfoPass;
+    P.info[r] = inf;
+    return;
   }
-  const uint8_t* q = rd.qual + m.slot;
+  const bool usable = usable_read(f);
+  auto fail = [&](uint64_t key) {
+    if (usable) report(&P.err[kErrObs], key);
+    report(&P.err[kErrAppPrep], key);
+  };
+  if (!(f & BQSR_F_HAS_QUAL)) {  // qualityScores: getQual.toString
+    fail(err_key(r, 0, kRankCtor, BQSR_ERR_NULL_FIELD));
+    P.info[r] = inf;
+    return;
+  }
+  const uint8_t* q = P.rd.qual + m.slot;
   const int lq = m.lq;
   int st = 0;
   while (st < lq && (int8_t)q[st] <= 2) ++st;  // isLowQualityBase, minQuality = 2
   int tail = 0;
   while (tail < lq && (int8_t)q[lq - 1 - tail] <= 2) ++tail;
   const int en = lq - tail;
+  inf.st = (uint16_t)min(st, 0xFFFF);
   if (!(f & BQSR_F_HAS_RG)) {  // QualByRG: 60 * getRecordGroupId
-    report(err, err_key(r, 0, kRankCtor, BQSR_ERR_NULL_RG));
-    return row;
+    fail(err_key(r, 0, kRankCtor, BQSR_ERR_NULL_RG));
+    P.info[r] = inf;
+    return;
   }
   if (!(f & BQSR_F_HAS_SEQ)) {  // DiscreteCycle: getSequence.toString
-    report(err, err_key(r, 0, kRankCtor, BQSR_ERR_NULL_FIELD));
-    return row;
+    fail(err_key(r, 0, kRankCtor, BQSR_ERR_NULL_FIELD));
+    P.info[r] = inf;
+    return;
   }
   if ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) {  // BaseContext reverse complement
-    report(err, err_key(r, 0, kRankCtor, BQSR_ERR_BAD_REVCOMP_BASE));
-    return row;
+    fail(err_key(r, 0, kRankCtor, BQSR_ERR_BAD_REVCOMP_BASE));
+    P.info[r] = inf;
+    return;
   }
-  if (st >= en) return row;  // no base is iterated
-  row.st = (uint16_t)st;
+  if (st >= en) {  // no base is iterated: an empty recalibrated quality string
+    P.info[r] = inf;
+    return;
+  }
+  const uint16_t check_fl = (usable ? kInfoObsCheck : 0) | kInfoAppCheck;
   if (!(f & BQSR_F_HAS_CIGAR) || !(f & BQSR_F_HAS_START)) {  // referencePositions
-    report(err, err_key(r, st, kRankCigar, BQSR_ERR_NULL_FIELD));
-    return row;
+    fail(err_key(r, st, kRankCigar, BQSR_ERR_NULL_FIELD));
+    inf.en = (uint16_t)st;
+    inf.fl = check_fl;
+    P.info[r] = inf;
+    return;
   }
+  const ReadAlign a = P.rd.align[r];
+  const uint32_t* cig = P.rd.cigar + a.cigar_off;
+  const uint8_t* md = P.rd.md + a.md_off;
   // walk the CIGAR once: clip, read-consuming and reference-consuming lengths
   const int ncig = a.n_cigar;
-  int64_t lead = 0;
+  int64_t lead = 0, rp_len = 0, ref_len = 0;
   bool leading = true, zero = false;
-  int64_t rp_len = 0, ref_len = 0;
   for (int i = 0; i < ncig; ++i) {
     uint32_t e = cig[i], op = cig_op(e), len = cig_len(e);
     if (leading && (op == BQSR_CIGAR_S || op == BQSR_CIGAR_H)) lead += len; else leading = false;
@@ -201,58 +216,58 @@ __device__ ReadRow prep_read(const ReadsDev& rd, const SitesDev& sites, uint64_t
     if (is_seg_op(op) && len == 0) zero = true;
     if (consumes_ref(op)) ref_len += len;
   }
-  if (zero) {  // Range(a, a).last
-    report(err, err_key(r, st, kRankCigar, BQSR_ERR_CIGAR_INVALID));
-    return row;
-  }
   const int64_t start = a.start;
   const int64_t unclipped = start - lead;
   const int64_t ref_end = start + ref_len;
-  if (unclipped < -2147483648LL || unclipped + rp_len + ref_len > 2147483647LL) {
+  uint64_t best = kNoError;
+  if (zero) {
+    best = err_key(r, st, kRankCigar, BQSR_ERR_CIGAR_INVALID);  // Range(a, a).last
+  } else if (unclipped < -2147483648LL || unclipped + rp_len + ref_len > 2147483647LL) {
     // the reference does this arithmetic in Int; positions that wrap are not supported here
-    report(err, err_key(r, st, kRankCigar, BQSR_ERR_UNSUPPORTED));
-    return row;
-  }
-  // first trimmed base that has a reference position
-  const int e1 = (int)min((int64_t)en, rp_len);
-  int o_first = -1;
-  {
-    int ro = 0;
-    for (int i = 0; i < ncig && o_first < 0; ++i) {
-      uint32_t e = cig[i], op = cig_op(e), len = cig_len(e);
-      if (is_seg_op(op)) {
-        int lo = max(ro, st), hi = min(ro + (int)len, e1);
-        if (lo < hi) o_first = lo;
-        ro += len;
-      } else if (op == BQSR_CIGAR_I) {
-        ro += len;
+    best = err_key(r, st, kRankCigar, BQSR_ERR_UNSUPPORTED);
+  } else {
+    // first trimmed base that has a reference position
+    const int e1 = (int)min((int64_t)en, rp_len);
+    int o_first = -1;
+    {
+      int ro = 0;
+      for (int i = 0; i < ncig && o_first < 0; ++i) {
+        uint32_t e = cig[i], op = cig_op(e), len = cig_len(e);
+        if (is_seg_op(op)) {
+          int lo = max(ro, st), hi = min(ro + (int)len, e1);
+          if (lo < hi) o_first = lo;
+          ro += len;
+        } else if (op == BQSR_CIGAR_I) {
+          ro += len;
+        }
       }
     }
-  }
-  uint64_t best = kNoError;
-  int64_t md_total = 0;
-  if (o_first >= 0) {
-    if (f & BQSR_F_HAS_MD) {
-      if (!md_scan(md, a.md_len, &md_total, [](int64_t) {}))
+    if (o_first >= 0) {
+      int64_t tot;
+      if ((f & BQSR_F_HAS_MD) && !md_scan(md, a.md_len, &tot, [](int64_t) {}))
         best = min(best, err_key(r, o_first, kRankMd, BQSR_ERR_MD_PARSE));
+      if (!(f & BQSR_F_HAS_REFNAME)) best = min(best, err_key(r, o_first, kRankSnp, BQSR_ERR_NULL_FIELD));
     }
-    if (!(f & BQSR_F_HAS_REFNAME)) best = min(best, err_key(r, o_first, kRankSnp, BQSR_ERR_NULL_FIELD));
+    if ((int64_t)en > rp_len)
+      best = min(best, err_key(r, (uint32_t)max((int64_t)st, rp_len), kRankCigar, BQSR_ERR_CIGAR_SHORT));
+    if (en > (int)m.ls) best = min(best, err_key(r, (uint32_t)max(st, (int)m.ls), kRankCov, BQSR_ERR_SEQ_SHORT));
   }
-  if ((int64_t)en > rp_len) best = min(best, err_key(r, (uint32_t)max((int64_t)st, rp_len), kRankCigar, BQSR_ERR_CIGAR_SHORT));
-  if (en > (int)m.ls) best = min(best, err_key(r, (uint32_t)max(st, (int)m.ls), kRankCov, BQSR_ERR_SEQ_SHORT));
   if (best != kNoError) {
-    report(err, best);
-    // bases before the failing one are still checked for negative quals
-    row.en = (uint16_t)((best >> 8) & 0xFFFFF);
-    row.fl = kRowQualCheck;
-    return row;
+    fail(best);
+    inf.en = (uint16_t)((best >> 8) & 0xFFFFF);  // bases before the failing one are still checked
+    inf.fl = check_fl;
+    P.info[r] = inf;
+    return;
   }
-  row.en = (uint16_t)en;
-  row.fl = kRowActive | ((f & BQSR_F_NEG_STRAND) ? kRowNeg : 0) |
-           (((f & BQSR_F_PAIRED) && (f & BQSR_F_SECOND_OF_PAIR)) ? kRowSecond : 0);
-  if (!kObserve) return row;
+  inf.en = (uint16_t)en;
+  inf.fl = kInfoApp | (usable ? kInfoObs : 0) | ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
+           (((f & BQSR_F_PAIRED) && (f & BQSR_F_SECOND_OF_PAIR)) ? kInfoSecond : 0);
+  P.info[r] = inf;
+  if (!usable) return;
 
   // ---- masked / mismatch bits over [st, en) ----
+  uint64_t* bw = P.bits + (int64_t)r * P.W;
+  for (int i = 0; i < P.W; ++i) bw[i] = 0;
   {
     int ro = 0;
     int64_t pos = unclipped;
@@ -265,14 +280,14 @@ __device__ ReadRow prep_read(const ReadsDev& rd, const SitesDev& sites, uint64_t
           int64_t w0 = (int64_t)ro + (start - pos), w1 = (int64_t)ro + (ref_end - pos);
           int a0 = (int)min(max(w0, (int64_t)lo), (int64_t)hi);
           int a1 = (int)min(max(w1, (int64_t)lo), (int64_t)hi);
-          lds_set_bits(maskbits, rslot + lo, rslot + a0);
-          lds_set_bits(maskbits, rslot + max(a1, a0), rslot + hi);
+          set_bits(bw, lo, a0, 0);
+          set_bits(bw, max(a1, a0), hi, 0);
         }
         ro += len;
         pos += len;
       } else if (op == BQSR_CIGAR_I) {  // insertion: refPos None
         int lo = max(ro, st), hi = min(ro + (int)len, en);
-        lds_set_bits(maskbits, rslot + lo, rslot + max(lo, hi));
+        set_bits(bw, lo, max(lo, hi), 0);
         ro += len;
       } else if (op != BQSR_CIGAR_H) {
         pos += len;
@@ -280,11 +295,12 @@ __device__ ReadRow prep_read(const ReadsDev& rd, const SitesDev& sites, uint64_t
     }
   }
   // MD non-match positions inside the overlap window
+  int64_t md_total = 0;
   md_scan(md, a.md_len, &md_total, [&](int64_t prel) {
     int64_t p = start + prel;
     if (p >= ref_end) return;
     int o = refpos_to_offset(cig, ncig, unclipped, p);
-    if (o >= st && o < en) lds_set_bits(mmbits, rslot + o, rslot + o + 1);
+    if (o >= st && o < en) set_bits(bw, o, o + 1, 32);
   });
   // positions past the MD span but before `end` are not matches either
   if (start + md_total < ref_end) {
@@ -297,7 +313,7 @@ __device__ ReadRow prep_read(const ReadsDev& rd, const SitesDev& sites, uint64_t
         int64_t p0 = max(pos, t0), p1 = min(pos + (int64_t)len, ref_end);
         if (p0 < p1) {
           int lo = max(ro + (int)(p0 - pos), st), hi = min(ro + (int)(p1 - pos), en);
-          if (lo < hi) lds_set_bits(mmbits, rslot + lo, rslot + hi);
+          if (lo < hi) set_bits(bw, lo, hi, 32);
         }
         ro += len;
         pos += len;
@@ -309,138 +325,138 @@ __device__ ReadRow prep_read(const ReadsDev& rd, const SitesDev& sites, uint64_t
     }
   }
   // known sites (SnpTable.isMaskedAtReadOffset): raw VCF POS vs 0-based refPos (Q7)
-  if (a.contig >= 0 && a.contig < sites.n_contigs) {
-    const int64_t* sp = sites.pos + sites.off[a.contig];
-    const int64_t ns = (int64_t)(sites.off[a.contig + 1] - sites.off[a.contig]);
+  if (a.contig >= 0 && a.contig < P.sites.n_contigs) {
+    const SitesDev& S = P.sites;
+    const int64_t* sp = S.pos + S.off[a.contig];
+    const int64_t ns = (int64_t)(S.off[a.contig + 1] - S.off[a.contig]);
     if (ns > 0) {
-      // reference span of the trimmed bases: refPos is increasing along the read
-      int64_t lo_p = unclipped, hi_p = unclipped + rp_len + ref_len;
-      const uint32_t* bk = sites.bucket + sites.bucket_off[a.contig];
-      const int64_t nb = (int64_t)(sites.bucket_off[a.contig + 1] - sites.bucket_off[a.contig]);
-      const int64_t base = sites.bucket_base[a.contig];
+      // reference span of the read: refPos increases along the read
+      const int64_t lo_p = unclipped, hi_p = unclipped + rp_len + ref_len;
+      const uint32_t* bk = S.bucket + S.bucket_off[a.contig];
+      const int64_t nb = (int64_t)(S.bucket_off[a.contig + 1] - S.bucket_off[a.contig]);
+      const int64_t base = S.bucket_base[a.contig];
       int64_t j;
-      int64_t bi = (lo_p - base) >> sites.shift;
+      const int64_t bi = (lo_p - base) >> S.shift;
       if (bi < 0) j = 0;
       else if (bi >= nb) j = ns;
       else j = bk[bi];
       while (j < ns && sp[j] < lo_p) ++j;
       for (; j < ns && sp[j] < hi_p; ++j) {
         int o = refpos_to_offset(cig, ncig, unclipped, sp[j]);
-        if (o >= st && o < en) lds_set_bits(maskbits, rslot + o, rslot + o + 1);
+        if (o >= st && o < en) set_bits(bw, o, o + 1, 0);
       }
     }
   }
-  return row;
 }
 
-// base code at tile-relative slot s (bases staged from absolute slot ts0 & ~1)
-__device__ __forceinline__ uint32_t base_code(const uint8_t* st_bases, int s_abs_rel) {
-  uint8_t b = st_bases[s_abs_rel >> 1];
-  return (s_abs_rel & 1) ? (b >> 4) : (b & 0xF);
+extern "C" __global__ void __launch_bounds__(256) bqsr_prep_kernel(PrepParams P) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += stride) prep_one(P, r);
 }
 
-// BaseContext(2) value of read offset o (StandardCovariate.scala:59-90),
-// including the mirrored reverse-strand indexing (quirk Q9).
-__device__ __forceinline__ int context_of(const uint8_t* stb, int bshift, int rslot, int o, int st, int en, bool neg) {
-  const int k = o - st;
-  if (k == 0) return 0;
-  uint32_t ca, cb;
-  if (!neg) {
-    ca = base_code(stb, bshift + rslot + o - 1);
-    cb = base_code(stb, bshift + rslot + o);
-    if (ca == kCodeN || cb == kCodeN) return 0;
-    int ia = ca < 4 ? (int)ca : -1, ib = cb < 4 ? (int)cb : -1;
-    return 1 + 4 * ia + ib;
+// ----------------------------------------------------------- tile setup ----
+
+__device__ __forceinline__ uint32_t base_code(const uint8_t* bases, uint64_t slot) {
+  const uint8_t b = bases[slot >> 1];
+  return (slot & 1) ? (b >> 4) : (b & 0xF);
+}
+
+// BaseContext.encode of the (previous, current) base codes
+// (StandardCovariate.scala:84-90); reverse-strand reads see complements,
+// whose ACGT index is 3 - index.  'other' bytes have index -1 (forward only:
+// reverse reads holding them fail in the prep kernel).
+__device__ __forceinline__ int ctx_code(uint32_t ca, uint32_t cb, bool neg) {
+  const int ia = neg ? 3 - (int)ca : (ca < 4 ? (int)ca : -1);
+  const int ib = neg ? 3 - (int)cb : (cb < 4 ? (int)cb : -1);
+  return (ca == kCodeN || cb == kCodeN) ? 0 : 1 + 4 * ia + ib;
+}
+
+// 4-bit code of tile-relative slot s (the tile's bases start at nibble bsh of bt[0])
+__device__ __forceinline__ uint32_t tile_code(const uint8_t* bt, int bsh, int s) {
+  const int n = s + bsh;
+  return (bt[n >> 1] >> ((n & 1) << 2)) & 0xFu;
+}
+
+constexpr int kUnroll = 4;
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  for (int off = 1; off < 64; off <<= 1) {
+    const int x = __shfl_up(v, off);
+    if (lane >= off) v += x;
   }
-  const int ia_o = en + st - o;  // complement of s[end - k], s[end - 1 - k]
-  ca = base_code(stb, bshift + rslot + ia_o);
-  cb = base_code(stb, bshift + rslot + ia_o - 1);
-  if (ca == kCodeN || cb == kCodeN) return 0;
-  return 1 + 4 * (3 - (int)ca) + (3 - (int)cb);
+  return v;
 }
 
-// ----------------------------------------------------------- tile staging --
-
-struct WaveStage {
-  uint8_t bases[kTileSlots / 2 + 16];
-  uint32_t mmbits[kTileSlots / 32 + 1];
-  uint32_t maskbits[kTileSlots / 32 + 1];
-  uint16_t rslot[kMaxTileReads + 1];
-  ReadRow rows[kMaxTileReads];
-  uint32_t hist[kQBins];
-  uint8_t md[kMdStage];
-  uint32_t cigar[kCigarStage];
-};
-
-struct TileInfo {
+struct Tile {
   int64_t r0;
   int nr;
   uint64_t ts0;  // absolute slot of the tile start
   int nslots;
-  int bshift;    // ts0 & 1 (the staged bases start at ts0 & ~1)
-  bool md_staged, cig_staged;
-  uint32_t md0, cig0;
 };
 
-// Load the tile's per-read records, stage bases / MD / CIGAR, and clear the
-// per-tile LDS state.  Returns this lane's read records.
-__device__ TileInfo stage_tile(const ReadsDev& rd, int64_t tile, WaveStage& ws, int lane, ReadMeta& m, ReadAlign& a,
-                               bool stage_bases) {
-  TileInfo ti;
-  ti.r0 = tile * (int64_t)rd.reads_per_tile;
+// Load the tile's reads into the wave's LDS state (see WaveTile).
+__device__ Tile setup_tile(const ReadsDev& rd, const ReadInfo* info, int64_t t, WaveTile& T, int lane, int L,
+                           ReadMeta& m, ReadInfo& inf) {
+  Tile ti;
+  ti.r0 = t * (int64_t)rd.reads_per_tile;
   ti.nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - ti.r0);
+  m = ReadMeta{0, 0, 0, 0, 0};
+  inf = ReadInfo{0, 0, 0, 0};
   if (lane < ti.nr) {
     m = rd.meta[ti.r0 + lane];
-    a = rd.align[ti.r0 + lane];
-  } else {
-    m = ReadMeta{0, 0, 0, 0, 0};
-    a = ReadAlign{0, 0, 0, -1, 0, 0};
+    inf = info[ti.r0 + lane];
   }
-  const int last = ti.nr - 1;
   ti.ts0 = __shfl(m.slot, 0);
-  const uint64_t last_slot = __shfl(m.slot, last);
-  const uint32_t last_len = __shfl((uint32_t)max(m.lq, m.ls), last);
-  const uint64_t ts1 = last_slot + last_len;
-  ti.nslots = (int)(ts1 - ti.ts0);
-  ti.bshift = (int)(ti.ts0 & 1);
-  if (lane < ti.nr) ws.rslot[lane] = (uint16_t)(m.slot - ti.ts0);
-  if (lane == 0) ws.rslot[ti.nr] = (uint16_t)ti.nslots;
-  // MD / CIGAR ranges of the tile are contiguous
-  ti.md0 = __shfl(a.md_off, 0);
-  const uint32_t md1 = __shfl(a.md_off + (uint32_t)a.md_len, last);
-  ti.cig0 = __shfl(a.cigar_off, 0);
-  const uint32_t cig1 = __shfl(a.cigar_off + (uint32_t)a.n_cigar, last);
-  ti.md_staged = (md1 - ti.md0) <= (uint32_t)kMdStage;
-  ti.cig_staged = (cig1 - ti.cig0) <= (uint32_t)kCigarStage;
-  if (ti.md_staged)
-    for (uint32_t i = lane; i < md1 - ti.md0; i += 64) ws.md[i] = rd.md[ti.md0 + i];
-  if (ti.cig_staged)
-    for (uint32_t i = lane; i < cig1 - ti.cig0; i += 64) ws.cigar[i] = rd.cigar[ti.cig0 + i];
-  if (stage_bases) {
-    const uint64_t b0 = ti.ts0 >> 1, b1 = (ts1 + 1) >> 1;
-    for (uint64_t i = lane; i < b1 - b0; i += 64) ws.bases[i] = rd.bases[b0 + i];
+  const uint32_t len = max(m.lq, m.ls);
+  const uint64_t last_end = __shfl(m.slot + len, ti.nr - 1);
+  ti.nslots = (int)(last_end - ti.ts0);
+  for (int i = lane; i < kTileSlots / 32; i += 64) T.sb[i] = 0;
+  for (int i = lane; i < kQBins; i += 64) T.hist[i] = 0;
+  // compact list of the reads that own slots
+  const bool own = lane < ti.nr && len > 0;
+  const unsigned long long bal = __ballot(own);
+  const int c = __popcll(bal & ((1ull << lane) - 1ull));
+  wave_sync();
+  if (own) {
+    const int rs = (int)(m.slot - ti.ts0);
+    // DiscreteCycle (StandardCovariate.scala:39-48) as a linear function of the
+    // slot: cell = cyc + L, cyc = neg ? ls - o : o + 1, negated for second of pair
+    const bool neg = inf.fl & kInfoNeg, sec = inf.fl & kInfoSecond;
+    int cb;
+    bool down;
+    if (!neg) {
+      cb = sec ? L - 1 + rs : L + 1 - rs;
+      down = sec;
+    } else {
+      cb = sec ? L - (int)m.ls - rs : L + (int)m.ls + rs;
+      down = !sec;
+    }
+    const uint32_t fl = inf.fl | (down ? kInfoCycNeg : 0);
+    const uint32_t st = (inf.fl & kInfoPass) ? 0u : inf.st, en = (inf.fl & kInfoPass) ? m.lq : inf.en;
+    const uint32_t cm = (uint32_t)(2 * rs + (int)inf.en + (int)inf.st);  // reverse-strand context mirror
+    T.rec[c] = make_uint4(st | (en << 16), fl | ((uint32_t)(cb & 0xFFFF) << 16), (uint32_t)rs | ((cm & 0xFFFF) << 16),
+                          (uint32_t)m.rg | ((uint32_t)lane << 16));
+    atomicOr(&T.sb[rs >> 5], 1u << (rs & 31));
   }
-  for (int i = lane; i < kTileSlots / 32 + 1; i += 64) {
-    ws.mmbits[i] = 0;
-    ws.maskbits[i] = 0;
-  }
-  for (int i = lane; i < kQBins; i += 64) ws.hist[i] = 0;
+  wave_sync();
+  // popcount prefix of the start bitmap, two words per lane
+  const uint32_t c0 = __popc(T.sb[2 * lane]), c1 = __popc(T.sb[2 * lane + 1]);
+  const int incl = wave_incl_scan((int)(c0 + c1), lane);
+  T.pre[2 * lane] = (uint16_t)(incl - (int)(c0 + c1));
+  T.pre[2 * lane + 1] = (uint16_t)(incl - (int)c1);
+  wave_sync();
   return ti;
 }
 
-__device__ __forceinline__ int find_row(const uint16_t* rslot, int nr, int s) {
-  int lo = 0, hi = nr;  // last i with rslot[i] <= s
-  while (hi - lo > 1) {
-    int mid = (lo + hi) >> 1;
-    if (rslot[mid] <= s) lo = mid; else hi = mid;
-  }
-  return lo;
+__device__ __forceinline__ int compact_of(const WaveTile& T, int s) {
+  const int w = s >> 5;
+  return (int)T.pre[w] + __popc(T.sb[w] & (0xFFFFFFFFu >> (31 - (s & 31)))) - 1;
 }
 
 // ------------------------------------------------------------ observe ------
 
 // LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32]
-//      [block hist 128 u32][tile counter] [WaveStage x 8]
+//      [block hist 128 u32][tile counter] [WaveTile x 16]
 extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -449,8 +465,8 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
   uint32_t* w_masked = w_mm + qw * cells;
   uint32_t* blk_hist = w_masked + qw;
   uint32_t* blk_next = blk_hist + kQBins;
-  uintptr_t stage_off = ((uintptr_t)(blk_next + 4) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
-  WaveStage* stages = (WaveStage*)(smem + stage_off);
+  const uintptr_t tile_off = ((uintptr_t)(blk_next + 4) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
+  WaveTile* tiles = (WaveTile*)(smem + tile_off);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < 2 * qw * cells + qw; i += blockDim.x) w_obs[i] = 0;
@@ -460,85 +476,88 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
   if (tid == 0) blk_next[0] = 0;
   __syncthreads();
 
-  WaveStage& ws = stages[wave];
+  WaveTile& T = tiles[wave];
+  const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
   for (;;) {
-    int64_t t;
-    {
-      uint32_t ti = 0;
-      if (lane == 0) ti = atomicAdd(&blk_next[0], 1u);
-      ti = __shfl(ti, 0);
-      t = tb0 + ti;
-    }
+    uint32_t tix = 0;
+    if (lane == 0) tix = atomicAdd(&blk_next[0], 1u);
+    const int64_t t = tb0 + __shfl(tix, 0);
     if (t >= tb1) break;
     ReadMeta m;
-    ReadAlign a;
-    TileInfo T = stage_tile(P.rd, t, ws, lane, m, a, true);
-    wave_sync();
-    if (lane < T.nr) {
-      const uint32_t* cig = T.cig_staged ? ws.cigar + (a.cigar_off - T.cig0) : P.rd.cigar + a.cigar_off;
-      const uint8_t* md = T.md_staged ? ws.md + (a.md_off - T.md0) : P.rd.md + a.md_off;
-      ws.rows[lane] = prep_read<true>(P.rd, P.sites, (uint64_t)(T.r0 + lane), m, a, (int)(m.slot - T.ts0), cig, md,
-                                      ws.mmbits, ws.maskbits, P.err);
-    }
-    wave_sync();
-    // ---- per-base pass: 16-slot chunks, one 16-B qual load per lane ----
-    const uint64_t c0 = T.ts0 >> 4, c1 = (T.ts0 + T.nslots + 15) >> 4;
-    for (uint64_t c = c0 + lane; c < c1; c += 64) {
-      const uint4 qv = *(const uint4*)(P.rd.qual + (c << 4));
-      const uint32_t qw4[4] = {qv.x, qv.y, qv.z, qv.w};
-      int s = (int)((int64_t)(c << 4) - (int64_t)T.ts0);  // tile-relative slot of the chunk's first byte
-      int i = find_row(ws.rslot, T.nr, max(s, 0));
-      int nexts = ws.rslot[i + 1];
-      ReadRow row = ws.rows[i];
-      int rs = ws.rslot[i];
-#pragma unroll 4
-      for (int j = 0; j < 16; ++j, ++s) {
-        if (s < 0 || s >= T.nslots) continue;
-        while (s >= nexts) {
-          ++i;
-          nexts = ws.rslot[i + 1];
-          row = ws.rows[i];
-          rs = ws.rslot[i];
-        }
-        if (!(row.fl & (kRowActive | kRowQualCheck))) continue;
-        const int o = s - rs;
-        if (o < row.st || o >= row.en) continue;
-        const int q = (int)(int8_t)((qw4[j >> 2] >> ((j & 3) * 8)) & 0xFF);
-        if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-          report(P.err, err_key((uint64_t)(T.r0 + i), o, kRankTable, BQSR_ERR_QUAL_RANGE));
+    ReadInfo inf;
+    const Tile ti = setup_tile(P.rd, P.info, t, T, lane, L, m, inf);
+    // uniform per-tile bases: per-base addresses are 32-bit offsets
+    const uint8_t* qt = P.rd.qual + ti.ts0;
+    const uint8_t* bt = P.rd.bases + (ti.ts0 >> 1);
+    const int bsh = (int)(ti.ts0 & 1);
+    const uint64_t* bits_t = P.bits + ti.r0 * P.W;
+    const int W = P.W;
+    // four slots per lane per step: the loads of all four issue before any use
+    for (int s0 = lane; s0 < ti.nslots; s0 += 64 * kUnroll) {
+      int sv[kUnroll], qv[kUnroll];
+      uint4 rc[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        sv[u] = s0 + 64 * u;
+        const int sc = sv[u] < ti.nslots ? sv[u] : 0;
+        qv[u] = (int)(int8_t)qt[sc];
+        rc[u] = T.rec[compact_of(T, sc)];
+      }
+      int ov[kUnroll];
+      bool act[kUnroll];
+      uint64_t bw[kUnroll];
+      uint32_t ca[kUnroll], cbv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
+        ov[u] = sv[u] - (int)(rc[u].z & 0xFFFF);
+        act[u] = sv[u] < ti.nslots && (fl & (kInfoObs | kInfoObsCheck)) && ov[u] >= st && ov[u] < en;
+        const bool full = act[u] && (fl & kInfoObs);
+        bw[u] = full ? bits_t[(int)(rc[u].w >> 16) * W + (ov[u] >> 5)] : 0ull;
+        // BaseContext(2) operands (StandardCovariate.scala:59-90): codes at s-1, s;
+        // the reverse strand reads them mirrored within [st, en) (quirk Q9)
+        const bool neg = fl & kInfoNeg;
+        const int na = neg ? (int)(rc[u].z >> 16) - sv[u] : sv[u] - 1;
+        const bool ctxon = full && ov[u] != st;
+        ca[u] = ctxon ? tile_code(bt, bsh, na) : 0u;
+        cbv[u] = ctxon ? tile_code(bt, bsh, neg ? na - 1 : sv[u]) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int q = qv[u];
+        if (!act[u]) continue;
+        const int o = ov[u], fl = (int)(rc[u].y & 0xFFFF);
+        if (__builtin_expect(q < 0, 0)) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+          report(P.err, err_key((uint64_t)(ti.r0 + (rc[u].w >> 16)), o, kRankTable, BQSR_ERR_QUAL_RANGE));
           continue;
         }
-        if (!(row.fl & kRowActive)) continue;
-        const bool neg = row.fl & kRowNeg;
-        const bool masked = (ws.maskbits[s >> 5] >> (s & 31)) & 1u;
-        const bool mism = (ws.mmbits[s >> 5] >> (s & 31)) & 1u;
-        int cyc = neg ? ((int)row.ls - o) : (o + 1);  // DiscreteCycle
-        if (row.fl & kRowSecond) cyc = -cyc;
-        const int ctx = context_of(ws.bases, T.bshift, rs, o, row.st, row.en, neg);
-        atomicAdd(&ws.hist[q], 1u);
-        const int slot = q - P.w.q_lo;
-        if ((int)row.rg == P.w.rg_lo && (unsigned)slot < (unsigned)qw) {
-          if (masked) {
-            atomicAdd(&w_masked[slot], 1u);
-          } else {
-            const int c_cyc = slot * cells + (cyc + L), c_ctx = slot * cells + C + (ctx + 4);
-            atomicAdd(&w_obs[c_cyc], 1u);
-            atomicAdd(&w_obs[c_ctx], 1u);
-            if (mism) {
-              atomicAdd(&w_mm[c_cyc], 1u);
-              atomicAdd(&w_mm[c_ctx], 1u);
-            }
+        if (!(fl & kInfoObs)) continue;
+        const bool masked = (bw[u] >> (o & 31)) & 1u;
+        const bool mism = (bw[u] >> (32 + (o & 31))) & 1u;
+        const int cb = (int)(int16_t)(rc[u].y >> 16);
+        const int ccell = (fl & kInfoCycNeg) ? cb - sv[u] : cb + sv[u];  // cycle + L
+        const int st = (int)(rc[u].x & 0xFFFF);
+        const int xcell = C + 4 + ((o == st) ? 0 : ctx_code(ca[u], cbv[u], fl & kInfoNeg));
+        atomicAdd(&T.hist[q], 1u);
+        const int rg = (int)(rc[u].w & 0xFFFF);
+        const int slot = q - q_lo;
+        if (rg == rg_lo && (unsigned)slot < (unsigned)qw) {
+          const int base = slot * cells;
+          atomicAdd(masked ? &w_masked[slot] : &w_obs[base + ccell], 1u);
+          if (!masked) atomicAdd(&w_obs[base + xcell], 1u);
+          if (__builtin_expect(mism && !masked, 0)) {
+            atomicAdd(&w_mm[base + ccell], 1u);
+            atomicAdd(&w_mm[base + xcell], 1u);
           }
         } else {  // outside the LDS window: straight to the int64 table
-          const int64_t key = (int64_t)q + (int64_t)kMaxQ * row.rg;
+          const int64_t key = (int64_t)q + (int64_t)kMaxQ * rg;
           atomicAdd((unsigned long long*)&P.touched[key], 1ull);
           if (!masked) {
-            const int64_t c_cyc = key * cells + (cyc + L), c_ctx = key * cells + C + (ctx + 4);
-            atomicAdd((unsigned long long*)&P.obs[c_cyc], 1ull);
-            atomicAdd((unsigned long long*)&P.obs[c_ctx], 1ull);
+            atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
+            atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
             if (mism) {
-              atomicAdd((unsigned long long*)&P.mm[c_cyc], 1ull);
-              atomicAdd((unsigned long long*)&P.mm[c_ctx], 1ull);
+              atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
+              atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
             }
           }
         }
@@ -547,7 +566,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
     wave_sync();
     // per-tile histogram of folded quals (input of the exact expectedMismatch fold)
     for (int k = lane; k < kQBins; k += 64) {
-      const uint32_t h = ws.hist[k];
+      const uint32_t h = T.hist[k];
       P.h2[t * kQBins + k] = (uint16_t)h;
       if (h) atomicAdd(&blk_hist[k], h);
     }
@@ -555,14 +574,14 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
   }
   __syncthreads();
   // ---- flush the window (int64 atomics) ----
-  const int64_t key0 = (int64_t)P.w.q_lo + (int64_t)kMaxQ * P.w.rg_lo;
+  const int64_t key0 = (int64_t)q_lo + (int64_t)kMaxQ * rg_lo;
   for (int i = tid; i < qw * cells; i += blockDim.x) {
     const int slot = i / cells, cell = i - slot * cells;
     if (key0 + slot >= P.g.K) continue;
     const uint32_t o = w_obs[i], mmv = w_mm[i];
-    const int64_t g = (key0 + slot) * cells + cell;
-    if (o) atomicAdd((unsigned long long*)&P.obs[g], (unsigned long long)o);
-    if (mmv) atomicAdd((unsigned long long*)&P.mm[g], (unsigned long long)mmv);
+    const int64_t gi = (key0 + slot) * cells + cell;
+    if (o) atomicAdd((unsigned long long*)&P.obs[gi], (unsigned long long)o);
+    if (mmv) atomicAdd((unsigned long long*)&P.mm[gi], (unsigned long long)mmv);
   }
   for (int slot = tid; slot < qw; slot += blockDim.x) {
     if (key0 + slot >= P.g.K) continue;
@@ -584,72 +603,82 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
 // the observe kernel give that sum for whole blocks / tiles at once.  Only the
 // additions that leave the binade (about log2(S_end/S_0) of them) or hit a
 // rounding tie are done one by one, in double arithmetic, exactly as the JVM
-// does.  One workgroup of 256 threads.
+// does.  One workgroup of 1024 threads.
 
-constexpr int kFoldThreads = 256;
+constexpr int kFoldThreads = 1024;
+constexpr int kFoldWaves = kFoldThreads / 64;
 
 struct FoldShared {
-  double t[kQBins];        // phredToErrorProbabilityCache
-  double inc[kQBins];      // round(t / u) at the current binade
-  uint8_t tie[kQBins];     // t / u is exactly a half-integer at the current binade
-  double red[kFoldThreads];
+  double t[kQBins];     // phredToErrorProbabilityCache
+  double inc[kQBins];   // round(t / u) at the current binade
+  uint8_t tie[kQBins];  // t / u is exactly a half-integer at the current binade
+  double wsum[kFoldWaves];
   uint8_t stream[kTileSlots];
   int32_t lens[kMaxTileReads + 1];
-  int32_t sts[kMaxTileReads];
+  uint64_t rbase[kMaxTileReads];
   double S;
   int32_t e;
-  int32_t mode_seq;
   int32_t found;
   int32_t ntot;
   double cut_sum;
 };
-
-__device__ __forceinline__ double two_pow(int k) { return ldexp(1.0, k); }
 
 // (re)derive the binade state of S and the increment table
 __device__ void fold_set_binade(FoldShared& F, int tid, double Sv) {
   __syncthreads();
   if (tid == 0) {
     F.S = Sv;
-    int e = ilogb(Sv);
-    F.e = e;
+    F.e = ilogb(Sv);
   }
   __syncthreads();
   const int e = F.e;
   for (int q = tid; q < kQBins; q += kFoldThreads) {
-    double x = ldexp(F.t[q], 52 - e);
-    double fl = floor(x);
-    F.tie[q] = (x - fl) == 0.5;
+    const double x = ldexp(F.t[q], 52 - e);
+    F.tie[q] = (x - floor(x)) == 0.5;
     F.inc[q] = rint(x);
   }
   __syncthreads();
 }
 
-// Materialise a tile's fold-order qual stream (usable reads, trimmed bases)
-// into LDS; returns its length.
-__device__ int fold_stream(const ReadsDev& rd, int64_t tile, FoldShared& F, int tid) {
+// block-wide inclusive scan of doubles (exact for integer values < 2^53)
+__device__ double block_scan(FoldShared& F, int tid, double v) {
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int off = 1; off < 64; off <<= 1) {
+    const double x = __shfl_up(v, off);
+    if (lane >= off) v += x;
+  }
+  if (lane == 63) F.wsum[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    double w = lane < kFoldWaves ? F.wsum[lane] : 0.0;
+    for (int off = 1; off < kFoldWaves; off <<= 1) {
+      const double x = __shfl_up(w, off);
+      if (lane >= off) w += x;
+    }
+    if (lane < kFoldWaves) F.wsum[lane] = w;
+  }
+  __syncthreads();
+  if (wave > 0) v += F.wsum[wave - 1];
+  __syncthreads();
+  return v;
+}
+
+// Materialise a tile's fold-order qual stream (usable valid reads, trimmed
+// bases) into LDS; returns its length.
+__device__ int fold_stream(const ReadsDev& rd, const ReadInfo* info, int64_t tile, FoldShared& F, int tid) {
   const int64_t r0 = tile * (int64_t)rd.reads_per_tile;
   const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
   if (tid < nr) {
-    const ReadMeta m = rd.meta[r0 + tid];
-    int st = 0, en = 0;
-    if (usable_read(m.flags) && (m.flags & BQSR_F_HAS_QUAL)) {
-      const uint8_t* q = rd.qual + m.slot;
-      const int lq = m.lq;
-      while (st < lq && (int8_t)q[st] <= 2) ++st;
-      int tail = 0;
-      while (tail < lq && (int8_t)q[lq - 1 - tail] <= 2) ++tail;
-      en = lq - tail;
-      if (en < st) en = st;
-    }
-    F.lens[tid] = en - st;
-    F.sts[tid] = st;
+    const ReadInfo inf = info[r0 + tid];
+    const bool on = (inf.fl & kInfoObs) && inf.en > inf.st;
+    F.lens[tid] = on ? inf.en - inf.st : 0;
+    F.rbase[tid] = rd.meta[r0 + tid].slot + inf.st;
   }
   __syncthreads();
   if (tid == 0) {
     int acc = 0;
     for (int i = 0; i < nr; ++i) {
-      int l = F.lens[i];
+      const int l = F.lens[i];
       F.lens[i] = acc;
       acc += l;
     }
@@ -657,34 +686,23 @@ __device__ int fold_stream(const ReadsDev& rd, int64_t tile, FoldShared& F, int 
     F.ntot = acc;
   }
   __syncthreads();
-  for (int i = 0; i < nr; ++i) {
-    const int b = F.lens[i], n = F.lens[i + 1] - b;
-    if (n == 0) continue;
-    const uint8_t* q = rd.qual + rd.meta[r0 + i].slot + F.sts[i];
-    for (int k = tid; k < n; k += kFoldThreads) F.stream[b + k] = q[k];
+  const int ntot = F.ntot;
+  for (int k = tid; k < ntot; k += kFoldThreads) {  // element k: the last read starting at or before it
+    int lo = 0, hi = nr;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (F.lens[mid] <= k) lo = mid; else hi = mid;
+    }
+    F.stream[k] = rd.qual[F.rbase[lo] + (uint64_t)(k - F.lens[lo])];
   }
   __syncthreads();
-  return F.ntot;
-}
-
-// block-wide inclusive scan of doubles (exact for integer values < 2^53)
-__device__ double block_scan(FoldShared& F, int tid, double v) {
-  F.red[tid] = v;
-  __syncthreads();
-  for (int off = 1; off < kFoldThreads; off <<= 1) {
-    double x = (tid >= off) ? F.red[tid - off] : 0.0;
-    __syncthreads();
-    F.red[tid] += x;
-    __syncthreads();
-  }
-  double r = F.red[tid];
-  __syncthreads();
-  return r;
+  return ntot;
 }
 
 // Fold one tile's stream exactly, starting from F.S.
-__device__ void fold_tile_exact(const ReadsDev& rd, int64_t tile, FoldShared& F, int tid, double seq_limit) {
-  const int n = fold_stream(rd, tile, F, tid);
+__device__ void fold_tile_exact(const ReadsDev& rd, const ReadInfo* info, int64_t tile, FoldShared& F, int tid,
+                                double seq_limit) {
+  const int n = fold_stream(rd, info, tile, F, tid);
   int pos = 0;
   while (pos < n) {
     if (F.S < seq_limit) {
@@ -702,111 +720,121 @@ __device__ void fold_tile_exact(const ReadsDev& rd, int64_t tile, FoldShared& F,
       continue;
     }
     // binade mode: per-thread contiguous runs of the remaining stream
-    const double N0 = ldexp(F.S, 52 - F.e);  // S / u, an integer < 2^53
-    const double head = 9007199254740992.0 - N0;  // additions allowed before leaving the binade
+    const double N0 = ldexp(F.S, 52 - F.e);       // S / u, an integer < 2^53
+    const double head = 9007199254740992.0 - N0;  // increments allowed before leaving the binade
     const int rem = n - pos;
     const int per = (rem + kFoldThreads - 1) / kFoldThreads;
     const int a = pos + tid * per, b = min(a + per, n);
     double mine = 0.0;
-    int stop = -1;
+    bool stop = false;
     for (int k = a; k < b; ++k) {
       const int q = F.stream[k];
-      if (F.tie[q]) { stop = k; break; }
+      if (F.tie[q]) {
+        stop = true;
+        break;
+      }
       mine += F.inc[q];
     }
-    // prefix over threads of the sums before each thread's stop (or whole run)
-    double incl = block_scan(F, tid, mine);
-    double excl = incl - mine;
-    // first element where the running count reaches `head` or a tie sits
+    const double incl = block_scan(F, tid, mine);
+    const double excl = incl - mine;
     if (tid == 0) F.found = 0x7FFFFFFF;
     __syncthreads();
-    {
-      int cand = 0x7FFFFFFF;
-      if (a < b) {
-        if (excl + mine >= head || stop >= 0) {
-          // locate inside this run
-          double run = excl;
-          for (int k = a; k < b; ++k) {
-            const int q = F.stream[k];
-            if (F.tie[q] || run + F.inc[q] >= head) { cand = k; break; }
-            run += F.inc[q];
-          }
+    if (a < b && (incl >= head || stop)) {  // the first event is in this run
+      double run = excl;
+      for (int k = a; k < b; ++k) {
+        const int q = F.stream[k];
+        if (F.tie[q] || run + F.inc[q] >= head) {
+          atomicMin(&F.found, k);
+          break;
         }
+        run += F.inc[q];
       }
-      if (cand != 0x7FFFFFFF) atomicMin(&F.found, cand);
     }
     __syncthreads();
     const int found = F.found;
     if (found == 0x7FFFFFFF) {
-      // whole remainder stays in the binade
+      // the whole remainder stays in the binade
       if (tid == kFoldThreads - 1) F.cut_sum = incl;
       __syncthreads();
       if (tid == 0) F.S = ldexp(N0 + F.cut_sum, F.e - 52);
       __syncthreads();
-      pos = n;
       break;
     }
     // sum of increments strictly before `found`
-    {
-      double part = 0.0;
-      if (a < b && a < found) {
-        const int hi = min(b, found);
-        for (int k = a; k < hi; ++k) part += F.inc[F.stream[k]];
-      }
-      double tot = block_scan(F, tid, part);
-      if (tid == kFoldThreads - 1) F.cut_sum = tot;
-      __syncthreads();
-    }
-    double Snew = 0.0;
+    double part = 0.0;
+    for (int k = a; k < min(b, found); ++k) part += F.inc[F.stream[k]];
+    const double tot = block_scan(F, tid, part);
+    if (tid == kFoldThreads - 1) F.cut_sum = tot;
+    __syncthreads();
     if (tid == 0) {
       double S = ldexp(N0 + F.cut_sum, F.e - 52);
       S = S + F.t[F.stream[found]];  // the exact IEEE addition the JVM performs
       F.S = S;
     }
     __syncthreads();
-    Snew = F.S;
     pos = found + 1;
-    fold_set_binade(F, tid, Snew);
+    fold_set_binade(F, tid, F.S);
   }
 }
 
-// Advance over `count` consecutive units (blocks or tiles) whose qual
-// histograms are hist(unit) while no unit leaves the binade; returns the index
-// of the first unit that would (or count).
-template <class H>
-__device__ int64_t fold_units(FoldShared& F, int tid, int64_t first, int64_t count, H&& hist) {
-  int64_t u = 0;
-  while (u < count) {
-    const int64_t my = first + u + tid;
-    const bool have = (u + tid) < count;
-    double d = 0.0;
-    bool tie = false;
-    if (have) {
-      for (int q = 0; q < kQBins; ++q) {
-        const uint32_t h = hist(my, q);
+// histogram row of a unit: 128 counters as 16-B vectors
+template <class T>
+__device__ __forceinline__ void unit_delta(const T* row, const FoldShared& F, double* d, bool* tie) {
+  constexpr int per = 16 / sizeof(T);   // counters per 16-B vector
+  constexpr int nv = kQBins / per;       // vectors per row
+  constexpr int chunk = 8;               // loads in flight per thread
+  const uint4* v = (const uint4*)row;
+  double acc = 0.0;
+  bool tt = false;
+#pragma unroll
+  for (int i0 = 0; i0 < nv; i0 += chunk) {
+    uint4 buf[chunk];
+#pragma unroll
+    for (int i = 0; i < chunk; ++i) buf[i] = v[i0 + i];
+#pragma unroll
+    for (int i = 0; i < chunk; ++i) {
+      const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
+#pragma unroll
+      for (int j = 0; j < per; ++j) {
+        const uint32_t h = (sizeof(T) == 4) ? w[j] : ((w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu);
+        const int q = (i0 + i) * per + j;
         if (h) {
-          d += (double)h * F.inc[q];
-          tie |= F.tie[q] != 0;
+          acc += (double)h * F.inc[q];
+          tt |= F.tie[q] != 0;
         }
       }
     }
+  }
+  *d = acc;
+  *tie = tt;
+}
+
+// Advance over `count` consecutive units (blocks or tiles) while none leaves
+// the binade; returns the index (relative to first) of the first unit that
+// would, or count.
+template <class T>
+__device__ int64_t fold_units(FoldShared& F, int tid, const T* rows, int64_t first, int64_t count) {
+  int64_t u = 0;
+  while (u < count) {
+    const bool have = (u + tid) < count;
+    double d = 0.0;
+    bool tie = false;
+    if (have) unit_delta(rows + (first + u + tid) * kQBins, F, &d, &tie);
     const double N0 = ldexp(F.S, 52 - F.e);
     const double head = 9007199254740992.0 - N0;
     if (d >= head) d = head;  // saturate: it crosses anyway
-    double incl = block_scan(F, tid, d);
+    const double incl = block_scan(F, tid, d);
     if (tid == 0) F.found = 0x7FFFFFFF;
     __syncthreads();
     if (have && (tie || incl >= head)) atomicMin(&F.found, tid);
     __syncthreads();
     const int found = F.found;
     const int take = (found == 0x7FFFFFFF) ? (int)min((int64_t)kFoldThreads, count - u) : found;
-    // commit the units before `found`
-    if (take > 0) {
+    if (take > 0) {  // commit the units before `found`
       if (tid == take - 1) F.cut_sum = incl;
       __syncthreads();
       if (tid == 0) F.S = ldexp(N0 + F.cut_sum, F.e - 52);
       __syncthreads();
-      // S may have become exactly 2^(e+1) only if a unit reached head; not here
     }
     u += take;
     if (found != 0x7FFFFFFF) return u;
@@ -823,20 +851,14 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
     F.e = 0;
   }
   __syncthreads();
-  // Binade mode needs S >= 2^1: every q >= 1 has t < 1 <= S/2 there, so no
-  // tie at that binade except q = 0's (t = 1, a tie only at 2^53); ties are
-  // still detected and added one by one, this is only where the fast path
-  // starts.
+  // Binade mode starts at S >= 2: every q >= 1 has t < 1 <= S/2 there.  Ties
+  // are still detected and added one by one; this is only where the fast
+  // path takes over from the plain sequential fold.
   const double seq_limit = 2.0;
   const int64_t nt = P.rd.n_tiles;
   for (int64_t b = 0; b < P.n_blocks; ++b) {
-    const int64_t tb0 = nt * b / P.n_blocks, tb1 = nt * (b + 1) / P.n_blocks;
-    if (tb0 == tb1) continue;
     if (F.S >= seq_limit) {
-      // whole blocks at once
-      const int64_t k = fold_units(F, tid, b, P.n_blocks - b,
-                                   [&](int64_t blk, int q) { return P.hq_block[blk * kQBins + q]; });
-      b += k;
+      b += fold_units(F, tid, P.hq_block, b, P.n_blocks - b);  // whole blocks at once
       if (b >= P.n_blocks) break;
     }
     // block b leaves the binade somewhere (or S is still small): tile level
@@ -844,11 +866,10 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
     int64_t t = c0;
     while (t < c1) {
       if (F.S >= seq_limit) {
-        const int64_t k = fold_units(F, tid, t, c1 - t, [&](int64_t tile, int q) { return (uint32_t)P.h2[tile * kQBins + q]; });
-        t += k;
+        t += fold_units(F, tid, P.h2, t, c1 - t);
         if (t >= c1) break;
       }
-      fold_tile_exact(P.rd, t, F, tid, seq_limit);
+      fold_tile_exact(P.rd, P.info, t, F, tid, seq_limit);
       ++t;
     }
   }
@@ -985,176 +1006,160 @@ extern "C" __global__ void bqsr_final_tables(const int64_t* obs, const int64_t* 
 
 // ----------------------------------------------------------------- apply ----
 
-// errorProbabilityToPhred(p) = javaD2I(-10 * log10(p)) by the threshold table
-// (see PhredThresholds in bqsr_capi.cpp): the float estimate is within one of
-// the answer, the two double comparisons make it exact.
-__device__ __forceinline__ int32_t phred_of(double p, const double* thr_lds, const double* thr, int32_t qmin, int32_t nthr) {
-  if (p != p) return 0;  // NaN
-  if (p <= 0.0) return p == 0.0 ? 2147483647 : 0;  // log10(0) = -inf; log10(<0) = NaN
-  if (p == __builtin_inf()) return (int32_t)0x80000000;
-  int E;
-  const double mant = frexp(p, &E);
-  const float gf = -10.0f * ((float)E + __log2f((float)mant)) * 0.30102999566398120f;
-  int n = (int)gf;  // trunc, the candidate
-  auto th = [&](int k) -> double {  // thr for Q = k (p <= thr(k)  <=>  Q >= k)
-    const int i = k - kThrLdsLo;
-    if ((unsigned)i < (unsigned)kThrLdsN) return thr_lds[i];
-    const int j = k - qmin;
-    if (j < 0) return __builtin_inf();
-    if (j >= nthr) return 0.0;
-    return thr[j];
-  };
-  for (int it = 0; it < 4 && p > th(n); ++it) --n;
-  for (int it = 0; it < 4 && p <= th(n + 1); ++it) ++n;
-  return n;
+// errorProbabilityToPhred(p) = javaD2I(-10 * log10(p)) from the bucketed
+// threshold table (PhredThresholds / PhredBuckets in bqsr_capi.cpp).
+__device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const int16_t* qb_q, const double* thr,
+                                           int qmin, int nthr) {
+  const uint64_t b = (uint64_t)__double_as_longlong(p);
+  if (b - 1ull < 0x7FEFFFFFFFFFFFFFull) {  // 0 < p < inf
+    const int e = (int)(b >> 52) - 1023;
+    if (e >= kQbElo && e <= kQbEhi) {
+      const int idx = ((e - kQbElo) << kQbBits) | (int)((b >> (52 - kQbBits)) & ((1u << kQbBits) - 1u));
+      const int q = qb_q[idx];
+      if (q != -32768) return p <= qb_thr[idx] ? q : q - 1;
+    }
+    int lo = 0, hi = nthr - 1;  // largest i with p <= thr[i]; thr[0] = DBL_MAX
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (p <= thr[mid]) lo = mid; else hi = mid - 1;
+    }
+    return qmin + lo;
+  }
+  if (p != p) return 0;                // NaN: (int)NaN = 0
+  if (p == 0.0) return 2147483647;     // log10(0) = -inf
+  if (p < 0.0) return 0;               // log10(p < 0) = NaN
+  return (int32_t)0x80000000;          // log10(inf) = inf
 }
 
+// LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16]
+//      [window ok qw u8][tile counter] [WaveTile x 16]
 extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int qw = P.w.qw, C = P.g.C;
-  double* w_s1 = (double*)smem;        // [qw][C]
-  double* w_d2 = w_s1 + qw * C;        // [qw][21]
-  double* thr_l = w_d2 + qw * kCtxSlots;  // [256]
-  uint8_t* w_ok = (uint8_t*)(thr_l + kThrLdsN);  // [qw]
+  const int qw = P.w.qw, C = P.g.C, L = P.g.L;
+  double* w_s1 = (double*)smem;
+  double* w_d2 = w_s1 + qw * C;
+  double* l_qbt = w_d2 + qw * kCtxSlots;
+  int16_t* l_qbq = (int16_t*)(l_qbt + kQbN);
+  uint8_t* w_ok = (uint8_t*)(l_qbq + kQbN);
   uint32_t* blk_next = (uint32_t*)(w_ok + ((qw + 15) & ~15));
-  uintptr_t stage_off = ((uintptr_t)(blk_next + 4) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
-  WaveStage* stages = (WaveStage*)(smem + stage_off);
+  const uintptr_t tile_off = ((uintptr_t)(blk_next + 4) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
+  WaveTile* tiles = (WaveTile*)(smem + tile_off);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t rq0 = (int64_t)P.w.rg_lo * kQBins + P.w.q_lo;
+  const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
+  const bool win_ok = rg_lo < P.n_rg;
+  const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
   for (int i = tid; i < qw * C; i += blockDim.x) {
     const int slot = i / C;
-    w_s1[i] = (P.w.rg_lo < P.n_rg && P.w.q_lo + slot < kQBins) ? P.s1[(rq0 + slot) * C + (i - slot * C)] : 0.0;
+    w_s1[i] = (win_ok && q_lo + slot < kQBins) ? P.s1[(rq0 + slot) * C + (i - slot * C)] : 0.0;
   }
   for (int i = tid; i < qw * kCtxSlots; i += blockDim.x) {
     const int slot = i / kCtxSlots;
-    w_d2[i] = (P.w.rg_lo < P.n_rg && P.w.q_lo + slot < kQBins) ? P.d2[(rq0 + slot) * kCtxSlots + (i - slot * kCtxSlots)]
-                                                                : 0.0;
+    w_d2[i] = (win_ok && q_lo + slot < kQBins) ? P.d2[(rq0 + slot) * kCtxSlots + (i - slot * kCtxSlots)] : 0.0;
   }
-  for (int i = tid; i < kThrLdsN; i += blockDim.x) {
-    const int j = i + kThrLdsLo - P.thr_qmin;
-    thr_l[i] = (j >= 0 && j < P.thr_n) ? P.thr[j] : 0.0;
+  for (int i = tid; i < kQbN; i += blockDim.x) {
+    l_qbt[i] = P.qb_thr[i];
+    l_qbq[i] = P.qb_q[i];
   }
-  for (int i = tid; i < qw; i += blockDim.x)
-    w_ok[i] = (P.w.rg_lo < P.n_rg && P.w.q_lo + i < kQBins) ? P.rq_ok[rq0 + i] : 0;
+  for (int i = tid; i < qw; i += blockDim.x) w_ok[i] = (win_ok && q_lo + i < kQBins) ? P.rq_ok[rq0 + i] : 0;
   const int64_t nt = P.rd.n_tiles;
   const int64_t tb0 = nt * blockIdx.x / gridDim.x, tb1 = nt * (blockIdx.x + 1) / gridDim.x;
   if (tid == 0) blk_next[0] = 0;
   __syncthreads();
-  WaveStage& ws = stages[wave];
-  const SitesDev no_sites{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+
+  WaveTile& T = tiles[wave];
   for (;;) {
-    int64_t t;
-    {
-      uint32_t ti = 0;
-      if (lane == 0) ti = atomicAdd(&blk_next[0], 1u);
-      ti = __shfl(ti, 0);
-      t = tb0 + ti;
-    }
+    uint32_t tix = 0;
+    if (lane == 0) tix = atomicAdd(&blk_next[0], 1u);
+    const int64_t t = tb0 + __shfl(tix, 0);
     if (t >= tb1) break;
     ReadMeta m;
-    ReadAlign a;
-    TileInfo T = stage_tile(P.rd, t, ws, lane, m, a, true);
-    wave_sync();
-    if (lane < T.nr) {
-      const uint32_t* cig = T.cig_staged ? ws.cigar + (a.cigar_off - T.cig0) : P.rd.cigar + a.cigar_off;
-      const uint8_t* md = T.md_staged ? ws.md + (a.md_off - T.md0) : P.rd.md + a.md_off;
-      const uint64_t r = (uint64_t)(T.r0 + lane);
-      ReadRow row = prep_read<false>(P.rd, no_sites, r, m, a, (int)(m.slot - T.ts0), cig, md, ws.mmbits, ws.maskbits,
-                                     P.err);
-      // pass-through reads keep their quality string
-      if (!eligible_read(m.flags)) {
-        row.fl = 0x100;
+    ReadInfo inf;
+    const Tile ti = setup_tile(P.rd, P.info, t, T, lane, L, m, inf);
+    if (lane < ti.nr) {
+      const int64_t r = ti.r0 + lane;
+      if (inf.fl & kInfoPass) {  // quality string passed through
         P.out_start[r] = 0;
         P.out_len[r] = (m.flags & BQSR_F_HAS_QUAL) ? m.lq : 0;
       } else {
-        P.out_start[r] = row.st;
-        P.out_len[r] = (row.fl & kRowActive) ? (uint32_t)(row.en - row.st) : 0;
+        P.out_start[r] = inf.st;
+        P.out_len[r] = (inf.fl & kInfoApp) ? (uint32_t)(inf.en - inf.st) : 0;
       }
-      ws.rows[lane] = row;
     }
-    wave_sync();
-    const uint64_t c0 = T.ts0 >> 4, c1 = (T.ts0 + T.nslots + 15) >> 4;
-    for (uint64_t c = c0 + lane; c < c1; c += 64) {
-      const uint4 qv = *(const uint4*)(P.rd.qual + (c << 4));
-      const uint32_t qin[4] = {qv.x, qv.y, qv.z, qv.w};
-      uint32_t qo[4] = {qv.x, qv.y, qv.z, qv.w};
-      uint32_t keep = 0;  // bit j: byte j of the chunk is written
-      int s = (int)((int64_t)(c << 4) - (int64_t)T.ts0);
-      int i = find_row(ws.rslot, T.nr, max(s, 0));
-      int nexts = ws.rslot[i + 1];
-      ReadRow row = ws.rows[i];
-      int rs = ws.rslot[i];
-      for (int j = 0; j < 16; ++j, ++s) {
-        if (s < 0 || s >= T.nslots) continue;
-        while (s >= nexts) {
-          ++i;
-          nexts = ws.rslot[i + 1];
-          row = ws.rows[i];
-          rs = ws.rslot[i];
-        }
-        const int o = s - rs;
-        const uint32_t qb = (qin[j >> 2] >> ((j & 3) * 8)) & 0xFF;
+    const uint8_t* qt = P.rd.qual + ti.ts0;
+    const uint8_t* bt = P.rd.bases + (ti.ts0 >> 1);
+    const int bsh = (int)(ti.ts0 & 1);
+    uint8_t* ot = P.out_qual + ti.ts0;
+    // four slots per lane per step: the loads of all four issue before any use
+    for (int s0 = lane; s0 < ti.nslots; s0 += 64 * kUnroll) {
+      int sv[kUnroll];
+      uint32_t qb[kUnroll];
+      uint4 rc[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        sv[u] = s0 + 64 * u;
+        const int sc = sv[u] < ti.nslots ? sv[u] : 0;
+        qb[u] = qt[sc];
+        rc[u] = T.rec[compact_of(T, sc)];
+      }
+      uint32_t ca[kUnroll], cbv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
+        const int o = sv[u] - (int)(rc[u].z & 0xFFFF);
+        const bool ctxon = sv[u] < ti.nslots && (fl & kInfoApp) && o > st && o < en;
+        const bool neg = fl & kInfoNeg;
+        const int na = neg ? (int)(rc[u].z >> 16) - sv[u] : sv[u] - 1;
+        ca[u] = ctxon ? tile_code(bt, bsh, na) : 0u;
+        cbv[u] = ctxon ? tile_code(bt, bsh, neg ? na - 1 : sv[u]) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
+        const int o = sv[u] - (int)(rc[u].z & 0xFFFF);
+        // pass-through reads carry st = 0, en = Lq
+        if (sv[u] >= ti.nslots || !(fl & (kInfoApp | kInfoAppCheck | kInfoPass)) || o < st || o >= en) continue;
         uint32_t code;
-        if (row.fl == 0x100) {  // pass-through: original char
-          if (o >= (int)P.rd.meta[T.r0 + i].lq) continue;
-          code = (qb + 33u) & 0xFFu;
+        if (fl & kInfoPass) {
+          code = qb[u] + 33u;  // the original quality char
         } else {
-          if (!(row.fl & (kRowActive | kRowQualCheck)) || o < row.st || o >= row.en) continue;
-          const int q = (int)(int8_t)qb;
-          const int64_t key = (int64_t)q + (int64_t)kMaxQ * row.rg;
+          const int q = (int)(int8_t)qb[u];
+          const int rg = (int)(rc[u].w & 0xFFFF);
+          const int slot = q - q_lo;
+          const int cb = (int)(int16_t)(rc[u].y >> 16);
+          const int ccell = (fl & kInfoCycNeg) ? cb - sv[u] : cb + sv[u];  // cycle + L
+          const int ctx = (o == st) ? 0 : ctx_code(ca[u], cbv[u], fl & kInfoNeg);
           double p;
-          bool ok;
-          const int slot = q - P.w.q_lo;
-          if ((int)row.rg == P.w.rg_lo && (unsigned)slot < (unsigned)qw) {
-            ok = w_ok[slot];
-            if (!ok || !(row.fl & kRowActive)) {
-              if (!ok) report(P.err, err_key((uint64_t)(T.r0 + i), o, kRankTable, BQSR_ERR_MISSING_KEY));
-              continue;
-            }
-            const bool neg = row.fl & kRowNeg;
-            int cyc = neg ? ((int)row.ls - o) : (o + 1);
-            if (row.fl & kRowSecond) cyc = -cyc;
-            const int ctx = context_of(ws.bases, T.bshift, rs, o, row.st, row.en, neg);
-            p = w_s1[slot * C + cyc + P.g.L] + w_d2[slot * kCtxSlots + ctx + 4];
+          if ((fl & kInfoApp) && rg == rg_lo && (unsigned)slot < (unsigned)qw && w_ok[slot]) {
+            // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+            p = w_s1[slot * C + ccell] + w_d2[slot * kCtxSlots + ctx + 4];
           } else {
-            // outside the window: validity as getReadGroupDelta / getQualScoreDelta see it
-            const int64_t r = (key - 1) / kMaxQ;
-            const bool grp = (r + 1) >= 0 && (r + 1) < P.n_groups && P.grp_ok[r + 1];
+            // key validity as getReadGroupDelta / getQualScoreDelta see it
+            const uint64_t r = (uint64_t)(ti.r0 + (rc[u].w >> 16));
+            const int64_t key = (int64_t)q + (int64_t)kMaxQ * rg;
+            const int64_t gr = (key - 1) / kMaxQ;
+            const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
             const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
             if (!grp || !kok) {
-              report(P.err, err_key((uint64_t)(T.r0 + i), o, kRankTable, BQSR_ERR_MISSING_KEY));
+              report(P.err, err_key(r, o, kRankTable, BQSR_ERR_MISSING_KEY));
               continue;
             }
             if (q < 0) {
-              report(P.err, err_key((uint64_t)(T.r0 + i), o, kRankTable, BQSR_ERR_QUAL_RANGE));
+              report(P.err, err_key(r, o, kRankTable, BQSR_ERR_QUAL_RANGE));
               continue;
             }
-            if (!(row.fl & kRowActive)) continue;
-            const bool neg = row.fl & kRowNeg;
-            int cyc = neg ? ((int)row.ls - o) : (o + 1);
-            if (row.fl & kRowSecond) cyc = -cyc;
-            const int ctx = context_of(ws.bases, T.bshift, rs, o, row.st, row.en, neg);
-            const int64_t rq = (int64_t)row.rg * kQBins + q;
-            p = P.s1[rq * C + cyc + P.g.L] + P.d2[rq * kCtxSlots + ctx + 4];
+            if (!(fl & kInfoApp)) continue;
+            const int64_t rq = (int64_t)rg * kQBins + q;
+            p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + ctx + 4];
           }
-          const int32_t Q = phred_of(p, thr_l, P.thr, P.thr_qmin, P.thr_n);
+          const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
           code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-          if (code > 0xFFu) {
+          if (__builtin_expect(code > 0xFFu, 0)) {
             const unsigned long long k = atomicAdd(P.n_exc, 1ull);
-            if ((int64_t)k < P.max_exc) P.exc[k] = ((unsigned long long)((c << 4) + j) << 16) | code;
-            code &= 0xFFu;
+            if ((int64_t)k < P.max_exc) P.exc[k] = ((ti.ts0 + (uint64_t)sv[u]) << 16) | code;
           }
         }
-        qo[j >> 2] = (qo[j >> 2] & ~(0xFFu << ((j & 3) * 8))) | (code << ((j & 3) * 8));
-        keep |= 1u << j;
-      }
-      uint8_t* dst = P.out_qual + (c << 4);
-      if (keep == 0xFFFFu) {
-        *(uint4*)dst = make_uint4(qo[0], qo[1], qo[2], qo[3]);
-      } else if (keep) {
-        for (int j = 0; j < 16; ++j)
-          if (keep & (1u << j)) dst[j] = (uint8_t)(qo[j >> 2] >> ((j & 3) * 8));
+        ot[sv[u]] = (uint8_t)code;
       }
     }
     wave_sync();

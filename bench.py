@@ -98,12 +98,14 @@ def main():
     lut = ctypes.c_void_p()
     torch.cuda.synchronize()
 
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    kt = {"observe": [], "fold": [], "apply": []}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+    kt = {"prep": [], "observe": [], "fold": [], "apply": []}
 
     def step(record: bool):
         check(L.bqsr_table_zero_async(th, sp))
         check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_RESET, sp))
+        ev[5].record(stream)
+        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_PREP, sp))
         ev[0].record(stream)
         check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_KERNEL, sp))
         ev[1].record(stream)
@@ -133,6 +135,7 @@ def main():
         nexc = ctypes.c_int64()
         check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
         if record:
+            kt["prep"].append(ev[5].elapsed_time(ev[0]))
             kt["observe"].append(ev[0].elapsed_time(ev[1]))
             kt["fold"].append(ev[1].elapsed_time(ev[2]))
             kt["apply"].append(ev[3].elapsed_time(ev[4]))

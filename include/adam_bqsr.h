@@ -243,9 +243,11 @@ bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* recs, cons
  * The calls above synchronise.  These enqueue on `stream` and return at once,
  * so a driver can keep a whole BQSR job on the device (the benchmark and the
  * multi-GPU path use them; RCCL collectives go between the stages). */
-enum { BQSR_STAGE_RESET = 1, BQSR_STAGE_KERNEL = 2, BQSR_STAGE_FOLD = 4 };
-/* observe stages: RESET clears the error word, KERNEL is the observe kernel,
- * FOLD the expectedMismatch fold (result at bqsr_batch_em_device_ptr). */
+enum { BQSR_STAGE_RESET = 1, BQSR_STAGE_KERNEL = 2, BQSR_STAGE_FOLD = 4, BQSR_STAGE_PREP = 8 };
+/* observe stages: RESET clears the error word, PREP is the per-read prep
+ * kernel (trimming, CIGAR/MD/known-site masks, validation), KERNEL the
+ * observe kernel, FOLD the expectedMismatch fold (result at
+ * bqsr_batch_em_device_ptr). */
 bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
                                int32_t stages, void* stream);
 bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
@@ -258,7 +260,9 @@ bqsr_status bqsr_table_zero_async(bqsr_table* t, void* stream);
 bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double expected_mismatch, bqsr_lut** out,
                                 void* stream);
 bqsr_status bqsr_finalize_result(bqsr_lut* l, void* stream);
-/* apply stages: RESET clears the error word and exception count, KERNEL the apply kernel */
+/* apply stages: RESET clears the error word and exception count, KERNEL the
+ * apply kernel; PREP (re)runs the prep kernel, which also runs by itself when
+ * observe has not prepared this batch */
 bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* l, uint8_t* out_qual,
                              uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
                              int32_t stages, void* stream);
