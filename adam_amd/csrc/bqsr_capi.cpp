@@ -169,26 +169,40 @@ TableGeom geom(const bqsr_dims& d) {
 }
 
 constexpr size_t kLdsMax = 163840;
-size_t tiles_bytes() { return sizeof(WaveTile) * kWaves; }
-size_t observe_lds(int qw, int cells) {
-  size_t head = (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4 + 16;
+size_t tiles_bytes(int ts) { return (size_t)tile_lds_bytes(ts) * kWaves; }
+size_t observe_lds(int qw, int cells, int ts) {
+  size_t head = (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4;
   head = (head + 15) & ~(size_t)15;
-  return head + tiles_bytes();
+  return head + tiles_bytes(ts);
 }
-size_t apply_lds(int qw, int C) {
-  size_t head = (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2) + ((qw + 15) & ~15) + 16;
+size_t apply_lds(int qw, int C, int ts) {
+  size_t head = (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2) + ((qw + 15) & ~15);
   head = (head + 15) & ~(size_t)15;
-  return head + tiles_bytes();
+  return head + tiles_bytes(ts);
 }
-int observe_qw(int cells) {
+int observe_qw(int cells, int ts) {
   int qw = 64;
-  while (qw > 1 && observe_lds(qw, cells) > kLdsMax) --qw;
+  while (qw > 1 && observe_lds(qw, cells, ts) > kLdsMax) --qw;
   return qw;
 }
-int apply_qw(int C) {
+int apply_qw(int C, int ts) {
   int qw = 64;
-  while (qw > 1 && apply_lds(qw, C) > kLdsMax) --qw;
+  while (qw > 1 && apply_lds(qw, C, ts) > kLdsMax) --qw;
   return qw;
+}
+// tile size: the smallest that holds the longest read
+int tile_size(int64_t max_slot_len) { return max_slot_len <= 1024 ? 1024 : max_slot_len <= 2048 ? 2048 : 4096; }
+
+template <int TS>
+void* observe_fn() { return (void*)&bqsr_observe_kernel<TS>; }
+template <int TS>
+void* apply_fn() { return (void*)&bqsr_apply_kernel<TS>; }
+void* observe_kernel_for(int ts) { return ts == 1024 ? observe_fn<1024>() : ts == 2048 ? observe_fn<2048>() : observe_fn<4096>(); }
+void* apply_kernel_for(int ts) { return ts == 1024 ? apply_fn<1024>() : ts == 2048 ? apply_fn<2048>() : apply_fn<4096>(); }
+template <class Params>
+hipError_t launch_tile(void* fn, int blocks, Params& P, size_t lds, hipStream_t s) {
+  void* args[] = {(void*)&P};
+  return hipLaunchKernel(fn, dim3(blocks), dim3(kBlockThreads), args, lds, s);
 }
 
 }  // namespace
@@ -228,17 +242,23 @@ struct bqsr_batch {
   std::vector<void*> allocs;
   // per-read prep results (valid once `prepped`)
   ReadInfo* d_info = nullptr;
-  uint64_t* d_bits = nullptr;
-  int32_t W = 1;  // bitmap words per read
+  uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
+  int64_t sbits_words = 0;
+  int32_t ts = 1024;            // tile size of the per-base passes
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
   // per-call scratch
   uint16_t* d_h2 = nullptr;
   uint32_t* d_hq = nullptr;
+  uint8_t* d_cand = nullptr;       // [n_blocks] fold candidates
+  int32_t* d_cand_list = nullptr;  // [n_blocks + 1]: list, then count
+  uint32_t* d_part = nullptr;      // per-block window counts
+  size_t part_words = 0;
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
   int32_t n_blocks = 0;
   ~bqsr_batch() {
+    if (d_part) (void)hipFree(d_part);
     for (void* p : allocs) (void)hipFree(p);
   }
 };
@@ -316,10 +336,10 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  for (int ts : {1024, 2048, 4096}) {
+    if (e == hipSuccess) e = hipFuncSetAttribute(observe_kernel_for(ts), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+    if (e == hipSuccess) e = hipFuncSetAttribute(apply_kernel_for(ts), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  }
   if (e != hipSuccess) {
     bqsr_context_destroy(c);
     return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
@@ -417,16 +437,23 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   if (max_slot_len > kMaxReadLen)
     return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
   const int64_t n = b->rd.n_reads;
-  b->rd.reads_per_tile = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kMaxTileReads, kTileSlots / std::max<int64_t>(1, max_slot_len)));
+  b->ts = tile_size(max_slot_len);
+  if (const char* e = getenv("ADAM_BQSR_TILE_SLOTS")) {  // tuning knob: a larger tile than needed
+    const int v = atoi(e);
+    if ((v == 1024 || v == 2048 || v == 4096) && v > b->ts) b->ts = v;
+  }
+  b->rd.reads_per_tile = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kMaxTileReads, b->ts / std::max<int64_t>(1, max_slot_len)));
   b->rd.n_tiles = (n + b->rd.reads_per_tile - 1) / b->rd.reads_per_tile;
-  b->n_blocks = b->ctx->n_cu;
+  b->n_blocks = std::min(b->ctx->n_cu, kMaxFoldBlocks);
   bqsr_status st;
   if ((st = dalloc(b->allocs, &b->d_h2, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kQBins)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_hq, (size_t)b->n_blocks * kQBins)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_cand, (size_t)b->n_blocks)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_cand_list, (size_t)b->n_blocks + 1)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_err, kErrWords)) != BQSR_OK) return st;
-  b->W = (int32_t)((std::max<int64_t>(1, max_slot_len) + 31) / 32);
   if ((st = dalloc(b->allocs, &b->d_info, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_bits, (size_t)std::max<int64_t>(1, n) * b->W)) != BQSR_OK) return st;
+  b->sbits_words = b->rd.n_slots / 32 + 2;
+  if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
   return BQSR_OK;
 }
@@ -557,6 +584,7 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
   b->ctx = ctx;
   b->owned = true;
   b->rd.n_reads = R->n_reads;
+  b->rd.n_slots = P.n_slots;
   b->n_slots = P.n_slots;
   b->n_bases = P.n_bases;
   b->dims = bqsr_dims{P.n_rg, P.max_len};
@@ -619,6 +647,7 @@ bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* d
   b->rd.cigar = dev->cigar;
   b->rd.md = dev->md;
   b->n_slots = dev->n_slots;
+  b->rd.n_slots = dev->n_slots;
   b->n_bases = -1;
   b->dims = dev->dims;
   b->q_lo = 0;
@@ -729,12 +758,12 @@ namespace {
 bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
   HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
   if (b->rd.n_reads > 0) {
+    HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
     PrepParams P{};
     P.rd = b->rd;
     if (sites) P.sites = sites->dev();
     P.info = b->d_info;
-    P.bits = b->d_bits;
-    P.W = b->W;
+    P.sbits = b->d_sbits;
     P.err = b->d_err;
     const int64_t blocks = std::min<int64_t>((b->rd.n_reads + 255) / 256, (int64_t)ctx->n_cu * 32);
     hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P);
@@ -767,29 +796,52 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     ObserveParams P{};
     P.rd = b->rd;
     P.info = b->d_info;
-    P.bits = b->d_bits;
-    P.W = b->W;
+    P.sbits = b->d_sbits;
     P.g = geom(t->dims);
-    P.w.qw = observe_qw(P.g.cells);
+    P.w.qw = observe_qw(P.g.cells, b->ts);
     P.w.q_lo = std::min(b->q_lo, kQBins - 1);
     P.w.rg_lo = b->rg_lo;
     P.touched = t->touched();
     P.obs = t->obs();
     P.mm = t->mm();
+    P.part_stride = 2 * P.w.qw * P.g.cells + P.w.qw;
+    const size_t need = (size_t)P.part_stride * b->n_blocks;
+    if (b->part_words < need) {  // grows with the table geometry; kept across calls
+      if (b->d_part) {
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(b->d_part);
+        b->d_part = nullptr;
+        b->part_words = 0;
+      }
+      HIP_TRY(hipMalloc((void**)&b->d_part, need * sizeof(uint32_t)));
+      b->part_words = need;
+    }
+    P.part = b->d_part;
     P.hq_block = b->d_hq;
-    P.h2 = b->d_h2;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = observe_lds(P.w.qw, P.g.cells);
-    hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    const size_t lds = observe_lds(P.w.qw, P.g.cells, b->ts);
+    HIP_TRY(launch_tile(observe_kernel_for(b->ts), b->n_blocks, P, lds, s));
+    const int rb = (int)std::min<int64_t>(1024, (P.part_stride + 255) / 256);
+    hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb), dim3(256), 0, s, (const uint32_t*)b->d_part, b->n_blocks,
+                       P.part_stride, P.w, P.g, P.touched, P.obs, P.mm);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
+    int32_t* n_cand = b->d_cand_list + b->n_blocks;
+    hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(256), 0, s, (const uint32_t*)b->d_hq, (const double*)ctx->d_pow10,
+                       b->n_blocks, b->d_cand, b->d_cand_list, n_cand);
+    HIP_TRY(hipGetLastError());
+    const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
+    hipLaunchKernelGGL(bqsr_tile_hist, dim3(ctx->n_cu * 4), dim3(256), 0, s, b->rd, (const ReadInfo*)b->d_info,
+                       (const int32_t*)b->d_cand_list, (const int32_t*)n_cand, b->n_blocks, max_tpb, b->d_h2);
+    HIP_TRY(hipGetLastError());
     FoldParams F{};
     F.rd = b->rd;
     F.info = b->d_info;
     F.hq_block = b->d_hq;
     F.h2 = b->d_h2;
+    F.cand = b->d_cand;
     F.pow10 = ctx->d_pow10;
     F.n_blocks = b->n_blocks;
     F.em_out = b->d_em;
@@ -1042,7 +1094,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.rd = b->rd;
   P.info = b->d_info;
   P.g = geom(L->dims);
-  P.w.qw = apply_qw(P.g.C);
+  P.w.qw = apply_qw(P.g.C, b->ts);
   P.w.q_lo = std::min(b->q_lo, kQBins - 1);
   P.w.rg_lo = b->rg_lo;
   P.n_rg = L->dims.n_rg;
@@ -1064,9 +1116,8 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
-  const size_t lds = apply_lds(P.w.qw, P.g.C);
-  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
-  HIP_TRY(hipGetLastError());
+  const size_t lds = apply_lds(P.w.qw, P.g.C, b->ts);
+  HIP_TRY(launch_tile(apply_kernel_for(b->ts), b->n_blocks, P, lds, s));
   return ok();
 }
 

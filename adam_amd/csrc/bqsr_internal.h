@@ -61,10 +61,12 @@ constexpr int kCtxSlots = 21;  // contexts -4..16
 constexpr int kQBins = 128;    // qual values 0..127 (Java byte >= 0)
 
 // Tile geometry of the per-base passes: a tile is `reads_per_tile`
-// consecutive reads (<= 64) whose base slots fit in kTileSlots; one wavefront
-// processes one tile at a time, one base per lane per step.
-constexpr int kTileSlots = 4096;
+// consecutive reads (<= 64) whose base slots fit in the batch's tile size TS
+// (1024, 2048 or 4096 slots: the smallest that holds the longest read); one
+// wavefront processes one tile at a time, one base per lane per step.
+constexpr int kTileSlots = 4096;  // largest tile
 constexpr int kMaxTileReads = 64;
+constexpr int kMaxFoldBlocks = 1024;  // workgroups of the per-base passes (one per CU)
 constexpr int kWaves = 16;  // waves per block of the per-base passes (1024 threads)
 constexpr int kBlockThreads = 64 * kWaves;
 constexpr int kMaxReadLen = 4096;  // longest read the device path takes
@@ -123,31 +125,33 @@ struct ReadsDev {
   const uint32_t* cigar;
   const uint8_t* md;
   int64_t n_reads;
+  int64_t n_slots;  // base slots of the batch (qual[] holds n_slots bytes, bases[] n_slots nibbles)
   int32_t reads_per_tile;
   int64_t n_tiles;
 };
 
+// Slot bitmap: u64 word i covers base slots 32i .. 32i+31 of the batch, bit j
+// of the low half = slot 32i+j is masked, of the high half = it mismatches.
 struct PrepParams {
   ReadsDev rd;
   SitesDev sites;
   ReadInfo* info;      // [n_reads]
-  uint64_t* bits;      // [n_reads][W]: per 32 read offsets, masked bits | mismatch bits << 32
-  int32_t W;           // words per read
+  uint64_t* sbits;     // [n_slots / 32 + 2], zeroed before the launch
   unsigned long long* err;  // error words
 };
 
 struct ObserveParams {
   ReadsDev rd;
   const ReadInfo* info;
-  const uint64_t* bits;  // PrepParams::bits
-  int32_t W;
+  const uint64_t* sbits;  // PrepParams::sbits
   TableGeom g;
   Window w;
   int64_t* touched;  // [K]
   int64_t* obs;      // [K*cells]
   int64_t* mm;       // [K*cells]
+  uint32_t* part;      // [n_blocks][part_stride] per-block window counts (obs, mm, touched)
+  int32_t part_stride; // 2*qw*cells + qw
   uint32_t* hq_block;  // [n_blocks][128] per-block qual histogram of folded bases
-  uint16_t* h2;        // [n_tiles][128]   per-tile qual histogram of folded bases
   unsigned long long* err;
   int32_t n_blocks;
 };
@@ -156,7 +160,8 @@ struct FoldParams {
   ReadsDev rd;
   const ReadInfo* info;
   const uint32_t* hq_block;
-  const uint16_t* h2;
+  const uint16_t* h2;     // [n_tiles][128] per-tile histograms (candidate blocks only)
+  const uint8_t* cand;    // [n_blocks] bqsr_fold_plan's candidate blocks
   const double* pow10;  // phredToErrorProbabilityCache[0..127]
   int32_t n_blocks;
   double* em_out;      // [1]
@@ -188,7 +193,7 @@ struct ApplyParams {
   int32_t thr_n;
   const double* qb_thr;   // [kQbN]
   const int16_t* qb_q;    // [kQbN]
-  uint8_t* out_qual;
+  uint8_t* out_qual;      // [n_slots]; slots outside the recalibrated ranges are scratch
   uint32_t* out_start;
   uint32_t* out_len;
   unsigned long long* exc;  // (slot << 16 | code16)
@@ -197,24 +202,43 @@ struct ApplyParams {
   unsigned long long* err;
 };
 
-// Per-wave tile state of the per-base passes (LDS).  Reads of the tile that
-// own at least one slot are listed in slot order ("compact" index c), one
-// 16-B record each (one ds_read_b128), all positions tile-relative slots:
+// Per-wave tile state of the per-base passes (LDS), for tiles of TS slots.
+// The tile's quals, 4-bit base codes and slot-bitmap words are staged here as
+// whole 16-B chunks (prefetched into registers while the previous tile runs),
+// so the per-base loop touches only LDS.  Reads of the tile that own at least
+// one slot are listed in slot order ("compact" index c), one 16-B record each
+// (one ds_read_b128), all positions tile-relative slots:
 //   x = st | en << 16       trimmed read offsets (pass-through reads: 0, Lq)
 //   y = fl | cb << 16       cycle cell of slot s = cb + s (kInfoCycNeg: cb - s)
 //   z = rslot | cm << 16    first slot; context operands of slot s are the
 //                           codes at s - 1, s (reverse strand: cm - s, cm - s - 1)
 //   w = rg | rtile << 16    read group, read index within the tile
-//   sb = one bit per slot marking compact read starts, pre = popcount prefix
-//   of sb per word: the compact index of slot s is
-//   pre[s >> 5] + popc(sb[s >> 5] & ones(s & 31)) - 1.
-struct WaveTile {
-  uint4 rec[kMaxTileReads];
-  uint32_t sb[kTileSlots / 32];
-  uint32_t hist[kQBins];
-  uint16_t pre[kTileSlots / 32];
+//   sbp[k].x = one bit per slot marking compact read starts, .y = popcount
+//   prefix of the start bits before word k: the compact index of slot s is
+//   sbp[s>>5].y + popc(sbp[s>>5].x & ones(s & 31)) - 1.
+template <int TS>
+struct TileCfg {
+  static constexpr int kSb = TS / 32;      // start-bitmap words
+  static constexpr int kQC = TS / 16 + 1;  // 16-B chunks of quals (+1: unaligned start)
+  static constexpr int kCC = TS / 32 + 1;  // 16-B chunks of base codes (2 per byte)
+  static constexpr int kBW = TS / 32 + 2;  // slot-bitmap words (even: keeps 16-B alignment)
+  static constexpr int nQ = (kQC + 63) / 64;  // chunks per lane
+  static constexpr int nC = (kCC + 63) / 64;
+  static constexpr int nB = (kBW + 63) / 64;
 };
-static_assert(sizeof(WaveTile) % 16 == 0, "WaveTile must keep 16-B alignment");
+template <int TS>
+struct TileLds {
+  uint4 rec[kMaxTileReads];
+  uint4 q[TileCfg<TS>::kQC];
+  uint4 c[TileCfg<TS>::kCC];
+  uint64_t bits[TileCfg<TS>::kBW];
+  uint2 sbp[TileCfg<TS>::kSb];
+};
+static_assert(sizeof(TileLds<1024>) % 16 == 0 && sizeof(TileLds<2048>) % 16 == 0 && sizeof(TileLds<4096>) % 16 == 0,
+              "TileLds must keep 16-B alignment");
+inline int tile_lds_bytes(int ts) {
+  return ts <= 1024 ? (int)sizeof(TileLds<1024>) : ts <= 2048 ? (int)sizeof(TileLds<2048>) : (int)sizeof(TileLds<4096>);
+}
 
 // finalize results read back by the host
 struct FinalOut {

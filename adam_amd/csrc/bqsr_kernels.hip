@@ -126,15 +126,18 @@ __device__ int refpos_to_offset(const uint32_t* cig, int ncig, int64_t unclipped
   return -1;
 }
 
-// set bits [lo, hi) of a read-private bitmap in global memory (single
-// writer): word i holds offsets 32i..32i+31 at bit `half` (0 masked, 32 mismatch)
-__device__ void set_bits(uint64_t* w, int lo, int hi, int half) {
+// set bits [lo, hi) (absolute base slots) of the batch's slot bitmap: word i
+// holds slots 32i..32i+31 at bit `half` (0 masked, 32 mismatch).  Two reads
+// can share a word, hence the atomics (few per read: most reads have no
+// masked base and a handful of mismatches).
+__device__ void set_sbits(uint64_t* sb, uint64_t lo, uint64_t hi, int half) {
   while (lo < hi) {
-    const int i = lo >> 5, b = lo & 31;
-    const int n = min(32 - b, hi - lo);
+    const uint64_t i = lo >> 5;
+    const int b = (int)(lo & 31);
+    const int n = (int)min((uint64_t)(32 - b), hi - lo);
     const uint32_t m = (n == 32) ? 0xFFFFFFFFu : (((1u << n) - 1u) << b);
-    w[i] |= (uint64_t)m << half;
-    lo += n;
+    atomicOr((unsigned long long*)&sb[i], (unsigned long long)m << half);
+    lo += (uint64_t)n;
   }
 }
 
@@ -266,8 +269,8 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
   if (!usable) return;
 
   // ---- masked / mismatch bits over [st, en) ----
-  uint64_t* bw = P.bits + (int64_t)r * P.W;
-  for (int i = 0; i < P.W; ++i) bw[i] = 0;
+  uint64_t* bw = P.sbits;
+  const uint64_t rs = m.slot;
   {
     int ro = 0;
     int64_t pos = unclipped;
@@ -280,14 +283,14 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
           int64_t w0 = (int64_t)ro + (start - pos), w1 = (int64_t)ro + (ref_end - pos);
           int a0 = (int)min(max(w0, (int64_t)lo), (int64_t)hi);
           int a1 = (int)min(max(w1, (int64_t)lo), (int64_t)hi);
-          set_bits(bw, lo, a0, 0);
-          set_bits(bw, max(a1, a0), hi, 0);
+          set_sbits(bw, rs + (uint64_t)(lo), rs + (uint64_t)(a0), 0);
+          set_sbits(bw, rs + (uint64_t)(max(a1, a0)), rs + (uint64_t)(hi), 0);
         }
         ro += len;
         pos += len;
       } else if (op == BQSR_CIGAR_I) {  // insertion: refPos None
         int lo = max(ro, st), hi = min(ro + (int)len, en);
-        set_bits(bw, lo, max(lo, hi), 0);
+        set_sbits(bw, rs + (uint64_t)(lo), rs + (uint64_t)(max(lo, hi)), 0);
         ro += len;
       } else if (op != BQSR_CIGAR_H) {
         pos += len;
@@ -300,7 +303,7 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
     int64_t p = start + prel;
     if (p >= ref_end) return;
     int o = refpos_to_offset(cig, ncig, unclipped, p);
-    if (o >= st && o < en) set_bits(bw, o, o + 1, 32);
+    if (o >= st && o < en) set_sbits(bw, rs + (uint64_t)(o), rs + (uint64_t)(o + 1), 32);
   });
   // positions past the MD span but before `end` are not matches either
   if (start + md_total < ref_end) {
@@ -313,7 +316,7 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
         int64_t p0 = max(pos, t0), p1 = min(pos + (int64_t)len, ref_end);
         if (p0 < p1) {
           int lo = max(ro + (int)(p0 - pos), st), hi = min(ro + (int)(p1 - pos), en);
-          if (lo < hi) set_bits(bw, lo, hi, 32);
+          if (lo < hi) set_sbits(bw, rs + (uint64_t)(lo), rs + (uint64_t)(hi), 32);
         }
         ro += len;
         pos += len;
@@ -343,7 +346,7 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
       while (j < ns && sp[j] < lo_p) ++j;
       for (; j < ns && sp[j] < hi_p; ++j) {
         int o = refpos_to_offset(cig, ncig, unclipped, sp[j]);
-        if (o >= st && o < en) set_bits(bw, o, o + 1, 0);
+        if (o >= st && o < en) set_sbits(bw, rs + (uint64_t)(o), rs + (uint64_t)(o + 1), 0);
       }
     }
   }
@@ -354,12 +357,7 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_prep_kernel(PrepParams P)
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += stride) prep_one(P, r);
 }
 
-// ----------------------------------------------------------- tile setup ----
-
-__device__ __forceinline__ uint32_t base_code(const uint8_t* bases, uint64_t slot) {
-  const uint8_t b = bases[slot >> 1];
-  return (slot & 1) ? (b >> 4) : (b & 0xF);
-}
+// ----------------------------------------------------------- tile staging --
 
 // BaseContext.encode of the (previous, current) base codes
 // (StandardCovariate.scala:84-90); reverse-strand reads see complements,
@@ -371,11 +369,8 @@ __device__ __forceinline__ int ctx_code(uint32_t ca, uint32_t cb, bool neg) {
   return (ca == kCodeN || cb == kCodeN) ? 0 : 1 + 4 * ia + ib;
 }
 
-// 4-bit code of tile-relative slot s (the tile's bases start at nibble bsh of bt[0])
-__device__ __forceinline__ uint32_t tile_code(const uint8_t* bt, int bsh, int s) {
-  const int n = s + bsh;
-  return (bt[n >> 1] >> ((n & 1) << 2)) & 0xFu;
-}
+// 4-bit code at nibble n of the staged codes
+__device__ __forceinline__ uint32_t lds_code(const uint8_t* c, int n) { return (c[n >> 1] >> ((n & 1) << 2)) & 0xFu; }
 
 constexpr int kUnroll = 4;
 
@@ -387,38 +382,120 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 struct Tile {
   int64_t r0;
   int nr;
   uint64_t ts0;  // absolute slot of the tile start
   int nslots;
+  int qoff;      // byte offset of slot 0 in the staged quals
+  int cnib;      // nibble offset of slot 0 in the staged codes
+  int boff;      // bit offset of slot 0 in the staged bitmap words
 };
 
-// Load the tile's reads into the wave's LDS state (see WaveTile).
-__device__ Tile setup_tile(const ReadsDev& rd, const ReadInfo* info, int64_t t, WaveTile& T, int lane, int L,
-                           ReadMeta& m, ReadInfo& inf) {
+// first base slot of tile t (every lane loads it; used once it has landed)
+__device__ __forceinline__ uint64_t tile_first_slot(const ReadsDev& rd, int64_t t) {
+  return rd.meta[t * (int64_t)rd.reads_per_tile].slot;
+}
+
+template <int TS>
+struct TileRegs {
+  ReadMeta m;
+  ReadInfo inf;
+  uint4 q[TileCfg<TS>::nQ];
+  uint4 c[TileCfg<TS>::nC];
+  uint64_t b[TileCfg<TS>::nB];
+};
+
+// Issue the global loads of tile t (first slot ts0) into registers; nothing
+// waits on them until tile_install, one tile later, so their latency hides
+// behind the current tile's LDS-only loop.  Chunks are 16-B aligned and each
+// holds at least one byte of its column, so no load leaves an allocation.
+template <int TS, bool kBits>
+__device__ __forceinline__ void tile_issue(const ReadsDev& rd, const ReadInfo* info, const uint64_t* sbits, int64_t t,
+                                           uint64_t ts0, int lane, TileRegs<TS>& R) {
+  using G = TileCfg<TS>;
+  const int64_t r0 = t * (int64_t)rd.reads_per_tile;
+  const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
+  R.m = ReadMeta{0, 0, 0, 0, 0};
+  R.inf = ReadInfo{0, 0, 0, 0};
+  if (lane < nr) {
+    R.m = rd.meta[r0 + lane];
+    R.inf = info[r0 + lane];
+  }
+  const bool any = rd.n_slots > 0;
+  const uintptr_t qa = (uintptr_t)(rd.qual + ts0) & ~(uintptr_t)15;
+  const uintptr_t qlast = (uintptr_t)rd.qual + (uintptr_t)(rd.n_slots - 1);
+#pragma unroll
+  for (int i = 0; i < G::nQ; ++i) {
+    const int k = lane + 64 * i;
+    const uintptr_t a = qa + 16 * (uintptr_t)k;
+    R.q[i] = (any && k < G::kQC && a <= qlast) ? *(const uint4*)a : make_uint4(0, 0, 0, 0);
+  }
+  const uintptr_t ca = (uintptr_t)(rd.bases + (ts0 >> 1)) & ~(uintptr_t)15;
+  const uintptr_t clast = (uintptr_t)rd.bases + (uintptr_t)((rd.n_slots - 1) >> 1);
+#pragma unroll
+  for (int i = 0; i < G::nC; ++i) {
+    const int k = lane + 64 * i;
+    const uintptr_t a = ca + 16 * (uintptr_t)k;
+    R.c[i] = (any && k < G::kCC && a <= clast) ? *(const uint4*)a : make_uint4(0, 0, 0, 0);
+  }
+  if (kBits) {
+    const int64_t wb = (int64_t)(ts0 >> 5);
+#pragma unroll
+    for (int i = 0; i < G::nB; ++i) {
+      const int k = lane + 64 * i;
+      R.b[i] = (k < G::kBW && (wb + k) * 32 < rd.n_slots) ? sbits[wb + k] : 0ull;
+    }
+  }
+}
+
+// Move a prefetched tile into the wave's LDS state (see TileLds).
+template <int TS, bool kBits>
+__device__ Tile tile_install(const ReadsDev& rd, int64_t t, uint64_t ts0, TileLds<TS>& T, const TileRegs<TS>& R,
+                             int lane, int L) {
+  using G = TileCfg<TS>;
   Tile ti;
   ti.r0 = t * (int64_t)rd.reads_per_tile;
   ti.nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - ti.r0);
-  m = ReadMeta{0, 0, 0, 0, 0};
-  inf = ReadInfo{0, 0, 0, 0};
-  if (lane < ti.nr) {
-    m = rd.meta[ti.r0 + lane];
-    inf = info[ti.r0 + lane];
-  }
-  ti.ts0 = __shfl(m.slot, 0);
+  ti.ts0 = ts0;
+  const ReadMeta& m = R.m;
+  const ReadInfo& inf = R.inf;
   const uint32_t len = max(m.lq, m.ls);
   const uint64_t last_end = __shfl(m.slot + len, ti.nr - 1);
-  ti.nslots = (int)(last_end - ti.ts0);
-  for (int i = lane; i < kTileSlots / 32; i += 64) T.sb[i] = 0;
-  for (int i = lane; i < kQBins; i += 64) T.hist[i] = 0;
+  ti.nslots = (int)(last_end - ts0);
+  ti.qoff = (int)((uintptr_t)(rd.qual + ts0) & 15);
+  ti.cnib = 2 * (int)((uintptr_t)(rd.bases + (ts0 >> 1)) & 15) + (int)(ts0 & 1);
+  ti.boff = (int)(ts0 & 31);
+#pragma unroll
+  for (int i = 0; i < G::nQ; ++i)
+    if (lane + 64 * i < G::kQC) T.q[lane + 64 * i] = R.q[i];
+#pragma unroll
+  for (int i = 0; i < G::nC; ++i)
+    if (lane + 64 * i < G::kCC) T.c[lane + 64 * i] = R.c[i];
+  if (kBits) {
+#pragma unroll
+    for (int i = 0; i < G::nB; ++i)
+      if (lane + 64 * i < G::kBW) T.bits[lane + 64 * i] = R.b[i];
+  }
+  for (int i = lane; i < G::kSb; i += 64) T.sbp[i].x = 0;
   // compact list of the reads that own slots
   const bool own = lane < ti.nr && len > 0;
   const unsigned long long bal = __ballot(own);
   const int c = __popcll(bal & ((1ull << lane) - 1ull));
   wave_sync();
   if (own) {
-    const int rs = (int)(m.slot - ti.ts0);
+    const int rs = (int)(m.slot - ts0);
     // DiscreteCycle (StandardCovariate.scala:39-48) as a linear function of the
     // slot: cell = cyc + L, cyc = neg ? ls - o : o + 1, negated for second of pair
     const bool neg = inf.fl & kInfoNeg, sec = inf.fl & kInfoSecond;
@@ -436,91 +513,115 @@ __device__ Tile setup_tile(const ReadsDev& rd, const ReadInfo* info, int64_t t, 
     const uint32_t cm = (uint32_t)(2 * rs + (int)inf.en + (int)inf.st);  // reverse-strand context mirror
     T.rec[c] = make_uint4(st | (en << 16), fl | ((uint32_t)(cb & 0xFFFF) << 16), (uint32_t)rs | ((cm & 0xFFFF) << 16),
                           (uint32_t)m.rg | ((uint32_t)lane << 16));
-    atomicOr(&T.sb[rs >> 5], 1u << (rs & 31));
+    atomicOr(&T.sbp[rs >> 5].x, 1u << (rs & 31));
   }
   wave_sync();
-  // popcount prefix of the start bitmap, two words per lane
-  const uint32_t c0 = __popc(T.sb[2 * lane]), c1 = __popc(T.sb[2 * lane + 1]);
-  const int incl = wave_incl_scan((int)(c0 + c1), lane);
-  T.pre[2 * lane] = (uint16_t)(incl - (int)(c0 + c1));
-  T.pre[2 * lane + 1] = (uint16_t)(incl - (int)c1);
+  // popcount prefix of the start bitmap
+  constexpr int wpl = G::kSb >= 64 ? G::kSb / 64 : 1;
+  uint32_t cnt[wpl];
+  int tot = 0;
+#pragma unroll
+  for (int j = 0; j < wpl; ++j) {
+    const int w = lane * wpl + j;
+    cnt[j] = w < G::kSb ? __popc(T.sbp[w].x) : 0u;
+    tot += (int)cnt[j];
+  }
+  int run = wave_incl_scan(tot, lane) - tot;
+#pragma unroll
+  for (int j = 0; j < wpl; ++j) {
+    const int w = lane * wpl + j;
+    if (w < G::kSb) T.sbp[w].y = (uint32_t)run;
+    run += (int)cnt[j];
+  }
   wave_sync();
   return ti;
 }
 
-__device__ __forceinline__ int compact_of(const WaveTile& T, int s) {
-  const int w = s >> 5;
-  return (int)T.pre[w] + __popc(T.sb[w] & (0xFFFFFFFFu >> (31 - (s & 31)))) - 1;
+template <int TS>
+__device__ __forceinline__ int compact_of(const TileLds<TS>& T, int s) {
+  const uint2 v = T.sbp[s >> 5];
+  return (int)v.y + __popc(v.x & (0xFFFFFFFFu >> (31 - (s & 31)))) - 1;
 }
 
 // ------------------------------------------------------------ observe ------
 
 // LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32]
-//      [block hist 128 u32][tile counter] [WaveTile x 16]
-extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
+//      [block hist 128 u32] [TileLds<TS> x 16]
+// Each wave walks tiles tb0 + wave, tb0 + wave + 16, ... of the block's range,
+// loading tile k+1 while it counts tile k.  The window holds the block's
+// counts for rows (rg_lo, q_lo..q_lo+qw-1); other keys go straight to the
+// int64 table.  The block's window is written to `part` and summed into the
+// table by bqsr_window_reduce.
+template <int TS>
+__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
   uint32_t* w_obs = (uint32_t*)smem;
   uint32_t* w_mm = w_obs + qw * cells;
   uint32_t* w_masked = w_mm + qw * cells;
   uint32_t* blk_hist = w_masked + qw;
-  uint32_t* blk_next = blk_hist + kQBins;
-  const uintptr_t tile_off = ((uintptr_t)(blk_next + 4) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
-  WaveTile* tiles = (WaveTile*)(smem + tile_off);
+  const uintptr_t tile_off = ((uintptr_t)(blk_hist + kQBins) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
+  TileLds<TS>* tiles = (TileLds<TS>*)(smem + tile_off);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int i = tid; i < 2 * qw * cells + qw; i += blockDim.x) w_obs[i] = 0;
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
   const int64_t nt = P.rd.n_tiles;
   const int64_t tb0 = nt * blockIdx.x / P.n_blocks, tb1 = nt * (blockIdx.x + 1) / P.n_blocks;
-  if (tid == 0) blk_next[0] = 0;
   __syncthreads();
 
-  WaveTile& T = tiles[wave];
+  TileLds<TS>& T = tiles[wave];
   const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
-  for (;;) {
-    uint32_t tix = 0;
-    if (lane == 0) tix = atomicAdd(&blk_next[0], 1u);
-    const int64_t t = tb0 + __shfl(tix, 0);
-    if (t >= tb1) break;
-    ReadMeta m;
-    ReadInfo inf;
-    const Tile ti = setup_tile(P.rd, P.info, t, T, lane, L, m, inf);
-    // uniform per-tile bases: per-base addresses are 32-bit offsets
-    const uint8_t* qt = P.rd.qual + ti.ts0;
-    const uint8_t* bt = P.rd.bases + (ti.ts0 >> 1);
-    const int bsh = (int)(ti.ts0 & 1);
-    const uint64_t* bits_t = P.bits + ti.r0 * P.W;
-    const int W = P.W;
-    // four slots per lane per step: the loads of all four issue before any use
+  int64_t t = tb0 + wave;
+  TileRegs<TS> R;
+  uint64_t ts_cur = 0, ts_nxt = 0;
+  if (t < tb1) ts_cur = tile_first_slot(P.rd, t);
+  if (t + kWaves < tb1) ts_nxt = tile_first_slot(P.rd, t + kWaves);
+  ts_cur = rfl64(ts_cur);
+  if (t < tb1) tile_issue<TS, true>(P.rd, P.info, P.sbits, t, ts_cur, lane, R);
+  for (; t < tb1; t += kWaves) {
+    const Tile ti = tile_install<TS, true>(P.rd, t, ts_cur, T, R, lane, L);
+    {  // prefetch the wave's next tile and the first slot of the one after
+      const int64_t t1 = t + kWaves, t2 = t + 2 * kWaves;
+      const uint64_t ts1 = rfl64(ts_nxt);
+      uint64_t ts2 = 0;
+      if (t2 < tb1) ts2 = tile_first_slot(P.rd, t2);
+      if (t1 < tb1) tile_issue<TS, true>(P.rd, P.info, P.sbits, t1, ts1, lane, R);
+      ts_cur = ts1;
+      ts_nxt = ts2;
+    }
+    const uint8_t* lq = (const uint8_t*)T.q + ti.qoff;
+    const uint8_t* lc = (const uint8_t*)T.c;
+    const int cnib = ti.cnib, boff = ti.boff;
+    // four slots per lane per step: the LDS loads of all four issue before any use
     for (int s0 = lane; s0 < ti.nslots; s0 += 64 * kUnroll) {
       int sv[kUnroll], qv[kUnroll];
       uint4 rc[kUnroll];
+      uint64_t bw[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         sv[u] = s0 + 64 * u;
         const int sc = sv[u] < ti.nslots ? sv[u] : 0;
-        qv[u] = (int)(int8_t)qt[sc];
+        qv[u] = (int)(int8_t)lq[sc];
         rc[u] = T.rec[compact_of(T, sc)];
+        bw[u] = T.bits[(boff + sc) >> 5];
       }
       int ov[kUnroll];
       bool act[kUnroll];
-      uint64_t bw[kUnroll];
       uint32_t ca[kUnroll], cbv[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
         ov[u] = sv[u] - (int)(rc[u].z & 0xFFFF);
         act[u] = sv[u] < ti.nslots && (fl & (kInfoObs | kInfoObsCheck)) && ov[u] >= st && ov[u] < en;
-        const bool full = act[u] && (fl & kInfoObs);
-        bw[u] = full ? bits_t[(int)(rc[u].w >> 16) * W + (ov[u] >> 5)] : 0ull;
         // BaseContext(2) operands (StandardCovariate.scala:59-90): codes at s-1, s;
         // the reverse strand reads them mirrored within [st, en) (quirk Q9)
         const bool neg = fl & kInfoNeg;
         const int na = neg ? (int)(rc[u].z >> 16) - sv[u] : sv[u] - 1;
-        const bool ctxon = full && ov[u] != st;
-        ca[u] = ctxon ? tile_code(bt, bsh, na) : 0u;
-        cbv[u] = ctxon ? tile_code(bt, bsh, neg ? na - 1 : sv[u]) : 0u;
+        const bool ctxon = act[u] && (fl & kInfoObs) && ov[u] != st;
+        ca[u] = ctxon ? lds_code(lc, cnib + na) : 0u;
+        cbv[u] = ctxon ? lds_code(lc, cnib + (neg ? na - 1 : sv[u])) : 0u;
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
@@ -532,13 +633,13 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
           continue;
         }
         if (!(fl & kInfoObs)) continue;
-        const bool masked = (bw[u] >> (o & 31)) & 1u;
-        const bool mism = (bw[u] >> (32 + (o & 31))) & 1u;
+        const int bit = (boff + sv[u]) & 31;
+        const bool masked = (bw[u] >> bit) & 1u;
+        const bool mism = (bw[u] >> (32 + bit)) & 1u;
         const int cb = (int)(int16_t)(rc[u].y >> 16);
         const int ccell = (fl & kInfoCycNeg) ? cb - sv[u] : cb + sv[u];  // cycle + L
         const int st = (int)(rc[u].x & 0xFFFF);
         const int xcell = C + 4 + ((o == st) ? 0 : ctx_code(ca[u], cbv[u], fl & kInfoNeg));
-        atomicAdd(&T.hist[q], 1u);
         const int rg = (int)(rc[u].w & 0xFFFF);
         const int slot = q - q_lo;
         if (rg == rg_lo && (unsigned)slot < (unsigned)qw) {
@@ -550,6 +651,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
             atomicAdd(&w_mm[base + xcell], 1u);
           }
         } else {  // outside the LDS window: straight to the int64 table
+          atomicAdd(&blk_hist[q], 1u);
           const int64_t key = (int64_t)q + (int64_t)kMaxQ * rg;
           atomicAdd((unsigned long long*)&P.touched[key], 1ull);
           if (!masked) {
@@ -564,32 +666,47 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
       }
     }
     wave_sync();
-    // per-tile histogram of folded quals (input of the exact expectedMismatch fold)
-    for (int k = lane; k < kQBins; k += 64) {
-      const uint32_t h = T.hist[k];
-      P.h2[t * kQBins + k] = (uint16_t)h;
-      if (h) atomicAdd(&blk_hist[k], h);
-    }
-    wave_sync();
   }
   __syncthreads();
-  // ---- flush the window (int64 atomics) ----
-  const int64_t key0 = (int64_t)q_lo + (int64_t)kMaxQ * rg_lo;
-  for (int i = tid; i < qw * cells; i += blockDim.x) {
-    const int slot = i / cells, cell = i - slot * cells;
-    if (key0 + slot >= P.g.K) continue;
-    const uint32_t o = w_obs[i], mmv = w_mm[i];
-    const int64_t gi = (key0 + slot) * cells + cell;
-    if (o) atomicAdd((unsigned long long*)&P.obs[gi], (unsigned long long)o);
-    if (mmv) atomicAdd((unsigned long long*)&P.mm[gi], (unsigned long long)mmv);
+  // ---- the block's window -> part; window rows into the block histogram ----
+  uint32_t* pb = P.part + (int64_t)blockIdx.x * P.part_stride;
+  for (int i = tid; i < 2 * qw * cells; i += blockDim.x) pb[i] = w_obs[i];
+  for (int slot = wave; slot < qw; slot += kWaves) {
+    uint32_t v = 0;
+    for (int c = lane; c < C; c += 64) v += w_obs[slot * cells + c];  // every unmasked base hits one cycle cell
+    v = wave_sum(v);
+    if (lane == 0) {
+      const uint32_t tot = v + w_masked[slot];
+      pb[2 * qw * cells + slot] = tot;
+      if (tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+    }
   }
-  for (int slot = tid; slot < qw; slot += blockDim.x) {
-    if (key0 + slot >= P.g.K) continue;
-    uint64_t tot = w_masked[slot];
-    for (int c = 0; c < C; ++c) tot += w_obs[slot * cells + c];  // every unmasked base hits one cycle cell
-    if (tot) atomicAdd((unsigned long long*)&P.touched[key0 + slot], (unsigned long long)tot);
-  }
+  __syncthreads();
   for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
+}
+
+// Sum the blocks' window counts into the int64 table (one thread per window
+// cell; the observe kernel's direct atomics have all landed by now).
+extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, int32_t n_blocks, int32_t stride, Window w,
+                                              TableGeom g, int64_t* touched, int64_t* obs, int64_t* mm) {
+  const int64_t key0 = (int64_t)w.q_lo + (int64_t)kMaxQ * w.rg_lo;
+  const int nc = w.qw * g.cells;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += gridDim.x * blockDim.x) {
+    uint64_t s = 0;
+    for (int b = 0; b < n_blocks; ++b) s += part[(int64_t)b * stride + i];
+    if (!s) continue;
+    if (i < 2 * nc) {
+      const int j = i < nc ? i : i - nc;
+      const int slot = j / g.cells, cell = j - slot * g.cells;
+      if (key0 + slot >= g.K) continue;
+      int64_t* dst = i < nc ? obs : mm;
+      dst[(key0 + slot) * g.cells + cell] += (int64_t)s;
+    } else {
+      const int slot = i - 2 * nc;
+      if (key0 + slot >= g.K) continue;
+      touched[key0 + slot] += (int64_t)s;
+    }
+  }
 }
 
 // ------------------------------------------------------ expectedMismatch --
@@ -606,6 +723,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(
 // does.  One workgroup of 1024 threads.
 
 constexpr int kFoldThreads = 1024;
+constexpr double kFoldSeqLimit = 2.0;
 constexpr int kFoldWaves = kFoldThreads / 64;
 
 struct FoldShared {
@@ -854,7 +972,7 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
   // Binade mode starts at S >= 2: every q >= 1 has t < 1 <= S/2 there.  Ties
   // are still detected and added one by one; this is only where the fast
   // path takes over from the plain sequential fold.
-  const double seq_limit = 2.0;
+  const double seq_limit = kFoldSeqLimit;
   const int64_t nt = P.rd.n_tiles;
   for (int64_t b = 0; b < P.n_blocks; ++b) {
     if (F.S >= seq_limit) {
@@ -863,6 +981,12 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
     }
     // block b leaves the binade somewhere (or S is still small): tile level
     const int64_t c0 = nt * b / P.n_blocks, c1 = nt * (b + 1) / P.n_blocks;
+    if (!P.cand[b]) {
+      // bqsr_fold_plan's bound said no event here, so it built no tile
+      // histograms for this block: fold every tile exactly (correct, slow)
+      for (int64_t t = c0; t < c1; ++t) fold_tile_exact(P.rd, P.info, t, F, tid, seq_limit);
+      continue;
+    }
     int64_t t = c0;
     while (t < c1) {
       if (F.S >= seq_limit) {
@@ -875,6 +999,127 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
   }
   __syncthreads();
   if (tid == 0) P.em_out[0] = F.S;
+}
+
+// Which blocks may hold a fold event (a binade crossing, a rounding tie, or
+// the sequential start S < kFoldSeqLimit)?  The exact fold S_k stays within a
+// relative k * 2^-53 of the real sum R_k of the increments (every rounding
+// error is at most half an ulp of a partial sum <= S_k), so a block whose
+// real-sum span [R_b, R_b+1], widened by delta = (N + 64) * 2^-52, lies inside
+// one binade at or above kFoldSeqLimit and has no tie there holds no event.
+// Only candidate blocks get per-tile histograms (bqsr_tile_hist).
+extern "C" __global__ void __launch_bounds__(256) bqsr_fold_plan(const uint32_t* hq_block, const double* pow10,
+                                                                   int32_t n_blocks, uint8_t* cand, int32_t* cand_list,
+                                                                   int32_t* n_cand) {
+  __shared__ double t[kQBins];
+  __shared__ double bsum[kMaxFoldBlocks + 1];
+  __shared__ uint64_t bcnt[kMaxFoldBlocks];
+  __shared__ double delta;
+  __shared__ int32_t nc;
+  const int tid = threadIdx.x;
+  for (int q = tid; q < kQBins; q += blockDim.x) t[q] = pow10[q];
+  if (tid == 0) nc = 0;
+  __syncthreads();
+  for (int b = tid; b < n_blocks; b += blockDim.x) {
+    double v = 0.0;
+    uint64_t n = 0;
+    for (int q = 0; q < kQBins; ++q) {
+      const uint32_t h = hq_block[(int64_t)b * kQBins + q];
+      v += (double)h * t[q];
+      n += h;
+    }
+    bsum[b + 1] = v;
+    bcnt[b] = n;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    bsum[0] = 0.0;
+    uint64_t n = 0;
+    for (int b = 0; b < n_blocks; ++b) {
+      bsum[b + 1] += bsum[b];
+      n += bcnt[b];
+    }
+    delta = ((double)n + 64.0) * 0x1p-52 + 1e-12;
+  }
+  __syncthreads();
+  for (int b = tid; b < n_blocks; b += blockDim.x) {
+    bool c = false;
+    if (bcnt[b]) {
+      const double lo = bsum[b] * (1.0 - delta), hi = bsum[b + 1] * (1.0 + delta);
+      if (lo < kFoldSeqLimit * (1.0 + delta) || ilogb(lo) != ilogb(hi)) {
+        c = true;
+      } else {
+        const int e = ilogb(lo);
+        for (int q = 0; q < kQBins && !c; ++q) {
+          if (!hq_block[(int64_t)b * kQBins + q]) continue;
+          const double x = ldexp(t[q], 52 - e);
+          c = (x - floor(x)) == 0.5;
+        }
+      }
+    }
+    cand[b] = c;
+    if (c) cand_list[atomicAdd(&nc, 1)] = b;
+  }
+  __syncthreads();
+  if (tid == 0) *n_cand = nc;
+}
+
+// Per-tile qual histograms of the folded bases of the candidate blocks' tiles
+// (one wavefront per tile: the folded ranges of the tile's reads become an LDS
+// slot bitmap, then every slot's qual is counted if its bit is set).
+extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, const ReadInfo* info,
+                                                                   const int32_t* cand_list, const int32_t* n_cand,
+                                                                   int32_t n_blocks, int64_t max_tpb, uint16_t* h2) {
+  __shared__ uint32_t hist[4][kQBins];
+  __shared__ uint32_t bm[4][kTileSlots / 32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nt = rd.n_tiles;
+  const int64_t total = (int64_t)(*n_cand) * max_tpb;
+  for (int64_t v = (int64_t)blockIdx.x * 4 + wv; v < total; v += (int64_t)gridDim.x * 4) {
+    const int64_t b = cand_list[v / max_tpb];
+    const int64_t t = nt * b / n_blocks + v % max_tpb;
+    if (t >= nt * (b + 1) / n_blocks) continue;
+    const int64_t r0 = t * (int64_t)rd.reads_per_tile;
+    const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
+    ReadMeta m{0, 0, 0, 0, 0};
+    ReadInfo inf{0, 0, 0, 0};
+    if (lane < nr) {
+      m = rd.meta[r0 + lane];
+      inf = info[r0 + lane];
+    }
+    const uint64_t ts0 = __shfl(m.slot, 0);
+    const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
+    for (int q = lane; q < kQBins; q += 64) hist[wv][q] = 0;
+    for (int i = lane; i < kTileSlots / 32; i += 64) bm[wv][i] = 0;
+    wave_sync();
+    if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
+      int lo = (int)(m.slot - ts0) + inf.st;
+      const int hi = (int)(m.slot - ts0) + inf.en;
+      while (lo < hi) {
+        const int n = min(32 - (lo & 31), hi - lo);
+        atomicOr(&bm[wv][lo >> 5], (n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (lo & 31));
+        lo += n;
+      }
+    }
+    wave_sync();
+    const uint8_t* qt = rd.qual + ts0;
+    for (int s0 = lane; s0 < nslots; s0 += 64 * kUnroll) {
+      int qv[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int s = s0 + 64 * u;
+        qv[u] = s < nslots ? (int)(int8_t)qt[s] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int s = s0 + 64 * u;
+        if (qv[u] >= 0 && ((bm[wv][s >> 5] >> (s & 31)) & 1u)) atomicAdd(&hist[wv][qv[u]], 1u);
+      }
+    }
+    wave_sync();
+    for (int q = lane; q < kQBins; q += 64) h2[t * kQBins + q] = (uint16_t)hist[wv][q];
+    wave_sync();
+  }
 }
 
 // -------------------------------------------------------------- finalize ----
@@ -1032,8 +1277,11 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
 }
 
 // LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16]
-//      [window ok qw u8][tile counter] [WaveTile x 16]
-extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
+//      [window ok qw u8] [TileLds<TS> x 16]
+// Tiles are staged and prefetched as in observe; the recalibrated chars are
+// written over the staged quals in LDS and leave as whole 16-B chunks.
+template <int TS>
+__global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
   double* w_s1 = (double*)smem;
@@ -1041,11 +1289,11 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
   double* l_qbt = w_d2 + qw * kCtxSlots;
   int16_t* l_qbq = (int16_t*)(l_qbt + kQbN);
   uint8_t* w_ok = (uint8_t*)(l_qbq + kQbN);
-  uint32_t* blk_next = (uint32_t*)(w_ok + ((qw + 15) & ~15));
-  const uintptr_t tile_off = ((uintptr_t)(blk_next + 4) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
-  WaveTile* tiles = (WaveTile*)(smem + tile_off);
+  const uintptr_t tile_off = ((uintptr_t)(w_ok + ((qw + 15) & ~15)) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
+  TileLds<TS>* tiles = (TileLds<TS>*)(smem + tile_off);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
   const bool win_ok = rg_lo < P.n_rg;
   const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
@@ -1064,33 +1312,43 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
   for (int i = tid; i < qw; i += blockDim.x) w_ok[i] = (win_ok && q_lo + i < kQBins) ? P.rq_ok[rq0 + i] : 0;
   const int64_t nt = P.rd.n_tiles;
   const int64_t tb0 = nt * blockIdx.x / gridDim.x, tb1 = nt * (blockIdx.x + 1) / gridDim.x;
-  if (tid == 0) blk_next[0] = 0;
+  // the output column starts at the same 16-B phase as the quals: chunk copies
+  const bool same_phase = (((uintptr_t)P.out_qual ^ (uintptr_t)P.rd.qual) & 15) == 0;
   __syncthreads();
 
-  WaveTile& T = tiles[wave];
-  for (;;) {
-    uint32_t tix = 0;
-    if (lane == 0) tix = atomicAdd(&blk_next[0], 1u);
-    const int64_t t = tb0 + __shfl(tix, 0);
-    if (t >= tb1) break;
-    ReadMeta m;
-    ReadInfo inf;
-    const Tile ti = setup_tile(P.rd, P.info, t, T, lane, L, m, inf);
+  TileLds<TS>& T = tiles[wave];
+  int64_t t = tb0 + wave;
+  TileRegs<TS> R;
+  uint64_t ts_cur = 0, ts_nxt = 0;
+  if (t < tb1) ts_cur = tile_first_slot(P.rd, t);
+  if (t + kWaves < tb1) ts_nxt = tile_first_slot(P.rd, t + kWaves);
+  ts_cur = rfl64(ts_cur);
+  if (t < tb1) tile_issue<TS, false>(P.rd, P.info, nullptr, t, ts_cur, lane, R);
+  for (; t < tb1; t += kWaves) {
+    const Tile ti = tile_install<TS, false>(P.rd, t, ts_cur, T, R, lane, L);
     if (lane < ti.nr) {
       const int64_t r = ti.r0 + lane;
-      if (inf.fl & kInfoPass) {  // quality string passed through
+      if (R.inf.fl & kInfoPass) {  // quality string passed through
         P.out_start[r] = 0;
-        P.out_len[r] = (m.flags & BQSR_F_HAS_QUAL) ? m.lq : 0;
+        P.out_len[r] = (R.m.flags & BQSR_F_HAS_QUAL) ? R.m.lq : 0;
       } else {
-        P.out_start[r] = inf.st;
-        P.out_len[r] = (inf.fl & kInfoApp) ? (uint32_t)(inf.en - inf.st) : 0;
+        P.out_start[r] = R.inf.st;
+        P.out_len[r] = (R.inf.fl & kInfoApp) ? (uint32_t)(R.inf.en - R.inf.st) : 0;
       }
     }
-    const uint8_t* qt = P.rd.qual + ti.ts0;
-    const uint8_t* bt = P.rd.bases + (ti.ts0 >> 1);
-    const int bsh = (int)(ti.ts0 & 1);
-    uint8_t* ot = P.out_qual + ti.ts0;
-    // four slots per lane per step: the loads of all four issue before any use
+    {  // prefetch the wave's next tile and the first slot of the one after
+      const int64_t t1 = t + kWaves, t2 = t + 2 * kWaves;
+      const uint64_t ts1 = rfl64(ts_nxt);
+      uint64_t ts2 = 0;
+      if (t2 < tb1) ts2 = tile_first_slot(P.rd, t2);
+      if (t1 < tb1) tile_issue<TS, false>(P.rd, P.info, nullptr, t1, ts1, lane, R);
+      ts_cur = ts1;
+      ts_nxt = ts2;
+    }
+    uint8_t* lq = (uint8_t*)T.q + ti.qoff;
+    const uint8_t* lc = (const uint8_t*)T.c;
+    const int cnib = ti.cnib;
+    // four slots per lane per step: the LDS loads of all four issue before any use
     for (int s0 = lane; s0 < ti.nslots; s0 += 64 * kUnroll) {
       int sv[kUnroll];
       uint32_t qb[kUnroll];
@@ -1099,7 +1357,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
       for (int u = 0; u < kUnroll; ++u) {
         sv[u] = s0 + 64 * u;
         const int sc = sv[u] < ti.nslots ? sv[u] : 0;
-        qb[u] = qt[sc];
+        qb[u] = lq[sc];
         rc[u] = T.rec[compact_of(T, sc)];
       }
       uint32_t ca[kUnroll], cbv[kUnroll];
@@ -1110,8 +1368,8 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
         const bool ctxon = sv[u] < ti.nslots && (fl & kInfoApp) && o > st && o < en;
         const bool neg = fl & kInfoNeg;
         const int na = neg ? (int)(rc[u].z >> 16) - sv[u] : sv[u] - 1;
-        ca[u] = ctxon ? tile_code(bt, bsh, na) : 0u;
-        cbv[u] = ctxon ? tile_code(bt, bsh, neg ? na - 1 : sv[u]) : 0u;
+        ca[u] = ctxon ? lds_code(lc, cnib + na) : 0u;
+        cbv[u] = ctxon ? lds_code(lc, cnib + (neg ? na - 1 : sv[u])) : 0u;
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
@@ -1159,8 +1417,27 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
             if ((int64_t)k < P.max_exc) P.exc[k] = ((ti.ts0 + (uint64_t)sv[u]) << 16) | code;
           }
         }
-        ot[sv[u]] = (uint8_t)code;
+        lq[sv[u]] = (uint8_t)code;  // in place: slot sv[u] is this lane's alone
       }
+    }
+    wave_sync();
+    // write the tile's slots back: whole chunks inside [0, nslots), bytes at the edges
+    uint8_t* ob = P.out_qual + ti.ts0;
+    if (same_phase) {
+      uint8_t* oa = (uint8_t*)((uintptr_t)ob & ~(uintptr_t)15);
+      const int nch = (ti.qoff + ti.nslots + 15) >> 4;
+      for (int k = lane; k < nch; k += 64) {
+        const int lo = 16 * k - ti.qoff;
+        if (lo >= 0 && lo + 16 <= ti.nslots) {
+          *(uint4*)(oa + 16 * k) = T.q[k];
+        } else {
+          const uint8_t* src = (const uint8_t*)&T.q[k];
+          for (int j = 0; j < 16; ++j)
+            if (lo + j >= 0 && lo + j < ti.nslots) oa[16 * k + j] = src[j];
+        }
+      }
+    } else {
+      for (int s = lane; s < ti.nslots; s += 64) ob[s] = lq[s];
     }
     wave_sync();
   }
@@ -1171,5 +1448,14 @@ extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     acc[i] += part[i];
 }
+
+// one instantiation per tile size
+#define BQSR_TILE_KERNELS(TS)                                                   \
+  template __global__ void bqsr_observe_kernel<TS>(ObserveParams);              \
+  template __global__ void bqsr_apply_kernel<TS>(ApplyParams);
+BQSR_TILE_KERNELS(1024)
+BQSR_TILE_KERNELS(2048)
+BQSR_TILE_KERNELS(4096)
+#undef BQSR_TILE_KERNELS
 
 }  // namespace bqsr

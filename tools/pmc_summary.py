@@ -19,7 +19,7 @@ def load(d):
 
 if __name__ == "__main__":
     out = load(sys.argv[1])
-    keys = [k for k in out if k.startswith("bqsr_")]
+    keys = [k for k in out if "bqsr_" in k]
     for k in keys:
         d = out[k]
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
