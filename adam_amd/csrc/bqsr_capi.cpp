@@ -169,40 +169,19 @@ TableGeom geom(const bqsr_dims& d) {
 }
 
 constexpr size_t kLdsMax = 163840;
-size_t tiles_bytes(int ts) { return (size_t)tile_lds_bytes(ts) * kWaves; }
-size_t observe_lds(int qw, int cells, int ts) {
-  size_t head = (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4;
-  head = (head + 15) & ~(size_t)15;
-  return head + tiles_bytes(ts);
+size_t observe_lds(int qw, int cells) { return (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4; }
+size_t apply_lds(int qw, int C) {
+  return (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2) + (size_t)qw;
 }
-size_t apply_lds(int qw, int C, int ts) {
-  size_t head = (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2) + ((qw + 15) & ~15);
-  head = (head + 15) & ~(size_t)15;
-  return head + tiles_bytes(ts);
-}
-int observe_qw(int cells, int ts) {
+int observe_qw(int cells) {
   int qw = 64;
-  while (qw > 1 && observe_lds(qw, cells, ts) > kLdsMax) --qw;
+  while (qw > 1 && observe_lds(qw, cells) > kLdsMax) --qw;
   return qw;
 }
-int apply_qw(int C, int ts) {
+int apply_qw(int C) {
   int qw = 64;
-  while (qw > 1 && apply_lds(qw, C, ts) > kLdsMax) --qw;
+  while (qw > 1 && apply_lds(qw, C) > kLdsMax) --qw;
   return qw;
-}
-// tile size: the smallest that holds the longest read
-int tile_size(int64_t max_slot_len) { return max_slot_len <= 1024 ? 1024 : max_slot_len <= 2048 ? 2048 : 4096; }
-
-template <int TS>
-void* observe_fn() { return (void*)&bqsr_observe_kernel<TS>; }
-template <int TS>
-void* apply_fn() { return (void*)&bqsr_apply_kernel<TS>; }
-void* observe_kernel_for(int ts) { return ts == 1024 ? observe_fn<1024>() : ts == 2048 ? observe_fn<2048>() : observe_fn<4096>(); }
-void* apply_kernel_for(int ts) { return ts == 1024 ? apply_fn<1024>() : ts == 2048 ? apply_fn<2048>() : apply_fn<4096>(); }
-template <class Params>
-hipError_t launch_tile(void* fn, int blocks, Params& P, size_t lds, hipStream_t s) {
-  void* args[] = {(void*)&P};
-  return hipLaunchKernel(fn, dim3(blocks), dim3(kBlockThreads), args, lds, s);
 }
 
 }  // namespace
@@ -244,7 +223,6 @@ struct bqsr_batch {
   ReadInfo* d_info = nullptr;
   uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
   int64_t sbits_words = 0;
-  int32_t ts = 1024;            // tile size of the per-base passes
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
   // per-call scratch
@@ -336,10 +314,10 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  for (int ts : {1024, 2048, 4096}) {
-    if (e == hipSuccess) e = hipFuncSetAttribute(observe_kernel_for(ts), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
-    if (e == hipSuccess) e = hipFuncSetAttribute(apply_kernel_for(ts), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
-  }
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e != hipSuccess) {
     bqsr_context_destroy(c);
     return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
@@ -437,12 +415,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   if (max_slot_len > kMaxReadLen)
     return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
   const int64_t n = b->rd.n_reads;
-  b->ts = tile_size(max_slot_len);
-  if (const char* e = getenv("ADAM_BQSR_TILE_SLOTS")) {  // tuning knob: a larger tile than needed
-    const int v = atoi(e);
-    if ((v == 1024 || v == 2048 || v == 4096) && v > b->ts) b->ts = v;
-  }
-  b->rd.reads_per_tile = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kMaxTileReads, b->ts / std::max<int64_t>(1, max_slot_len)));
+  b->rd.reads_per_tile = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kMaxTileReads, kTileSlots / std::max<int64_t>(1, max_slot_len)));
   b->rd.n_tiles = (n + b->rd.reads_per_tile - 1) / b->rd.reads_per_tile;
   b->n_blocks = std::min(b->ctx->n_cu, kMaxFoldBlocks);
   bqsr_status st;
@@ -510,8 +483,9 @@ bqsr_status pack(const bqsr_records* R, Packed& P) {
   if (md_tot > 0xFFFFFFFFull || cig_tot > 0xFFFFFFFFull)
     return fail(BQSR_ERR_UNSUPPORTED, "partition MD / CIGAR columns exceed 4 GiB");
   P.n_slots = (int64_t)slot;
-  P.qual.assign(((size_t)slot + 15) / 16 * 16 + 16, 0);
-  P.bases.assign((size_t)slot / 2 + 16, 0);
+  // kColumnPad readable bytes past each column's end: the per-base passes load 16 B at a time
+  P.qual.assign((size_t)slot + kColumnPad, 0);
+  P.bases.assign((size_t)slot / 2 + 1 + kColumnPad, 0);
   P.md.resize(std::max<uint64_t>(md_tot, 1));
   P.cigar.resize(std::max<uint64_t>(cig_tot, 1));
   P.rghist.assign((size_t)P.n_rg, 0);
@@ -798,7 +772,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
-    P.w.qw = observe_qw(P.g.cells, b->ts);
+    P.w.qw = observe_qw(P.g.cells);
     P.w.q_lo = std::min(b->q_lo, kQBins - 1);
     P.w.rg_lo = b->rg_lo;
     P.touched = t->touched();
@@ -820,8 +794,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = observe_lds(P.w.qw, P.g.cells, b->ts);
-    HIP_TRY(launch_tile(observe_kernel_for(b->ts), b->n_blocks, P, lds, s));
+    const size_t lds = observe_lds(P.w.qw, P.g.cells);
+    hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(1024, (P.part_stride + 255) / 256);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb), dim3(256), 0, s, (const uint32_t*)b->d_part, b->n_blocks,
                        P.part_stride, P.w, P.g, P.touched, P.obs, P.mm);
@@ -1094,7 +1069,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.rd = b->rd;
   P.info = b->d_info;
   P.g = geom(L->dims);
-  P.w.qw = apply_qw(P.g.C, b->ts);
+  P.w.qw = apply_qw(P.g.C);
   P.w.q_lo = std::min(b->q_lo, kQBins - 1);
   P.w.rg_lo = b->rg_lo;
   P.n_rg = L->dims.n_rg;
@@ -1116,8 +1091,9 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
-  const size_t lds = apply_lds(P.w.qw, P.g.C, b->ts);
-  HIP_TRY(launch_tile(apply_kernel_for(b->ts), b->n_blocks, P, lds, s));
+  const size_t lds = apply_lds(P.w.qw, P.g.C);
+  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  HIP_TRY(hipGetLastError());
   return ok();
 }
 

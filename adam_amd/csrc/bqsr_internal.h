@@ -60,16 +60,17 @@ constexpr int kMaxQ = 60;      // RecalUtil.Constants.MAX_REASONABLE_QSCORE
 constexpr int kCtxSlots = 21;  // contexts -4..16
 constexpr int kQBins = 128;    // qual values 0..127 (Java byte >= 0)
 
-// Tile geometry of the per-base passes: a tile is `reads_per_tile`
-// consecutive reads (<= 64) whose base slots fit in the batch's tile size TS
-// (1024, 2048 or 4096 slots: the smallest that holds the longest read); one
-// wavefront processes one tile at a time, one base per lane per step.
-constexpr int kTileSlots = 4096;  // largest tile
+// Read tiles: `reads_per_tile` consecutive reads (<= 64) whose base slots fit
+// in kTileSlots.  Tiles are the unit of the expectedMismatch fold (per-tile
+// qual histograms); the per-base passes split the batch into per-workgroup
+// ranges of whole tiles and give each lane one read.
+constexpr int kTileSlots = 4096;
 constexpr int kMaxTileReads = 64;
 constexpr int kMaxFoldBlocks = 1024;  // workgroups of the per-base passes (one per CU)
-constexpr int kWaves = 16;  // waves per block of the per-base passes (1024 threads)
+constexpr int kWaves = 16;  // waves per workgroup of the per-base passes (1024 threads)
 constexpr int kBlockThreads = 64 * kWaves;
 constexpr int kMaxReadLen = 4096;  // longest read the device path takes
+constexpr int kColumnPad = 32;     // readable bytes past the end of the qual / bases columns
 
 // Error reporting: u64 words, atomicMin of
 //   read << 28 | read_offset << 8 | rank << 4 | code
@@ -201,44 +202,6 @@ struct ApplyParams {
   unsigned long long* n_exc;
   unsigned long long* err;
 };
-
-// Per-wave tile state of the per-base passes (LDS), for tiles of TS slots.
-// The tile's quals, 4-bit base codes and slot-bitmap words are staged here as
-// whole 16-B chunks (prefetched into registers while the previous tile runs),
-// so the per-base loop touches only LDS.  Reads of the tile that own at least
-// one slot are listed in slot order ("compact" index c), one 16-B record each
-// (one ds_read_b128), all positions tile-relative slots:
-//   x = st | en << 16       trimmed read offsets (pass-through reads: 0, Lq)
-//   y = fl | cb << 16       cycle cell of slot s = cb + s (kInfoCycNeg: cb - s)
-//   z = rslot | cm << 16    first slot; context operands of slot s are the
-//                           codes at s - 1, s (reverse strand: cm - s, cm - s - 1)
-//   w = rg | rtile << 16    read group, read index within the tile
-//   sbp[k].x = one bit per slot marking compact read starts, .y = popcount
-//   prefix of the start bits before word k: the compact index of slot s is
-//   sbp[s>>5].y + popc(sbp[s>>5].x & ones(s & 31)) - 1.
-template <int TS>
-struct TileCfg {
-  static constexpr int kSb = TS / 32;      // start-bitmap words
-  static constexpr int kQC = TS / 16 + 1;  // 16-B chunks of quals (+1: unaligned start)
-  static constexpr int kCC = TS / 32 + 1;  // 16-B chunks of base codes (2 per byte)
-  static constexpr int kBW = TS / 32 + 2;  // slot-bitmap words (even: keeps 16-B alignment)
-  static constexpr int nQ = (kQC + 63) / 64;  // chunks per lane
-  static constexpr int nC = (kCC + 63) / 64;
-  static constexpr int nB = (kBW + 63) / 64;
-};
-template <int TS>
-struct TileLds {
-  uint4 rec[kMaxTileReads];
-  uint4 q[TileCfg<TS>::kQC];
-  uint4 c[TileCfg<TS>::kCC];
-  uint64_t bits[TileCfg<TS>::kBW];
-  uint2 sbp[TileCfg<TS>::kSb];
-};
-static_assert(sizeof(TileLds<1024>) % 16 == 0 && sizeof(TileLds<2048>) % 16 == 0 && sizeof(TileLds<4096>) % 16 == 0,
-              "TileLds must keep 16-B alignment");
-inline int tile_lds_bytes(int ts) {
-  return ts <= 1024 ? (int)sizeof(TileLds<1024>) : ts <= 2048 ? (int)sizeof(TileLds<2048>) : (int)sizeof(TileLds<4096>);
-}
 
 // finalize results read back by the host
 struct FinalOut {

@@ -357,202 +357,151 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_prep_kernel(PrepParams P)
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += stride) prep_one(P, r);
 }
 
-// ----------------------------------------------------------- tile staging --
+// ------------------------------------------------------- lane-per-read ----
+//
+// The per-base passes give each lane one read: a wavefront takes 64
+// consecutive reads and every lane walks its own read's offsets in chunks of
+// 16, holding the chunk's quals (one 16-B load), its 17 base codes (one 16-B
+// load, reverse-complemented in registers for reverse-strand reads) and its
+// masked / mismatch bits (two 8-B loads) in registers.  Everything that is
+// per read (trimming, strand, cycle direction, read group, window row test)
+// is decoded once per read, so the per-base work is a few bit-field extracts
+// and the table update.  Loads are unaligned 16-B accesses: the columns need
+// 32 B of readable padding past their ends (bqsr_device_reads).
 
-// BaseContext.encode of the (previous, current) base codes
-// (StandardCovariate.scala:84-90); reverse-strand reads see complements,
-// whose ACGT index is 3 - index.  'other' bytes have index -1 (forward only:
-// reverse reads holding them fail in the prep kernel).
-__device__ __forceinline__ int ctx_code(uint32_t ca, uint32_t cb, bool neg) {
-  const int ia = neg ? 3 - (int)ca : (ca < 4 ? (int)ca : -1);
-  const int ib = neg ? 3 - (int)cb : (cb < 4 ? (int)cb : -1);
-  return (ca == kCodeN || cb == kCodeN) ? 0 : 1 + 4 * ia + ib;
-}
-
-// 4-bit code at nibble n of the staged codes
-__device__ __forceinline__ uint32_t lds_code(const uint8_t* c, int n) { return (c[n >> 1] >> ((n & 1) << 2)) & 0xFu; }
-
-constexpr int kUnroll = 4;
-
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-  for (int off = 1; off < 64; off <<= 1) {
-    const int x = __shfl_up(v, off);
-    if (lane >= off) v += x;
-  }
-  return v;
-}
+constexpr int kChunk = 16;
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
 }
 
-__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
+// BaseContext.encode of the (previous, current) base codes
+// (StandardCovariate.scala:84-90) with forward-strand indices: A0 C1 G2 T3,
+// 'other' -1, N -> context 0.  Reverse-strand reads pass their complemented
+// codes (revcomp_window), whose index is then the forward one.
+__device__ __forceinline__ int ctx_code(uint32_t ca, uint32_t cb) {
+  const int ia = ca < 4 ? (int)ca : -1;
+  const int ib = cb < 4 ? (int)cb : -1;
+  return (ca == kCodeN || cb == kCodeN) ? 0 : 1 + 4 * ia + ib;
 }
 
-struct Tile {
-  int64_t r0;
-  int nr;
-  uint64_t ts0;  // absolute slot of the tile start
-  int nslots;
-  int qoff;      // byte offset of slot 0 in the staged quals
-  int cnib;      // nibble offset of slot 0 in the staged codes
-  int boff;      // bit offset of slot 0 in the staged bitmap words
+// 17 base codes from nibble n0 >= 0 of the packed column:
+// nibble k of (lo, hi) = code(n0 + k), k = 0..16.
+__device__ __forceinline__ void load_window(const uint8_t* bases, int64_t n0, uint64_t& lo, uint32_t& hi) {
+  const uint4 v = *(const uint4*)(bases + (n0 >> 1));
+  const uint32_t sh = (uint32_t)(n0 & 1) * 4u;
+  const uint32_t d0 = __builtin_amdgcn_alignbit(v.y, v.x, sh);
+  const uint32_t d1 = __builtin_amdgcn_alignbit(v.z, v.y, sh);
+  const uint32_t d2 = __builtin_amdgcn_alignbit(v.w, v.z, sh);
+  lo = ((uint64_t)d1 << 32) | d0;
+  hi = d2 & 0xFu;
+}
+
+// the same window for the batch's first bases, where n0 < 0 (nibble k of the
+// result = code(n0 + k) for n0 + k >= 0, else 0); rare, byte by byte
+__device__ __forceinline__ void load_window_head(const uint8_t* bases, int64_t n0, int64_t n_slots, uint64_t& lo,
+                                              uint32_t& hi) {
+  lo = 0;
+  hi = 0;
+  for (int k = 0; k <= 16; ++k) {
+    const int64_t n = n0 + k;
+    if (n < 0 || n >= n_slots) continue;
+    const uint64_t c = (bases[n >> 1] >> ((n & 1) * 4)) & 0xFu;
+    if (k < 16) lo |= c << (4 * k); else hi = (uint32_t)c;
+  }
+}
+
+__device__ __forceinline__ uint32_t nibrev32(uint32_t u) {
+  u = __builtin_bswap32(u);
+  return ((u >> 4) & 0x0F0F0F0Fu) | ((u << 4) & 0xF0F0F0F0u);
+}
+
+// reverse strand: R.nib(k) = complement(W.nib(16 - k)), k = 0..16; A<->T, C<->G
+// (index 3 - index), N stays N (BaseContext.simpleReverseComplement).
+__device__ __forceinline__ void revcomp_window(uint64_t& lo, uint32_t& hi) {
+  const uint64_t z = (uint64_t)nibrev32((uint32_t)(lo >> 32)) | ((uint64_t)nibrev32((uint32_t)lo) << 32);
+  uint64_t rlo = (z << 4) | (hi & 0xFu);
+  uint32_t rhi = (uint32_t)(z >> 60);
+  const uint64_t m = (~rlo >> 2) & 0x1111111111111111ull;  // nibbles holding A/C/G/T
+  rlo ^= m | (m << 1);
+  const uint32_t mh = (~rhi >> 2) & 1u;
+  rhi ^= mh | (mh << 1);
+  lo = rlo;
+  hi = rhi;
+}
+
+// codes (previous, current) for chunk slot k
+__device__ __forceinline__ void pair_at(uint64_t lo, uint32_t hi, int k, uint32_t& ca, uint32_t& cb) {
+  ca = (uint32_t)(lo >> (4 * k)) & 0xFu;
+  cb = k < 15 ? (uint32_t)(lo >> (4 * k + 4)) & 0xFu : hi;
+}
+
+// Per-lane read decode shared by observe and apply.
+struct LaneRead {
+  int64_t r;      // read index
+  uint64_t slot;  // first base slot
+  int st, en;     // visited offsets [st, en)
+  int fl;         // kInfo* bits
+  int rg;
+  int lq, ls;
+  int cell0, dir; // cycle cell of offset o = cell0 + dir * o (DiscreteCycle + L)
 };
 
-// first base slot of tile t (every lane loads it; used once it has landed)
-__device__ __forceinline__ uint64_t tile_first_slot(const ReadsDev& rd, int64_t t) {
-  return rd.meta[t * (int64_t)rd.reads_per_tile].slot;
+__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, int64_t r_end, int L) {
+  LaneRead x;
+  x.r = r;
+  ReadMeta m{0, 0, 0, 0, 0};
+  ReadInfo inf{0, 0, 0, 0};
+  if (r < r_end) {
+    m = rd.meta[r];
+    inf = info[r];
+  }
+  x.slot = m.slot;
+  x.fl = inf.fl;
+  x.rg = m.rg;
+  x.lq = m.lq;
+  x.ls = m.ls;
+  const bool pass = inf.fl & kInfoPass;
+  x.st = pass ? 0 : inf.st;
+  x.en = pass ? ((m.flags & BQSR_F_HAS_QUAL) ? m.lq : 0) : inf.en;
+  // DiscreteCycle (StandardCovariate.scala:39-48): cyc = neg ? ls - o : o + 1,
+  // negated for the second read of a pair
+  const bool neg = inf.fl & kInfoNeg, sec = inf.fl & kInfoSecond;
+  if (!neg) {
+    x.cell0 = sec ? L - 1 : L + 1;
+    x.dir = sec ? -1 : 1;
+  } else {
+    x.cell0 = sec ? L - (int)m.ls : L + (int)m.ls;
+    x.dir = sec ? 1 : -1;
+  }
+  return x;
 }
 
-template <int TS>
-struct TileRegs {
-  ReadMeta m;
-  ReadInfo inf;
-  uint4 q[TileCfg<TS>::nQ];
-  uint4 c[TileCfg<TS>::nC];
-  uint64_t b[TileCfg<TS>::nB];
-};
-
-// Issue the global loads of tile t (first slot ts0) into registers; nothing
-// waits on them until tile_install, one tile later, so their latency hides
-// behind the current tile's LDS-only loop.  Chunks are 16-B aligned and each
-// holds at least one byte of its column, so no load leaves an allocation.
-template <int TS, bool kBits>
-__device__ __forceinline__ void tile_issue(const ReadsDev& rd, const ReadInfo* info, const uint64_t* sbits, int64_t t,
-                                           uint64_t ts0, int lane, TileRegs<TS>& R) {
-  using G = TileCfg<TS>;
-  const int64_t r0 = t * (int64_t)rd.reads_per_tile;
-  const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
-  R.m = ReadMeta{0, 0, 0, 0, 0};
-  R.inf = ReadInfo{0, 0, 0, 0};
-  if (lane < nr) {
-    R.m = rd.meta[r0 + lane];
-    R.inf = info[r0 + lane];
-  }
-  const bool any = rd.n_slots > 0;
-  const uintptr_t qa = (uintptr_t)(rd.qual + ts0) & ~(uintptr_t)15;
-  const uintptr_t qlast = (uintptr_t)rd.qual + (uintptr_t)(rd.n_slots - 1);
-#pragma unroll
-  for (int i = 0; i < G::nQ; ++i) {
-    const int k = lane + 64 * i;
-    const uintptr_t a = qa + 16 * (uintptr_t)k;
-    R.q[i] = (any && k < G::kQC && a <= qlast) ? *(const uint4*)a : make_uint4(0, 0, 0, 0);
-  }
-  const uintptr_t ca = (uintptr_t)(rd.bases + (ts0 >> 1)) & ~(uintptr_t)15;
-  const uintptr_t clast = (uintptr_t)rd.bases + (uintptr_t)((rd.n_slots - 1) >> 1);
-#pragma unroll
-  for (int i = 0; i < G::nC; ++i) {
-    const int k = lane + 64 * i;
-    const uintptr_t a = ca + 16 * (uintptr_t)k;
-    R.c[i] = (any && k < G::kCC && a <= clast) ? *(const uint4*)a : make_uint4(0, 0, 0, 0);
-  }
-  if (kBits) {
-    const int64_t wb = (int64_t)(ts0 >> 5);
-#pragma unroll
-    for (int i = 0; i < G::nB; ++i) {
-      const int k = lane + 64 * i;
-      R.b[i] = (k < G::kBW && (wb + k) * 32 < rd.n_slots) ? sbits[wb + k] : 0ull;
-    }
-  }
+// masked (low) and mismatch (high) bits of offsets o0 .. o0+31 of a read
+__device__ __forceinline__ void load_bits(const uint64_t* sbits, uint64_t s, uint32_t& masked, uint32_t& mism) {
+  const uint64_t w0 = sbits[s >> 5], w1 = sbits[(s >> 5) + 1];
+  const uint32_t sh = (uint32_t)(s & 31);
+  masked = __builtin_amdgcn_alignbit((uint32_t)w1, (uint32_t)w0, sh);
+  mism = __builtin_amdgcn_alignbit((uint32_t)(w1 >> 32), (uint32_t)(w0 >> 32), sh);
 }
 
-// Move a prefetched tile into the wave's LDS state (see TileLds).
-template <int TS, bool kBits>
-__device__ Tile tile_install(const ReadsDev& rd, int64_t t, uint64_t ts0, TileLds<TS>& T, const TileRegs<TS>& R,
-                             int lane, int L) {
-  using G = TileCfg<TS>;
-  Tile ti;
-  ti.r0 = t * (int64_t)rd.reads_per_tile;
-  ti.nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - ti.r0);
-  ti.ts0 = ts0;
-  const ReadMeta& m = R.m;
-  const ReadInfo& inf = R.inf;
-  const uint32_t len = max(m.lq, m.ls);
-  const uint64_t last_end = __shfl(m.slot + len, ti.nr - 1);
-  ti.nslots = (int)(last_end - ts0);
-  ti.qoff = (int)((uintptr_t)(rd.qual + ts0) & 15);
-  ti.cnib = 2 * (int)((uintptr_t)(rd.bases + (ts0 >> 1)) & 15) + (int)(ts0 & 1);
-  ti.boff = (int)(ts0 & 31);
-#pragma unroll
-  for (int i = 0; i < G::nQ; ++i)
-    if (lane + 64 * i < G::kQC) T.q[lane + 64 * i] = R.q[i];
-#pragma unroll
-  for (int i = 0; i < G::nC; ++i)
-    if (lane + 64 * i < G::kCC) T.c[lane + 64 * i] = R.c[i];
-  if (kBits) {
-#pragma unroll
-    for (int i = 0; i < G::nB; ++i)
-      if (lane + 64 * i < G::kBW) T.bits[lane + 64 * i] = R.b[i];
-  }
-  for (int i = lane; i < G::kSb; i += 64) T.sbp[i].x = 0;
-  // compact list of the reads that own slots
-  const bool own = lane < ti.nr && len > 0;
-  const unsigned long long bal = __ballot(own);
-  const int c = __popcll(bal & ((1ull << lane) - 1ull));
-  wave_sync();
-  if (own) {
-    const int rs = (int)(m.slot - ts0);
-    // DiscreteCycle (StandardCovariate.scala:39-48) as a linear function of the
-    // slot: cell = cyc + L, cyc = neg ? ls - o : o + 1, negated for second of pair
-    const bool neg = inf.fl & kInfoNeg, sec = inf.fl & kInfoSecond;
-    int cb;
-    bool down;
-    if (!neg) {
-      cb = sec ? L - 1 + rs : L + 1 - rs;
-      down = sec;
-    } else {
-      cb = sec ? L - (int)m.ls - rs : L + (int)m.ls + rs;
-      down = !sec;
-    }
-    const uint32_t fl = inf.fl | (down ? kInfoCycNeg : 0);
-    const uint32_t st = (inf.fl & kInfoPass) ? 0u : inf.st, en = (inf.fl & kInfoPass) ? m.lq : inf.en;
-    const uint32_t cm = (uint32_t)(2 * rs + (int)inf.en + (int)inf.st);  // reverse-strand context mirror
-    T.rec[c] = make_uint4(st | (en << 16), fl | ((uint32_t)(cb & 0xFFFF) << 16), (uint32_t)rs | ((cm & 0xFFFF) << 16),
-                          (uint32_t)m.rg | ((uint32_t)lane << 16));
-    atomicOr(&T.sbp[rs >> 5].x, 1u << (rs & 31));
-  }
-  wave_sync();
-  // popcount prefix of the start bitmap
-  constexpr int wpl = G::kSb >= 64 ? G::kSb / 64 : 1;
-  uint32_t cnt[wpl];
-  int tot = 0;
-#pragma unroll
-  for (int j = 0; j < wpl; ++j) {
-    const int w = lane * wpl + j;
-    cnt[j] = w < G::kSb ? __popc(T.sbp[w].x) : 0u;
-    tot += (int)cnt[j];
-  }
-  int run = wave_incl_scan(tot, lane) - tot;
-#pragma unroll
-  for (int j = 0; j < wpl; ++j) {
-    const int w = lane * wpl + j;
-    if (w < G::kSb) T.sbp[w].y = (uint32_t)run;
-    run += (int)cnt[j];
-  }
-  wave_sync();
-  return ti;
-}
-
-template <int TS>
-__device__ __forceinline__ int compact_of(const TileLds<TS>& T, int s) {
-  const uint2 v = T.sbp[s >> 5];
-  return (int)v.y + __popc(v.x & (0xFFFFFFFFu >> (31 - (s & 31)))) - 1;
+// the 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
+// reverse: the mirrored codes, complemented -- quirk Q9)
+__device__ __forceinline__ void chunk_codes(const ReadsDev& rd, const LaneRead& x, int o0, uint64_t& lo, uint32_t& hi) {
+  const bool neg = x.fl & kInfoNeg;
+  const int64_t n0 = (int64_t)x.slot + (neg ? (int64_t)(x.en + x.st - o0 - 16) : (int64_t)(o0 - 1));
+  if (__builtin_expect(n0 >= 0, 1)) load_window(rd.bases, n0, lo, hi);
+  else load_window_head(rd.bases, n0, rd.n_slots, lo, hi);
+  if (neg) revcomp_window(lo, hi);
 }
 
 // ------------------------------------------------------------ observe ------
 
-// LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32]
-//      [block hist 128 u32] [TileLds<TS> x 16]
-// Each wave walks tiles tb0 + wave, tb0 + wave + 16, ... of the block's range,
-// loading tile k+1 while it counts tile k.  The window holds the block's
-// counts for rows (rg_lo, q_lo..q_lo+qw-1); other keys go straight to the
-// int64 table.  The block's window is written to `part` and summed into the
-// table by bqsr_window_reduce.
-template <int TS>
+// LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32][block hist 128 u32]
+// The window holds the block's counts for rows (rg_lo, q_lo..q_lo+qw-1); other
+// keys go straight to the int64 table.  The block's window is written to
+// `part` and summed into the table by bqsr_window_reduce.
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -560,8 +509,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   uint32_t* w_mm = w_obs + qw * cells;
   uint32_t* w_masked = w_mm + qw * cells;
   uint32_t* blk_hist = w_masked + qw;
-  const uintptr_t tile_off = ((uintptr_t)(blk_hist + kQBins) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
-  TileLds<TS>* tiles = (TileLds<TS>*)(smem + tile_off);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -569,90 +516,55 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
   const int64_t nt = P.rd.n_tiles;
   const int64_t tb0 = nt * blockIdx.x / P.n_blocks, tb1 = nt * (blockIdx.x + 1) / P.n_blocks;
+  const int64_t r_begin = tb0 * P.rd.reads_per_tile, r_end = min(tb1 * (int64_t)P.rd.reads_per_tile, P.rd.n_reads);
   __syncthreads();
 
-  TileLds<TS>& T = tiles[wave];
   const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
-  int64_t t = tb0 + wave;
-  TileRegs<TS> R;
-  uint64_t ts_cur = 0, ts_nxt = 0;
-  if (t < tb1) ts_cur = tile_first_slot(P.rd, t);
-  if (t + kWaves < tb1) ts_nxt = tile_first_slot(P.rd, t + kWaves);
-  ts_cur = rfl64(ts_cur);
-  if (t < tb1) tile_issue<TS, true>(P.rd, P.info, P.sbits, t, ts_cur, lane, R);
-  for (; t < tb1; t += kWaves) {
-    const Tile ti = tile_install<TS, true>(P.rd, t, ts_cur, T, R, lane, L);
-    {  // prefetch the wave's next tile and the first slot of the one after
-      const int64_t t1 = t + kWaves, t2 = t + 2 * kWaves;
-      const uint64_t ts1 = rfl64(ts_nxt);
-      uint64_t ts2 = 0;
-      if (t2 < tb1) ts2 = tile_first_slot(P.rd, t2);
-      if (t1 < tb1) tile_issue<TS, true>(P.rd, P.info, P.sbits, t1, ts1, lane, R);
-      ts_cur = ts1;
-      ts_nxt = ts2;
-    }
-    const uint8_t* lq = (const uint8_t*)T.q + ti.qoff;
-    const uint8_t* lc = (const uint8_t*)T.c;
-    const int cnib = ti.cnib, boff = ti.boff;
-    // four slots per lane per step: the LDS loads of all four issue before any use
-    for (int s0 = lane; s0 < ti.nslots; s0 += 64 * kUnroll) {
-      int sv[kUnroll], qv[kUnroll];
-      uint4 rc[kUnroll];
-      uint64_t bw[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        sv[u] = s0 + 64 * u;
-        const int sc = sv[u] < ti.nslots ? sv[u] : 0;
-        qv[u] = (int)(int8_t)lq[sc];
-        rc[u] = T.rec[compact_of(T, sc)];
-        bw[u] = T.bits[(boff + sc) >> 5];
+  for (int64_t g0 = r_begin + 64 * wave; g0 < r_end; g0 += 64 * kWaves) {
+    const LaneRead x = lane_read(P.rd, P.info, g0 + lane, r_end, L);
+    const bool act = x.fl & (kInfoObs | kInfoObsCheck);
+    const bool full = x.fl & kInfoObs;
+    const int n = act ? x.en - x.st : 0;
+    const bool rgwin = x.rg == rg_lo;
+    const uint8_t* qp = P.rd.qual + x.slot;
+    for (int j = 0; __builtin_amdgcn_ballot_w64(j < n); j += kChunk) {
+      if (j >= n) continue;
+      const int o0 = x.st + j;
+      const uint4 qv = *(const uint4*)(qp + o0);
+      uint32_t bm = 0, bx = 0;
+      uint64_t clo = 0;
+      uint32_t chi = 0;
+      if (full) {
+        load_bits(P.sbits, x.slot + (uint64_t)o0, bm, bx);
+        chunk_codes(P.rd, x, o0, clo, chi);
       }
-      int ov[kUnroll];
-      bool act[kUnroll];
-      uint32_t ca[kUnroll], cbv[kUnroll];
+      const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+      const int cc0 = x.cell0 + x.dir * o0;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
-        ov[u] = sv[u] - (int)(rc[u].z & 0xFFFF);
-        act[u] = sv[u] < ti.nslots && (fl & (kInfoObs | kInfoObsCheck)) && ov[u] >= st && ov[u] < en;
-        // BaseContext(2) operands (StandardCovariate.scala:59-90): codes at s-1, s;
-        // the reverse strand reads them mirrored within [st, en) (quirk Q9)
-        const bool neg = fl & kInfoNeg;
-        const int na = neg ? (int)(rc[u].z >> 16) - sv[u] : sv[u] - 1;
-        const bool ctxon = act[u] && (fl & kInfoObs) && ov[u] != st;
-        ca[u] = ctxon ? lds_code(lc, cnib + na) : 0u;
-        cbv[u] = ctxon ? lds_code(lc, cnib + (neg ? na - 1 : sv[u])) : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int q = qv[u];
-        if (!act[u]) continue;
-        const int o = ov[u], fl = (int)(rc[u].y & 0xFFFF);
-        if (__builtin_expect(q < 0, 0)) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-          report(P.err, err_key((uint64_t)(ti.r0 + (rc[u].w >> 16)), o, kRankTable, BQSR_ERR_QUAL_RANGE));
-          continue;
-        }
-        if (!(fl & kInfoObs)) continue;
-        const int bit = (boff + sv[u]) & 31;
-        const bool masked = (bw[u] >> bit) & 1u;
-        const bool mism = (bw[u] >> (32 + bit)) & 1u;
-        const int cb = (int)(int16_t)(rc[u].y >> 16);
-        const int ccell = (fl & kInfoCycNeg) ? cb - sv[u] : cb + sv[u];  // cycle + L
-        const int st = (int)(rc[u].x & 0xFFFF);
-        const int xcell = C + 4 + ((o == st) ? 0 : ctx_code(ca[u], cbv[u], fl & kInfoNeg));
-        const int rg = (int)(rc[u].w & 0xFFFF);
-        const int slot = q - q_lo;
-        if (rg == rg_lo && (unsigned)slot < (unsigned)qw) {
-          const int base = slot * cells;
-          atomicAdd(masked ? &w_masked[slot] : &w_obs[base + ccell], 1u);
-          if (!masked) atomicAdd(&w_obs[base + xcell], 1u);
-          if (__builtin_expect(mism && !masked, 0)) {
-            atomicAdd(&w_mm[base + ccell], 1u);
-            atomicAdd(&w_mm[base + xcell], 1u);
+      for (int k = 0; k < kChunk; ++k) {
+        if (j + k >= n) break;
+        const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+        const int row = q - q_lo;
+        const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
+        uint32_t ca, cb;
+        pair_at(clo, chi, k, ca, cb);
+        const int ccell = cc0 + x.dir * k;
+        const int xcell = C + 4 + ((j + k == 0) ? 0 : ctx_code(ca, cb));
+        if (__builtin_expect(full && rgwin && (unsigned)row < (unsigned)qw, 1)) {
+          const int base = row * cells;
+          atomicAdd(masked ? &w_masked[row] : &w_obs[base + ccell], 1u);
+          if (!masked) {
+            atomicAdd(&w_obs[base + xcell], 1u);
+            if (__builtin_expect(mism, 0)) {
+              atomicAdd(&w_mm[base + ccell], 1u);
+              atomicAdd(&w_mm[base + xcell], 1u);
+            }
           }
-        } else {  // outside the LDS window: straight to the int64 table
+        } else if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+          report(P.err, err_key((uint64_t)x.r, (uint32_t)(o0 + k), kRankTable, BQSR_ERR_QUAL_RANGE));
+        } else if (full) {  // outside the LDS window: straight to the int64 table
           atomicAdd(&blk_hist[q], 1u);
-          const int64_t key = (int64_t)q + (int64_t)kMaxQ * rg;
+          const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
           atomicAdd((unsigned long long*)&P.touched[key], 1ull);
           if (!masked) {
             atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
@@ -665,7 +577,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
         }
       }
     }
-    wave_sync();
   }
   __syncthreads();
   // ---- the block's window -> part; window rows into the block histogram ----
@@ -1064,6 +975,8 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_fold_plan(const uint32_t*
   if (tid == 0) *n_cand = nc;
 }
 
+constexpr int kUnroll = 4;
+
 // Per-tile qual histograms of the folded bases of the candidate blocks' tiles
 // (one wavefront per tile: the folded ranges of the tile's reads become an LDS
 // slot bitmap, then every slot's qual is counted if its bit is set).
@@ -1276,11 +1189,9 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
   return (int32_t)0x80000000;          // log10(inf) = inf
 }
 
-// LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16]
-//      [window ok qw u8] [TileLds<TS> x 16]
-// Tiles are staged and prefetched as in observe; the recalibrated chars are
-// written over the staged quals in LDS and leave as whole 16-B chunks.
-template <int TS>
+// LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16][window ok qw u8]
+// Lane per read as in observe; each chunk's 16 recalibrated chars leave as one
+// 16-B store (the read's last, partial chunk byte by byte).
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
@@ -1289,8 +1200,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   double* l_qbt = w_d2 + qw * kCtxSlots;
   int16_t* l_qbq = (int16_t*)(l_qbt + kQbN);
   uint8_t* w_ok = (uint8_t*)(l_qbq + kQbN);
-  const uintptr_t tile_off = ((uintptr_t)(w_ok + ((qw + 15) & ~15)) - (uintptr_t)smem + 15) & ~(uintptr_t)15;
-  TileLds<TS>* tiles = (TileLds<TS>*)(smem + tile_off);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1312,134 +1221,89 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   for (int i = tid; i < qw; i += blockDim.x) w_ok[i] = (win_ok && q_lo + i < kQBins) ? P.rq_ok[rq0 + i] : 0;
   const int64_t nt = P.rd.n_tiles;
   const int64_t tb0 = nt * blockIdx.x / gridDim.x, tb1 = nt * (blockIdx.x + 1) / gridDim.x;
-  // the output column starts at the same 16-B phase as the quals: chunk copies
-  const bool same_phase = (((uintptr_t)P.out_qual ^ (uintptr_t)P.rd.qual) & 15) == 0;
+  const int64_t r_begin = tb0 * P.rd.reads_per_tile, r_end = min(tb1 * (int64_t)P.rd.reads_per_tile, P.rd.n_reads);
   __syncthreads();
 
-  TileLds<TS>& T = tiles[wave];
-  int64_t t = tb0 + wave;
-  TileRegs<TS> R;
-  uint64_t ts_cur = 0, ts_nxt = 0;
-  if (t < tb1) ts_cur = tile_first_slot(P.rd, t);
-  if (t + kWaves < tb1) ts_nxt = tile_first_slot(P.rd, t + kWaves);
-  ts_cur = rfl64(ts_cur);
-  if (t < tb1) tile_issue<TS, false>(P.rd, P.info, nullptr, t, ts_cur, lane, R);
-  for (; t < tb1; t += kWaves) {
-    const Tile ti = tile_install<TS, false>(P.rd, t, ts_cur, T, R, lane, L);
-    if (lane < ti.nr) {
-      const int64_t r = ti.r0 + lane;
-      if (R.inf.fl & kInfoPass) {  // quality string passed through
-        P.out_start[r] = 0;
-        P.out_len[r] = (R.m.flags & BQSR_F_HAS_QUAL) ? R.m.lq : 0;
+  for (int64_t g0 = r_begin + 64 * wave; g0 < r_end; g0 += 64 * kWaves) {
+    const LaneRead x = lane_read(P.rd, P.info, g0 + lane, r_end, L);
+    if (x.r < r_end) {
+      if (x.fl & kInfoPass) {  // quality string passed through
+        P.out_start[x.r] = 0;
+        P.out_len[x.r] = (uint32_t)x.en;
       } else {
-        P.out_start[r] = R.inf.st;
-        P.out_len[r] = (R.inf.fl & kInfoApp) ? (uint32_t)(R.inf.en - R.inf.st) : 0;
+        P.out_start[x.r] = (uint32_t)x.st;
+        P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
       }
     }
-    {  // prefetch the wave's next tile and the first slot of the one after
-      const int64_t t1 = t + kWaves, t2 = t + 2 * kWaves;
-      const uint64_t ts1 = rfl64(ts_nxt);
-      uint64_t ts2 = 0;
-      if (t2 < tb1) ts2 = tile_first_slot(P.rd, t2);
-      if (t1 < tb1) tile_issue<TS, false>(P.rd, P.info, nullptr, t1, ts1, lane, R);
-      ts_cur = ts1;
-      ts_nxt = ts2;
-    }
-    uint8_t* lq = (uint8_t*)T.q + ti.qoff;
-    const uint8_t* lc = (const uint8_t*)T.c;
-    const int cnib = ti.cnib;
-    // four slots per lane per step: the LDS loads of all four issue before any use
-    for (int s0 = lane; s0 < ti.nslots; s0 += 64 * kUnroll) {
-      int sv[kUnroll];
-      uint32_t qb[kUnroll];
-      uint4 rc[kUnroll];
+    const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
+    const int n = (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) ? x.en - x.st : 0;
+    const bool rgwin = x.rg == rg_lo;
+    const uint8_t* qp = P.rd.qual + x.slot;
+    uint8_t* op = P.out_qual + x.slot;
+    for (int j = 0; __builtin_amdgcn_ballot_w64(j < n); j += kChunk) {
+      if (j >= n) continue;
+      const int o0 = x.st + j;
+      const uint4 qv = *(const uint4*)(qp + o0);
+      uint32_t out[4];
+      if (pass) {  // the original chars: (qual + 33) byte-wise
+        const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        sv[u] = s0 + 64 * u;
-        const int sc = sv[u] < ti.nslots ? sv[u] : 0;
-        qb[u] = lq[sc];
-        rc[u] = T.rec[compact_of(T, sc)];
-      }
-      uint32_t ca[kUnroll], cbv[kUnroll];
+        for (int i = 0; i < 4; ++i) out[i] = ((qd[i] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i] & 0x80808080u);
+      } else {
+        uint64_t clo = 0;
+        uint32_t chi = 0;
+        chunk_codes(P.rd, x, o0, clo, chi);
+        const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+        const int cc0 = x.cell0 + x.dir * o0;
+        out[0] = out[1] = out[2] = out[3] = 0;
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
-        const int o = sv[u] - (int)(rc[u].z & 0xFFFF);
-        const bool ctxon = sv[u] < ti.nslots && (fl & kInfoApp) && o > st && o < en;
-        const bool neg = fl & kInfoNeg;
-        const int na = neg ? (int)(rc[u].z >> 16) - sv[u] : sv[u] - 1;
-        ca[u] = ctxon ? lds_code(lc, cnib + na) : 0u;
-        cbv[u] = ctxon ? lds_code(lc, cnib + (neg ? na - 1 : sv[u])) : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int st = (int)(rc[u].x & 0xFFFF), en = (int)(rc[u].x >> 16), fl = (int)(rc[u].y & 0xFFFF);
-        const int o = sv[u] - (int)(rc[u].z & 0xFFFF);
-        // pass-through reads carry st = 0, en = Lq
-        if (sv[u] >= ti.nslots || !(fl & (kInfoApp | kInfoAppCheck | kInfoPass)) || o < st || o >= en) continue;
-        uint32_t code;
-        if (fl & kInfoPass) {
-          code = qb[u] + 33u;  // the original quality char
-        } else {
-          const int q = (int)(int8_t)qb[u];
-          const int rg = (int)(rc[u].w & 0xFFFF);
-          const int slot = q - q_lo;
-          const int cb = (int)(int16_t)(rc[u].y >> 16);
-          const int ccell = (fl & kInfoCycNeg) ? cb - sv[u] : cb + sv[u];  // cycle + L
-          const int ctx = (o == st) ? 0 : ctx_code(ca[u], cbv[u], fl & kInfoNeg);
+        for (int k = 0; k < kChunk; ++k) {
+          if (j + k >= n) break;
+          const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+          const int row = q - q_lo;
+          uint32_t ca, cb;
+          pair_at(clo, chi, k, ca, cb);
+          const int ccell = cc0 + x.dir * k;
+          const int ctx = (j + k == 0) ? 0 : ctx_code(ca, cb);
           double p;
-          if ((fl & kInfoApp) && rg == rg_lo && (unsigned)slot < (unsigned)qw && w_ok[slot]) {
+          uint32_t code;
+          if (__builtin_expect(app && rgwin && (unsigned)row < (unsigned)qw && w_ok[row], 1)) {
             // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-            p = w_s1[slot * C + ccell] + w_d2[slot * kCtxSlots + ctx + 4];
+            p = w_s1[row * C + ccell] + w_d2[row * kCtxSlots + ctx + 4];
           } else {
             // key validity as getReadGroupDelta / getQualScoreDelta see it
-            const uint64_t r = (uint64_t)(ti.r0 + (rc[u].w >> 16));
-            const int64_t key = (int64_t)q + (int64_t)kMaxQ * rg;
+            const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
             const int64_t gr = (key - 1) / kMaxQ;
             const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
             const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
             if (!grp || !kok) {
-              report(P.err, err_key(r, o, kRankTable, BQSR_ERR_MISSING_KEY));
+              report(P.err, err_key((uint64_t)x.r, (uint32_t)(o0 + k), kRankTable, BQSR_ERR_MISSING_KEY));
               continue;
             }
             if (q < 0) {
-              report(P.err, err_key(r, o, kRankTable, BQSR_ERR_QUAL_RANGE));
+              report(P.err, err_key((uint64_t)x.r, (uint32_t)(o0 + k), kRankTable, BQSR_ERR_QUAL_RANGE));
               continue;
             }
-            if (!(fl & kInfoApp)) continue;
-            const int64_t rq = (int64_t)rg * kQBins + q;
+            if (!app) continue;
+            const int64_t rq = (int64_t)x.rg * kQBins + q;
             p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + ctx + 4];
           }
           const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
           code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
           if (__builtin_expect(code > 0xFFu, 0)) {
-            const unsigned long long k = atomicAdd(P.n_exc, 1ull);
-            if ((int64_t)k < P.max_exc) P.exc[k] = ((ti.ts0 + (uint64_t)sv[u]) << 16) | code;
+            const unsigned long long e = atomicAdd(P.n_exc, 1ull);
+            if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)(o0 + k)) << 16) | code;
           }
-        }
-        lq[sv[u]] = (uint8_t)code;  // in place: slot sv[u] is this lane's alone
-      }
-    }
-    wave_sync();
-    // write the tile's slots back: whole chunks inside [0, nslots), bytes at the edges
-    uint8_t* ob = P.out_qual + ti.ts0;
-    if (same_phase) {
-      uint8_t* oa = (uint8_t*)((uintptr_t)ob & ~(uintptr_t)15);
-      const int nch = (ti.qoff + ti.nslots + 15) >> 4;
-      for (int k = lane; k < nch; k += 64) {
-        const int lo = 16 * k - ti.qoff;
-        if (lo >= 0 && lo + 16 <= ti.nslots) {
-          *(uint4*)(oa + 16 * k) = T.q[k];
-        } else {
-          const uint8_t* src = (const uint8_t*)&T.q[k];
-          for (int j = 0; j < 16; ++j)
-            if (lo + j >= 0 && lo + j < ti.nslots) oa[16 * k + j] = src[j];
+          out[k >> 2] |= (code & 0xFFu) << (8 * (k & 3));
         }
       }
-    } else {
-      for (int s = lane; s < ti.nslots; s += 64) ob[s] = lq[s];
+      if (!(app || pass)) continue;
+      if (j + kChunk <= n) {
+        *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
+      } else {
+        for (int k = 0; k < n - j; ++k) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+      }
     }
-    wave_sync();
   }
 }
 
@@ -1448,14 +1312,5 @@ extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     acc[i] += part[i];
 }
-
-// one instantiation per tile size
-#define BQSR_TILE_KERNELS(TS)                                                   \
-  template __global__ void bqsr_observe_kernel<TS>(ObserveParams);              \
-  template __global__ void bqsr_apply_kernel<TS>(ApplyParams);
-BQSR_TILE_KERNELS(1024)
-BQSR_TILE_KERNELS(2048)
-BQSR_TILE_KERNELS(4096)
-#undef BQSR_TILE_KERNELS
 
 }  // namespace bqsr

@@ -159,8 +159,10 @@ typedef struct bqsr_device_reads {
   int64_t n_slots;        /* total base slots (sum of max(Ls, Lq) per read)           */
   const void* meta;       /* [n] 16-B records {u64 slot; u16 lq; u16 ls; u16 flags; u16 rg} */
   const void* align;      /* [n] 24-B records {i64 start; u32 cigar_off; u32 md_off; i32 contig; u16 n_cigar; u16 md_len} */
-  const uint8_t* qual;    /* [n_slots] phred bytes (qual char - 33, as Java byte)    */
-  const uint8_t* bases;   /* [(n_slots+1)/2] 4-bit codes A0 C1 G2 T3 N4 other5         */
+  const uint8_t* qual;    /* [n_slots + 32] phred bytes (qual char - 33, as Java byte);
+                             the 32 bytes past the end must be readable (16-B loads) */
+  const uint8_t* bases;   /* [(n_slots+1)/2 + 32] 4-bit codes A0 C1 G2 T3 N4 other5,
+                             low nibble first; 32 readable bytes of padding likewise */
   const uint32_t* cigar;  /* BAM elements                                             */
   const uint8_t* md;      /* MD bytes                                                 */
   bqsr_dims dims;
