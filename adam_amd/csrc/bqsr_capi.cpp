@@ -425,7 +425,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   if ((st = dalloc(b->allocs, &b->d_cand_list, (size_t)b->n_blocks + 1)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_err, kErrWords)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_info, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
-  b->sbits_words = b->rd.n_slots / 32 + 2;
+  b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
   return BQSR_OK;

@@ -486,14 +486,47 @@ __device__ __forceinline__ void load_bits(const uint64_t* sbits, uint64_t s, uin
   mism = __builtin_amdgcn_alignbit((uint32_t)(w1 >> 32), (uint32_t)(w0 >> 32), sh);
 }
 
-// the 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
-// reverse: the mirrored codes, complemented -- quirk Q9)
-__device__ __forceinline__ void chunk_codes(const ReadsDev& rd, const LaneRead& x, int o0, uint64_t& lo, uint32_t& hi) {
+// The 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
+// reverse: the mirrored codes, complemented -- quirk Q9).  Split in two so a
+// super-chunk's loads all issue before any is used: chunk_n0 / chunk_raw
+// issue the 16-B load, chunk_finish shifts (and reverse-complements).
+__device__ __forceinline__ int64_t chunk_n0(const LaneRead& x, int o0) {
   const bool neg = x.fl & kInfoNeg;
-  const int64_t n0 = (int64_t)x.slot + (neg ? (int64_t)(x.en + x.st - o0 - 16) : (int64_t)(o0 - 1));
-  if (__builtin_expect(n0 >= 0, 1)) load_window(rd.bases, n0, lo, hi);
-  else load_window_head(rd.bases, n0, rd.n_slots, lo, hi);
-  if (neg) revcomp_window(lo, hi);
+  return (int64_t)x.slot + (neg ? (int64_t)(x.en + x.st - o0 - 16) : (int64_t)(o0 - 1));
+}
+__device__ __forceinline__ uint4 chunk_raw(const ReadsDev& rd, int64_t n0) {
+  return n0 >= 0 ? *(const uint4*)(rd.bases + (n0 >> 1)) : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void chunk_finish(const ReadsDev& rd, const LaneRead& x, int64_t n0, uint4 v, uint64_t& lo,
+                                             uint32_t& hi) {
+  if (__builtin_expect(n0 >= 0, 1)) {
+    const uint32_t sh = (uint32_t)(n0 & 1) * 4u;
+    const uint32_t d0 = __builtin_amdgcn_alignbit(v.y, v.x, sh);
+    const uint32_t d1 = __builtin_amdgcn_alignbit(v.z, v.y, sh);
+    const uint32_t d2 = __builtin_amdgcn_alignbit(v.w, v.z, sh);
+    lo = ((uint64_t)d1 << 32) | d0;
+    hi = d2 & 0xFu;
+  } else {
+    load_window_head(rd.bases, n0, rd.n_slots, lo, hi);
+  }
+  if (x.fl & kInfoNeg) revcomp_window(lo, hi);
+}
+
+// Offsets per super-chunk: the loads of kSub chunks of one read are issued
+// together, so the few cache lines a read spans are fetched once while hot
+// instead of once per chunk.
+constexpr int kSub = 4;
+constexpr int kSuper = kSub * kChunk;
+
+// 16 masked / mismatch bits of sub-chunk i from the super-chunk's three
+// bitmap words (w[0] holds the slot of the super-chunk's first offset at bit b0)
+__device__ __forceinline__ void sub_bits(const uint64_t w[3], uint32_t b0, int i, uint32_t& masked, uint32_t& mism) {
+  const uint32_t b = b0 + 16u * (uint32_t)i;
+  const uint32_t wi = b >> 5, sh = b & 31;
+  const uint64_t lo = wi == 0 ? w[0] : (wi == 1 ? w[1] : w[2]);
+  const uint64_t hi = wi == 0 ? w[1] : w[2];
+  masked = __builtin_amdgcn_alignbit((uint32_t)hi, (uint32_t)lo, sh);
+  mism = __builtin_amdgcn_alignbit((uint32_t)(hi >> 32), (uint32_t)(lo >> 32), sh);
 }
 
 // ------------------------------------------------------------ observe ------
@@ -527,16 +560,38 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     const int n = act ? x.en - x.st : 0;
     const bool rgwin = x.rg == rg_lo;
     const uint8_t* qp = P.rd.qual + x.slot;
-    for (int j = 0; __builtin_amdgcn_ballot_w64(j < n); j += kChunk) {
+    for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
+      if (j0 >= n) continue;
+      // issue every load of the super-chunk first
+      uint4 qs[kSub], cr[kSub];
+      int64_t cn0[kSub];
+      uint64_t bw[3] = {0, 0, 0};
+      const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
+#pragma unroll
+      for (int i = 0; i < kSub; ++i) {
+        const bool live = j0 + kChunk * i < n;
+        const int o0 = x.st + j0 + kChunk * i;
+        qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
+        cn0[i] = chunk_n0(x, o0);
+        cr[i] = (live && full) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
+      }
+      if (full) {
+        bw[0] = P.sbits[s0 >> 5];
+        bw[1] = P.sbits[(s0 >> 5) + 1];
+        bw[2] = P.sbits[(s0 >> 5) + 2];
+      }
+#pragma clang loop unroll(full)
+      for (int i = 0; i < kSub; ++i) {
+      const int j = j0 + kChunk * i;
       if (j >= n) continue;
       const int o0 = x.st + j;
-      const uint4 qv = *(const uint4*)(qp + o0);
+      const uint4 qv = qs[i];
       uint32_t bm = 0, bx = 0;
       uint64_t clo = 0;
       uint32_t chi = 0;
       if (full) {
-        load_bits(P.sbits, x.slot + (uint64_t)o0, bm, bx);
-        chunk_codes(P.rd, x, o0, clo, chi);
+        sub_bits(bw, (uint32_t)(s0 & 31), i, bm, bx);
+        chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
       }
       const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
       const int cc0 = x.cell0 + x.dir * o0;
@@ -575,6 +630,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
             }
           }
         }
+      }
       }
     }
   }
@@ -1206,9 +1262,12 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
   const bool win_ok = rg_lo < P.n_rg;
   const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
+  // rows whose key is not in the table hold NaN: the fast path sends such
+  // bases to the checked path below (a valid a2 + deltas is never NaN)
   for (int i = tid; i < qw * C; i += blockDim.x) {
     const int slot = i / C;
-    w_s1[i] = (win_ok && q_lo + slot < kQBins) ? P.s1[(rq0 + slot) * C + (i - slot * C)] : 0.0;
+    const bool ok = win_ok && q_lo + slot < kQBins && P.rq_ok[rq0 + slot];
+    w_s1[i] = ok ? P.s1[(rq0 + slot) * C + (i - slot * C)] : __builtin_nan("");
   }
   for (int i = tid; i < qw * kCtxSlots; i += blockDim.x) {
     const int slot = i / kCtxSlots;
@@ -1240,21 +1299,36 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     const bool rgwin = x.rg == rg_lo;
     const uint8_t* qp = P.rd.qual + x.slot;
     uint8_t* op = P.out_qual + x.slot;
-    for (int j = 0; __builtin_amdgcn_ballot_w64(j < n); j += kChunk) {
+    for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
+      if (j0 >= n) continue;
+      // issue every load of the super-chunk first
+      uint4 qs[kSub], cr[kSub];
+      int64_t cn0[kSub];
+#pragma unroll
+      for (int i = 0; i < kSub; ++i) {
+        const bool live = j0 + kChunk * i < n;
+        const int o0 = x.st + j0 + kChunk * i;
+        qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
+        cn0[i] = chunk_n0(x, o0);
+        cr[i] = (live && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
+      }
+#pragma clang loop unroll(full)
+      for (int i = 0; i < kSub; ++i) {
+      const int j = j0 + kChunk * i;
       if (j >= n) continue;
       const int o0 = x.st + j;
-      const uint4 qv = *(const uint4*)(qp + o0);
+      const uint4 qv = qs[i];
       uint32_t out[4];
       if (pass) {  // the original chars: (qual + 33) byte-wise
         const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) out[i] = ((qd[i] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i] & 0x80808080u);
+        for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
       } else {
         uint64_t clo = 0;
         uint32_t chi = 0;
-        chunk_codes(P.rd, x, o0, clo, chi);
+        chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
         const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
-        const int cc0 = x.cell0 + x.dir * o0;
+      const int cc0 = x.cell0 + x.dir * o0;
         out[0] = out[1] = out[2] = out[3] = 0;
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) {
@@ -1265,12 +1339,12 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
           pair_at(clo, chi, k, ca, cb);
           const int ccell = cc0 + x.dir * k;
           const int ctx = (j + k == 0) ? 0 : ctx_code(ca, cb);
-          double p;
           uint32_t code;
-          if (__builtin_expect(app && rgwin && (unsigned)row < (unsigned)qw && w_ok[row], 1)) {
-            // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-            p = w_s1[row * C + ccell] + w_d2[row * kCtxSlots + ctx + 4];
-          } else {
+          // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+          const bool inwin = app && rgwin && (unsigned)row < (unsigned)qw;
+          const int rowc = inwin ? row : 0;
+          double p = w_s1[rowc * C + ccell] + w_d2[rowc * kCtxSlots + ctx + 4];
+          if (__builtin_expect(!inwin || p != p, 0)) {
             // key validity as getReadGroupDelta / getQualScoreDelta see it
             const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
             const int64_t gr = (key - 1) / kMaxQ;
@@ -1301,7 +1375,10 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
       if (j + kChunk <= n) {
         *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
       } else {
-        for (int k = 0; k < n - j; ++k) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k)
+          if (k < n - j) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+      }
       }
     }
   }
