@@ -169,14 +169,22 @@ TableGeom geom(const bqsr_dims& d) {
 }
 
 constexpr size_t kLdsMax = 163840;
-size_t observe_lds(int qw, int cells) { return (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4; }
+size_t observe_lds(int qw, int cells) { return (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4 + 64 * 4; }
 size_t apply_lds(int qw, int C) {
-  return (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2) + (size_t)qw;
+  return (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2);
 }
 int observe_qw(int cells) {
   int qw = 64;
   while (qw > 1 && observe_lds(qw, cells) > kLdsMax) --qw;
   return qw;
+}
+// observe fast-path variant (bqsr_observe_kernel<V>); ADAM_BQSR_OBSERVE_VARIANT overrides while tuning
+int observe_variant() {
+  static const int v = [] {
+    const char* e = getenv("ADAM_BQSR_OBSERVE_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 int apply_qw(int C) {
   int qw = 64;
@@ -314,8 +322,9 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  for (const void* f : {(const void*)bqsr_observe_kernel<0>, (const void*)bqsr_observe_kernel<1>,
+                        (const void*)bqsr_observe_kernel<2>})
+    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e != hipSuccess) {
@@ -486,8 +495,8 @@ bqsr_status pack(const bqsr_records* R, Packed& P) {
   // kColumnPad readable bytes past each column's end: the per-base passes load 16 B at a time
   P.qual.assign((size_t)slot + kColumnPad, 0);
   P.bases.assign((size_t)slot / 2 + 1 + kColumnPad, 0);
-  P.md.resize(std::max<uint64_t>(md_tot, 1));
-  P.cigar.resize(std::max<uint64_t>(cig_tot, 1));
+  P.md.resize(md_tot + kColumnPad);        // the prep kernel loads 32 B of MD at a time
+  P.cigar.resize(cig_tot + kColumnPad / 4);  // and 16 B of CIGAR
   P.rghist.assign((size_t)P.n_rg, 0);
   // per-base columns, parallel over read ranges
   const int nth = (int)std::max<int64_t>(1, std::min<int64_t>(16, n / 65536));
@@ -795,7 +804,11 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
     const size_t lds = observe_lds(P.w.qw, P.g.cells);
-    hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    switch (observe_variant()) {
+      case 1: hipLaunchKernelGGL(bqsr_observe_kernel<1>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P); break;
+      case 2: hipLaunchKernelGGL(bqsr_observe_kernel<2>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P); break;
+      default: hipLaunchKernelGGL(bqsr_observe_kernel<0>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P); break;
+    }
     HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(1024, (P.part_stride + 255) / 256);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb), dim3(256), 0, s, (const uint32_t*)b->d_part, b->n_blocks,

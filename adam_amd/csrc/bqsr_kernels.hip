@@ -151,8 +151,32 @@ __device__ void set_sbits(uint64_t* sb, uint64_t lo, uint64_t hi, int half) {
 //   mismatch = !MdTag.isMatch(refPos)  (RichADAMRecord.scala:138-154).
 // Errors of usable reads are errors of observe; those of every eligible read
 // are errors of apply (observe runs first).
-__device__ void prep_one(const PrepParams& P, int64_t r) {
+// First index k < n (n <= 16) of the 16 bytes w whose qual is above 2
+// (isLowQualityBase: qual <= minQuality = 2, Java signed byte), or 16; with
+// `rev` the bytes are scanned from byte 15 down.
+__device__ __forceinline__ int first_good(const uint4 v, int n, bool rev) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  int first = 16;
+#pragma unroll
+  for (int k = 15; k >= 0; --k) {
+    const int i = rev ? 15 - k : k;
+    const int b = (int)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    if (k < n && b > 2) first = k;
+  }
+  return first;
+}
+
+// Per-thread LDS copies of a read's CIGAR (<= kPrepCig ops) and MD (<= kPrepMd
+// bytes): the parsers below then walk LDS instead of issuing one dependent
+// global load per element.  Strides of 5 and 9 dwords keep the 64 lanes'
+// slots in distinct banks.
+constexpr int kPrepThreads = 256;
+constexpr int kPrepCig = 4, kPrepCigStride = 5;
+constexpr int kPrepMd = 32, kPrepMdStride = 9;
+
+__device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32_t* s_md) {
   const ReadMeta m = P.rd.meta[r];
+  const ReadAlign a = P.rd.align[r];  // issued with the meta load: one round trip for both
   ReadInfo inf{0, 0, 0, 0};
   const uint16_t f = m.flags;
   if (!eligible_read(f)) {
@@ -172,10 +196,19 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
   }
   const uint8_t* q = P.rd.qual + m.slot;
   const int lq = m.lq;
-  int st = 0;
-  while (st < lq && (int8_t)q[st] <= 2) ++st;  // isLowQualityBase, minQuality = 2
-  int tail = 0;
-  while (tail < lq && (int8_t)q[lq - 1 - tail] <= 2) ++tail;
+  int st = 0, tail = 0;
+  bool more_st = true, more_tail = true;
+  if (lq >= 16) {  // the first and last 16 quals, one load each
+    const uint4 head = *(const uint4*)q, back = *(const uint4*)(q + lq - 16);
+    st = first_good(head, 16, false);
+    tail = first_good(back, 16, true);
+    more_st = st == 16;
+    more_tail = tail == 16;
+  }
+  if (more_st)
+    while (st < lq && (int8_t)q[st] <= 2) ++st;  // isLowQualityBase, minQuality = 2
+  if (more_tail)
+    while (tail < lq && (int8_t)q[lq - 1 - tail] <= 2) ++tail;
   const int en = lq - tail;
   inf.st = (uint16_t)min(st, 0xFFFF);
   if (!(f & BQSR_F_HAS_RG)) {  // QualByRG: 60 * getRecordGroupId
@@ -205,9 +238,35 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
     P.info[r] = inf;
     return;
   }
-  const ReadAlign a = P.rd.align[r];
   const uint32_t* cig = P.rd.cigar + a.cigar_off;
   const uint8_t* md = P.rd.md + a.md_off;
+  {  // short CIGAR / MD (the common case): stage into this thread's LDS slots
+    const bool sc = a.n_cigar <= kPrepCig, sm = (f & BQSR_F_HAS_MD) && a.md_len <= kPrepMd;
+    uint4 c4 = make_uint4(0, 0, 0, 0), m0 = c4, m1 = c4;
+    if (sc) c4 = *(const uint4*)cig;
+    if (sm) {
+      m0 = *(const uint4*)md;
+      m1 = *(const uint4*)(md + 16);
+    }
+    if (sc) {
+      s_cig[0] = c4.x;
+      s_cig[1] = c4.y;
+      s_cig[2] = c4.z;
+      s_cig[3] = c4.w;
+      cig = s_cig;
+    }
+    if (sm) {
+      s_md[0] = m0.x;
+      s_md[1] = m0.y;
+      s_md[2] = m0.z;
+      s_md[3] = m0.w;
+      s_md[4] = m1.x;
+      s_md[5] = m1.y;
+      s_md[6] = m1.z;
+      s_md[7] = m1.w;
+      md = (const uint8_t*)s_md;
+    }
+  }
   // walk the CIGAR once: clip, read-consuming and reference-consuming lengths
   const int ncig = a.n_cigar;
   int64_t lead = 0, rp_len = 0, ref_len = 0;
@@ -352,9 +411,12 @@ __device__ void prep_one(const PrepParams& P, int64_t r) {
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) bqsr_prep_kernel(PrepParams P) {
+extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
+  __shared__ uint32_t s_cig[kPrepThreads * kPrepCigStride];
+  __shared__ uint32_t s_md[kPrepThreads * kPrepMdStride];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += stride) prep_one(P, r);
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += stride)
+    prep_one(P, r, &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
 }
 
 // ------------------------------------------------------- lane-per-read ----
@@ -376,27 +438,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// BaseContext.encode of the (previous, current) base codes
-// (StandardCovariate.scala:84-90) with forward-strand indices: A0 C1 G2 T3,
-// 'other' -1, N -> context 0.  Reverse-strand reads pass their complemented
-// codes (revcomp_window), whose index is then the forward one.
-__device__ __forceinline__ int ctx_code(uint32_t ca, uint32_t cb) {
-  const int ia = ca < 4 ? (int)ca : -1;
-  const int ib = cb < 4 ? (int)cb : -1;
-  return (ca == kCodeN || cb == kCodeN) ? 0 : 1 + 4 * ia + ib;
-}
 
-// 17 base codes from nibble n0 >= 0 of the packed column:
-// nibble k of (lo, hi) = code(n0 + k), k = 0..16.
-__device__ __forceinline__ void load_window(const uint8_t* bases, int64_t n0, uint64_t& lo, uint32_t& hi) {
-  const uint4 v = *(const uint4*)(bases + (n0 >> 1));
-  const uint32_t sh = (uint32_t)(n0 & 1) * 4u;
-  const uint32_t d0 = __builtin_amdgcn_alignbit(v.y, v.x, sh);
-  const uint32_t d1 = __builtin_amdgcn_alignbit(v.z, v.y, sh);
-  const uint32_t d2 = __builtin_amdgcn_alignbit(v.w, v.z, sh);
-  lo = ((uint64_t)d1 << 32) | d0;
-  hi = d2 & 0xFu;
-}
 
 // the same window for the batch's first bases, where n0 < 0 (nibble k of the
 // result = code(n0 + k) for n0 + k >= 0, else 0); rare, byte by byte
@@ -431,11 +473,6 @@ __device__ __forceinline__ void revcomp_window(uint64_t& lo, uint32_t& hi) {
   hi = rhi;
 }
 
-// codes (previous, current) for chunk slot k
-__device__ __forceinline__ void pair_at(uint64_t lo, uint32_t hi, int k, uint32_t& ca, uint32_t& cb) {
-  ca = (uint32_t)(lo >> (4 * k)) & 0xFu;
-  cb = k < 15 ? (uint32_t)(lo >> (4 * k + 4)) & 0xFu : hi;
-}
 
 // Per-lane read decode shared by observe and apply.
 struct LaneRead {
@@ -478,13 +515,6 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
   return x;
 }
 
-// masked (low) and mismatch (high) bits of offsets o0 .. o0+31 of a read
-__device__ __forceinline__ void load_bits(const uint64_t* sbits, uint64_t s, uint32_t& masked, uint32_t& mism) {
-  const uint64_t w0 = sbits[s >> 5], w1 = sbits[(s >> 5) + 1];
-  const uint32_t sh = (uint32_t)(s & 31);
-  masked = __builtin_amdgcn_alignbit((uint32_t)w1, (uint32_t)w0, sh);
-  mism = __builtin_amdgcn_alignbit((uint32_t)(w1 >> 32), (uint32_t)(w0 >> 32), sh);
-}
 
 // The 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
 // reverse: the mirrored codes, complemented -- quirk Q9).  Split in two so a
@@ -529,12 +559,50 @@ __device__ __forceinline__ void sub_bits(const uint64_t w[3], uint32_t b0, int i
   mism = __builtin_amdgcn_alignbit((uint32_t)(hi >> 32), (uint32_t)(lo >> 32), sh);
 }
 
+// Context slots (ctx + 4) of the 16 offsets of a chunk, one per byte
+// (xo[k >> 2] byte k & 3), from its 17-code window: with A = idx(a) + 1 and
+// B = idx(b) + 1 (0 for 'other'), ctx + 4 = 4A + B, and 4 when either base is
+// N.  The per-byte lookups are v_perm byte selects on the 3-bit codes.
+__device__ __forceinline__ void spread8(uint32_t x, uint32_t& s0, uint32_t& s1) {
+  const uint32_t e = x & 0x0F0F0F0Fu, o = (x >> 4) & 0x0F0F0F0Fu;
+  s0 = __builtin_amdgcn_perm(o, e, 0x05010400u);  // nibbles 0..3 -> bytes
+  s1 = __builtin_amdgcn_perm(o, e, 0x07030602u);  // nibbles 4..7 -> bytes
+}
+__device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[4]) {
+  uint32_t as[4], bs[4];
+  spread8((uint32_t)lo, as[0], as[1]);
+  spread8((uint32_t)(lo >> 32), as[2], as[3]);
+  spread8((uint32_t)(lo >> 4), bs[0], bs[1]);
+  spread8((uint32_t)(lo >> 36) | (hi << 28), bs[2], bs[3]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t A = __builtin_amdgcn_perm(0u, 0x04030201u, as[i]);  // A0 C1 G2 T3 -> 1..4, N/other -> 0
+    const uint32_t B = __builtin_amdgcn_perm(0u, 0x04030201u, bs[i]);
+    const uint32_t N = __builtin_amdgcn_perm(0x000000FFu, 0u, as[i]) | __builtin_amdgcn_perm(0x000000FFu, 0u, bs[i]);
+    const uint32_t v = (A << 2) + B;
+    xo[i] = (v & ~N) | (0x04040404u & N);
+  }
+}
+
+// 16 bytes rotated right by r (0..15) bytes: byte k of the result = byte (k + r) & 15
+__device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
+  const uint32_t d = r >> 2, b = r & 3;
+  uint32_t t0 = (d & 1) ? w[1] : w[0], t1 = (d & 1) ? w[2] : w[1];
+  uint32_t t2 = (d & 1) ? w[3] : w[2], t3 = (d & 1) ? w[0] : w[3];
+  const uint32_t u0 = (d & 2) ? t2 : t0, u1 = (d & 2) ? t3 : t1, u2 = (d & 2) ? t0 : t2, u3 = (d & 2) ? t1 : t3;
+  w[0] = __builtin_amdgcn_alignbyte(u1, u0, b);
+  w[1] = __builtin_amdgcn_alignbyte(u2, u1, b);
+  w[2] = __builtin_amdgcn_alignbyte(u3, u2, b);
+  w[3] = __builtin_amdgcn_alignbyte(u0, u3, b);
+}
+
 // ------------------------------------------------------------ observe ------
 
 // LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32][block hist 128 u32]
 // The window holds the block's counts for rows (rg_lo, q_lo..q_lo+qw-1); other
 // keys go straight to the int64 table.  The block's window is written to
 // `part` and summed into the table by bqsr_window_reduce.
+template <int kObsVariant>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -542,6 +610,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   uint32_t* w_mm = w_obs + qw * cells;
   uint32_t* w_masked = w_mm + qw * cells;
   uint32_t* blk_hist = w_masked + qw;
+  uint32_t* dummy = blk_hist + kQBins;  // [64] sink of the branch-free fast path
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -558,13 +627,12 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     const bool act = x.fl & (kInfoObs | kInfoObsCheck);
     const bool full = x.fl & kInfoObs;
     const int n = act ? x.en - x.st : 0;
-    const bool rgwin = x.rg == rg_lo;
+    const bool full_rg = full && x.rg == rg_lo;
     const uint8_t* qp = P.rd.qual + x.slot;
     for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
       if (j0 >= n) continue;
       // issue every load of the super-chunk first
       uint4 qs[kSub], cr[kSub];
-      int64_t cn0[kSub];
       uint64_t bw[3] = {0, 0, 0};
       const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
 #pragma unroll
@@ -572,8 +640,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
         const bool live = j0 + kChunk * i < n;
         const int o0 = x.st + j0 + kChunk * i;
         qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
-        cn0[i] = chunk_n0(x, o0);
-        cr[i] = (live && full) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
+        cr[i] = (live && full) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
       }
       if (full) {
         bw[0] = P.sbits[s0 >> 5];
@@ -582,55 +649,99 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
       }
 #pragma clang loop unroll(full)
       for (int i = 0; i < kSub; ++i) {
-      const int j = j0 + kChunk * i;
-      if (j >= n) continue;
-      const int o0 = x.st + j;
-      const uint4 qv = qs[i];
-      uint32_t bm = 0, bx = 0;
-      uint64_t clo = 0;
-      uint32_t chi = 0;
-      if (full) {
-        sub_bits(bw, (uint32_t)(s0 & 31), i, bm, bx);
-        chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
-      }
-      const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
-      const int cc0 = x.cell0 + x.dir * o0;
+        const int j = j0 + kChunk * i;
+        if (j >= n) continue;
+        const int o0 = x.st + j;
+        const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
+        uint32_t bm = 0, bx = 0;
+        uint32_t xo[4] = {4u, 4u, 4u, 4u};
+        if (full) {
+          sub_bits(bw, (uint32_t)(s0 & 31), i, bm, bx);
+          uint64_t clo;
+          uint32_t chi;
+          chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
+          ctx_slots(clo, chi, xo);
+          if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+        }
+        const int cc0 = x.cell0 + x.dir * o0;
+        // Fast path.  kObsVariant (A/B knob while tuning): 0 = predicated
+        // increments; 1 = branch-free, offsets that do not count add to the
+        // lane's dummy word; 2 = as 1, with lane l visiting the chunk's
+        // offsets rotated by l & 15 so a wavefront's lanes hit different cycle
+        // cells at each step.  Offsets the fast path skips are redone below.
+        const uint32_t rot = kObsVariant == 2 ? (uint32_t)lane & 15u : 0u;
+        uint32_t qr[4] = {qd[0], qd[1], qd[2], qd[3]}, xr[4] = {xo[0], xo[1], xo[2], xo[3]};
+        uint32_t bmr = bm & 0xFFFFu;
+        if (kObsVariant == 2) {
+          rotr16(qr, rot);
+          rotr16(xr, rot);
+          bmr = ((bmr | (bm << 16)) >> rot) & 0xFFFFu;
+        }
+        uint32_t slow = 0, mmk = 0;
 #pragma unroll
-      for (int k = 0; k < kChunk; ++k) {
-        if (j + k >= n) break;
-        const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
-        const int row = q - q_lo;
-        const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
-        uint32_t ca, cb;
-        pair_at(clo, chi, k, ca, cb);
-        const int ccell = cc0 + x.dir * k;
-        const int xcell = C + 4 + ((j + k == 0) ? 0 : ctx_code(ca, cb));
-        if (__builtin_expect(full && rgwin && (unsigned)row < (unsigned)qw, 1)) {
+        for (int k = 0; k < kChunk; ++k) {
+          const int kk = kObsVariant == 2 ? (k + (int)rot) & 15 : k;  // the chunk offset this step visits
+          const int q = (int)(int8_t)(uint8_t)(qr[k >> 2] >> (8 * (k & 3)));
+          const int row = q - q_lo;
+          const bool valid = j + kk < n;
+          const bool fast = full_rg && valid && (unsigned)row < (unsigned)qw;
+          const bool masked = (bmr >> k) & 1u;
+          const int ccell = cc0 + x.dir * kk;
+          const int xcell = C + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu);
           const int base = row * cells;
-          atomicAdd(masked ? &w_masked[row] : &w_obs[base + ccell], 1u);
-          if (!masked) {
-            atomicAdd(&w_obs[base + xcell], 1u);
-            if (__builtin_expect(mism, 0)) {
-              atomicAdd(&w_mm[base + ccell], 1u);
-              atomicAdd(&w_mm[base + xcell], 1u);
+          if (kObsVariant == 0) {
+            if (fast) {
+              atomicAdd(masked ? &w_masked[row] : &w_obs[base + ccell], 1u);
+              if (!masked) atomicAdd(&w_obs[base + xcell], 1u);
             }
+          } else {
+            uint32_t* a1 = fast ? (masked ? &w_masked[row] : &w_obs[base + ccell]) : &dummy[lane];
+            uint32_t* a2 = fast ? &w_obs[base + xcell] : &dummy[lane];
+            atomicAdd(a1, 1u);
+            atomicAdd(a2, masked ? 0u : 1u);
           }
-        } else if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-          report(P.err, err_key((uint64_t)x.r, (uint32_t)(o0 + k), kRankTable, BQSR_ERR_QUAL_RANGE));
-        } else if (full) {  // outside the LDS window: straight to the int64 table
-          atomicAdd(&blk_hist[q], 1u);
-          const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
-          atomicAdd((unsigned long long*)&P.touched[key], 1ull);
-          if (!masked) {
-            atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
-            atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
-            if (mism) {
-              atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
-              atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+          slow |= (uint32_t)(valid && !fast) << kk;
+          mmk |= (uint32_t)(fast && !masked) << kk;
+        }
+        mmk &= bx;
+        if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
+          const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+          while (mmk) {
+            const int k = __builtin_ctz(mmk);
+            mmk &= mmk - 1;
+            const int q = (int)(int8_t)qp[o0 + k];
+            const int base = (q - q_lo) * cells;
+            atomicAdd(&w_mm[base + cc0 + x.dir * k], 1u);
+            atomicAdd(&w_mm[base + C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
+          }
+        }
+        if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+          const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+          while (slow) {
+            const int k = __builtin_ctz(slow);
+            slow &= slow - 1;
+            const int o = o0 + k;
+            const int q = (int)(int8_t)qp[o];
+            if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+            } else if (full) {  // outside the LDS window: straight to the int64 table
+              const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
+              const int ccell = cc0 + x.dir * k;
+              const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
+              atomicAdd(&blk_hist[q], 1u);
+              const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
+              atomicAdd((unsigned long long*)&P.touched[key], 1ull);
+              if (!masked) {
+                atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
+                atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
+                if (mism) {
+                  atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
+                  atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+                }
+              }
             }
           }
         }
-      }
       }
     }
   }
@@ -793,9 +904,21 @@ __device__ void fold_tile_exact(const ReadsDev& rd, const ReadInfo* info, int64_
     if (F.S < seq_limit) {
       // small S: the binade changes every few additions -- plain sequential fold
       if (tid == 0) {
+        // eight increments are looked up ahead of their additions; the
+        // additions stay in stream order (a sequential fold is exact at any S,
+        // seq_limit only decides when the binade mode takes over)
         double S = F.S;
         int p = pos;
-        for (; p < n && S < seq_limit; ++p) S = S + F.t[F.stream[p]];
+        while (p < n && S < seq_limit) {
+          const int m = min(8, n - p);
+          double tv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) tv[i] = i < m ? F.t[F.stream[p + i]] : 0.0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (i < m) S = S + tv[i];
+          p += m;
+        }
         F.S = S;
         F.ntot = p;
       }
@@ -1245,9 +1368,22 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
   return (int32_t)0x80000000;          // log10(inf) = inf
 }
 
-// LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16][window ok qw u8]
-// Lane per read as in observe; each chunk's 16 recalibrated chars leave as one
-// 16-B store (the read's last, partial chunk byte by byte).
+// errorProbabilityToPhred bucket of p: the unbiased exponent's offset from
+// kQbElo and the top kQbBits mantissa bits, read straight off the high word
+// (sign, exponent, mantissa).  Values outside [0, kQbN) -- p <= 0, NaN, inf,
+// subnormal or out-of-range binades -- take phred_q's full path.
+constexpr uint32_t kQbBase = (uint32_t)(1023 + kQbElo) << kQbBits;
+__device__ __forceinline__ uint32_t phred_bucket(double p) {
+  return ((uint32_t)((uint64_t)__double_as_longlong(p) >> 32) >> (20 - kQbBits)) - kQbBase;
+}
+
+// LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16]
+// Lane per read as in observe.  Per offset the fast path is branch-free: two
+// LDS doubles, one add, the bucket's threshold and Q; offsets it cannot
+// finish (key outside the window or not in the table, p outside the bucket
+// range, a char above 0xFF, the read only being checked) set a bit of `slow`
+// and are redone after the chunk's store by the exact checked path.  Each
+// chunk's 16 chars leave as one 16-B store (a read's last chunk byte-wise).
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
@@ -1255,15 +1391,15 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   double* w_d2 = w_s1 + qw * C;
   double* l_qbt = w_d2 + qw * kCtxSlots;
   int16_t* l_qbq = (int16_t*)(l_qbt + kQbN);
-  uint8_t* w_ok = (uint8_t*)(l_qbq + kQbN);
 
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
   const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
   const bool win_ok = rg_lo < P.n_rg;
   const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
   // rows whose key is not in the table hold NaN: the fast path sends such
-  // bases to the checked path below (a valid a2 + deltas is never NaN)
+  // bases to the checked path (a valid a2 + deltas is never NaN)
   for (int i = tid; i < qw * C; i += blockDim.x) {
     const int slot = i / C;
     const bool ok = win_ok && q_lo + slot < kQBins && P.rq_ok[rq0 + slot];
@@ -1277,7 +1413,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     l_qbt[i] = P.qb_thr[i];
     l_qbq[i] = P.qb_q[i];
   }
-  for (int i = tid; i < qw; i += blockDim.x) w_ok[i] = (win_ok && q_lo + i < kQBins) ? P.rq_ok[rq0 + i] : 0;
   const int64_t nt = P.rd.n_tiles;
   const int64_t tb0 = nt * blockIdx.x / gridDim.x, tb1 = nt * (blockIdx.x + 1) / gridDim.x;
   const int64_t r_begin = tb0 * P.rd.reads_per_tile, r_end = min(tb1 * (int64_t)P.rd.reads_per_tile, P.rd.n_reads);
@@ -1296,7 +1431,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     }
     const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
     const int n = (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) ? x.en - x.st : 0;
-    const bool rgwin = x.rg == rg_lo;
+    const bool fast_rd = app && x.rg == rg_lo;
     const uint8_t* qp = P.rd.qual + x.slot;
     uint8_t* op = P.out_qual + x.slot;
     for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
@@ -1312,77 +1447,113 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
         cn0[i] = chunk_n0(x, o0);
         cr[i] = (live && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
       }
+      // the super-chunk's chars, stored together after its last chunk so the
+      // lines they share are written while resident in L2
+      uint4 outs[kSub];
 #pragma clang loop unroll(full)
       for (int i = 0; i < kSub; ++i) {
-      const int j = j0 + kChunk * i;
-      if (j >= n) continue;
-      const int o0 = x.st + j;
-      const uint4 qv = qs[i];
-      uint32_t out[4];
-      if (pass) {  // the original chars: (qual + 33) byte-wise
-        const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+        const int j = j0 + kChunk * i;
+        if (j >= n) continue;
+        const int o0 = x.st + j;
+        const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
+        uint32_t out[4];
+        uint32_t slow = 0;
+        uint32_t xo[4] = {4u, 4u, 4u, 4u};
+        if (pass) {  // the original chars: (qual + 33) byte-wise
 #pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
-      } else {
-        uint64_t clo = 0;
-        uint32_t chi = 0;
-        chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
-        const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
-      const int cc0 = x.cell0 + x.dir * o0;
-        out[0] = out[1] = out[2] = out[3] = 0;
+          for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
+        } else {
+          uint64_t clo = 0;
+          uint32_t chi = 0;
+          chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
+          ctx_slots(clo, chi, xo);
+          if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+          const int cc0 = x.cell0 + x.dir * o0;
+          out[0] = out[1] = out[2] = out[3] = 0;
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-          if (j + k >= n) break;
-          const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
-          const int row = q - q_lo;
-          uint32_t ca, cb;
-          pair_at(clo, chi, k, ca, cb);
-          const int ccell = cc0 + x.dir * k;
-          const int ctx = (j + k == 0) ? 0 : ctx_code(ca, cb);
-          uint32_t code;
-          // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-          const bool inwin = app && rgwin && (unsigned)row < (unsigned)qw;
-          const int rowc = inwin ? row : 0;
-          double p = w_s1[rowc * C + ccell] + w_d2[rowc * kCtxSlots + ctx + 4];
-          if (__builtin_expect(!inwin || p != p, 0)) {
+          for (int k = 0; k < kChunk; ++k) {
+            const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+            const int row = q - q_lo;
+            const bool inwin = fast_rd && (unsigned)row < (unsigned)qw;
+            const int rowc = inwin ? row : 0;
+            const int ccell = cc0 + x.dir * k;
+            const int xs = (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+            // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+            const double p = w_s1[rowc * C + ccell] + w_d2[rowc * kCtxSlots + xs];
+            const uint32_t b = phred_bucket(p);
+            const bool bok = b < (uint32_t)kQbN;
+            const uint32_t bc = bok ? b : 0u;
+            const int qq = l_qbq[bc];
+            const int Q = p <= l_qbt[bc] ? qq : qq - 1;
+            const uint32_t code = (uint32_t)(Q + 33);  // (Q + 33).toChar, <= 0xFF on this path
+            const bool good = inwin && bok && qq != -32768 && code <= 0xFFu;
+            slow |= (uint32_t)(!good && j + k < n) << k;
+            out[k >> 2] |= (code & 0xFFu) << (8 * (k & 3));
+          }
+        }
+        // ---- the checked path, in offset order (the first failing offset wins) ----
+        if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+          const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+          while (slow) {
+            const int k = __builtin_ctz(slow);
+            slow &= slow - 1;
+            const int o = o0 + k;
+            const int q = (int)(int8_t)qp[o];
+            const int xs = (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
             // key validity as getReadGroupDelta / getQualScoreDelta see it
             const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
             const int64_t gr = (key - 1) / kMaxQ;
             const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
             const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
             if (!grp || !kok) {
-              report(P.err, err_key((uint64_t)x.r, (uint32_t)(o0 + k), kRankTable, BQSR_ERR_MISSING_KEY));
+              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
               continue;
             }
             if (q < 0) {
-              report(P.err, err_key((uint64_t)x.r, (uint32_t)(o0 + k), kRankTable, BQSR_ERR_QUAL_RANGE));
+              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
               continue;
             }
             if (!app) continue;
             const int64_t rq = (int64_t)x.rg * kQBins + q;
-            p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + ctx + 4];
-          }
-          const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
-          code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-          if (__builtin_expect(code > 0xFFu, 0)) {
-            const unsigned long long e = atomicAdd(P.n_exc, 1ull);
-            if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)(o0 + k)) << 16) | code;
-          }
-          out[k >> 2] |= (code & 0xFFu) << (8 * (k & 3));
-        }
-      }
-      if (!(app || pass)) continue;
-      if (j + kChunk <= n) {
-        *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
-      } else {
+            const int ccell = x.cell0 + x.dir * o;
+            const double p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + xs];
+            const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
+            const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+            if (code > 0xFFu) {
+              const unsigned long long e = atomicAdd(P.n_exc, 1ull);
+              if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
+            }
+            const uint32_t sh = 8u * (uint32_t)(k & 3);
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k)
-          if (k < n - j) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+            for (int w = 0; w < 4; ++w)
+              if (w == (k >> 2)) out[w] = (out[w] & ~(0xFFu << sh)) | ((code & 0xFFu) << sh);
+          }
+        }
+        outs[i] = make_uint4(out[0], out[1], out[2], out[3]);
       }
+      if (app || pass) {
+#pragma clang loop unroll(full)
+        for (int i = 0; i < kSub; ++i) {
+          const int j = j0 + kChunk * i;
+          if (j >= n) continue;
+          const int o0 = x.st + j;
+          if (j + kChunk <= n) {
+            *(uint4*)(op + o0) = outs[i];
+          } else {
+            const uint32_t ov[4] = {outs[i].x, outs[i].y, outs[i].z, outs[i].w};
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k)
+              if (k < n - j) op[o0 + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+          }
+        }
       }
     }
   }
 }
+
+template __global__ void bqsr_observe_kernel<0>(ObserveParams);
+template __global__ void bqsr_observe_kernel<1>(ObserveParams);
+template __global__ void bqsr_observe_kernel<2>(ObserveParams);
 
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {

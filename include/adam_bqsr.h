@@ -163,8 +163,8 @@ typedef struct bqsr_device_reads {
                              the 32 bytes past the end must be readable (16-B loads) */
   const uint8_t* bases;   /* [(n_slots+1)/2 + 32] 4-bit codes A0 C1 G2 T3 N4 other5,
                              low nibble first; 32 readable bytes of padding likewise */
-  const uint32_t* cigar;  /* BAM elements                                             */
-  const uint8_t* md;      /* MD bytes                                                 */
+  const uint32_t* cigar;  /* BAM elements; 32 readable bytes of padding past the end     */
+  const uint8_t* md;      /* MD bytes; 32 readable bytes of padding past the end        */
   bqsr_dims dims;
 } bqsr_device_reads;
 bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* dev, bqsr_batch** out);
