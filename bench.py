@@ -53,6 +53,7 @@ def main():
     import torch.distributed as dist
 
     from adam_amd import _capi, bqsr, synth
+    from adam_amd import distributed as D
     from adam_amd._capi import Dims, check
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,15 +114,10 @@ def main():
         ev[2].record(stream)
         em = ctypes.c_double()
         check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
-        if world > 1:
-            dist.all_reduce(table_t)  # exact int64 sum over xGMI (RCCL)
-            ems = torch.zeros(world, dtype=torch.float64, device=dev)
-            dist.all_gather_into_tensor(ems, torch.tensor([em.value], dtype=torch.float64, device=dev))
-            total = 0.0
-            for v in ems.tolist():  # RecalTable.++ in rank order
-                total = total + v
-        else:
-            total = 0.0 + em.value
+        # RecalTable.++ across ranks: exact int64 all-reduce over xGMI (RCCL),
+        # expectedMismatch folded in rank order (adam_amd/distributed.py)
+        D.allreduce_table(table_t)
+        total = D.fold_expected_mismatch(em.value, dev)
         check(L.bqsr_finalize_async(ctx.handle, th, total, ctypes.byref(lut), sp))
         check(L.bqsr_finalize_result(lut, sp))
         check(L.bqsr_apply_stage(ctx.handle, bh, lut, ctypes.c_void_p(out_qual.data_ptr()),

@@ -1,0 +1,93 @@
+"""The multi-rank path (adam_amd/distributed.py) with world_size 2 on gloo:
+each rank observes its contiguous shard, the int64 tables are all-reduced, the
+expectedMismatch doubles are all-gathered and folded in rank order, and every
+rank finalizes the same table.  The per-rank observe here is the CPU oracle
+(the same call sequence the GPU ranks make through the C ABI in bench.py);
+the result must equal a single process folding the same shards as
+consecutive partitions."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from adam_amd import distributed as D
+    from adam_amd import synth
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        batch = synth.generate(3000, (100,), 2, 77)
+        d = O.Dims(2, 100)
+        r0, r1 = D.shard_bounds(batch.n_reads, rank, WORLD)
+        words, em = O.observe(batch, None, d, r0, r1)
+        t = torch.from_numpy(words.copy())
+        D.allreduce_table(t)
+        total = D.fold_expected_mismatch(em)
+        fin = O.Final(d, t.numpy(), total)
+        out, out_len = O.apply(batch, fin, r0, r1)
+        np.savez(os.path.join(out_dir, "rank%d.npz" % rank), words=t.numpy(), em=np.array([total]),
+                 out=out, out_len=out_len, r0=r0, r1=r1)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_table_allreduce_and_rank_order_fold(tmp_path):
+    import oracle as O
+    from adam_amd import synth
+    from adam_amd.distributed import shard_bounds
+
+    mp.start_processes(_rank_main, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    batch = synth.generate(3000, (100,), 2, 77)
+    d = O.Dims(2, 100)
+    # single process, the two shards as consecutive partitions merged in order
+    words = np.zeros(O.table_words(d), dtype=np.int64)
+    em = 0.0
+    for rank in range(WORLD):
+        r0, r1 = shard_bounds(batch.n_reads, rank, WORLD)
+        w, e = O.observe(batch, None, d, r0, r1)
+        words += w
+        em = em + e
+    fin = O.Final(d, words, em)
+    ref_out, ref_len = O.apply(batch, fin)
+    for rank in range(WORLD):
+        z = np.load(tmp_path / ("rank%d.npz" % rank))
+        assert np.array_equal(z["words"], words)
+        assert z["em"][0] == em  # bit-exact: rank-order fold == partition-order merge
+        r0, r1 = int(z["r0"]), int(z["r1"])
+        a, b = int(batch.qual_offset[r0]), int(batch.qual_offset[r1])
+        assert np.array_equal(z["out"][a:b], ref_out[a:b])
+        assert np.array_equal(z["out_len"][r0:r1], ref_len[r0:r1])
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (10, 3), (1001, 8)])
+def test_shard_bounds_cover_in_order(n, world):
+    from adam_amd.distributed import shard_bounds
+    bounds = [shard_bounds(n, r, world) for r in range(world)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == n
+    assert all(bounds[i][1] == bounds[i + 1][0] for i in range(world - 1))
+    sizes = [b - a for a, b in bounds]
+    assert max(sizes) - min(sizes) <= 1

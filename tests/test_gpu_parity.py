@@ -159,3 +159,25 @@ def test_all_masked():
     # every observed base is an insertion: avg = em / 0 -> NaN shifts -> Q0
     recs = [rec(cigar="10I", mismatching_positions="0"), rec(mismatching_positions=None)]
     check([RecordBatch.from_records(recs)])
+
+
+# ---- committed golden fixtures (tests/golden/g1_g2.json) ------------------------
+
+@pytest.mark.parametrize("name", ["g1", "g2"])
+def test_golden_fixture(name):
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden import g1_batch, g2_batch
+    with open(os.path.join(os.path.dirname(__file__), "golden", "g1_g2.json")) as fh:
+        fx = json.load(fh)[name]
+    b = g1_batch() if name == "g1" else g2_batch()
+    g = run_gpu([b])
+    assert g.error is None
+    nz = np.nonzero(g.words)[0]
+    assert {str(int(i)): int(g.words[i]) for i in nz} == fx["table_nonzero"]
+    assert float(g.em).hex() == fx["expected_mismatch"]
+    chars, out_len = g.outs[0]
+    got = [[int(c) for c in chars[int(b.qual_offset[r]):int(b.qual_offset[r]) + int(out_len[r])]]
+           for r in range(b.n_reads)]
+    assert got == fx["chars"]

@@ -1,0 +1,65 @@
+"""Host-side ingest: SAM -> ADAMRecord columns with SAMRecordConverter
+semantics (converters/SAMRecordConverter.scala:26-144,
+models/RecordGroupDictionary.scala:36-43), and the RecordBatch round trip the
+C ABI consumes."""
+import os
+
+import numpy as np
+import pytest
+
+from adam_amd import records as R
+from adam_amd.records import ADAMRecord, RecordBatch, cigar_to_text, parse_cigar, read_sam
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_resources")
+
+
+def recs(name):
+    return read_sam(os.path.join(GOLD, name)).to_records()
+
+
+def test_flag_zero_reads_are_unmapped_and_non_primary():
+    # Q2: the converter sets flags only when flags != 0 (SAMRecordConverter.scala:74)
+    rs = recs("small.sam")
+    zero = [r for r in rs if not (r.read_mapped or r.read_negative_strand or r.read_paired)]
+    assert zero and all(not r.read_mapped and not r.primary_alignment for r in zero)
+    rev = [r for r in rs if r.read_negative_strand]
+    assert rev and all(r.read_mapped and r.primary_alignment for r in rev)
+
+
+def test_start_is_zero_based_and_qual_star_kept():
+    r = recs("small.sam")[0]
+    assert r.start == 26472784 - 1
+    assert r.qual == "*"  # getBaseQualityString is "*" and is stored as is
+    assert r.mismatching_positions is None
+
+
+def test_record_group_index_is_sorted_name_order():
+    rs = recs("artificial.realigned.sam")
+    assert {r.record_group_id for r in rs} == {0}
+    rs = recs("artificial.sam")  # MD but no RG header entry -> null recordGroupId (Q1)
+    assert all(r.record_group_id is None for r in rs)
+    assert any(r.mismatching_positions is not None for r in rs)
+
+
+def test_flags_of_realigned_pairs():
+    rs = recs("artificial.realigned.sam")
+    first = [r for r in rs if r.read_paired and not r.second_of_pair]
+    second = [r for r in rs if r.second_of_pair]
+    assert len(first) == 5 and len(second) == 5
+    assert sum(r.mismatching_positions is not None for r in first) == 3
+
+
+@pytest.mark.parametrize("text", ["10M", "3H2S5M4S", "1S28M1D32M1I15M1D23M", "3M1P2N7M", "5=2X"])
+def test_cigar_round_trip(text):
+    assert cigar_to_text(parse_cigar(text)) == text
+
+
+def test_batch_round_trip_and_offsets():
+    b = read_sam(os.path.join(GOLD, "small_realignment_targets.sam"))
+    rs = b.to_records()
+    b2 = RecordBatch.from_records(rs)
+    assert b2.n_reads == b.n_reads
+    assert np.array_equal(b2.flags, b.flags)
+    assert np.array_equal(b2.qual_offset, b.qual_offset)
+    assert b.n_bases == int(sum(len(r.sequence) for r in rs))
+    assert [r.flag_bits & R.F_HAS_MD != 0 for r in rs] == [r.mismatching_positions is not None for r in rs]
