@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the config's)")
-    ap.add_argument("--cpu-reads", type=int, default=1_000_000, help="oracle baseline sample (reads)")
+    ap.add_argument("--cpu-reads", type=int, default=10_000_000, help="oracle baseline sample (reads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
@@ -166,11 +166,13 @@ def main():
         dom = "observe" if ms["observe"] >= ms["apply"] else "apply"
         achieved = alg[dom] / (ms[dom] * 1e-3) / 1e9
         traffic = None
-        try:
+        kname = "bqsr_%s_kernel" % dom
+        try:  # PMC bytes of the same kernel on the same workload (tools/fetch_profile.sh)
             with open(args.traffic) as fh:
                 tr = json.load(fh)
             if tr.get("config") == args.config and tr.get("reads_per_gpu") == R:
                 traffic = tr["kernels"].get(dom, {}).get("hbm_bytes_per_launch")
+                kname = tr["kernels"].get(dom, {}).get("kernel", kname)
         except (OSError, ValueError, KeyError):
             traffic = None
         value = args.steps * total_bases / elapsed
@@ -198,7 +200,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "bqsr_%s_kernel" % dom,
+                "kernel": kname,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -212,22 +214,23 @@ def main():
             "gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args, cfg)
+            line["cpu_baseline"] = cpu_baseline(args, cfg, batch, sites)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, cfg):
-    """The oracle (C++ restatement of ADAM BQSR, oracle/) on a bounded sample of
-    the same workload, std::thread x cores; partitions = threads."""
+def cpu_baseline(args, cfg, batch, sites):
+    """The oracle (C++ restatement of ADAM BQSR, oracle/) timed on this host's
+    cores over a bounded sample of the same workload: the first --cpu-reads
+    reads of the GPU's own shard, observe per partition -> merge in order ->
+    finalize -> apply, one std::thread per partition; plus one thread on an
+    eighth of the sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    from adam_amd import synth
     cores = min(16, len(os.sched_getaffinity(0)))
-    n = args.cpu_reads
-    sample = synth.generate(n, cfg["lens"], cfg["n_rg"], cfg["seed"])
-    sites = synth.known_sites(cfg["sites"]) if cfg["sites"] else None
+    n = min(args.cpu_reads, batch.n_reads)
+    sample = batch.slice(0, n) if n < batch.n_reads else batch
     osites = O.Sites(sites) if sites else None
     d = O.Dims(cfg["n_rg"], max(cfg["lens"]))
     t = time.perf_counter()
@@ -238,9 +241,10 @@ def cpu_baseline(args, cfg):
     O.bqsr(one, osites, d, n_parts=1, nthreads=1)
     dt1 = time.perf_counter() - t1
     return {"value": sample.n_bases / dt, "unit": "bases/s", "cores": cores, "kind": "port",
-            "sample": "%d reads (%d bases) of %s, observe+merge+finalize+apply, %d partitions" %
-                      (n, sample.n_bases, args.config, cores),
-            "value_1thread": one.n_bases / dt1, "seconds": dt}
+            "sample": "first %d reads (%d bases) of the %s shard, observe+merge+finalize+apply, %d partitions "
+                      "on %d threads (%.1f s); value_1thread on the first %d reads (%.1f s)" %
+                      (n, sample.n_bases, args.config, cores, cores, dt, one.n_reads, dt1),
+            "value_1thread": one.n_bases / dt1}
 
 
 if __name__ == "__main__":
