@@ -178,14 +178,6 @@ int observe_qw(int cells) {
   while (qw > 1 && observe_lds(qw, cells) > kLdsMax) --qw;
   return qw;
 }
-// observe fast-path variant (bqsr_observe_kernel<V>); ADAM_BQSR_OBSERVE_VARIANT overrides while tuning
-int observe_variant() {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_OBSERVE_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 int apply_qw(int C) {
   int qw = 64;
   while (qw > 1 && apply_lds(qw, C) > kLdsMax) --qw;
@@ -226,6 +218,8 @@ struct bqsr_batch {
   int64_t n_slots = 0;
   int64_t n_bases = 0;
   int32_t q_lo = 0, rg_lo = 0;  // LDS window choice
+  bool have_qhist = false;      // q_lo follows qhist at each launch's window width
+  int64_t qhist[kQBins] = {0};
   std::vector<void*> allocs;
   // per-read prep results (valid once `prepped`)
   ReadInfo* d_info = nullptr;
@@ -243,6 +237,17 @@ struct bqsr_batch {
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
   int32_t n_blocks = 0;
+  // read-group buckets (OrderDev): several read groups -> the per-base passes
+  // walk the reads grouped by read group
+  bool bucketed = false;
+  int32_t n_keys = 1;
+  uint32_t* d_perm = nullptr;
+  int64_t* d_key_off = nullptr;
+  uint32_t* d_key_cnt = nullptr;
+  uint32_t* d_cursor = nullptr;
+  OrderDev order() const {
+    return bucketed ? OrderDev{d_perm, d_key_off, n_keys} : OrderDev{nullptr, nullptr, 1};
+  }
   ~bqsr_batch() {
     if (d_part) (void)hipFree(d_part);
     for (void* p : allocs) (void)hipFree(p);
@@ -322,9 +327,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  for (const void* f : {(const void*)bqsr_observe_kernel<0>, (const void*)bqsr_observe_kernel<1>,
-                        (const void*)bqsr_observe_kernel<2>})
-    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e != hipSuccess) {
@@ -437,6 +441,16 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
+  // read-group buckets: on for several read groups (ADAM_BQSR_ORDER=read / group forces either)
+  const char* ord = getenv("ADAM_BQSR_ORDER");
+  b->bucketed = ord ? strcmp(ord, "group") == 0 : b->dims.n_rg > 1;
+  if (b->bucketed) {
+    b->n_keys = std::max<int32_t>(1, b->dims.n_rg);
+    if ((st = dalloc(b->allocs, &b->d_perm, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
+    if ((st = dalloc(b->allocs, &b->d_key_off, (size_t)b->n_keys + 1)) != BQSR_OK) return st;
+    if ((st = dalloc(b->allocs, &b->d_key_cnt, (size_t)b->n_keys)) != BQSR_OK) return st;
+    if ((st = dalloc(b->allocs, &b->d_cursor, (size_t)b->n_keys)) != BQSR_OK) return st;
+  }
   return BQSR_OK;
 }
 
@@ -578,6 +592,8 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
     if (P.rghist[(size_t)i] > P.rghist[(size_t)rg_lo]) rg_lo = i;
   b->rg_lo = rg_lo;
   b->q_lo = best_q_lo(P.qhist, 40);
+  b->have_qhist = true;
+  for (int q = 0; q < kQBins; ++q) b->qhist[q] = P.qhist[q];
   ReadMeta* meta;
   ReadAlign* align;
   uint8_t *qual, *bases, *md;
@@ -655,6 +671,7 @@ bqsr_status bqsr_batch_set_window(bqsr_batch* b, int32_t q_lo, int32_t rg_lo) {
   if (!b || q_lo < 0 || q_lo >= kQBins || rg_lo < 0) return fail(BQSR_ERR_INVALID_ARG, "bad window");
   b->q_lo = q_lo;
   b->rg_lo = rg_lo;
+  b->have_qhist = false;
   return ok();
 }
 int32_t bqsr_batch_reads_per_tile(const bqsr_batch* b) { return b ? b->rd.reads_per_tile : -1; }
@@ -723,6 +740,11 @@ bqsr_status bqsr_table_merge(bqsr_table* acc, const bqsr_table* part, double* ac
 // -------------------------------------------------------------- observe ----
 
 namespace {
+// first window row: the densest qw-wide qual range of the batch when its
+// histogram is known, else the caller's choice (bqsr_batch_set_window)
+int32_t window_q_lo(const bqsr_batch* b, int qw) {
+  return b->have_qhist ? best_q_lo(b->qhist, qw) : std::min(b->q_lo, kQBins - 1);
+}
 bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
   if (b->dims.n_rg > t->dims.n_rg || b->dims.max_len > t->dims.max_len)
     return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's (n_rg / max_len)");
@@ -751,6 +773,19 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     const int64_t blocks = std::min<int64_t>((b->rd.n_reads + 255) / 256, (int64_t)ctx->n_cu * 32);
     hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P);
     HIP_TRY(hipGetLastError());
+    if (b->bucketed) {  // counting sort of the reads by read group
+      const int64_t n = b->rd.n_reads;
+      HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
+      const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
+      hipLaunchKernelGGL(bqsr_key_count, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
+                         b->d_key_cnt);
+      hipLaunchKernelGGL(bqsr_key_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)b->d_key_cnt, b->n_keys,
+                         b->d_key_off, b->d_cursor);
+      const unsigned sb = (unsigned)std::min<int64_t>((n + 4095) / 4096, (int64_t)ctx->n_cu * 8);
+      hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
+                         b->d_cursor, b->d_perm);
+      HIP_TRY(hipGetLastError());
+    }
   }
   b->prepped = true;
   b->prep_sites = sites;
@@ -778,17 +813,18 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   if (stages & BQSR_STAGE_KERNEL) {
     ObserveParams P{};
     P.rd = b->rd;
+    P.ord = b->order();
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
     P.w.qw = observe_qw(P.g.cells);
-    P.w.q_lo = std::min(b->q_lo, kQBins - 1);
+    P.w.q_lo = window_q_lo(b, P.w.qw);
     P.w.rg_lo = b->rg_lo;
     P.touched = t->touched();
     P.obs = t->obs();
     P.mm = t->mm();
     P.part_stride = 2 * P.w.qw * P.g.cells + P.w.qw;
-    const size_t need = (size_t)P.part_stride * b->n_blocks;
+    const size_t need = (size_t)P.part_stride * (b->n_blocks + b->n_keys - 1);  // slabs w + key
     if (b->part_words < need) {  // grows with the table geometry; kept across calls
       if (b->d_part) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -804,18 +840,19 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
     const size_t lds = observe_lds(P.w.qw, P.g.cells);
-    switch (observe_variant()) {
-      case 1: hipLaunchKernelGGL(bqsr_observe_kernel<1>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P); break;
-      case 2: hipLaunchKernelGGL(bqsr_observe_kernel<2>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P); break;
-      default: hipLaunchKernelGGL(bqsr_observe_kernel<0>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P); break;
-    }
+    hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
-    const int rb = (int)std::min<int64_t>(1024, (P.part_stride + 255) / 256);
-    hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb), dim3(256), 0, s, (const uint32_t*)b->d_part, b->n_blocks,
-                       P.part_stride, P.w, P.g, P.touched, P.obs, P.mm);
+    const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_keys : 1) + 255) / 256);
+    hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
+                       b->n_blocks, P.part_stride, P.w, P.g, P.touched, P.obs, P.mm);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
+    if (b->bucketed) {  // the observe kernel did not walk the fold's blocks: their histograms
+      hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks), dim3(1024), 0, s, b->rd, (const ReadInfo*)b->d_info,
+                         b->n_blocks, b->d_hq);
+      HIP_TRY(hipGetLastError());
+    }
     int32_t* n_cand = b->d_cand_list + b->n_blocks;
     hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(256), 0, s, (const uint32_t*)b->d_hq, (const double*)ctx->d_pow10,
                        b->n_blocks, b->d_cand, b->d_cand_list, n_cand);
@@ -1080,10 +1117,11 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   if (b->rd.n_reads == 0 || !(stages & BQSR_STAGE_KERNEL)) return ok();
   ApplyParams P{};
   P.rd = b->rd;
+  P.ord = b->order();
   P.info = b->d_info;
   P.g = geom(L->dims);
   P.w.qw = apply_qw(P.g.C);
-  P.w.q_lo = std::min(b->q_lo, kQBins - 1);
+  P.w.q_lo = window_q_lo(b, P.w.qw);
   P.w.rg_lo = b->rg_lo;
   P.n_rg = L->dims.n_rg;
   P.s1 = L->s1;

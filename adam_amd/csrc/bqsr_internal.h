@@ -141,8 +141,23 @@ struct PrepParams {
   unsigned long long* err;  // error words
 };
 
+// Read order of the per-base passes.  With one read group the passes walk the
+// batch in read order (perm == nullptr).  With several, reads are bucketed by
+// read group (a device counting sort, bqsr_key_*): sorted position i holds
+// read perm[i], and key_off[g] .. key_off[g+1] are the positions of group g.
+// Workgroup w takes the positions [a_w, a_w+1) (tile-aligned, wg_begin) and
+// walks them as "pieces", one per read group it meets, with that group's rows
+// in its LDS window: a piece's counts go to slab (w + g).  (w + g is unique:
+// the group is nondecreasing along the sorted order.)
+struct OrderDev {
+  const uint32_t* perm;    // [n_reads] or nullptr (identity, one piece per workgroup, group = Window::rg_lo)
+  const int64_t* key_off;  // [n_keys + 1]
+  int32_t n_keys;
+};
+
 struct ObserveParams {
   ReadsDev rd;
+  OrderDev ord;
   const ReadInfo* info;
   const uint64_t* sbits;  // PrepParams::sbits
   TableGeom g;
@@ -150,9 +165,10 @@ struct ObserveParams {
   int64_t* touched;  // [K]
   int64_t* obs;      // [K*cells]
   int64_t* mm;       // [K*cells]
-  uint32_t* part;      // [n_blocks][part_stride] per-block window counts (obs, mm, touched)
+  uint32_t* part;      // [n_blocks + n_keys - 1][part_stride] per-piece window counts (obs, mm, touched)
   int32_t part_stride; // 2*qw*cells + qw
-  uint32_t* hq_block;  // [n_blocks][128] per-block qual histogram of folded bases
+  uint32_t* hq_block;  // [n_blocks][128] per-block qual histogram of folded bases (identity order only;
+                       // bucketed batches get it from bqsr_fold_hist)
   unsigned long long* err;
   int32_t n_blocks;
 };
@@ -179,6 +195,7 @@ constexpr int kQbN = (kQbEhi - kQbElo + 1) << kQbBits;
 
 struct ApplyParams {
   ReadsDev rd;
+  OrderDev ord;
   const ReadInfo* info;
   TableGeom g;
   Window w;

@@ -485,12 +485,12 @@ struct LaneRead {
   int cell0, dir; // cycle cell of offset o = cell0 + dir * o (DiscreteCycle + L)
 };
 
-__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, int64_t r_end, int L) {
+__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L) {
   LaneRead x;
-  x.r = r;
+  x.r = live ? r : rd.n_reads;
   ReadMeta m{0, 0, 0, 0, 0};
   ReadInfo inf{0, 0, 0, 0};
-  if (r < r_end) {
+  if (live) {
     m = rd.meta[r];
     inf = info[r];
   }
@@ -514,6 +514,33 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
   }
   return x;
 }
+
+// ---- read order and pieces (OrderDev) ----
+// first sorted position of workgroup w's range: whole tiles, as the fold's
+// blocks (identity order: workgroup w's range IS fold block w)
+__device__ __forceinline__ int64_t wg_begin(const ReadsDev& rd, int64_t w, int G) {
+  return min(rd.n_tiles * w / G * (int64_t)rd.reads_per_tile, rd.n_reads);
+}
+// the workgroup whose range holds sorted position p (the largest w with wg_begin(w) <= p)
+__device__ __forceinline__ int64_t wg_of(const ReadsDev& rd, int64_t p, int G) {
+  const int64_t t = p / rd.reads_per_tile;
+  return min((int64_t)G - 1, ((t + 1) * G - 1) / rd.n_tiles);
+}
+__device__ __forceinline__ int order_keys(const OrderDev& o) { return o.perm ? o.n_keys : 1; }
+__device__ __forceinline__ int64_t key_begin(const OrderDev& o, int64_t n, int g) {
+  return o.perm ? o.key_off[g] : (g == 0 ? 0 : n);
+}
+// the key holding sorted position p: the largest g with key_off[g] <= p
+__device__ __forceinline__ int key_at(const OrderDev& o, int64_t p) {
+  if (!o.perm) return 0;
+  int lo = 0, hi = o.n_keys - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (o.key_off[mid] <= p) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+__device__ __forceinline__ int64_t order_read(const OrderDev& o, int64_t i) { return o.perm ? (int64_t)o.perm[i] : i; }
 
 
 // The 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
@@ -584,25 +611,13 @@ __device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[
   }
 }
 
-// 16 bytes rotated right by r (0..15) bytes: byte k of the result = byte (k + r) & 15
-__device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
-  const uint32_t d = r >> 2, b = r & 3;
-  uint32_t t0 = (d & 1) ? w[1] : w[0], t1 = (d & 1) ? w[2] : w[1];
-  uint32_t t2 = (d & 1) ? w[3] : w[2], t3 = (d & 1) ? w[0] : w[3];
-  const uint32_t u0 = (d & 2) ? t2 : t0, u1 = (d & 2) ? t3 : t1, u2 = (d & 2) ? t0 : t2, u3 = (d & 2) ? t1 : t3;
-  w[0] = __builtin_amdgcn_alignbyte(u1, u0, b);
-  w[1] = __builtin_amdgcn_alignbyte(u2, u1, b);
-  w[2] = __builtin_amdgcn_alignbyte(u3, u2, b);
-  w[3] = __builtin_amdgcn_alignbyte(u0, u3, b);
-}
-
 // ------------------------------------------------------------ observe ------
 
 // LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32][block hist 128 u32]
-// The window holds the block's counts for rows (rg_lo, q_lo..q_lo+qw-1); other
-// keys go straight to the int64 table.  The block's window is written to
-// `part` and summed into the table by bqsr_window_reduce.
-template <int kObsVariant>
+// The window holds a piece's counts for rows (rg, q_lo..q_lo+qw-1) where rg is
+// the piece's read group; other keys go straight to the int64 table.  Each
+// piece's window is written to its slab of `part` and summed into the table by
+// bqsr_window_reduce.
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -610,133 +625,122 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   uint32_t* w_mm = w_obs + qw * cells;
   uint32_t* w_masked = w_mm + qw * cells;
   uint32_t* blk_hist = w_masked + qw;
-  uint32_t* dummy = blk_hist + kQBins;  // [64] sink of the branch-free fast path
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < 2 * qw * cells + qw; i += blockDim.x) w_obs[i] = 0;
+  const int G = P.n_blocks;
+  const bool ident = P.ord.perm == nullptr;
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
-  const int64_t nt = P.rd.n_tiles;
-  const int64_t tb0 = nt * blockIdx.x / P.n_blocks, tb1 = nt * (blockIdx.x + 1) / P.n_blocks;
-  const int64_t r_begin = tb0 * P.rd.reads_per_tile, r_end = min(tb1 * (int64_t)P.rd.reads_per_tile, P.rd.n_reads);
-  __syncthreads();
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+  const int q_lo = P.w.q_lo;
+  const int nk = order_keys(P.ord);
 
-  const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
-  for (int64_t g0 = r_begin + 64 * wave; g0 < r_end; g0 += 64 * kWaves) {
-    const LaneRead x = lane_read(P.rd, P.info, g0 + lane, r_end, L);
-    const bool act = x.fl & (kInfoObs | kInfoObsCheck);
-    const bool full = x.fl & kInfoObs;
-    const int n = act ? x.en - x.st : 0;
-    const bool full_rg = full && x.rg == rg_lo;
-    const uint8_t* qp = P.rd.qual + x.slot;
-    for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
-      if (j0 >= n) continue;
-      // issue every load of the super-chunk first
-      uint4 qs[kSub], cr[kSub];
-      uint64_t bw[3] = {0, 0, 0};
-      const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
+  for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
+    const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
+    const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
+    if (p0 >= wb) break;
+    if (p0 >= p1) continue;
+    const int rg_w = ident ? P.w.rg_lo : key;  // the read group of the window rows
+    for (int i = tid; i < 2 * qw * cells + qw; i += blockDim.x) w_obs[i] = 0;
+    __syncthreads();
+
+    for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
+      const bool live = g0 + lane < p1;
+      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + lane) : 0, live, L);
+      const bool act = x.fl & (kInfoObs | kInfoObsCheck);
+      const bool full = x.fl & kInfoObs;
+      const int n = act ? x.en - x.st : 0;
+      const bool full_rg = full && x.rg == rg_w;
+      const uint8_t* qp = P.rd.qual + x.slot;
+      for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
+        if (j0 >= n) continue;
+        // issue every load of the super-chunk first
+        uint4 qs[kSub], cr[kSub];
+        uint64_t bw[3] = {0, 0, 0};
+        const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
 #pragma unroll
-      for (int i = 0; i < kSub; ++i) {
-        const bool live = j0 + kChunk * i < n;
-        const int o0 = x.st + j0 + kChunk * i;
-        qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
-        cr[i] = (live && full) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
-      }
-      if (full) {
-        bw[0] = P.sbits[s0 >> 5];
-        bw[1] = P.sbits[(s0 >> 5) + 1];
-        bw[2] = P.sbits[(s0 >> 5) + 2];
-      }
-#pragma clang loop unroll(full)
-      for (int i = 0; i < kSub; ++i) {
-        const int j = j0 + kChunk * i;
-        if (j >= n) continue;
-        const int o0 = x.st + j;
-        const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
-        uint32_t bm = 0, bx = 0;
-        uint32_t xo[4] = {4u, 4u, 4u, 4u};
+        for (int i = 0; i < kSub; ++i) {
+          const bool lv = j0 + kChunk * i < n;
+          const int o0 = x.st + j0 + kChunk * i;
+          qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
+          cr[i] = (lv && full) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
+        }
         if (full) {
-          sub_bits(bw, (uint32_t)(s0 & 31), i, bm, bx);
-          uint64_t clo;
-          uint32_t chi;
-          chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
-          ctx_slots(clo, chi, xo);
-          if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+          bw[0] = P.sbits[s0 >> 5];
+          bw[1] = P.sbits[(s0 >> 5) + 1];
+          bw[2] = P.sbits[(s0 >> 5) + 2];
         }
-        const int cc0 = x.cell0 + x.dir * o0;
-        // Fast path.  kObsVariant (A/B knob while tuning): 0 = predicated
-        // increments; 1 = branch-free, offsets that do not count add to the
-        // lane's dummy word; 2 = as 1, with lane l visiting the chunk's
-        // offsets rotated by l & 15 so a wavefront's lanes hit different cycle
-        // cells at each step.  Offsets the fast path skips are redone below.
-        const uint32_t rot = kObsVariant == 2 ? (uint32_t)lane & 15u : 0u;
-        uint32_t qr[4] = {qd[0], qd[1], qd[2], qd[3]}, xr[4] = {xo[0], xo[1], xo[2], xo[3]};
-        uint32_t bmr = bm & 0xFFFFu;
-        if (kObsVariant == 2) {
-          rotr16(qr, rot);
-          rotr16(xr, rot);
-          bmr = ((bmr | (bm << 16)) >> rot) & 0xFFFFu;
-        }
-        uint32_t slow = 0, mmk = 0;
+#pragma clang loop unroll(full)
+        for (int i = 0; i < kSub; ++i) {
+          const int j = j0 + kChunk * i;
+          if (j >= n) continue;
+          const int o0 = x.st + j;
+          const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
+          uint32_t bm = 0, bx = 0;
+          uint32_t xo[4] = {4u, 4u, 4u, 4u};
+          if (full) {
+            sub_bits(bw, (uint32_t)(s0 & 31), i, bm, bx);
+            uint64_t clo;
+            uint32_t chi;
+            chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
+            ctx_slots(clo, chi, xo);
+            if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+          }
+          const int cc0 = x.cell0 + x.dir * o0;
+          // fast path: window rows; offsets it skips are redone below
+          uint32_t slow = 0, mmk = 0;
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-          const int kk = kObsVariant == 2 ? (k + (int)rot) & 15 : k;  // the chunk offset this step visits
-          const int q = (int)(int8_t)(uint8_t)(qr[k >> 2] >> (8 * (k & 3)));
-          const int row = q - q_lo;
-          const bool valid = j + kk < n;
-          const bool fast = full_rg && valid && (unsigned)row < (unsigned)qw;
-          const bool masked = (bmr >> k) & 1u;
-          const int ccell = cc0 + x.dir * kk;
-          const int xcell = C + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-          const int base = row * cells;
-          if (kObsVariant == 0) {
+          for (int k = 0; k < kChunk; ++k) {
+            const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+            const int row = q - q_lo;
+            const bool valid = j + k < n;
+            const bool fast = full_rg && valid && (unsigned)row < (unsigned)qw;
+            const bool masked = (bm >> k) & 1u;
+            const int ccell = cc0 + x.dir * k;
+            const int xcell = C + (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+            const int base = row * cells;
             if (fast) {
               atomicAdd(masked ? &w_masked[row] : &w_obs[base + ccell], 1u);
               if (!masked) atomicAdd(&w_obs[base + xcell], 1u);
             }
-          } else {
-            uint32_t* a1 = fast ? (masked ? &w_masked[row] : &w_obs[base + ccell]) : &dummy[lane];
-            uint32_t* a2 = fast ? &w_obs[base + xcell] : &dummy[lane];
-            atomicAdd(a1, 1u);
-            atomicAdd(a2, masked ? 0u : 1u);
+            slow |= (uint32_t)(valid && !fast) << k;
+            mmk |= (uint32_t)(fast && !masked) << k;
           }
-          slow |= (uint32_t)(valid && !fast) << kk;
-          mmk |= (uint32_t)(fast && !masked) << kk;
-        }
-        mmk &= bx;
-        if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
-          const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-          while (mmk) {
-            const int k = __builtin_ctz(mmk);
-            mmk &= mmk - 1;
-            const int q = (int)(int8_t)qp[o0 + k];
-            const int base = (q - q_lo) * cells;
-            atomicAdd(&w_mm[base + cc0 + x.dir * k], 1u);
-            atomicAdd(&w_mm[base + C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
+          mmk &= bx;
+          if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
+            const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+            while (mmk) {
+              const int k = __builtin_ctz(mmk);
+              mmk &= mmk - 1;
+              const int q = (int)(int8_t)qp[o0 + k];
+              const int base = (q - q_lo) * cells;
+              atomicAdd(&w_mm[base + cc0 + x.dir * k], 1u);
+              atomicAdd(&w_mm[base + C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
+            }
           }
-        }
-        if (__builtin_amdgcn_ballot_w64(slow != 0)) {
-          const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-          while (slow) {
-            const int k = __builtin_ctz(slow);
-            slow &= slow - 1;
-            const int o = o0 + k;
-            const int q = (int)(int8_t)qp[o];
-            if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
-            } else if (full) {  // outside the LDS window: straight to the int64 table
-              const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
-              const int ccell = cc0 + x.dir * k;
-              const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
-              atomicAdd(&blk_hist[q], 1u);
-              const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
-              atomicAdd((unsigned long long*)&P.touched[key], 1ull);
-              if (!masked) {
-                atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
-                atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
-                if (mism) {
-                  atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
-                  atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+          if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+            const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+            while (slow) {
+              const int k = __builtin_ctz(slow);
+              slow &= slow - 1;
+              const int o = o0 + k;
+              const int q = (int)(int8_t)qp[o];
+              if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+                report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+              } else if (full) {  // outside the LDS window: straight to the int64 table
+                const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
+                const int ccell = cc0 + x.dir * k;
+                const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
+                if (ident) atomicAdd(&blk_hist[q], 1u);
+                const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
+                atomicAdd((unsigned long long*)&P.touched[key], 1ull);
+                if (!masked) {
+                  atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
+                  atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
+                  if (mism) {
+                    atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
+                    atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+                  }
                 }
               }
             }
@@ -744,46 +748,224 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
         }
       }
     }
-  }
-  __syncthreads();
-  // ---- the block's window -> part; window rows into the block histogram ----
-  uint32_t* pb = P.part + (int64_t)blockIdx.x * P.part_stride;
-  for (int i = tid; i < 2 * qw * cells; i += blockDim.x) pb[i] = w_obs[i];
-  for (int slot = wave; slot < qw; slot += kWaves) {
-    uint32_t v = 0;
-    for (int c = lane; c < C; c += 64) v += w_obs[slot * cells + c];  // every unmasked base hits one cycle cell
-    v = wave_sum(v);
-    if (lane == 0) {
-      const uint32_t tot = v + w_masked[slot];
-      pb[2 * qw * cells + slot] = tot;
-      if (tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+    __syncthreads();
+    // ---- the piece's window -> its slab; window rows into the block histogram ----
+    uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
+    for (int i = tid; i < 2 * qw * cells; i += blockDim.x) pb[i] = w_obs[i];
+    for (int slot = wave; slot < qw; slot += kWaves) {
+      uint32_t v = 0;
+      for (int c = lane; c < C; c += 64) v += w_obs[slot * cells + c];  // every unmasked base hits one cycle cell
+      v = wave_sum(v);
+      if (lane == 0) {
+        const uint32_t tot = v + w_masked[slot];
+        pb[2 * qw * cells + slot] = tot;
+        if (ident && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+      }
     }
+    __syncthreads();
   }
-  __syncthreads();
-  for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
+  if (ident)
+    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
 }
 
-// Sum the blocks' window counts into the int64 table (one thread per window
-// cell; the observe kernel's direct atomics have all landed by now).
-extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, int32_t n_blocks, int32_t stride, Window w,
-                                              TableGeom g, int64_t* touched, int64_t* obs, int64_t* mm) {
-  const int64_t key0 = (int64_t)w.q_lo + (int64_t)kMaxQ * w.rg_lo;
+// Sum the pieces' window counts into the int64 table: one thread per (key,
+// window cell), over the slabs (w + key) of the workgroups whose range meets
+// the key's positions (the observe kernel's direct atomics have all landed).
+extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd, OrderDev ord, int32_t n_blocks,
+                                              int32_t stride, Window w, TableGeom g, int64_t* touched, int64_t* obs,
+                                              int64_t* mm) {
+  const int nk = order_keys(ord);
   const int nc = w.qw * g.cells;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < stride; i += gridDim.x * blockDim.x) {
+  const int64_t total = (int64_t)nk * stride;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int key = (int)(t / stride);
+    const int i = (int)(t - (int64_t)key * stride);
+    const int64_t k0 = key_begin(ord, rd.n_reads, key), k1 = key_begin(ord, rd.n_reads, key + 1);
+    if (k0 >= k1) continue;
+    const int64_t w0 = wg_of(rd, k0, n_blocks), w1 = wg_of(rd, k1 - 1, n_blocks);
     uint64_t s = 0;
-    for (int b = 0; b < n_blocks; ++b) s += part[(int64_t)b * stride + i];
+    for (int64_t b = w0; b <= w1; ++b) {
+      // a workgroup with an empty range in between wrote no slab
+      if (max(k0, wg_begin(rd, b, n_blocks)) >= min(k1, wg_begin(rd, b + 1, n_blocks))) continue;
+      s += part[(b + (ord.perm ? key : 0)) * stride + i];
+    }
     if (!s) continue;
+    const int rg = ord.perm ? key : w.rg_lo;
+    const int64_t key0 = (int64_t)w.q_lo + (int64_t)kMaxQ * rg;
     if (i < 2 * nc) {
       const int j = i < nc ? i : i - nc;
       const int slot = j / g.cells, cell = j - slot * g.cells;
       if (key0 + slot >= g.K) continue;
+      // atomics: two read groups' rows can alias one key (q >= 60, quirk Q3)
       int64_t* dst = i < nc ? obs : mm;
-      dst[(key0 + slot) * g.cells + cell] += (int64_t)s;
+      atomicAdd((unsigned long long*)&dst[(key0 + slot) * g.cells + cell], (unsigned long long)s);
     } else {
       const int slot = i - 2 * nc;
       if (key0 + slot >= g.K) continue;
-      touched[key0 + slot] += (int64_t)s;
+      atomicAdd((unsigned long long*)&touched[key0 + slot], (unsigned long long)s);
     }
+  }
+}
+
+// ------------------------------------------------------ read-group buckets --
+//
+// Bucketed batches (several read groups) walk their reads grouped by read
+// group so that a workgroup's LDS window always holds the rows of the group it
+// is counting (OrderDev).  A counting sort on the device: per-key counts, an
+// exclusive scan, then a scatter in which each workgroup reserves one range
+// per key it holds (one global atomic per workgroup and key) and ranks its
+// reads inside it with LDS atomics.  The order inside a key is immaterial:
+// counts commute, apply writes by read, errors are reduced by read index.
+
+constexpr int kSortThreads = 256;
+constexpr int kSortPer = 16;             // reads per thread in the scatter
+constexpr int kSortLdsKeys = 4096;       // keys kept in LDS; more go straight to global atomics
+
+__device__ __forceinline__ int sort_key(const ReadMeta& m, int n_keys) { return min((int)m.rg, n_keys - 1); }
+
+extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_count(const ReadMeta* meta, int64_t n,
+                                                                            int32_t n_keys, uint32_t* counts) {
+  __shared__ uint32_t h[kSortLdsKeys];
+  const bool lds = n_keys <= kSortLdsKeys;
+  if (lds)
+    for (int i = threadIdx.x; i < n_keys; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int k = sort_key(meta[r], n_keys);
+    if (lds) atomicAdd(&h[k], 1u); else atomicAdd(&counts[k], 1u);
+  }
+  __syncthreads();
+  if (lds)
+    for (int i = threadIdx.x; i < n_keys; i += blockDim.x)
+      if (h[i]) atomicAdd(&counts[i], h[i]);
+}
+
+// one workgroup: key_off = exclusive scan of counts (key_off[n_keys] = n), cursor = key_off
+extern "C" __global__ void __launch_bounds__(1024) bqsr_key_scan(const uint32_t* counts, int32_t n_keys,
+                                                                   int64_t* key_off, uint32_t* cursor) {
+  __shared__ int64_t part[1024];
+  const int tid = threadIdx.x;
+  const int per = (n_keys + 1023) / 1024;
+  const int k0 = min(n_keys, tid * per), k1 = min(n_keys, k0 + per);
+  int64_t s = 0;
+  for (int k = k0; k < k1; ++k) s += counts[k];
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int64_t acc = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int64_t v = part[i];
+      part[i] = acc;
+      acc += v;
+    }
+    key_off[n_keys] = acc;
+  }
+  __syncthreads();
+  int64_t acc = part[tid];
+  for (int k = k0; k < k1; ++k) {
+    key_off[k] = acc;
+    cursor[k] = (uint32_t)acc;
+    acc += counts[k];
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(const ReadMeta* meta, int64_t n,
+                                                                              int32_t n_keys, uint32_t* cursor,
+                                                                              uint32_t* perm) {
+  __shared__ uint32_t h[kSortLdsKeys];
+  const bool lds = n_keys <= kSortLdsKeys;
+  const int tid = threadIdx.x;
+  for (int64_t c0 = (int64_t)blockIdx.x * kSortThreads * kSortPer; c0 < n;
+       c0 += (int64_t)gridDim.x * kSortThreads * kSortPer) {
+    if (!lds) {
+      for (int i = 0; i < kSortPer; ++i) {
+        const int64_t r = c0 + (int64_t)i * kSortThreads + tid;
+        if (r < n) perm[atomicAdd(&cursor[sort_key(meta[r], n_keys)], 1u)] = (uint32_t)r;
+      }
+      continue;
+    }
+    for (int i = tid; i < n_keys; i += kSortThreads) h[i] = 0;
+    __syncthreads();
+    int key[kSortPer];
+    uint32_t rank[kSortPer];
+#pragma unroll
+    for (int i = 0; i < kSortPer; ++i) {
+      const int64_t r = c0 + (int64_t)i * kSortThreads + tid;
+      key[i] = r < n ? sort_key(meta[r], n_keys) : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < kSortPer; ++i) rank[i] = key[i] >= 0 ? atomicAdd(&h[key[i]], 1u) : 0u;
+    __syncthreads();
+    for (int i = tid; i < n_keys; i += kSortThreads)
+      if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);  // the workgroup's range of key i
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kSortPer; ++i)
+      if (key[i] >= 0) perm[h[key[i]] + rank[i]] = (uint32_t)(c0 + (int64_t)i * kSortThreads + tid);
+    __syncthreads();
+  }
+}
+
+// Per-block qual histograms of the folded bases (usable valid reads, trimmed
+// ranges) in read order, for bucketed batches whose observe kernel does not
+// walk the fold's blocks.  One workgroup per block, one wavefront per tile:
+// the tile's folded ranges become an LDS slot bitmap, then each lane takes 16
+// consecutive slots per step (one 16-B load) and counts the set ones into
+// its wavefront's histogram (four copies by lane & 3 against same-bin
+// conflicts).
+constexpr int kFhWaves = 16;
+extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(ReadsDev rd, const ReadInfo* info,
+                                                                             int32_t n_blocks, uint32_t* hq_block) {
+  __shared__ uint32_t hist[kFhWaves][4][kQBins];
+  __shared__ uint32_t bm[kFhWaves][kTileSlots / 32 + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < kFhWaves * 4 * kQBins; i += blockDim.x) (&hist[0][0][0])[i] = 0;
+  __syncthreads();
+  const int64_t nt = rd.n_tiles;
+  const int64_t t0 = nt * blockIdx.x / n_blocks, t1 = nt * (blockIdx.x + 1) / n_blocks;
+  uint32_t* hw = hist[wv][lane & 3];
+  for (int64_t t = t0 + wv; t < t1; t += kFhWaves) {
+    const int64_t r0 = t * (int64_t)rd.reads_per_tile;
+    const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
+    ReadMeta m{0, 0, 0, 0, 0};
+    ReadInfo inf{0, 0, 0, 0};
+    if (lane < nr) {
+      m = rd.meta[r0 + lane];
+      inf = info[r0 + lane];
+    }
+    const uint64_t ts0 = __shfl(m.slot, 0);
+    const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
+    for (int i = lane; i < kTileSlots / 32 + 1; i += 64) bm[wv][i] = 0;
+    wave_sync();
+    if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
+      int lo = (int)(m.slot - ts0) + inf.st;
+      const int hi = (int)(m.slot - ts0) + inf.en;
+      while (lo < hi) {
+        const int c = min(32 - (lo & 31), hi - lo);
+        atomicOr(&bm[wv][lo >> 5], (c == 32 ? 0xFFFFFFFFu : ((1u << c) - 1u)) << (lo & 31));
+        lo += c;
+      }
+    }
+    wave_sync();
+    const uint8_t* qt = rd.qual + ts0;
+    for (int s0 = 16 * lane; s0 < nslots; s0 += 16 * 64) {
+      const uint4 v = *(const uint4*)(qt + s0);  // the column's padding covers the tail
+      uint32_t bits = (bm[wv][s0 >> 5] >> (s0 & 31)) & 0xFFFFu;
+      if (s0 + 16 > nslots) bits &= (1u << (nslots - s0)) - 1u;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      while (bits) {
+        const int k = __builtin_ctz(bits);
+        bits &= bits - 1;
+        atomicAdd(&hw[(w[k >> 2] >> (8 * (k & 3))) & 0x7Fu], 1u);
+      }
+    }
+    wave_sync();
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < kQBins; q += blockDim.x) {
+    uint32_t s = 0;
+    for (int i = 0; i < kFhWaves * 4; ++i) s += (&hist[0][0][0])[i * kQBins + q];
+    hq_block[(int64_t)blockIdx.x * kQBins + q] = s;
   }
 }
 
@@ -1395,165 +1577,174 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
-  const int q_lo = P.w.q_lo, rg_lo = P.w.rg_lo;
-  const bool win_ok = rg_lo < P.n_rg;
-  const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
-  // rows whose key is not in the table hold NaN: the fast path sends such
-  // bases to the checked path (a valid a2 + deltas is never NaN)
-  for (int i = tid; i < qw * C; i += blockDim.x) {
-    const int slot = i / C;
-    const bool ok = win_ok && q_lo + slot < kQBins && P.rq_ok[rq0 + slot];
-    w_s1[i] = ok ? P.s1[(rq0 + slot) * C + (i - slot * C)] : __builtin_nan("");
-  }
-  for (int i = tid; i < qw * kCtxSlots; i += blockDim.x) {
-    const int slot = i / kCtxSlots;
-    w_d2[i] = (win_ok && q_lo + slot < kQBins) ? P.d2[(rq0 + slot) * kCtxSlots + (i - slot * kCtxSlots)] : 0.0;
-  }
+  const int q_lo = P.w.q_lo;
   for (int i = tid; i < kQbN; i += blockDim.x) {
     l_qbt[i] = P.qb_thr[i];
     l_qbq[i] = P.qb_q[i];
   }
-  const int64_t nt = P.rd.n_tiles;
-  const int64_t tb0 = nt * blockIdx.x / gridDim.x, tb1 = nt * (blockIdx.x + 1) / gridDim.x;
-  const int64_t r_begin = tb0 * P.rd.reads_per_tile, r_end = min(tb1 * (int64_t)P.rd.reads_per_tile, P.rd.n_reads);
-  __syncthreads();
+  const int G = gridDim.x;
+  const bool ident = P.ord.perm == nullptr;
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+  const int nk = order_keys(P.ord);
 
-  for (int64_t g0 = r_begin + 64 * wave; g0 < r_end; g0 += 64 * kWaves) {
-    const LaneRead x = lane_read(P.rd, P.info, g0 + lane, r_end, L);
-    if (x.r < r_end) {
-      if (x.fl & kInfoPass) {  // quality string passed through
-        P.out_start[x.r] = 0;
-        P.out_len[x.r] = (uint32_t)x.en;
-      } else {
-        P.out_start[x.r] = (uint32_t)x.st;
-        P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
-      }
+  for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
+    const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
+    const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
+    if (p0 >= wb) break;
+    if (p0 >= p1) continue;
+    // the piece's window rows: read group rg_lo, quals q_lo .. q_lo + qw - 1.
+    // Rows whose key is not in the table hold NaN: the fast path sends such
+    // bases to the checked path (a valid a2 + deltas is never NaN)
+    const int rg_lo = ident ? P.w.rg_lo : key;
+    const bool win_ok = rg_lo < P.n_rg;
+    const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
+    __syncthreads();  // the previous piece is done with the window
+    for (int i = tid; i < qw * C; i += blockDim.x) {
+      const int slot = i / C;
+      const bool ok = win_ok && q_lo + slot < kQBins && P.rq_ok[rq0 + slot];
+      w_s1[i] = ok ? P.s1[(rq0 + slot) * C + (i - slot * C)] : __builtin_nan("");
     }
-    const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
-    const int n = (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) ? x.en - x.st : 0;
-    const bool fast_rd = app && x.rg == rg_lo;
-    const uint8_t* qp = P.rd.qual + x.slot;
-    uint8_t* op = P.out_qual + x.slot;
-    for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
-      if (j0 >= n) continue;
-      // issue every load of the super-chunk first
-      uint4 qs[kSub], cr[kSub];
-      int64_t cn0[kSub];
-#pragma unroll
-      for (int i = 0; i < kSub; ++i) {
-        const bool live = j0 + kChunk * i < n;
-        const int o0 = x.st + j0 + kChunk * i;
-        qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
-        cn0[i] = chunk_n0(x, o0);
-        cr[i] = (live && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
-      }
-      // the super-chunk's chars, stored together after its last chunk so the
-      // lines they share are written while resident in L2
-      uint4 outs[kSub];
-#pragma clang loop unroll(full)
-      for (int i = 0; i < kSub; ++i) {
-        const int j = j0 + kChunk * i;
-        if (j >= n) continue;
-        const int o0 = x.st + j;
-        const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
-        uint32_t out[4];
-        uint32_t slow = 0;
-        uint32_t xo[4] = {4u, 4u, 4u, 4u};
-        if (pass) {  // the original chars: (qual + 33) byte-wise
-#pragma unroll
-          for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
+    for (int i = tid; i < qw * kCtxSlots; i += blockDim.x) {
+      const int slot = i / kCtxSlots;
+      w_d2[i] = (win_ok && q_lo + slot < kQBins) ? P.d2[(rq0 + slot) * kCtxSlots + (i - slot * kCtxSlots)] : 0.0;
+    }
+    __syncthreads();
+
+    for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
+      const bool live = g0 + lane < p1;
+      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + lane) : 0, live, L);
+      if (live) {
+        if (x.fl & kInfoPass) {  // quality string passed through
+          P.out_start[x.r] = 0;
+          P.out_len[x.r] = (uint32_t)x.en;
         } else {
-          uint64_t clo = 0;
-          uint32_t chi = 0;
-          chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
-          ctx_slots(clo, chi, xo);
-          if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
-          const int cc0 = x.cell0 + x.dir * o0;
-          out[0] = out[1] = out[2] = out[3] = 0;
-#pragma unroll
-          for (int k = 0; k < kChunk; ++k) {
-            const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
-            const int row = q - q_lo;
-            const bool inwin = fast_rd && (unsigned)row < (unsigned)qw;
-            const int rowc = inwin ? row : 0;
-            const int ccell = cc0 + x.dir * k;
-            const int xs = (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-            // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-            const double p = w_s1[rowc * C + ccell] + w_d2[rowc * kCtxSlots + xs];
-            const uint32_t b = phred_bucket(p);
-            const bool bok = b < (uint32_t)kQbN;
-            const uint32_t bc = bok ? b : 0u;
-            const int qq = l_qbq[bc];
-            const int Q = p <= l_qbt[bc] ? qq : qq - 1;
-            const uint32_t code = (uint32_t)(Q + 33);  // (Q + 33).toChar, <= 0xFF on this path
-            const bool good = inwin && bok && qq != -32768 && code <= 0xFFu;
-            slow |= (uint32_t)(!good && j + k < n) << k;
-            out[k >> 2] |= (code & 0xFFu) << (8 * (k & 3));
-          }
+          P.out_start[x.r] = (uint32_t)x.st;
+          P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
         }
-        // ---- the checked path, in offset order (the first failing offset wins) ----
-        if (__builtin_amdgcn_ballot_w64(slow != 0)) {
-          const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-          while (slow) {
-            const int k = __builtin_ctz(slow);
-            slow &= slow - 1;
-            const int o = o0 + k;
-            const int q = (int)(int8_t)qp[o];
-            const int xs = (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
-            // key validity as getReadGroupDelta / getQualScoreDelta see it
-            const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
-            const int64_t gr = (key - 1) / kMaxQ;
-            const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
-            const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
-            if (!grp || !kok) {
-              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
-              continue;
-            }
-            if (q < 0) {
-              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
-              continue;
-            }
-            if (!app) continue;
-            const int64_t rq = (int64_t)x.rg * kQBins + q;
-            const int ccell = x.cell0 + x.dir * o;
-            const double p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + xs];
-            const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
-            const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-            if (code > 0xFFu) {
-              const unsigned long long e = atomicAdd(P.n_exc, 1ull);
-              if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
-            }
-            const uint32_t sh = 8u * (uint32_t)(k & 3);
-#pragma unroll
-            for (int w = 0; w < 4; ++w)
-              if (w == (k >> 2)) out[w] = (out[w] & ~(0xFFu << sh)) | ((code & 0xFFu) << sh);
-          }
-        }
-        outs[i] = make_uint4(out[0], out[1], out[2], out[3]);
       }
-      if (app || pass) {
-#pragma clang loop unroll(full)
+      const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
+      const int n = (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) ? x.en - x.st : 0;
+      const bool fast_rd = app && x.rg == rg_lo;
+      const uint8_t* qp = P.rd.qual + x.slot;
+      uint8_t* op = P.out_qual + x.slot;
+      for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
+        if (j0 >= n) continue;
+        // issue every load of the super-chunk first
+        uint4 qs[kSub], cr[kSub];
+        int64_t cn0[kSub];
+  #pragma unroll
+        for (int i = 0; i < kSub; ++i) {
+          const bool live = j0 + kChunk * i < n;
+          const int o0 = x.st + j0 + kChunk * i;
+          qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
+          cn0[i] = chunk_n0(x, o0);
+          cr[i] = (live && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
+        }
+        // the super-chunk's chars, stored together after its last chunk so the
+        // lines they share are written while resident in L2
+        uint4 outs[kSub];
+  #pragma clang loop unroll(full)
         for (int i = 0; i < kSub; ++i) {
           const int j = j0 + kChunk * i;
           if (j >= n) continue;
           const int o0 = x.st + j;
-          if (j + kChunk <= n) {
-            *(uint4*)(op + o0) = outs[i];
+          const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
+          uint32_t out[4];
+          uint32_t slow = 0;
+          uint32_t xo[4] = {4u, 4u, 4u, 4u};
+          if (pass) {  // the original chars: (qual + 33) byte-wise
+  #pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
           } else {
-            const uint32_t ov[4] = {outs[i].x, outs[i].y, outs[i].z, outs[i].w};
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k)
-              if (k < n - j) op[o0 + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+            uint64_t clo = 0;
+            uint32_t chi = 0;
+            chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
+            ctx_slots(clo, chi, xo);
+            if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+            const int cc0 = x.cell0 + x.dir * o0;
+            out[0] = out[1] = out[2] = out[3] = 0;
+  #pragma unroll
+            for (int k = 0; k < kChunk; ++k) {
+              const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+              const int row = q - q_lo;
+              const bool inwin = fast_rd && (unsigned)row < (unsigned)qw;
+              const int rowc = inwin ? row : 0;
+              const int ccell = cc0 + x.dir * k;
+              const int xs = (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+              // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+              const double p = w_s1[rowc * C + ccell] + w_d2[rowc * kCtxSlots + xs];
+              const uint32_t b = phred_bucket(p);
+              const bool bok = b < (uint32_t)kQbN;
+              const uint32_t bc = bok ? b : 0u;
+              const int qq = l_qbq[bc];
+              const int Q = p <= l_qbt[bc] ? qq : qq - 1;
+              const uint32_t code = (uint32_t)(Q + 33);  // (Q + 33).toChar, <= 0xFF on this path
+              const bool good = inwin && bok && qq != -32768 && code <= 0xFFu;
+              slow |= (uint32_t)(!good && j + k < n) << k;
+              out[k >> 2] |= (code & 0xFFu) << (8 * (k & 3));
+            }
+          }
+          // ---- the checked path, in offset order (the first failing offset wins) ----
+          if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+            const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+            while (slow) {
+              const int k = __builtin_ctz(slow);
+              slow &= slow - 1;
+              const int o = o0 + k;
+              const int q = (int)(int8_t)qp[o];
+              const int xs = (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
+              // key validity as getReadGroupDelta / getQualScoreDelta see it
+              const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
+              const int64_t gr = (key - 1) / kMaxQ;
+              const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
+              const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
+              if (!grp || !kok) {
+                report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
+                continue;
+              }
+              if (q < 0) {
+                report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+                continue;
+              }
+              if (!app) continue;
+              const int64_t rq = (int64_t)x.rg * kQBins + q;
+              const int ccell = x.cell0 + x.dir * o;
+              const double p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + xs];
+              const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
+              const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+              if (code > 0xFFu) {
+                const unsigned long long e = atomicAdd(P.n_exc, 1ull);
+                if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
+              }
+              const uint32_t sh = 8u * (uint32_t)(k & 3);
+  #pragma unroll
+              for (int w = 0; w < 4; ++w)
+                if (w == (k >> 2)) out[w] = (out[w] & ~(0xFFu << sh)) | ((code & 0xFFu) << sh);
+            }
+          }
+          outs[i] = make_uint4(out[0], out[1], out[2], out[3]);
+        }
+        if (app || pass) {
+  #pragma clang loop unroll(full)
+          for (int i = 0; i < kSub; ++i) {
+            const int j = j0 + kChunk * i;
+            if (j >= n) continue;
+            const int o0 = x.st + j;
+            if (j + kChunk <= n) {
+              *(uint4*)(op + o0) = outs[i];
+            } else {
+              const uint32_t ov[4] = {outs[i].x, outs[i].y, outs[i].z, outs[i].w};
+  #pragma unroll
+              for (int k = 0; k < kChunk; ++k)
+                if (k < n - j) op[o0 + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+            }
           }
         }
       }
     }
-  }
+  }  // pieces
 }
 
-template __global__ void bqsr_observe_kernel<0>(ObserveParams);
-template __global__ void bqsr_observe_kernel<1>(ObserveParams);
-template __global__ void bqsr_observe_kernel<2>(ObserveParams);
 
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {

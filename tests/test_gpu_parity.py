@@ -76,6 +76,32 @@ def test_synthetic_many_read_groups_mixed_lengths():
     check([b])
 
 
+@pytest.fixture
+def read_order(request, monkeypatch):
+    """ADAM_BQSR_ORDER: 'read' = the per-base passes walk reads in batch order,
+    'group' = bucketed by read group (device counting sort, pieces per read
+    group); the library picks 'group' for several read groups by default."""
+    monkeypatch.setenv("ADAM_BQSR_ORDER", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
+@pytest.mark.parametrize("n_reads,n_rg,lens,seed", [
+    (6000, 96, (150, 250), 21),    # many groups, a few reads per workgroup and group
+    (40000, 8, (100,), 22),        # few groups, each spread over many workgroups
+    (20000, 1, (101,), 23),        # one group
+    (3000, 3, (60, 100, 140), 24),
+])
+def test_read_orders(read_order, n_reads, n_rg, lens, seed):
+    b = synth.generate(n_reads, lens, n_rg, seed=seed)
+    check([b.slice(0, n_reads // 3), b.slice(n_reads // 3, n_reads)], synth.known_sites(2_000_000, seed=5))
+
+
+@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
+def test_read_orders_edge_cases(read_order):
+    check([RecordBatch.from_records(EDGE * 3)], sites={"1": [10002, 10005, 40, 44, 10013]})
+
+
 def test_fold_many_binades():
     # 3M bases: the expectedMismatch fold crosses many binades and uses the
     # block / tile / exact levels
