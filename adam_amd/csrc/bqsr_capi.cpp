@@ -169,18 +169,26 @@ TableGeom geom(const bqsr_dims& d) {
 }
 
 constexpr size_t kLdsMax = 163840;
-size_t observe_lds(int qw, int cells) { return (size_t)qw * cells * 8 + (size_t)qw * 4 + kQBins * 4 + 64 * 4; }
-size_t apply_lds(int qw, int C) {
-  return (size_t)qw * C * 8 + (size_t)qw * kCtxSlots * 8 + (size_t)kQbN * (8 + 2);
-}
-int observe_qw(int cells) {
-  int qw = 64;
-  while (qw > 1 && observe_lds(qw, cells) > kLdsMax) --qw;
+// LDS of the per-base passes: observe's u32 window [qw][wcells] x {obs, mm}
+// + masked counts + block histogram; apply's char table [qw][cw][21]
+size_t observe_lds(int qw, int wcells) { return (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4; }
+size_t apply_lds(int qw, int cw) { return (size_t)qw * cw * kCtxSlots; }
+int observe_rows(int wcells) {
+  int qw = kQBins;
+  while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;
   return qw;
 }
-int apply_qw(int C) {
-  int qw = 64;
-  while (qw > 1 && apply_lds(qw, C) > kLdsMax) --qw;
+// observe's rotated fast path (bqsr_observe_kernel<true>); ADAM_BQSR_OBSERVE_ROTATE=0/1 overrides
+bool observe_rotate() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_OBSERVE_ROTATE");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return v;
+}
+int apply_rows(int cw) {
+  int qw = kQBins;
+  while (qw > 1 && apply_lds(qw, cw) > kLdsMax) --qw;
   return qw;
 }
 
@@ -327,8 +335,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_observe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  for (const void* f : {(const void*)bqsr_observe_kernel<false>, (const void*)bqsr_observe_kernel<true>})
+    if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e != hipSuccess) {
@@ -424,6 +432,8 @@ inline uint8_t code_of(uint8_t c) {
   }
 }
 
+Window window_rows(const bqsr_batch* b, int max_rows);
+
 bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   if (max_slot_len > kMaxReadLen)
     return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
@@ -441,11 +451,26 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
-  // read-group buckets: on for several read groups (ADAM_BQSR_ORDER=read / group forces either)
+  // read-group buckets (OrderDev): on for several read groups, or when the
+  // apply window over all cycle cells would leave more than 0.1% of the bases
+  // outside its qual rows (ADAM_BQSR_ORDER=read / group forces either)
   const char* ord = getenv("ADAM_BQSR_ORDER");
-  b->bucketed = ord ? strcmp(ord, "group") == 0 : b->dims.n_rg > 1;
+  if (ord) {
+    b->bucketed = strcmp(ord, "group") == 0;
+  } else {
+    b->bucketed = b->dims.n_rg > 1;
+    if (!b->bucketed && b->have_qhist) {
+      const Window w = window_rows(b, apply_rows(geom(b->dims).C));
+      int64_t in = 0, all = 0;
+      for (int q = 0; q < kQBins; ++q) {
+        all += b->qhist[q];
+        if (q >= w.q_lo && q < w.q_lo + w.qw) in += b->qhist[q];
+      }
+      b->bucketed = (double)(all - in) > 1e-3 * (double)all;
+    }
+  }
   if (b->bucketed) {
-    b->n_keys = std::max<int32_t>(1, b->dims.n_rg);
+    b->n_keys = 2 * std::max<int32_t>(1, b->dims.n_rg);  // 2 * read group + mate class
     if ((st = dalloc(b->allocs, &b->d_perm, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_off, (size_t)b->n_keys + 1)) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_cnt, (size_t)b->n_keys)) != BQSR_OK) return st;
@@ -740,11 +765,30 @@ bqsr_status bqsr_table_merge(bqsr_table* acc, const bqsr_table* part, double* ac
 // -------------------------------------------------------------- observe ----
 
 namespace {
-// first window row: the densest qw-wide qual range of the batch when its
-// histogram is known, else the caller's choice (bqsr_batch_set_window)
-int32_t window_q_lo(const bqsr_batch* b, int qw) {
-  return b->have_qhist ? best_q_lo(b->qhist, qw) : std::min(b->q_lo, kQBins - 1);
+// window rows (q_lo, qw) for at most max_rows rows: the batch's whole qual
+// span when it fits, else the densest max_rows-wide range; without a
+// histogram the caller's choice (bqsr_batch_set_window)
+Window window_rows(const bqsr_batch* b, int max_rows) {
+  Window w{max_rows, std::min(b->q_lo, kQBins - 1), b->rg_lo};
+  if (!b->have_qhist) {
+    w.qw = std::min(w.qw, kQBins - w.q_lo);
+    return w;
+  }
+  int lo = 0, hi = kQBins - 1;
+  while (lo < kQBins - 1 && b->qhist[lo] == 0) ++lo;
+  while (hi > lo && b->qhist[hi] == 0) --hi;
+  if (hi - lo + 1 <= max_rows) {
+    w.q_lo = lo;
+    w.qw = hi - lo + 1;
+  } else {
+    w.q_lo = best_q_lo(b->qhist, max_rows);
+  }
+  w.qw = std::min(w.qw, kQBins - w.q_lo);  // rows stay below qual 128 (Java byte >= 0)
+  return w;
 }
+// cycle cells of the windows: all of them in read order, one mate class's
+// half when bucketed (OrderDev, WinGeom)
+int window_cw(const bqsr_batch* b, const TableGeom& g) { return b->bucketed ? g.L : g.C; }
 bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
   if (b->dims.n_rg > t->dims.n_rg || b->dims.max_len > t->dims.max_len)
     return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's (n_rg / max_len)");
@@ -817,13 +861,12 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
-    P.w.qw = observe_qw(P.g.cells);
-    P.w.q_lo = window_q_lo(b, P.w.qw);
-    P.w.rg_lo = b->rg_lo;
+    P.wcells = window_cw(b, P.g) + kCtxSlots;
+    P.w = window_rows(b, observe_rows(P.wcells));
     P.touched = t->touched();
     P.obs = t->obs();
     P.mm = t->mm();
-    P.part_stride = 2 * P.w.qw * P.g.cells + P.w.qw;
+    P.part_stride = 2 * P.w.qw * P.wcells + P.w.qw;
     const size_t need = (size_t)P.part_stride * (b->n_blocks + b->n_keys - 1);  // slabs w + key
     if (b->part_words < need) {  // grows with the table geometry; kept across calls
       if (b->d_part) {
@@ -839,12 +882,16 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = observe_lds(P.w.qw, P.g.cells);
-    hipLaunchKernelGGL(bqsr_observe_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    const size_t lds = observe_lds(P.w.qw, P.wcells);
+    if (observe_rotate())
+      hipLaunchKernelGGL(bqsr_observe_kernel<true>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    else
+      hipLaunchKernelGGL(bqsr_observe_kernel<false>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_keys : 1) + 255) / 256);
-    hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
-                       b->n_blocks, P.part_stride, P.w, P.g, P.touched, P.obs, P.mm);
+    const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
+    hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb, ry), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
+                       b->n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
@@ -1120,9 +1167,8 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.ord = b->order();
   P.info = b->d_info;
   P.g = geom(L->dims);
-  P.w.qw = apply_qw(P.g.C);
-  P.w.q_lo = window_q_lo(b, P.w.qw);
-  P.w.rg_lo = b->rg_lo;
+  const int cw = window_cw(b, P.g);
+  P.w = window_rows(b, apply_rows(cw));
   P.n_rg = L->dims.n_rg;
   P.s1 = L->s1;
   P.d2 = L->d2;
@@ -1142,7 +1188,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
-  const size_t lds = apply_lds(P.w.qw, P.g.C);
+  const size_t lds = apply_lds(P.w.qw, cw);
   hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
   return ok();

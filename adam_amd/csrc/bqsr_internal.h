@@ -71,6 +71,7 @@ constexpr int kWaves = 16;  // waves per workgroup of the per-base passes (1024 
 constexpr int kBlockThreads = 64 * kWaves;
 constexpr int kMaxReadLen = 4096;  // longest read the device path takes
 constexpr int kColumnPad = 32;     // readable bytes past the end of the qual / bases columns
+constexpr int kRedSlabs = 16;      // slabs one bqsr_window_reduce thread sums (grid y splits the rest)
 
 // Error reporting: u64 words, atomicMin of
 //   read << 28 | read_offset << 8 | rank << 4 | code
@@ -141,18 +142,22 @@ struct PrepParams {
   unsigned long long* err;  // error words
 };
 
-// Read order of the per-base passes.  With one read group the passes walk the
-// batch in read order (perm == nullptr).  With several, reads are bucketed by
-// read group (a device counting sort, bqsr_key_*): sorted position i holds
-// read perm[i], and key_off[g] .. key_off[g+1] are the positions of group g.
-// Workgroup w takes the positions [a_w, a_w+1) (tile-aligned, wg_begin) and
-// walks them as "pieces", one per read group it meets, with that group's rows
-// in its LDS window: a piece's counts go to slab (w + g).  (w + g is unique:
-// the group is nondecreasing along the sorted order.)
+// Read order of the per-base passes.  With one read group whose table rows
+// fit the LDS windows, the passes walk the batch in read order (perm ==
+// nullptr).  Otherwise reads are bucketed by key = 2 * read group + mate
+// class (a device counting sort, bqsr_key_*): sorted position i holds read
+// perm[i], and key_off[k] .. key_off[k+1] are the positions of key k.  The
+// mate class (readPaired && secondOfPair) decides the sign of DiscreteCycle,
+// so a key's reads only use half of the cycle cells: cycles 1..L (cells
+// L+1..2L) for class 0, -L..-1 (cells 0..L-1) for class 1 -- the windows
+// hold that half only (WinGeom).  Workgroup w takes the positions [a_w,
+// a_w+1) (tile-aligned, wg_begin) and walks them as "pieces", one per key it
+// meets, with that key's rows in its LDS window: a piece's counts go to slab
+// (w + k).  (w + k is unique: the key is nondecreasing along the order.)
 struct OrderDev {
   const uint32_t* perm;    // [n_reads] or nullptr (identity, one piece per workgroup, group = Window::rg_lo)
   const int64_t* key_off;  // [n_keys + 1]
-  int32_t n_keys;
+  int32_t n_keys;          // 2 * n_rg when bucketed
 };
 
 struct ObserveParams {
@@ -166,11 +171,12 @@ struct ObserveParams {
   int64_t* obs;      // [K*cells]
   int64_t* mm;       // [K*cells]
   uint32_t* part;      // [n_blocks + n_keys - 1][part_stride] per-piece window counts (obs, mm, touched)
-  int32_t part_stride; // 2*qw*cells + qw
+  int32_t part_stride; // 2*qw*wcells + qw, wcells = WinGeom::cw + 21
   uint32_t* hq_block;  // [n_blocks][128] per-block qual histogram of folded bases (identity order only;
                        // bucketed batches get it from bqsr_fold_hist)
   unsigned long long* err;
   int32_t n_blocks;
+  int32_t wcells;      // window row length: WinGeom::cw + 21
 };
 
 struct FoldParams {
@@ -198,7 +204,7 @@ struct ApplyParams {
   OrderDev ord;
   const ReadInfo* info;
   TableGeom g;
-  Window w;
+  Window w;               // qw rows of the per-piece char table
   int32_t n_rg;
   const double* s1;       // [n_rg*128][C]  a2 + cycleDelta
   const double* d2;       // [n_rg*128][21] contextDelta

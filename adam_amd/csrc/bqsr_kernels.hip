@@ -541,6 +541,17 @@ __device__ __forceinline__ int key_at(const OrderDev& o, int64_t p) {
   return lo;
 }
 __device__ __forceinline__ int64_t order_read(const OrderDev& o, int64_t i) { return o.perm ? (int64_t)o.perm[i] : i; }
+// the read group of a key's window rows
+__device__ __forceinline__ int key_rg(const OrderDev& o, int key, int rg_lo) { return o.perm ? key >> 1 : rg_lo; }
+// the cycle cells a piece's windows hold: all of them in read order, the
+// key's mate-class half when bucketed (OrderDev)
+struct WinGeom {
+  int c_lo, cw;
+};
+__device__ __forceinline__ WinGeom win_geom(const OrderDev& o, const TableGeom& g, int key) {
+  if (!o.perm) return WinGeom{0, g.C};
+  return (key & 1) ? WinGeom{0, g.L} : WinGeom{g.L + 1, g.L};
+}
 
 
 // The 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
@@ -611,19 +622,36 @@ __device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[
   }
 }
 
+// 16 bytes rotated right by r (0..15) bytes: byte k of the result = byte (k + r) & 15
+__device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
+  const uint32_t d = r >> 2, b = r & 3;
+  const uint32_t t0 = (d & 1) ? w[1] : w[0], t1 = (d & 1) ? w[2] : w[1];
+  const uint32_t t2 = (d & 1) ? w[3] : w[2], t3 = (d & 1) ? w[0] : w[3];
+  const uint32_t u0 = (d & 2) ? t2 : t0, u1 = (d & 2) ? t3 : t1, u2 = (d & 2) ? t0 : t2, u3 = (d & 2) ? t1 : t3;
+  w[0] = __builtin_amdgcn_alignbyte(u1, u0, b);
+  w[1] = __builtin_amdgcn_alignbyte(u2, u1, b);
+  w[2] = __builtin_amdgcn_alignbyte(u3, u2, b);
+  w[3] = __builtin_amdgcn_alignbyte(u0, u3, b);
+}
+
 // ------------------------------------------------------------ observe ------
 
-// LDS: [obs window qw*cells u32][mm window qw*cells u32][masked qw u32][block hist 128 u32]
+// LDS: [obs window qw*wcells u32][mm window qw*wcells u32][masked qw u32][block hist 128 u32]
 // The window holds a piece's counts for rows (rg, q_lo..q_lo+qw-1) where rg is
 // the piece's read group; other keys go straight to the int64 table.  Each
 // piece's window is written to its slab of `part` and summed into the table by
 // bqsr_window_reduce.
+// kRot: lane l visits a chunk's offsets rotated by l & 15, so the lanes of a
+// wavefront (reads of equal length at equal offsets) hit different cycle
+// cells in each step instead of piling onto one LDS address.
+template <bool kRot>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
+  const int wcells = P.wcells;  // window row: [cycle cells cw][contexts 21]
   uint32_t* w_obs = (uint32_t*)smem;
-  uint32_t* w_mm = w_obs + qw * cells;
-  uint32_t* w_masked = w_mm + qw * cells;
+  uint32_t* w_mm = w_obs + qw * wcells;
+  uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -640,8 +668,10 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
     if (p0 >= wb) break;
     if (p0 >= p1) continue;
-    const int rg_w = ident ? P.w.rg_lo : key;  // the read group of the window rows
-    for (int i = tid; i < 2 * qw * cells + qw; i += blockDim.x) w_obs[i] = 0;
+    const int rg_w = key_rg(P.ord, key, P.w.rg_lo);  // the read group of the window rows
+    const WinGeom gm = win_geom(P.ord, P.g, key);
+    const int c_lo = gm.c_lo, cw = gm.cw;
+    for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
 
     for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
@@ -686,36 +716,50 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
             ctx_slots(clo, chi, xo);
             if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
           }
-          const int cc0 = x.cell0 + x.dir * o0;
-          // fast path: window rows; offsets it skips are redone below
-          uint32_t slow = 0, mmk = 0;
+          const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
+          const int wc0 = cc0 - c_lo;                     // ... and window cycle cell
+          // the cycle cells of the chunk's valid offsets inside the window
+          // (monotone in k: both ends)
+          const uint32_t nv = (uint32_t)min(kChunk, n - j);
+          const bool cok = full_rg && (unsigned)wc0 < (unsigned)cw && (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
+          const uint32_t vmask = nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u);
+          // fast path: window rows of the piece's read group; offsets it skips
+          // are redone below
+          const uint32_t rot = kRot ? (uint32_t)lane & 15u : 0u;
+          uint32_t qr[4] = {qd[0], qd[1], qd[2], qd[3]}, xr[4] = {xo[0], xo[1], xo[2], xo[3]};
+          uint32_t bmr = bm & 0xFFFFu, vr = vmask;
+          if (kRot) {
+            rotr16(qr, rot);
+            rotr16(xr, rot);
+            bmr = ((bmr | (bmr << 16)) >> rot) & 0xFFFFu;
+            vr = ((vr | (vr << 16)) >> rot) & 0xFFFFu;
+          }
+          uint32_t fastm = 0;
 #pragma unroll
           for (int k = 0; k < kChunk; ++k) {
-            const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+            const int kk = kRot ? (k + (int)rot) & 15 : k;  // the chunk offset visited
+            const int q = (int)((qr[k >> 2] >> (8 * (k & 3))) & 0xFFu);
             const int row = q - q_lo;
-            const bool valid = j + k < n;
-            const bool fast = full_rg && valid && (unsigned)row < (unsigned)qw;
-            const bool masked = (bm >> k) & 1u;
-            const int ccell = cc0 + x.dir * k;
-            const int xcell = C + (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-            const int base = row * cells;
-            if (fast) {
-              atomicAdd(masked ? &w_masked[row] : &w_obs[base + ccell], 1u);
-              if (!masked) atomicAdd(&w_obs[base + xcell], 1u);
+            const bool f = cok && (unsigned)row < (unsigned)qw && ((vr >> k) & 1u);
+            const bool m = (bmr >> k) & 1u;
+            const int base = row * wcells;
+            if (f) {
+              atomicAdd(m ? &w_masked[row] : &w_obs[base + wc0 + x.dir * kk], 1u);
+              if (!m) atomicAdd(&w_obs[base + cw + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu)], 1u);
             }
-            slow |= (uint32_t)(valid && !fast) << k;
-            mmk |= (uint32_t)(fast && !masked) << k;
+            fastm |= (uint32_t)f << kk;
           }
-          mmk &= bx;
+          uint32_t slow = vmask & ~fastm;
+          uint32_t mmk = fastm & ~bm & bx;
           if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
             const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
             while (mmk) {
               const int k = __builtin_ctz(mmk);
               mmk &= mmk - 1;
               const int q = (int)(int8_t)qp[o0 + k];
-              const int base = (q - q_lo) * cells;
-              atomicAdd(&w_mm[base + cc0 + x.dir * k], 1u);
-              atomicAdd(&w_mm[base + C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
+              const int base = (q - q_lo) * wcells;
+              atomicAdd(&w_mm[base + wc0 + x.dir * k], 1u);
+              atomicAdd(&w_mm[base + cw + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
             }
           }
           if (__builtin_amdgcn_ballot_w64(slow != 0)) {
@@ -751,14 +795,14 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     __syncthreads();
     // ---- the piece's window -> its slab; window rows into the block histogram ----
     uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
-    for (int i = tid; i < 2 * qw * cells; i += blockDim.x) pb[i] = w_obs[i];
+    for (int i = tid; i < 2 * qw * wcells; i += blockDim.x) pb[i] = w_obs[i];
     for (int slot = wave; slot < qw; slot += kWaves) {
       uint32_t v = 0;
-      for (int c = lane; c < C; c += 64) v += w_obs[slot * cells + c];  // every unmasked base hits one cycle cell
+      for (int c = lane; c < cw; c += 64) v += w_obs[slot * wcells + c];  // every unmasked base hits one cycle cell
       v = wave_sum(v);
       if (lane == 0) {
         const uint32_t tot = v + w_masked[slot];
-        pb[2 * qw * cells + slot] = tot;
+        pb[2 * qw * wcells + slot] = tot;
         if (ident && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
       }
     }
@@ -769,32 +813,43 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
 }
 
 // Sum the pieces' window counts into the int64 table: one thread per (key,
-// window cell), over the slabs (w + key) of the workgroups whose range meets
-// the key's positions (the observe kernel's direct atomics have all landed).
+// window cell, slab group), over the slabs (w + key) of the workgroups whose
+// range meets the key's positions (the observe kernel's direct atomics have
+// all landed).
 extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd, OrderDev ord, int32_t n_blocks,
-                                              int32_t stride, Window w, TableGeom g, int64_t* touched, int64_t* obs,
-                                              int64_t* mm) {
+                                              int32_t stride, int32_t wcells, Window w, TableGeom g, int64_t* touched,
+                                              int64_t* obs, int64_t* mm) {
   const int nk = order_keys(ord);
-  const int nc = w.qw * g.cells;
+  const int nc = w.qw * wcells;
   const int64_t total = (int64_t)nk * stride;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int key = (int)(t / stride);
     const int i = (int)(t - (int64_t)key * stride);
     const int64_t k0 = key_begin(ord, rd.n_reads, key), k1 = key_begin(ord, rd.n_reads, key + 1);
     if (k0 >= k1) continue;
-    const int64_t w0 = wg_of(rd, k0, n_blocks), w1 = wg_of(rd, k1 - 1, n_blocks);
+    // grid y: thread y takes the groups y, y + gridDim.y, ... of kRedSlabs
+    // slabs of the key's range
+    const int64_t wk1 = wg_of(rd, k1 - 1, n_blocks);
     uint64_t s = 0;
-    for (int64_t b = w0; b <= w1; ++b) {
-      // a workgroup with an empty range in between wrote no slab
-      if (max(k0, wg_begin(rd, b, n_blocks)) >= min(k1, wg_begin(rd, b + 1, n_blocks))) continue;
-      s += part[(b + (ord.perm ? key : 0)) * stride + i];
+    for (int64_t w0 = wg_of(rd, k0, n_blocks) + (int64_t)blockIdx.y * kRedSlabs; w0 <= wk1;
+         w0 += (int64_t)gridDim.y * kRedSlabs) {
+      const int64_t w1 = min(wk1, w0 + kRedSlabs - 1);
+#pragma unroll 8
+      for (int64_t b = w0; b <= w1; ++b) {
+        // a workgroup with an empty range in between wrote no slab (its words
+        // are read but not added: the loads stay independent)
+        const uint32_t v = part[(b + (ord.perm ? key : 0)) * stride + i];
+        if (max(k0, wg_begin(rd, b, n_blocks)) < min(k1, wg_begin(rd, b + 1, n_blocks))) s += v;
+      }
     }
     if (!s) continue;
-    const int rg = ord.perm ? key : w.rg_lo;
+    const int rg = key_rg(ord, key, w.rg_lo);
+    const WinGeom gm = win_geom(ord, g, key);
     const int64_t key0 = (int64_t)w.q_lo + (int64_t)kMaxQ * rg;
     if (i < 2 * nc) {
       const int j = i < nc ? i : i - nc;
-      const int slot = j / g.cells, cell = j - slot * g.cells;
+      const int slot = j / wcells, wc = j - slot * wcells;
+      const int cell = wc < gm.cw ? gm.c_lo + wc : g.C + (wc - gm.cw);
       if (key0 + slot >= g.K) continue;
       // atomics: two read groups' rows can alias one key (q >= 60, quirk Q3)
       int64_t* dst = i < nc ? obs : mm;
@@ -821,7 +876,11 @@ constexpr int kSortThreads = 256;
 constexpr int kSortPer = 16;             // reads per thread in the scatter
 constexpr int kSortLdsKeys = 4096;       // keys kept in LDS; more go straight to global atomics
 
-__device__ __forceinline__ int sort_key(const ReadMeta& m, int n_keys) { return min((int)m.rg, n_keys - 1); }
+// key = 2 * read group + mate class (OrderDev); n_keys = 2 * n_rg
+__device__ __forceinline__ int sort_key(const ReadMeta& m, int n_keys) {
+  const int cls = ((m.flags & BQSR_F_PAIRED) && (m.flags & BQSR_F_SECOND_OF_PAIR)) ? 1 : 0;
+  return 2 * min((int)m.rg, n_keys / 2 - 1) + cls;
+}
 
 extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_count(const ReadMeta* meta, int64_t n,
                                                                             int32_t n_keys, uint32_t* counts) {
@@ -1441,28 +1500,45 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_
                                                                       uint8_t* key_ok, double* a2, uint8_t* rq_ok,
                                                                       FinalOut* out) {
   const int tid = threadIdx.x;
+  __shared__ int64_t s_go[256], s_gm[256];
+  __shared__ int s_any[256];
+  // readgroups = keys.sorted.groupBy((t - 1) / 60) (Java division): group r
+  // (index r + 1) holds keys 0..60 for r = 0 and 60r+1 .. 60r+60 above; one
+  // thread per group
+  int64_t go = 0, gm = 0;
+  int any = 0;
   for (int i = tid; i < n_groups; i += blockDim.x) {
-    grp_obs[i] = 0;
-    grp_mm[i] = 0;
-    grp_ok[i] = 0;
+    const int r = i - 1;
+    int64_t so = 0, sm = 0;
+    int ok = 0;
+    if (r >= 0) {
+      const int k0 = r == 0 ? 0 : kMaxQ * r + 1, k1 = min(g.K - 1, kMaxQ * r + kMaxQ);
+      for (int k = k0; k <= k1; ++k) {
+        if (!touched[k]) continue;
+        ok = 1;
+        so += qk_obs[k];
+        sm += qk_mm[k];
+      }
+    }
+    grp_obs[i] = so;
+    grp_mm[i] = sm;
+    grp_ok[i] = (uint8_t)ok;
+    go += so;
+    gm += sm;
+    any |= ok;
   }
+  for (int k = tid; k < g.K; k += blockDim.x) key_ok[k] = touched[k] != 0;
+  s_go[tid] = go;
+  s_gm[tid] = gm;
+  s_any[tid] = any;
   __syncthreads();
   if (tid == 0) {
-    // readgroups = keys.sorted.groupBy((t - 1) / 60) (Java division)
-    int64_t go = 0, gm = 0;
-    int any = 0;
-    for (int k = 0; k < g.K; ++k) {
-      key_ok[k] = touched[k] != 0;
-      if (!touched[k]) continue;
-      any = 1;
-      const int r = (k - 1) / kMaxQ;  // C++ division truncates like Java's
-      grp_obs[r + 1] += qk_obs[k];
-      grp_mm[r + 1] += qk_mm[k];
-      grp_ok[r + 1] = 1;
-    }
-    for (int i = 0; i < n_groups; ++i) {
-      go += grp_obs[i];
-      gm += grp_mm[i];
+    go = gm = 0;
+    any = 0;
+    for (int i = 0; i < (int)blockDim.x; ++i) {  // integer sums: the order is immaterial
+      go += s_go[i];
+      gm += s_gm[i];
+      any |= s_any[i];
     }
     out->g_obs = go;
     out->g_mm = gm;
@@ -1550,40 +1626,26 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
   return (int32_t)0x80000000;          // log10(inf) = inf
 }
 
-// errorProbabilityToPhred bucket of p: the unbiased exponent's offset from
-// kQbElo and the top kQbBits mantissa bits, read straight off the high word
-// (sign, exponent, mantissa).  Values outside [0, kQbN) -- p <= 0, NaN, inf,
-// subnormal or out-of-range binades -- take phred_q's full path.
-constexpr uint32_t kQbBase = (uint32_t)(1023 + kQbElo) << kQbBits;
-__device__ __forceinline__ uint32_t phred_bucket(double p) {
-  return ((uint32_t)((uint64_t)__double_as_longlong(p) >> 32) >> (20 - kQbBits)) - kQbBase;
-}
-
-// LDS: [s1 window qw*C f64][d2 window qw*21 f64][bucket thresholds f64][bucket Q i16]
-// Lane per read as in observe.  Per offset the fast path is branch-free: two
-// LDS doubles, one add, the bucket's threshold and Q; offsets it cannot
-// finish (key outside the window or not in the table, p outside the bucket
-// range, a char above 0xFF, the read only being checked) set a bit of `slow`
-// and are redone after the chunk's store by the exact checked path.  Each
-// chunk's 16 chars leave as one 16-B store (a read's last chunk byte-wise).
+// LDS: the piece's char table [qw rows][cw cycle cells][21 contexts] u8.
+// Built once per piece (bqsr_apply_kernel's prologue) from the exact LUT:
+// char = (errorProbabilityToPhred(s1[c] + d2[x]) + 33) for every (qual row,
+// cycle cell, context) of the piece's read group, 0 where the checked path
+// must decide (key not in the table, a char above 0xFF, or a genuine 0).
+// Lane per read as in observe; per offset the fast path is one LDS byte
+// read.  Offsets it cannot finish (qual outside the rows, entry 0, the read
+// only being checked) set a bit of `slow` and are redone after the chunk by
+// the exact checked path.  A super-chunk's chars leave as 16-B stores (a
+// read's last chunk byte-wise).
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
-  double* w_s1 = (double*)smem;
-  double* w_d2 = w_s1 + qw * C;
-  double* l_qbt = w_d2 + qw * kCtxSlots;
-  int16_t* l_qbq = (int16_t*)(l_qbt + kQbN);
+  uint8_t* lut = smem;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int q_lo = P.w.q_lo;
-  for (int i = tid; i < kQbN; i += blockDim.x) {
-    l_qbt[i] = P.qb_thr[i];
-    l_qbq[i] = P.qb_q[i];
-  }
   const int G = gridDim.x;
-  const bool ident = P.ord.perm == nullptr;
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
 
@@ -1592,21 +1654,30 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
     if (p0 >= wb) break;
     if (p0 >= p1) continue;
-    // the piece's window rows: read group rg_lo, quals q_lo .. q_lo + qw - 1.
-    // Rows whose key is not in the table hold NaN: the fast path sends such
-    // bases to the checked path (a valid a2 + deltas is never NaN)
-    const int rg_lo = ident ? P.w.rg_lo : key;
+    const int rg_lo = key_rg(P.ord, key, P.w.rg_lo);
+    const WinGeom gm = win_geom(P.ord, P.g, key);
+    const int c_lo = gm.c_lo, cw = gm.cw, cw21 = cw * kCtxSlots;
     const bool win_ok = rg_lo < P.n_rg;
     const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
-    __syncthreads();  // the previous piece is done with the window
-    for (int i = tid; i < qw * C; i += blockDim.x) {
-      const int slot = i / C;
-      const bool ok = win_ok && q_lo + slot < kQBins && P.rq_ok[rq0 + slot];
-      w_s1[i] = ok ? P.s1[(rq0 + slot) * C + (i - slot * C)] : __builtin_nan("");
-    }
-    for (int i = tid; i < qw * kCtxSlots; i += blockDim.x) {
-      const int slot = i / kCtxSlots;
-      w_d2[i] = (win_ok && q_lo + slot < kQBins) ? P.d2[(rq0 + slot) * kCtxSlots + (i - slot * kCtxSlots)] : 0.0;
+    __syncthreads();  // the previous piece is done with the table
+    // ---- the piece's char table: one thread per (row, cycle cell), 21 contexts each ----
+    for (int i = tid; i < qw * cw; i += blockDim.x) {
+      const int row = i / cw, c = i - row * cw;
+      const int64_t rq = rq0 + row;
+      const bool ok = win_ok && q_lo + row < kQBins && P.rq_ok[rq];
+      uint8_t* dst = lut + (int64_t)i * kCtxSlots;
+      if (!ok) {
+        for (int x = 0; x < kCtxSlots; ++x) dst[x] = 0;
+        continue;
+      }
+      const double s1 = P.s1[rq * C + c_lo + c];
+      const double* d2 = P.d2 + rq * kCtxSlots;
+      for (int x = 0; x < kCtxSlots; ++x) {
+        // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+        const int32_t Q = phred_q(s1 + d2[x], P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
+        const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+        dst[x] = code <= 0xFFu ? (uint8_t)code : 0;
+      }
     }
     __syncthreads();
 
@@ -1632,18 +1703,18 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
         // issue every load of the super-chunk first
         uint4 qs[kSub], cr[kSub];
         int64_t cn0[kSub];
-  #pragma unroll
+#pragma unroll
         for (int i = 0; i < kSub; ++i) {
-          const bool live = j0 + kChunk * i < n;
+          const bool lv = j0 + kChunk * i < n;
           const int o0 = x.st + j0 + kChunk * i;
-          qs[i] = live ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
+          qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
           cn0[i] = chunk_n0(x, o0);
-          cr[i] = (live && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
+          cr[i] = (lv && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
         }
         // the super-chunk's chars, stored together after its last chunk so the
         // lines they share are written while resident in L2
         uint4 outs[kSub];
-  #pragma clang loop unroll(full)
+#pragma clang loop unroll(full)
         for (int i = 0; i < kSub; ++i) {
           const int j = j0 + kChunk * i;
           if (j >= n) continue;
@@ -1653,7 +1724,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
           uint32_t slow = 0;
           uint32_t xo[4] = {4u, 4u, 4u, 4u};
           if (pass) {  // the original chars: (qual + 33) byte-wise
-  #pragma unroll
+#pragma unroll
             for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
           } else {
             uint64_t clo = 0;
@@ -1661,28 +1732,27 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
             chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
             ctx_slots(clo, chi, xo);
             if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
-            const int cc0 = x.cell0 + x.dir * o0;
+            const int wc0 = x.cell0 + __mul24(x.dir, o0) - c_lo;  // window cycle cell of offset k: wc0 + dir * k
+            // the cycle cells of the chunk's valid offsets inside the table
+            // (monotone in k: both ends); invalid offsets may index past the
+            // table's rows: their reads are masked to entry 0
+            const uint32_t nv = (uint32_t)min(kChunk, n - j);
+            const bool cok = fast_rd && (unsigned)wc0 < (unsigned)cw && (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
+            const uint32_t vmask = nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u);
+            const int cx0 = wc0 * kCtxSlots, dx = x.dir * kCtxSlots;
             out[0] = out[1] = out[2] = out[3] = 0;
-  #pragma unroll
+            uint32_t goodm = 0;
+#pragma unroll
             for (int k = 0; k < kChunk; ++k) {
-              const int q = (int)(int8_t)(uint8_t)(qd[k >> 2] >> (8 * (k & 3)));
+              const int q = (int)((qd[k >> 2] >> (8 * (k & 3))) & 0xFFu);
               const int row = q - q_lo;
-              const bool inwin = fast_rd && (unsigned)row < (unsigned)qw;
-              const int rowc = inwin ? row : 0;
-              const int ccell = cc0 + x.dir * k;
+              const bool ok = cok && (unsigned)row < (unsigned)qw && k < (int)nv;
               const int xs = (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-              // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-              const double p = w_s1[rowc * C + ccell] + w_d2[rowc * kCtxSlots + xs];
-              const uint32_t b = phred_bucket(p);
-              const bool bok = b < (uint32_t)kQbN;
-              const uint32_t bc = bok ? b : 0u;
-              const int qq = l_qbq[bc];
-              const int Q = p <= l_qbt[bc] ? qq : qq - 1;
-              const uint32_t code = (uint32_t)(Q + 33);  // (Q + 33).toChar, <= 0xFF on this path
-              const bool good = inwin && bok && qq != -32768 && code <= 0xFFu;
-              slow |= (uint32_t)(!good && j + k < n) << k;
-              out[k >> 2] |= (code & 0xFFu) << (8 * (k & 3));
+              const uint32_t code = lut[ok ? row * cw21 + cx0 + dx * k + xs : 0];
+              goodm |= (uint32_t)(ok && code != 0u) << k;
+              out[k >> 2] |= code << (8 * (k & 3));
             }
+            slow = vmask & ~goodm;
           }
           // ---- the checked path, in offset order (the first failing offset wins) ----
           if (__builtin_amdgcn_ballot_w64(slow != 0)) {
@@ -1710,14 +1780,14 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
               const int64_t rq = (int64_t)x.rg * kQBins + q;
               const int ccell = x.cell0 + x.dir * o;
               const double p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + xs];
-              const int32_t Q = phred_q(p, l_qbt, l_qbq, P.thr, P.thr_qmin, P.thr_n);
+              const int32_t Q = phred_q(p, P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
               const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
               if (code > 0xFFu) {
                 const unsigned long long e = atomicAdd(P.n_exc, 1ull);
                 if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
               }
               const uint32_t sh = 8u * (uint32_t)(k & 3);
-  #pragma unroll
+#pragma unroll
               for (int w = 0; w < 4; ++w)
                 if (w == (k >> 2)) out[w] = (out[w] & ~(0xFFu << sh)) | ((code & 0xFFu) << sh);
             }
@@ -1725,7 +1795,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
           outs[i] = make_uint4(out[0], out[1], out[2], out[3]);
         }
         if (app || pass) {
-  #pragma clang loop unroll(full)
+#pragma clang loop unroll(full)
           for (int i = 0; i < kSub; ++i) {
             const int j = j0 + kChunk * i;
             if (j >= n) continue;
@@ -1734,7 +1804,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
               *(uint4*)(op + o0) = outs[i];
             } else {
               const uint32_t ov[4] = {outs[i].x, outs[i].y, outs[i].z, outs[i].w};
-  #pragma unroll
+#pragma unroll
               for (int k = 0; k < kChunk; ++k)
                 if (k < n - j) op[o0 + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
             }
@@ -1745,6 +1815,8 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   }  // pieces
 }
 
+template __global__ void bqsr_observe_kernel<false>(ObserveParams);
+template __global__ void bqsr_observe_kernel<true>(ObserveParams);
 
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {
