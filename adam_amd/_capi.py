@@ -58,7 +58,8 @@ class FinalStats(ctypes.Structure):
 class DeviceReads(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_int64), ("n_slots", ctypes.c_int64), ("meta", ctypes.c_void_p),
                 ("align", ctypes.c_void_p), ("qual", ctypes.c_void_p), ("bases", ctypes.c_void_p),
-                ("cigar", ctypes.c_void_p), ("md", ctypes.c_void_p), ("dims", Dims)]
+                ("cigar", ctypes.c_void_p), ("md", ctypes.c_void_p), ("dims", Dims),
+                ("slots_aligned", ctypes.c_int32)]
 
 
 _lib = None

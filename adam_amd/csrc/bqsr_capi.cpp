@@ -178,7 +178,29 @@ int observe_rows(int wcells) {
   while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;
   return qw;
 }
-// observe's rotated fast path (bqsr_observe_kernel<true>); ADAM_BQSR_OBSERVE_ROTATE=0/1 overrides
+// 16-aligned packed layout (ReadsDev::slots_aligned); ADAM_BQSR_ALIGN=0 packs reads back to back
+bool align_slots() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_ALIGN");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+// per-base passes with lanes per super-chunk or a lane per read (kCL):
+// apply always takes the former, observe the former for bucketed batches
+// (measured: a lane per read is faster for observe in read order, where its
+// LDS window counts dominate); ADAM_BQSR_LANES=read / chunk forces either
+bool chunk_lanes(bool dflt) {
+  static const int v = [] {
+    const char* e = getenv("ADAM_BQSR_LANES");
+    return !e ? -1 : strcmp(e, "read") == 0 ? 0 : 1;
+  }();
+  return v < 0 ? dflt : v != 0;
+}
+// lanes per read of the lane-per-super-chunk passes: 2^s >= the super-chunks
+// (64 offsets) of the batch's longest read (at most 64; longer reads loop)
+int lane_shift(const bqsr_batch* b);
+// observe's rotated fast path (bqsr_observe_kernel<true, false>); ADAM_BQSR_OBSERVE_ROTATE=0/1 overrides
 bool observe_rotate() {
   static const bool v = [] {
     const char* e = getenv("ADAM_BQSR_OBSERVE_ROTATE");
@@ -335,10 +357,10 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  for (const void* f : {(const void*)bqsr_observe_kernel<false>, (const void*)bqsr_observe_kernel<true>})
+  for (const void* f : {(const void*)bqsr_observe_kernel<false, false>, (const void*)bqsr_observe_kernel<true, false>,
+                        (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel<false>,
+                        (const void*)bqsr_apply_kernel<true>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_apply_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e != hipSuccess) {
     bqsr_context_destroy(c);
     return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
@@ -519,7 +541,7 @@ bqsr_status pack(const bqsr_records* R, Packed& P) {
     a.contig = R->contig_id[r];
     a.n_cigar = (uint16_t)ncig;
     a.md_len = (uint16_t)nmd;
-    const uint64_t sl = std::max(lq, ls);
+    const uint64_t sl = align_slots() ? slot_span(lq, ls) : std::max(lq, ls);  // ReadsDev::slots_aligned
     slot += sl;
     P.max_slot = std::max<int64_t>(P.max_slot, (int64_t)sl);
     md_tot += nmd;
@@ -642,6 +664,7 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
   b->rd.bases = bases;
   b->rd.md = md;
   b->rd.cigar = cigar;
+  b->rd.slots_aligned = align_slots();
   if ((st = finish_batch(b, P.max_slot)) != BQSR_OK) {
     delete b;
     return st;
@@ -676,7 +699,9 @@ bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* d
   b->dims = dev->dims;
   b->q_lo = 0;
   b->rg_lo = 0;
-  bqsr_status st = finish_batch(b, dev->dims.max_len);
+  b->rd.slots_aligned = dev->slots_aligned != 0;
+  bqsr_status st = finish_batch(b, b->rd.slots_aligned ? (int64_t)slot_span(0, (uint64_t)dev->dims.max_len)
+                                                       : (int64_t)dev->dims.max_len);
   if (st != BQSR_OK) {
     delete b;
     return st;
@@ -789,6 +814,12 @@ Window window_rows(const bqsr_batch* b, int max_rows) {
 // cycle cells of the windows: all of them in read order, one mate class's
 // half when bucketed (OrderDev, WinGeom)
 int window_cw(const bqsr_batch* b, const TableGeom& g) { return b->bucketed ? g.L : g.C; }
+int lane_shift(const bqsr_batch* b) {
+  const int c = (b->dims.max_len + kSuper - 1) / kSuper;
+  int s = 0;
+  while ((1 << s) < c && s < 6) ++s;
+  return s;
+}
 bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
   if (b->dims.n_rg > t->dims.n_rg || b->dims.max_len > t->dims.max_len)
     return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's (n_rg / max_len)");
@@ -883,10 +914,13 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
     const size_t lds = observe_lds(P.w.qw, P.wcells);
-    if (observe_rotate())
-      hipLaunchKernelGGL(bqsr_observe_kernel<true>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    P.lane_shift = lane_shift(b);
+    if (chunk_lanes(b->bucketed))
+      hipLaunchKernelGGL((bqsr_observe_kernel<false, true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    else if (observe_rotate())
+      hipLaunchKernelGGL((bqsr_observe_kernel<true, false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else
-      hipLaunchKernelGGL(bqsr_observe_kernel<false>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+      hipLaunchKernelGGL((bqsr_observe_kernel<false, false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_keys : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
@@ -1189,7 +1223,11 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
   const size_t lds = apply_lds(P.w.qw, cw);
-  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  P.lane_shift = lane_shift(b);
+  if (chunk_lanes(true))
+    hipLaunchKernelGGL(bqsr_apply_kernel<true>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  else
+    hipLaunchKernelGGL(bqsr_apply_kernel<false>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
   return ok();
 }
@@ -1257,7 +1295,7 @@ bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* R, const b
         const uint32_t f = R->flags[r];
         const uint64_t lq = (f & BQSR_F_HAS_QUAL) ? R->qual_offset[r + 1] - R->qual_offset[r] : 0;
         const uint64_t ls = (f & BQSR_F_HAS_SEQ) ? R->seq_offset[r + 1] - R->seq_offset[r] : 0;
-        slot[(size_t)r + 1] = slot[(size_t)r] + std::max(lq, ls);
+        slot[(size_t)r + 1] = slot[(size_t)r] + (b->rd.slots_aligned ? slot_span(lq, ls) : std::max(lq, ls));
       }
       std::vector<uint16_t> wide;  // exceptions keyed by slot
       std::vector<std::pair<uint64_t, uint16_t>> ex;

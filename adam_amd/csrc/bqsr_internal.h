@@ -130,7 +130,14 @@ struct ReadsDev {
   int64_t n_slots;  // base slots of the batch (qual[] holds n_slots bytes, bases[] n_slots nibbles)
   int32_t reads_per_tile;
   int64_t n_tiles;
+  int32_t slots_aligned;  // every read's slot is a multiple of 16 and its slot range is padded to 16
+                          // (slot_span): the per-base passes then walk 16-aligned chunks
 };
+// slots a read takes in the packed layout (bqsr_batch_create pads to 16)
+__host__ __device__ inline uint64_t slot_span(uint64_t lq, uint64_t ls) {
+  const uint64_t sl = lq > ls ? lq : ls;
+  return (sl + 15) & ~(uint64_t)15;
+}
 
 // Slot bitmap: u64 word i covers base slots 32i .. 32i+31 of the batch, bit j
 // of the low half = slot 32i+j is masked, of the high half = it mismatches.
@@ -177,6 +184,7 @@ struct ObserveParams {
   unsigned long long* err;
   int32_t n_blocks;
   int32_t wcells;      // window row length: WinGeom::cw + 21
+  int32_t lane_shift;  // lane-per-chunk kernels: log2(lanes per read)
 };
 
 struct FoldParams {
@@ -224,6 +232,7 @@ struct ApplyParams {
   int64_t max_exc;
   unsigned long long* n_exc;
   unsigned long long* err;
+  int32_t lane_shift;  // lane-per-chunk kernel: log2(lanes per read)
 };
 
 // finalize results read back by the host

@@ -622,6 +622,18 @@ __device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[
   }
 }
 
+// context slot of chunk offset k := 4 (context 0); shifts on two u64 halves,
+// not a dynamically indexed array (which the compiler would put in scratch)
+__device__ __forceinline__ void ctx_first(uint32_t xo[4], int k) {
+  const uint64_t m = 0xFFull << (8 * (k & 7)), v = 0x0404040404040404ull & m;
+  uint64_t lo = ((uint64_t)xo[1] << 32) | xo[0], hi = ((uint64_t)xo[3] << 32) | xo[2];
+  if (k < 8) lo = (lo & ~m) | v; else hi = (hi & ~m) | v;
+  xo[0] = (uint32_t)lo;
+  xo[1] = (uint32_t)(lo >> 32);
+  xo[2] = (uint32_t)hi;
+  xo[3] = (uint32_t)(hi >> 32);
+}
+
 // 16 bytes rotated right by r (0..15) bytes: byte k of the result = byte (k + r) & 15
 __device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
   const uint32_t d = r >> 2, b = r & 3;
@@ -644,7 +656,8 @@ __device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
 // kRot: lane l visits a chunk's offsets rotated by l & 15, so the lanes of a
 // wavefront (reads of equal length at equal offsets) hit different cycle
 // cells in each step instead of piling onto one LDS address.
-template <bool kRot>
+// kCL: lane per chunk (see kCL below).
+template <bool kRot, bool kCL>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -662,6 +675,16 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   const int q_lo = P.w.q_lo;
   const int nk = order_keys(P.ord);
+  // kCL (lane per super-chunk): a wavefront step takes 64 >> ls reads with
+  // 2^ls lanes each, lane `sub` of a read taking its super-chunks (kSub
+  // chunks, 64 offsets) sub, sub + 2^ls, ...: the lanes of a read cover
+  // neighbouring 64-B pieces of its columns, so a wavefront's loads and
+  // stores fill whole cache lines at once.  Otherwise a lane per read walks
+  // all its super-chunks.
+  const int ls = kCL ? P.lane_shift : 6;
+  const int sub = kCL ? lane & ((1 << ls) - 1) : 0, rl = kCL ? lane >> ls : lane, rpw = kCL ? 64 >> ls : 64;
+  constexpr int NS = kSub;
+  const int jstep = kSuper << (kCL ? ls : 0);
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -674,22 +697,25 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
 
-    for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
-      const bool live = g0 + lane < p1;
-      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + lane) : 0, live, L);
+    for (int64_t g0 = p0 + (int64_t)rpw * wave; g0 < p1; g0 += (int64_t)rpw * kWaves) {
+      const bool live = g0 + rl < p1;
+      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + rl) : 0, live, L);
       const bool act = x.fl & (kInfoObs | kInfoObsCheck);
       const bool full = x.fl & kInfoObs;
       const int n = act ? x.en - x.st : 0;
       const bool full_rg = full && x.rg == rg_w;
+      // chunks start at offset st, or at st rounded down to 16 in the aligned
+      // layout (then the first chunk's offsets below st are not visited)
+      const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;
       const uint8_t* qp = P.rd.qual + x.slot;
-      for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
+      for (int j0 = jb + kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += jstep) {
         if (j0 >= n) continue;
         // issue every load of the super-chunk first
-        uint4 qs[kSub], cr[kSub];
+        uint4 qs[NS], cr[NS];
         uint64_t bw[3] = {0, 0, 0};
         const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
 #pragma unroll
-        for (int i = 0; i < kSub; ++i) {
+        for (int i = 0; i < NS; ++i) {
           const bool lv = j0 + kChunk * i < n;
           const int o0 = x.st + j0 + kChunk * i;
           qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
@@ -701,7 +727,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           bw[2] = P.sbits[(s0 >> 5) + 2];
         }
 #pragma clang loop unroll(full)
-        for (int i = 0; i < kSub; ++i) {
+        for (int i = 0; i < NS; ++i) {
           const int j = j0 + kChunk * i;
           if (j >= n) continue;
           const int o0 = x.st + j;
@@ -714,15 +740,17 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
             uint32_t chi;
             chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
             ctx_slots(clo, chi, xo);
-            if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+            if (j <= 0) ctx_first(xo, -j);  // the read's first visited offset: context 0
           }
           const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
           const int wc0 = cc0 - c_lo;                     // ... and window cycle cell
           // the cycle cells of the chunk's valid offsets inside the window
           // (monotone in k: both ends)
           const uint32_t nv = (uint32_t)min(kChunk, n - j);
-          const bool cok = full_rg && (unsigned)wc0 < (unsigned)cw && (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
-          const uint32_t vmask = nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u);
+          const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
+          const bool cok = full_rg && (unsigned)(wc0 + klo * x.dir) < (unsigned)cw &&
+                           (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
+          const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
           // fast path: window rows of the piece's read group; offsets it skips
           // are redone below
           const uint32_t rot = kRot ? (uint32_t)lane & 15u : 0u;
@@ -1636,6 +1664,7 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
 // only being checked) set a bit of `slow` and are redone after the chunk by
 // the exact checked path.  A super-chunk's chars leave as 16-B stores (a
 // read's last chunk byte-wise).
+template <bool kCL>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
@@ -1648,6 +1677,16 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   const int G = gridDim.x;
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
+  // kCL (lane per super-chunk): a wavefront step takes 64 >> ls reads with
+  // 2^ls lanes each, lane `sub` of a read taking its super-chunks (kSub
+  // chunks, 64 offsets) sub, sub + 2^ls, ...: the lanes of a read cover
+  // neighbouring 64-B pieces of its columns, so a wavefront's loads and
+  // stores fill whole cache lines at once.  Otherwise a lane per read walks
+  // all its super-chunks.
+  const int ls = kCL ? P.lane_shift : 6;
+  const int sub = kCL ? lane & ((1 << ls) - 1) : 0, rl = kCL ? lane >> ls : lane, rpw = kCL ? 64 >> ls : 64;
+  constexpr int NS = kSub;
+  const int jstep = kSuper << (kCL ? ls : 0);
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -1681,10 +1720,10 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     }
     __syncthreads();
 
-    for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
-      const bool live = g0 + lane < p1;
-      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + lane) : 0, live, L);
-      if (live) {
+    for (int64_t g0 = p0 + (int64_t)rpw * wave; g0 < p1; g0 += (int64_t)rpw * kWaves) {
+      const bool live = g0 + rl < p1;
+      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + rl) : 0, live, L);
+      if (live && sub == 0) {
         if (x.fl & kInfoPass) {  // quality string passed through
           P.out_start[x.r] = 0;
           P.out_len[x.r] = (uint32_t)x.en;
@@ -1696,26 +1735,22 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
       const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
       const int n = (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) ? x.en - x.st : 0;
       const bool fast_rd = app && x.rg == rg_lo;
+      const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;  // as in observe
       const uint8_t* qp = P.rd.qual + x.slot;
       uint8_t* op = P.out_qual + x.slot;
-      for (int j0 = 0; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper) {
+      for (int j0 = jb + kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += jstep) {
         if (j0 >= n) continue;
         // issue every load of the super-chunk first
-        uint4 qs[kSub], cr[kSub];
-        int64_t cn0[kSub];
+        uint4 qs[NS], cr[NS];
 #pragma unroll
-        for (int i = 0; i < kSub; ++i) {
+        for (int i = 0; i < NS; ++i) {
           const bool lv = j0 + kChunk * i < n;
           const int o0 = x.st + j0 + kChunk * i;
           qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
-          cn0[i] = chunk_n0(x, o0);
-          cr[i] = (lv && !pass) ? chunk_raw(P.rd, cn0[i]) : make_uint4(0, 0, 0, 0);
+          cr[i] = (lv && !pass) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
         }
-        // the super-chunk's chars, stored together after its last chunk so the
-        // lines they share are written while resident in L2
-        uint4 outs[kSub];
 #pragma clang loop unroll(full)
-        for (int i = 0; i < kSub; ++i) {
+        for (int i = 0; i < NS; ++i) {
           const int j = j0 + kChunk * i;
           if (j >= n) continue;
           const int o0 = x.st + j;
@@ -1729,16 +1764,18 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
           } else {
             uint64_t clo = 0;
             uint32_t chi = 0;
-            chunk_finish(P.rd, x, cn0[i], cr[i], clo, chi);
+            chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
             ctx_slots(clo, chi, xo);
-            if (j == 0) xo[0] = (xo[0] & ~0xFFu) | 4u;  // the read's first offset: context 0
+            if (j <= 0) ctx_first(xo, -j);  // the read's first visited offset: context 0
             const int wc0 = x.cell0 + __mul24(x.dir, o0) - c_lo;  // window cycle cell of offset k: wc0 + dir * k
             // the cycle cells of the chunk's valid offsets inside the table
             // (monotone in k: both ends); invalid offsets may index past the
             // table's rows: their reads are masked to entry 0
             const uint32_t nv = (uint32_t)min(kChunk, n - j);
-            const bool cok = fast_rd && (unsigned)wc0 < (unsigned)cw && (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
-            const uint32_t vmask = nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u);
+            const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
+            const bool cok = fast_rd && (unsigned)(wc0 + klo * x.dir) < (unsigned)cw &&
+                             (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
+            const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
             const int cx0 = wc0 * kCtxSlots, dx = x.dir * kCtxSlots;
             out[0] = out[1] = out[2] = out[3] = 0;
             uint32_t goodm = 0;
@@ -1746,7 +1783,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
             for (int k = 0; k < kChunk; ++k) {
               const int q = (int)((qd[k >> 2] >> (8 * (k & 3))) & 0xFFu);
               const int row = q - q_lo;
-              const bool ok = cok && (unsigned)row < (unsigned)qw && k < (int)nv;
+              const bool ok = cok && (unsigned)row < (unsigned)qw && ((vmask >> k) & 1u);
               const int xs = (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
               const uint32_t code = lut[ok ? row * cw21 + cx0 + dx * k + xs : 0];
               goodm |= (uint32_t)(ok && code != 0u) << k;
@@ -1786,27 +1823,23 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
                 const unsigned long long e = atomicAdd(P.n_exc, 1ull);
                 if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
               }
-              const uint32_t sh = 8u * (uint32_t)(k & 3);
-#pragma unroll
-              for (int w = 0; w < 4; ++w)
-                if (w == (k >> 2)) out[w] = (out[w] & ~(0xFFu << sh)) | ((code & 0xFFu) << sh);
+              // byte k of out[] := code (u64 halves: no dynamically indexed array)
+              const uint64_t m = 0xFFull << (8 * (k & 7)), v = (uint64_t)(code & 0xFFu) << (8 * (k & 7));
+              uint64_t lo = ((uint64_t)out[1] << 32) | out[0], hi = ((uint64_t)out[3] << 32) | out[2];
+              if (k < 8) lo = (lo & ~m) | v; else hi = (hi & ~m) | v;
+              out[0] = (uint32_t)lo;
+              out[1] = (uint32_t)(lo >> 32);
+              out[2] = (uint32_t)hi;
+              out[3] = (uint32_t)(hi >> 32);
             }
           }
-          outs[i] = make_uint4(out[0], out[1], out[2], out[3]);
-        }
-        if (app || pass) {
-#pragma clang loop unroll(full)
-          for (int i = 0; i < kSub; ++i) {
-            const int j = j0 + kChunk * i;
-            if (j >= n) continue;
-            const int o0 = x.st + j;
-            if (j + kChunk <= n) {
-              *(uint4*)(op + o0) = outs[i];
+          if (app || pass) {
+            if (j + kChunk <= n || P.rd.slots_aligned) {  // aligned: the chunk's other bytes are this read's scratch
+              *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
             } else {
-              const uint32_t ov[4] = {outs[i].x, outs[i].y, outs[i].z, outs[i].w};
 #pragma unroll
               for (int k = 0; k < kChunk; ++k)
-                if (k < n - j) op[o0 + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+                if (k < n - j) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
             }
           }
         }
@@ -1815,8 +1848,11 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   }  // pieces
 }
 
-template __global__ void bqsr_observe_kernel<false>(ObserveParams);
-template __global__ void bqsr_observe_kernel<true>(ObserveParams);
+template __global__ void bqsr_observe_kernel<false, false>(ObserveParams);
+template __global__ void bqsr_observe_kernel<true, false>(ObserveParams);
+template __global__ void bqsr_observe_kernel<false, true>(ObserveParams);
+template __global__ void bqsr_apply_kernel<false>(ApplyParams);
+template __global__ void bqsr_apply_kernel<true>(ApplyParams);
 
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {

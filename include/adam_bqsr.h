@@ -166,6 +166,10 @@ typedef struct bqsr_device_reads {
   const uint32_t* cigar;  /* BAM elements; 32 readable bytes of padding past the end     */
   const uint8_t* md;      /* MD bytes; 32 readable bytes of padding past the end        */
   bqsr_dims dims;
+  int32_t slots_aligned;  /* nonzero: every slot is a multiple of 16 and each read's
+                             slot range is max(Ls, Lq) rounded up to 16 (the layout
+                             bqsr_batch_create builds); the per-base passes then use
+                             aligned 16-B accesses                                    */
 } bqsr_device_reads;
 bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* dev, bqsr_batch** out);
 
@@ -278,7 +282,8 @@ bqsr_status bqsr_apply_result(bqsr_batch* b, int64_t* n_exceptions, void* stream
  * rg_lo, quals q_lo.. (chosen from the packed quals; settable for device batches). */
 bqsr_status bqsr_batch_set_window(bqsr_batch* b, int32_t q_lo, int32_t rg_lo);
 int32_t bqsr_batch_reads_per_tile(const bqsr_batch* b);
-/* base slots of the packed layout (sum over reads of max(Ls, Lq)): the size of apply's out_qual */
+/* base slots of the packed layout (sum over reads of max(Ls, Lq) rounded up to 16): the size of
+ * apply's out_qual */
 int64_t bqsr_batch_slots(const bqsr_batch* b);
 /* read-group counts of a finalized table, group r at (r >= -1): 1 found, 0 absent, -1 error */
 int bqsr_lut_group(const bqsr_lut* l, int32_t r, int64_t* obs, int64_t* mm);
