@@ -115,6 +115,8 @@ def lib():
             "bqsr_finalize": (ctypes.c_int, [vp, vp, dbl, pp]),
             "bqsr_finalize_async": (ctypes.c_int, [vp, vp, dbl, pp, vp]),
             "bqsr_finalize_result": (ctypes.c_int, [vp, vp]),
+            "bqsr_finalize_device": (ctypes.c_int, [vp, vp, vp, pp, vp]),
+            "bqsr_batch_em_copy_async": (ctypes.c_int, [vp, vp, vp]),
             "bqsr_lut_destroy": (None, [vp]),
             "bqsr_lut_stats": (ctypes.c_int, [vp, ctypes.POINTER(FinalStats)]),
             "bqsr_lut_group": (ctypes.c_int, [vp, i32, ctypes.POINTER(i64), ctypes.POINTER(i64)]),

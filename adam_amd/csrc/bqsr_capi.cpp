@@ -361,6 +361,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
                         (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel<false>,
                         (const void*)bqsr_apply_kernel<true>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
   if (e != hipSuccess) {
     bqsr_context_destroy(c);
     return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
@@ -930,8 +932,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   }
   if (stages & BQSR_STAGE_FOLD) {
     if (b->bucketed) {  // the observe kernel did not walk the fold's blocks: their histograms
-      hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks), dim3(1024), 0, s, b->rd, (const ReadInfo*)b->d_info,
-                         b->n_blocks, b->d_hq);
+      HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
+      hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
+                         b->n_blocks, lane_shift(b), b->d_hq);
       HIP_TRY(hipGetLastError());
     }
     int32_t* n_cand = b->d_cand_list + b->n_blocks;
@@ -1013,7 +1016,9 @@ bqsr_status bqsr_observe_records(bqsr_context* ctx, const bqsr_records* recs, co
 
 // ------------------------------------------------------------- finalize ----
 
-bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double em, bqsr_lut** out, void* stream) {
+namespace {
+bqsr_status finalize_impl(bqsr_context* ctx, const bqsr_table* t, double em, const double* em_dev, bqsr_lut** out,
+                          void* stream) {
   if (!ctx || !t || !out) return fail(BQSR_ERR_INVALID_ARG, "null");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
@@ -1044,7 +1049,7 @@ bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double e
   hipLaunchKernelGGL(bqsr_final_keys, dim3((g.K + 3) / 4), dim3(256), 0, s, t->touched(), t->obs(), t->mm(), g, L->qk_obs,
                      L->qk_mm);
   hipLaunchKernelGGL(bqsr_final_groups, dim3(1), dim3(256), 0, s, t->touched(), L->qk_obs, L->qk_mm, g, n_rg, em,
-                     ctx->d_pow10, L->n_groups, L->grp_obs, L->grp_mm, L->grp_ok, L->key_ok, L->a2, L->rq_ok, L->d_out);
+                     em_dev, ctx->d_pow10, L->n_groups, L->grp_obs, L->grp_mm, L->grp_ok, L->key_ok, L->a2, L->rq_ok, L->d_out);
   const int64_t ncell = (int64_t)n_rg * kQBins * (g.C + kCtxSlots);
   hipLaunchKernelGGL(bqsr_final_tables, dim3((unsigned)std::min<int64_t>(8192, (ncell + 255) / 256)), dim3(256), 0, s,
                      t->obs(), t->mm(), g, n_rg, L->a2, L->rq_ok, pow10tab().v[kMaxQ], L->s1, L->d2);
@@ -1055,6 +1060,24 @@ bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double e
     return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
   }
   *out = L;
+  return ok();
+}
+}  // namespace
+
+bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double em, bqsr_lut** out, void* stream) {
+  return finalize_impl(ctx, t, em, nullptr, out, stream);
+}
+
+bqsr_status bqsr_finalize_device(bqsr_context* ctx, const bqsr_table* t, const double* em_device, bqsr_lut** out,
+                                 void* stream) {
+  if (!em_device) return fail(BQSR_ERR_INVALID_ARG, "null em_device");
+  return finalize_impl(ctx, t, 0.0, em_device, out, stream);
+}
+
+bqsr_status bqsr_batch_em_copy_async(bqsr_batch* b, double* dst, void* stream) {
+  if (!b || !dst) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  HIP_TRY(hipMemcpyAsync(dst, b->d_em, sizeof(double), hipMemcpyDeviceToDevice, S(stream)));
   return ok();
 }
 

@@ -995,64 +995,62 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
 
 // Per-block qual histograms of the folded bases (usable valid reads, trimmed
 // ranges) in read order, for bucketed batches whose observe kernel does not
-// walk the fold's blocks.  One workgroup per block, one wavefront per tile:
-// the tile's folded ranges become an LDS slot bitmap, then each lane takes 16
-// consecutive slots per step (one 16-B load) and counts the set ones into
-// its wavefront's histogram (four copies by lane & 3 against same-bin
-// conflicts).
+// walk the fold's blocks.  kFhSplit workgroups per block, each adding its
+// part into hq_block (zeroed first); lanes as in the lane-per-super-chunk
+// passes (2^ls lanes per read, 64 offsets each, 16-B loads), every folded
+// base one LDS atomic into its wavefront's histogram: kFhCopies copies by
+// lane & 7 against same-bin conflicts, rows kQBins + 1 words apart so one
+// bin's copies sit in different LDS banks.  66 KB of LDS: two workgroups per
+// CU.
 constexpr int kFhWaves = 16;
+constexpr int kFhSplit = 2;
+constexpr int kFhCopies = 8;
+constexpr int kFhStride = kQBins + 1;
+constexpr size_t fold_hist_lds() { return (size_t)kFhWaves * kFhCopies * kFhStride * 4; }
 extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(ReadsDev rd, const ReadInfo* info,
-                                                                             int32_t n_blocks, uint32_t* hq_block) {
-  __shared__ uint32_t hist[kFhWaves][4][kQBins];
-  __shared__ uint32_t bm[kFhWaves][kTileSlots / 32 + 1];
+                                                                             int32_t n_blocks, int32_t ls,
+                                                                             uint32_t* hq_block) {
+  extern __shared__ uint32_t fh_smem[];
+  uint32_t* hist = fh_smem;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < kFhWaves * 4 * kQBins; i += blockDim.x) (&hist[0][0][0])[i] = 0;
+  for (int i = threadIdx.x; i < kFhWaves * kFhCopies * kFhStride; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  const int64_t nt = rd.n_tiles;
-  const int64_t t0 = nt * blockIdx.x / n_blocks, t1 = nt * (blockIdx.x + 1) / n_blocks;
-  uint32_t* hw = hist[wv][lane & 3];
-  for (int64_t t = t0 + wv; t < t1; t += kFhWaves) {
-    const int64_t r0 = t * (int64_t)rd.reads_per_tile;
-    const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
-    ReadMeta m{0, 0, 0, 0, 0};
-    ReadInfo inf{0, 0, 0, 0};
-    if (lane < nr) {
-      m = rd.meta[r0 + lane];
-      inf = info[r0 + lane];
-    }
-    const uint64_t ts0 = __shfl(m.slot, 0);
-    const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
-    for (int i = lane; i < kTileSlots / 32 + 1; i += 64) bm[wv][i] = 0;
-    wave_sync();
-    if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
-      int lo = (int)(m.slot - ts0) + inf.st;
-      const int hi = (int)(m.slot - ts0) + inf.en;
-      while (lo < hi) {
-        const int c = min(32 - (lo & 31), hi - lo);
-        atomicOr(&bm[wv][lo >> 5], (c == 32 ? 0xFFFFFFFFu : ((1u << c) - 1u)) << (lo & 31));
-        lo += c;
+  const int blk = blockIdx.x / kFhSplit, part = blockIdx.x - blk * kFhSplit;
+  const int64_t b0 = wg_begin(rd, blk, n_blocks), b1 = wg_begin(rd, blk + 1, n_blocks);
+  const int64_t r0 = b0 + (b1 - b0) * part / kFhSplit, r1 = b0 + (b1 - b0) * (part + 1) / kFhSplit;
+  uint32_t* hw = hist + (wv * kFhCopies + (lane & (kFhCopies - 1))) * kFhStride;
+  const int sub = lane & ((1 << ls) - 1), rl = lane >> ls, rpw = 64 >> ls;
+  for (int64_t g0 = r0 + (int64_t)rpw * wv; g0 < r1; g0 += (int64_t)rpw * kFhWaves) {
+    const int64_t r = g0 + rl;
+    int n = 0;
+    const uint8_t* qp = rd.qual;
+    if (r < r1) {
+      const ReadInfo inf = info[r];
+      if ((inf.fl & kInfoObs) && inf.en > inf.st) {
+        n = inf.en - inf.st;
+        qp = rd.qual + rd.meta[r].slot + inf.st;
       }
     }
-    wave_sync();
-    const uint8_t* qt = rd.qual + ts0;
-    for (int s0 = 16 * lane; s0 < nslots; s0 += 16 * 64) {
-      const uint4 v = *(const uint4*)(qt + s0);  // the column's padding covers the tail
-      uint32_t bits = (bm[wv][s0 >> 5] >> (s0 & 31)) & 0xFFFFu;
-      if (s0 + 16 > nslots) bits &= (1u << (nslots - s0)) - 1u;
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      while (bits) {
-        const int k = __builtin_ctz(bits);
-        bits &= bits - 1;
-        atomicAdd(&hw[(w[k >> 2] >> (8 * (k & 3))) & 0x7Fu], 1u);
+    for (int j0 = kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper << ls) {
+      if (j0 >= n) continue;
+      uint4 v[kSub];
+#pragma unroll
+      for (int i = 0; i < kSub; ++i) v[i] = j0 + kChunk * i < n ? *(const uint4*)(qp + j0 + kChunk * i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < kSub; ++i) {
+        const int m = n - j0 - kChunk * i;  // valid bytes of chunk i (all when >= 16)
+        const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k)
+          if (k < m) atomicAdd(&hw[(w[k >> 2] >> (8 * (k & 3))) & 0x7Fu], 1u);
       }
     }
-    wave_sync();
   }
   __syncthreads();
   for (int q = threadIdx.x; q < kQBins; q += blockDim.x) {
     uint32_t s = 0;
-    for (int i = 0; i < kFhWaves * 4; ++i) s += (&hist[0][0][0])[i * kQBins + q];
-    hq_block[(int64_t)blockIdx.x * kQBins + q] = s;
+    for (int i = 0; i < kFhWaves * kFhCopies; ++i) s += hist[i * kFhStride + q];
+    if (s) atomicAdd(&hq_block[(int64_t)blk * kQBins + q], s);
   }
 }
 
@@ -1424,6 +1422,8 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_fold_plan(const uint32_t*
 }
 
 constexpr int kUnroll = 4;
+constexpr int kThCopies = 8;
+constexpr int kThStride = kQBins + 1;
 
 // Per-tile qual histograms of the folded bases of the candidate blocks' tiles
 // (one wavefront per tile: the folded ranges of the tile's reads become an LDS
@@ -1431,7 +1431,7 @@ constexpr int kUnroll = 4;
 extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, const ReadInfo* info,
                                                                    const int32_t* cand_list, const int32_t* n_cand,
                                                                    int32_t n_blocks, int64_t max_tpb, uint16_t* h2) {
-  __shared__ uint32_t hist[4][kQBins];
+  __shared__ uint32_t hist[4][kThCopies * kThStride];  // copies by lane & 7, rows one word apart in banks
   __shared__ uint32_t bm[4][kTileSlots / 32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nt = rd.n_tiles;
@@ -1450,7 +1450,7 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, co
     }
     const uint64_t ts0 = __shfl(m.slot, 0);
     const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
-    for (int q = lane; q < kQBins; q += 64) hist[wv][q] = 0;
+    for (int q = lane; q < kThCopies * kThStride; q += 64) hist[wv][q] = 0;
     for (int i = lane; i < kTileSlots / 32; i += 64) bm[wv][i] = 0;
     wave_sync();
     if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
@@ -1474,11 +1474,16 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, co
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const int s = s0 + 64 * u;
-        if (qv[u] >= 0 && ((bm[wv][s >> 5] >> (s & 31)) & 1u)) atomicAdd(&hist[wv][qv[u]], 1u);
+        if (qv[u] >= 0 && ((bm[wv][s >> 5] >> (s & 31)) & 1u))
+          atomicAdd(&hist[wv][(lane & (kThCopies - 1)) * kThStride + qv[u]], 1u);
       }
     }
     wave_sync();
-    for (int q = lane; q < kQBins; q += 64) h2[t * kQBins + q] = (uint16_t)hist[wv][q];
+    for (int q = lane; q < kQBins; q += 64) {
+      uint32_t v = 0;
+      for (int c = 0; c < kThCopies; ++c) v += hist[wv][c * kThStride + q];
+      h2[t * kQBins + q] = (uint16_t)v;
+    }
     wave_sync();
   }
 }
@@ -1523,7 +1528,8 @@ __device__ __forceinline__ bool err_prob(int64_t obs, int64_t mm, double mre, do
 // one workgroup: groups, globals, average, then a2 per (rg, q)
 extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_t* touched, const int64_t* qk_obs,
                                                                       const int64_t* qk_mm, TableGeom g, int32_t n_rg,
-                                                                      double em, const double* pow10, int32_t n_groups,
+                                                                      double em_host, const double* em_dev,
+                                                                      const double* pow10, int32_t n_groups,
                                                                       int64_t* grp_obs, int64_t* grp_mm, uint8_t* grp_ok,
                                                                       uint8_t* key_ok, double* a2, uint8_t* rq_ok,
                                                                       FinalOut* out) {
@@ -1571,6 +1577,7 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_
     out->g_obs = go;
     out->g_mm = gm;
     out->any_key = any;
+    const double em = em_dev ? *em_dev : em_host;
     const double avg = em / (double)go;  // averageReportedError
     out->avg = avg;
     double ge;

@@ -53,3 +53,21 @@ def fold_expected_mismatch(em: float, device: torch.device | str = "cpu") -> flo
     for v in ems.tolist():
         total = total + v
     return total
+
+
+def fold_expected_mismatch_device(mine: torch.Tensor) -> torch.Tensor:
+    """fold_expected_mismatch without leaving the device: `mine` is this
+    rank's expectedMismatch as a 1-element float64 tensor; returns the
+    rank-order fold ((0.0 + e_0) + e_1) + ... as a 1-element tensor (each `+`
+    one IEEE double addition, as on the host)."""
+    if mine.dtype != torch.float64 or mine.numel() != 1:
+        raise TypeError("expectedMismatch is one float64")
+    total = torch.zeros(1, dtype=torch.float64, device=mine.device)
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return total + mine.reshape(1)
+    world = dist.get_world_size()
+    ems = torch.empty(world, dtype=torch.float64, device=mine.device)
+    dist.all_gather_into_tensor(ems, mine.reshape(1))
+    for i in range(world):
+        total = total + ems[i:i + 1]
+    return total

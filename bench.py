@@ -100,6 +100,8 @@ def main():
     torch.cuda.synchronize()
 
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+    em_t = torch.zeros(1, dtype=torch.float64, device=dev)
+    keep = {}
     kt = {"prep": [], "observe": [], "fold": [], "apply": []}
 
     def step(record: bool):
@@ -112,14 +114,17 @@ def main():
         ev[1].record(stream)
         check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_FOLD, sp))
         ev[2].record(stream)
-        em = ctypes.c_double()
-        check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
         # RecalTable.++ across ranks: exact int64 all-reduce over xGMI (RCCL),
-        # expectedMismatch folded in rank order (adam_amd/distributed.py)
-        D.allreduce_table(table_t)
-        total = D.fold_expected_mismatch(em.value, dev)
-        check(L.bqsr_finalize_async(ctx.handle, th, total, ctypes.byref(lut), sp))
-        check(L.bqsr_finalize_result(lut, sp))
+        # expectedMismatch all-gathered and folded in rank order on the device
+        # (adam_amd/distributed.py); no host round trip until the job's end
+        if world > 1:
+            check(L.bqsr_batch_em_copy_async(bh, ctypes.c_void_p(em_t.data_ptr()), sp))
+            D.allreduce_table(table_t)
+            keep["em"] = D.fold_expected_mismatch_device(em_t)
+            em_ptr = ctypes.c_void_p(keep["em"].data_ptr())
+        else:
+            em_ptr = ctypes.c_void_p(L.bqsr_batch_em_device_ptr(bh))
+        check(L.bqsr_finalize_device(ctx.handle, th, em_ptr, ctypes.byref(lut), sp))
         check(L.bqsr_apply_stage(ctx.handle, bh, lut, ctypes.c_void_p(out_qual.data_ptr()),
                                  ctypes.c_void_p(out_start.data_ptr()), ctypes.c_void_p(out_len.data_ptr()),
                                  ctypes.c_void_p(exc.data_ptr()), max_exc, _capi.STAGE_RESET, sp))
@@ -128,6 +133,10 @@ def main():
                                  ctypes.c_void_p(out_start.data_ptr()), ctypes.c_void_p(out_len.data_ptr()),
                                  ctypes.c_void_p(exc.data_ptr()), max_exc, _capi.STAGE_KERNEL, sp))
         ev[4].record(stream)
+        # the job's results and errors, in the order the reference raises them
+        em = ctypes.c_double()
+        check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
+        check(L.bqsr_finalize_result(lut, sp))
         nexc = ctypes.c_int64()
         check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
         if record:

@@ -266,6 +266,14 @@ bqsr_status bqsr_table_zero_async(bqsr_table* t, void* stream);
 bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double expected_mismatch, bqsr_lut** out,
                                 void* stream);
 bqsr_status bqsr_finalize_result(bqsr_lut* l, void* stream);
+/* as bqsr_finalize_async, with the expectedMismatch read on the device (one
+ * double at em_device: bqsr_batch_em_device_ptr, or the rank-order fold of
+ * the all-gathered values), so observe -> finalize -> apply needs no host
+ * round trip */
+bqsr_status bqsr_finalize_device(bqsr_context* ctx, const bqsr_table* t, const double* em_device, bqsr_lut** out,
+                                 void* stream);
+/* copy the batch's expectedMismatch (one double) to a device buffer, on `stream` */
+bqsr_status bqsr_batch_em_copy_async(bqsr_batch* b, double* dst_device, void* stream);
 /* apply stages: RESET clears the error word and exception count, KERNEL the
  * apply kernel; PREP (re)runs the prep kernel, which also runs by itself when
  * observe has not prepared this batch */

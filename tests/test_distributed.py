@@ -46,6 +46,9 @@ def _rank_main(rank, port, out_dir):
         t = torch.from_numpy(words.copy())
         D.allreduce_table(t)
         total = D.fold_expected_mismatch(em)
+        # the device form the benchmark uses (gloo: CPU tensors) folds identically
+        dev_total = float(D.fold_expected_mismatch_device(torch.tensor([em], dtype=torch.float64))[0])
+        assert dev_total == total
         fin = O.Final(d, t.numpy(), total)
         out, out_len = O.apply(batch, fin, r0, r1)
         np.savez(os.path.join(out_dir, "rank%d.npz" % rank), words=t.numpy(), em=np.array([total]),
