@@ -261,6 +261,9 @@ struct bqsr_batch {
   uint16_t* d_h2 = nullptr;
   uint32_t* d_hq = nullptr;
   uint8_t* d_cand = nullptr;       // [n_blocks] fold candidates
+  double* d_dblk = nullptr;        // FoldParams::dblk / dtile / elo
+  double* d_dtile = nullptr;
+  int16_t* d_elo = nullptr;
   int32_t* d_cand_list = nullptr;  // [n_blocks + 1]: list, then count
   uint32_t* d_part = nullptr;      // per-block window counts
   size_t part_words = 0;
@@ -469,6 +472,9 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   if ((st = dalloc(b->allocs, &b->d_h2, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kQBins)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_hq, (size_t)b->n_blocks * kQBins)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_cand, (size_t)b->n_blocks)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_dblk, (size_t)b->n_blocks * kFoldE)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_elo, (size_t)b->n_blocks)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_dtile, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kFoldE)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_cand_list, (size_t)b->n_blocks + 1)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_err, kErrWords)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_info, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
@@ -939,11 +945,12 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     }
     int32_t* n_cand = b->d_cand_list + b->n_blocks;
     hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(256), 0, s, (const uint32_t*)b->d_hq, (const double*)ctx->d_pow10,
-                       b->n_blocks, b->d_cand, b->d_cand_list, n_cand);
+                       b->n_blocks, b->d_cand, b->d_cand_list, n_cand, b->d_dblk, b->d_elo);
     HIP_TRY(hipGetLastError());
     const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
     hipLaunchKernelGGL(bqsr_tile_hist, dim3(ctx->n_cu * 4), dim3(256), 0, s, b->rd, (const ReadInfo*)b->d_info,
-                       (const int32_t*)b->d_cand_list, (const int32_t*)n_cand, b->n_blocks, max_tpb, b->d_h2);
+                       (const int32_t*)b->d_cand_list, (const int32_t*)n_cand, b->n_blocks, max_tpb, b->d_h2,
+                       (const int16_t*)b->d_elo, (const double*)ctx->d_pow10, b->d_dtile);
     HIP_TRY(hipGetLastError());
     FoldParams F{};
     F.rd = b->rd;
@@ -951,6 +958,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     F.hq_block = b->d_hq;
     F.h2 = b->d_h2;
     F.cand = b->d_cand;
+    F.dblk = b->d_dblk;
+    F.dtile = b->d_dtile;
+    F.elo = b->d_elo;
     F.pow10 = ctx->d_pow10;
     F.n_blocks = b->n_blocks;
     F.em_out = b->d_em;

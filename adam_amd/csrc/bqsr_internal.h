@@ -187,12 +187,22 @@ struct ObserveParams {
   int32_t lane_shift;  // lane-per-chunk kernels: log2(lanes per read)
 };
 
+constexpr int kFoldE = 4;
+constexpr double kFoldTie = -1.0, kFoldUnknown = -2.0;
 struct FoldParams {
   ReadsDev rd;
   const ReadInfo* info;
   const uint32_t* hq_block;
   const uint16_t* h2;     // [n_tiles][128] per-tile histograms (candidate blocks only)
   const uint8_t* cand;    // [n_blocks] bqsr_fold_plan's candidate blocks
+  // increments of a unit (block / candidate block's tile) at binades
+  // e_lo .. e_lo + kFoldE - 1, e_lo = elo[block] (bqsr_fold_plan,
+  // bqsr_tile_hist): the fold's unit scans read one double instead of a
+  // 128-bin histogram row.  kFoldTie: the unit holds a tie at that binade;
+  // kFoldUnknown: not tabulated (scan the row).
+  const double* dblk;     // [n_blocks][kFoldE]
+  const double* dtile;    // [n_tiles][kFoldE] (candidate blocks' tiles)
+  const int16_t* elo;     // [n_blocks]
   const double* pow10;  // phredToErrorProbabilityCache[0..127]
   int32_t n_blocks;
   double* em_out;      // [1]

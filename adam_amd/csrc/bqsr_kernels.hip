@@ -1068,7 +1068,7 @@ extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(Reads
 // does.  One workgroup of 1024 threads.
 
 constexpr int kFoldThreads = 1024;
-constexpr double kFoldSeqLimit = 2.0;
+constexpr double kFoldSeqLimit = 0.0625;
 constexpr int kFoldWaves = kFoldThreads / 64;
 
 struct FoldShared {
@@ -1077,6 +1077,7 @@ struct FoldShared {
   uint8_t tie[kQBins];  // t / u is exactly a half-integer at the current binade
   double wsum[kFoldWaves];
   uint8_t stream[kTileSlots];
+  double tv[kTileSlots];  // t[stream[k]]: the sequential fold's operands, one LDS read each
   int32_t lens[kMaxTileReads + 1];
   uint64_t rbase[kMaxTileReads];
   double S;
@@ -1084,6 +1085,9 @@ struct FoldShared {
   int32_t found;
   int32_t ntot;
   double cut_sum;
+#ifdef BQSR_FOLD_PROFILE
+  long long p_stream, p_seq, p_bin, n_bin, n_seq;
+#endif
 };
 
 // (re)derive the binade state of S and the increment table
@@ -1156,7 +1160,9 @@ __device__ int fold_stream(const ReadsDev& rd, const ReadInfo* info, int64_t til
       const int mid = (lo + hi) >> 1;
       if (F.lens[mid] <= k) lo = mid; else hi = mid;
     }
-    F.stream[k] = rd.qual[F.rbase[lo] + (uint64_t)(k - F.lens[lo])];
+    const uint8_t q = rd.qual[F.rbase[lo] + (uint64_t)(k - F.lens[lo])];
+    F.stream[k] = q;
+    F.tv[k] = F.t[q];
   }
   __syncthreads();
   return ntot;
@@ -1165,26 +1171,47 @@ __device__ int fold_stream(const ReadsDev& rd, const ReadInfo* info, int64_t til
 // Fold one tile's stream exactly, starting from F.S.
 __device__ void fold_tile_exact(const ReadsDev& rd, const ReadInfo* info, int64_t tile, FoldShared& F, int tid,
                                 double seq_limit) {
+#ifdef BQSR_FOLD_PROFILE
+  long long c0 = clock64();
+#endif
   const int n = fold_stream(rd, info, tile, F, tid);
+#ifdef BQSR_FOLD_PROFILE
+  if (tid == 0) F.p_stream += clock64() - c0;
+#endif
   int pos = 0;
   while (pos < n) {
+#ifdef BQSR_FOLD_PROFILE
+    c0 = clock64();
+    const bool was_seq = F.S < seq_limit;
+#endif
     if (F.S < seq_limit) {
       // small S: the binade changes every few additions -- plain sequential fold
       if (tid == 0) {
-        // eight increments are looked up ahead of their additions; the
-        // additions stay in stream order (a sequential fold is exact at any S,
-        // seq_limit only decides when the binade mode takes over)
+        // batches of eight operands, the next batch's LDS reads in flight
+        // while the current one is added; the additions stay in stream order
+        // (a sequential fold is exact at any S, seq_limit only decides when
+        // the binade mode takes over)
         double S = F.S;
         int p = pos;
-        while (p < n && S < seq_limit) {
-          const int m = min(8, n - p);
-          double tv[8];
+        double a[8], b[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) tv[i] = i < m ? F.t[F.stream[p + i]] : 0.0;
+        for (int i = 0; i < 8; ++i) a[i] = p + i < n ? F.tv[p + i] : 0.0;
+        while (p < n && S < seq_limit) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) b[i] = p + 8 + i < n ? F.tv[p + 8 + i] : 0.0;
+          const int m = min(8, n - p);
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            if (i < m) S = S + tv[i];
+            if (i < m) S = S + a[i];
           p += m;
+          if (p >= n || S >= seq_limit) break;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = p + 8 + i < n ? F.tv[p + 8 + i] : 0.0;
+          const int m2 = min(8, n - p);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (i < m2) S = S + b[i];
+          p += m2;
         }
         F.S = S;
         F.ntot = p;
@@ -1192,6 +1219,12 @@ __device__ void fold_tile_exact(const ReadsDev& rd, const ReadInfo* info, int64_
       __syncthreads();
       pos = F.ntot;
       if (F.S >= seq_limit) fold_set_binade(F, tid, F.S);
+#ifdef BQSR_FOLD_PROFILE
+      if (tid == 0) {
+        F.p_seq += clock64() - c0;
+        F.n_seq++;
+      }
+#endif
       continue;
     }
     // binade mode: per-thread contiguous runs of the remaining stream
@@ -1249,6 +1282,12 @@ __device__ void fold_tile_exact(const ReadsDev& rd, const ReadInfo* info, int64_
     __syncthreads();
     pos = found + 1;
     fold_set_binade(F, tid, F.S);
+#ifdef BQSR_FOLD_PROFILE
+    if (tid == 0) {
+      F.p_bin += clock64() - c0;
+      F.n_bin++;
+    }
+#endif
   }
 }
 
@@ -1287,14 +1326,24 @@ __device__ __forceinline__ void unit_delta(const T* row, const FoldShared& F, do
 // Advance over `count` consecutive units (blocks or tiles) while none leaves
 // the binade; returns the index (relative to first) of the first unit that
 // would, or count.
+// dtab[unit][k]: the unit's increment at binade elo + k (FoldParams::dblk);
+// elo is read at elo_p[unit * elo_stride].
 template <class T>
-__device__ int64_t fold_units(FoldShared& F, int tid, const T* rows, int64_t first, int64_t count) {
+__device__ int64_t fold_units(FoldShared& F, int tid, const T* rows, int64_t first, int64_t count, const double* dtab,
+                              const int16_t* elo_p, int elo_stride) {
   int64_t u = 0;
   while (u < count) {
     const bool have = (u + tid) < count;
     double d = 0.0;
     bool tie = false;
-    if (have) unit_delta(rows + (first + u + tid) * kQBins, F, &d, &tie);
+    if (have) {
+      const int64_t unit = first + u + tid;
+      const int k = F.e - (int)elo_p[(u + tid) * elo_stride];
+      const double v = (k >= 0 && k < kFoldE) ? dtab[unit * kFoldE + k] : kFoldUnknown;
+      if (v >= 0.0) d = v;
+      else if (v == kFoldTie) tie = true;
+      else unit_delta(rows + unit * kQBins, F, &d, &tie);
+    }
     const double N0 = ldexp(F.S, 52 - F.e);
     const double head = 9007199254740992.0 - N0;
     if (d >= head) d = head;  // saturate: it crosses anyway
@@ -1324,16 +1373,33 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
   if (tid == 0) {
     F.S = 0.0;
     F.e = 0;
+#ifdef BQSR_FOLD_PROFILE
+    F.p_stream = F.p_seq = F.p_bin = F.n_bin = F.n_seq = 0;
+#endif
   }
   __syncthreads();
-  // Binade mode starts at S >= 2: every q >= 1 has t < 1 <= S/2 there.  Ties
-  // are still detected and added one by one; this is only where the fast
-  // path takes over from the plain sequential fold.
+  // Binade mode starts at S >= 1/16 (it is exact for any S > 0 as long as the
+  // sum stays in the binade; below, crossings come every few additions and
+  // the plain sequential fold is cheaper).  Ties are detected and added one
+  // by one.
   const double seq_limit = kFoldSeqLimit;
   const int64_t nt = P.rd.n_tiles;
+#ifdef BQSR_FOLD_PROFILE
+  long long tb = 0, tt = 0, te = 0, ne = 0, nbk = 0, ntu = 0, c;
+#define FP_T0 c = clock64();
+#define FP_T1(acc) acc += clock64() - c;
+#else
+#define FP_T0
+#define FP_T1(acc)
+#endif
   for (int64_t b = 0; b < P.n_blocks; ++b) {
     if (F.S >= seq_limit) {
-      b += fold_units(F, tid, P.hq_block, b, P.n_blocks - b);  // whole blocks at once
+      FP_T0
+      b += fold_units(F, tid, P.hq_block, b, P.n_blocks - b, P.dblk, P.elo + b, 1);  // whole blocks at once
+      FP_T1(tb)
+#ifdef BQSR_FOLD_PROFILE
+      ++nbk;
+#endif
       if (b >= P.n_blocks) break;
     }
     // block b leaves the binade somewhere (or S is still small): tile level
@@ -1347,15 +1413,31 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
     int64_t t = c0;
     while (t < c1) {
       if (F.S >= seq_limit) {
-        t += fold_units(F, tid, P.h2, t, c1 - t);
+        FP_T0
+        t += fold_units(F, tid, P.h2, t, c1 - t, P.dtile, P.elo + b, 0);
+        FP_T1(tt)
+#ifdef BQSR_FOLD_PROFILE
+        ++ntu;
+#endif
         if (t >= c1) break;
       }
+      FP_T0
       fold_tile_exact(P.rd, P.info, t, F, tid, seq_limit);
+      FP_T1(te)
+#ifdef BQSR_FOLD_PROFILE
+      ++ne;
+#endif
       ++t;
     }
   }
   __syncthreads();
   if (tid == 0) P.em_out[0] = F.S;
+#ifdef BQSR_FOLD_PROFILE
+  if (tid == 0)
+    printf("FOLDPROF blocks_calls %lld cyc %lld tiles_calls %lld cyc %lld exact_tiles %lld cyc %lld | stream %lld seq %lld "
+           "(%lld) bin %lld (%lld)\n",
+           nbk, tb, ntu, tt, ne, te, F.p_stream, F.p_seq, F.n_seq, F.p_bin, F.n_bin);
+#endif
 }
 
 // Which blocks may hold a fold event (a binade crossing, a rounding tie, or
@@ -1365,9 +1447,52 @@ extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(Fold
 // real-sum span [R_b, R_b+1], widened by delta = (N + 64) * 2^-52, lies inside
 // one binade at or above kFoldSeqLimit and has no tie there holds no event.
 // Only candidate blocks get per-tile histograms (bqsr_tile_hist).
+// A unit's increment at binade e from its histogram: the sum of h[q] *
+// round(t[q] / 2^(e-52)), kFoldTie when a present qual ties there,
+// kFoldUnknown when the sum may be inexact (>= 2^52: such a unit crosses).
+template <class H>
+__device__ double unit_inc(const H* h, const double* t, int e) {
+  // 2^(52 - e) built from its exponent bits (ldexp is a library call here);
+  // outside the normal range the unit is left to the row scan
+  const int be = 1023 + 52 - e;
+  if (be < 1 || be > 2046) return kFoldUnknown;
+  const double scale = __longlong_as_double((long long)be << 52);
+  double acc = 0.0;
+  bool tie = false;
+  for (int q = 0; q < kQBins; ++q) {
+    const double c = (double)h[q];
+    const double x = t[q] * scale;  // exact: a power-of-two scaling of a normal double
+    const double r = rint(x);
+    tie |= c != 0.0 && x - floor(x) == 0.5;
+    acc += c * r;
+  }
+  if (tie) return kFoldTie;
+  return acc < 0x1p51 ? acc : kFoldUnknown;  // below 2^51 every partial sum was exact
+}
+// the same, one wavefront over one histogram (two bins per lane)
+template <class H>
+__device__ double unit_inc_wave(const H* h, const double* t, int e, int lane) {
+  const int be = 1023 + 52 - e;
+  if (be < 1 || be > 2046) return kFoldUnknown;
+  const double scale = __longlong_as_double((long long)be << 52);
+  double acc = 0.0;
+  bool tie = false;
+  for (int q = lane; q < kQBins; q += 64) {
+    const double c = (double)h[q];
+    const double x = t[q] * scale;
+    tie |= c != 0.0 && x - floor(x) == 0.5;
+    acc += c * rint(x);
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (__builtin_amdgcn_ballot_w64(tie)) return kFoldTie;
+  return acc < 0x1p51 ? acc : kFoldUnknown;
+}
+// the lowest binade of a unit that starts at real partial sum lo (see bqsr_fold_plan)
+__device__ __forceinline__ int unit_elo(double lo) { return lo >= 0x1p-60 ? ilogb(lo) : -60; }
+
 extern "C" __global__ void __launch_bounds__(256) bqsr_fold_plan(const uint32_t* hq_block, const double* pow10,
                                                                    int32_t n_blocks, uint8_t* cand, int32_t* cand_list,
-                                                                   int32_t* n_cand) {
+                                                                   int32_t* n_cand, double* dblk, int16_t* elo) {
   __shared__ double t[kQBins];
   __shared__ double bsum[kMaxFoldBlocks + 1];
   __shared__ uint64_t bcnt[kMaxFoldBlocks];
@@ -1416,6 +1541,10 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_fold_plan(const uint32_t*
     }
     cand[b] = c;
     if (c) cand_list[atomicAdd(&nc, 1)] = b;
+    const int e0 = unit_elo(bsum[b] * (1.0 - delta));
+    elo[b] = (int16_t)e0;
+    for (int k = 0; k < kFoldE; ++k)
+      dblk[(int64_t)b * kFoldE + k] = bcnt[b] ? unit_inc(hq_block + (int64_t)b * kQBins, t, e0 + k) : 0.0;
   }
   __syncthreads();
   if (tid == 0) *n_cand = nc;
@@ -1430,7 +1559,13 @@ constexpr int kThStride = kQBins + 1;
 // slot bitmap, then every slot's qual is counted if its bit is set).
 extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, const ReadInfo* info,
                                                                    const int32_t* cand_list, const int32_t* n_cand,
-                                                                   int32_t n_blocks, int64_t max_tpb, uint16_t* h2) {
+                                                                   int32_t n_blocks, int64_t max_tpb, uint16_t* h2,
+                                                                   const int16_t* elo, const double* pow10,
+                                                                   double* dtile) {
+  __shared__ double tq[kQBins];
+  __shared__ uint32_t hsum[4][kQBins];
+  for (int q = threadIdx.x; q < kQBins; q += blockDim.x) tq[q] = pow10[q];
+  __syncthreads();
   __shared__ uint32_t hist[4][kThCopies * kThStride];  // copies by lane & 7, rows one word apart in banks
   __shared__ uint32_t bm[4][kTileSlots / 32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1483,6 +1618,12 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, co
       uint32_t v = 0;
       for (int c = 0; c < kThCopies; ++c) v += hist[wv][c * kThStride + q];
       h2[t * kQBins + q] = (uint16_t)v;
+      hsum[wv][q] = v;
+    }
+    wave_sync();
+    for (int k = 0; k < kFoldE; ++k) {
+      const double v = unit_inc_wave(hsum[wv], tq, (int)elo[b] + k, lane);
+      if (lane == 0) dtile[t * kFoldE + k] = v;
     }
     wave_sync();
   }
