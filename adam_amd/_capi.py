@@ -28,6 +28,8 @@ EXPORTS = [
     "bqsr_table_create", "bqsr_table_destroy", "bqsr_table_dims", "bqsr_table_device_ptr", "bqsr_table_download",
     "bqsr_table_upload", "bqsr_observe", "bqsr_observe_records", "bqsr_table_merge", "bqsr_finalize",
     "bqsr_lut_destroy", "bqsr_lut_stats", "bqsr_lut_shifts", "bqsr_apply", "bqsr_apply_records",
+    "bqsr_stage_records", "bqsr_staged_destroy", "bqsr_staged_bytes", "bqsr_staged_reads", "bqsr_staged_bases",
+    "bqsr_batch_create_staged", "bqsr_batch_upload_async",
 ]
 
 
@@ -75,6 +77,15 @@ def lib():
             return _lib
         if not os.path.exists(LIB_PATH):
             raise NativeLibraryMissing("%s is not built; run __graft_entry__.build()" % LIB_PATH)
+        # one HIP runtime per process: let torch load and initialise its
+        # libamdhip64 first, so the library binds to the same one (loading ours
+        # first left whichever initialised second without a device on the box)
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
         pp = ctypes.POINTER(ctypes.c_void_p)
@@ -94,6 +105,13 @@ def lib():
             "bqsr_batch_slots": (i64, [vp]),
             "bqsr_batch_dims": (Dims, [vp]),
             "bqsr_batch_wrap_device": (ctypes.c_int, [vp, ctypes.POINTER(DeviceReads), pp]),
+            "bqsr_stage_records": (ctypes.c_int, [vp, vp, pp]),
+            "bqsr_staged_destroy": (None, [vp]),
+            "bqsr_staged_bytes": (i64, [vp]),
+            "bqsr_staged_reads": (i64, [vp]),
+            "bqsr_staged_bases": (i64, [vp]),
+            "bqsr_batch_create_staged": (ctypes.c_int, [vp, vp, pp]),
+            "bqsr_batch_upload_async": (ctypes.c_int, [vp, vp, vp]),
             "bqsr_batch_set_window": (ctypes.c_int, [vp, i32, i32]),
             "bqsr_batch_reads_per_tile": (i32, [vp]),
             "bqsr_table_words": (i64, [Dims]),

@@ -251,6 +251,7 @@ struct bqsr_batch {
   bool have_qhist = false;      // q_lo follows qhist at each launch's window width
   int64_t qhist[kQBins] = {0};
   std::vector<void*> allocs;
+  std::vector<size_t> staged_cnt;  // column element counts (bqsr_batch_create_staged)
   // per-read prep results (valid once `prepped`)
   ReadInfo* d_info = nullptr;
   uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
@@ -683,6 +684,118 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
     return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
   }
   *out = b;
+  return ok();
+}
+
+// ---- host-staged partitions: pinned device-layout columns, async upload ----
+// The streaming form of bqsr_batch_create (cfg5: partitions streamed from
+// the host).  bqsr_stage_records packs a partition once into one pinned
+// block; bqsr_batch_create_staged allocates matching device columns;
+// bqsr_batch_upload_async enqueues the six H2D copies on a copy stream, so
+// the next partition's transfer overlaps the current one's kernels.
+struct bqsr_staged {
+  unsigned char* host = nullptr;  // pinned: meta | align | qual | bases | md | cigar
+  size_t bytes = 0;
+  size_t off[6] = {0, 0, 0, 0, 0, 0}, cnt[6] = {0, 0, 0, 0, 0, 0};  // byte offset, element count per column
+  int64_t n_reads = 0, n_slots = 0, n_bases = 0, max_slot = 0;
+  bqsr_dims dims{1, 1};
+  int32_t rg_lo = 0, q_lo = 0;
+  int64_t qhist[kQBins] = {0};
+  ~bqsr_staged() {
+    if (host) (void)hipHostFree(host);
+  }
+};
+
+bqsr_status bqsr_stage_records(bqsr_context* ctx, const bqsr_records* R, bqsr_staged** out) {
+  if (!ctx || !R || !out || R->n_reads < 0) return fail(BQSR_ERR_INVALID_ARG, "bqsr_stage_records: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  Packed P;
+  bqsr_status st = pack(R, P);
+  if (st != BQSR_OK) return st;
+  if (P.max_slot > kMaxReadLen)
+    return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
+  std::unique_ptr<bqsr_staged> s(new bqsr_staged);
+  const size_t esz[6] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t)};
+  const size_t cnt[6] = {P.meta.size(), P.align.size(), P.qual.size(), P.bases.size(), P.md.size(), P.cigar.size()};
+  const void* src[6] = {P.meta.data(), P.align.data(), P.qual.data(), P.bases.data(), P.md.data(), P.cigar.data()};
+  size_t tot = 0;
+  for (int i = 0; i < 6; ++i) {
+    s->off[i] = tot;
+    s->cnt[i] = cnt[i];
+    tot = (tot + cnt[i] * esz[i] + 255) & ~(size_t)255;
+  }
+  HIP_TRY(hipHostMalloc((void**)&s->host, std::max<size_t>(tot, 1), hipHostMallocDefault));
+  s->bytes = tot;
+  for (int i = 0; i < 6; ++i)
+    if (cnt[i]) memcpy(s->host + s->off[i], src[i], cnt[i] * esz[i]);
+  s->n_reads = R->n_reads;
+  s->n_slots = P.n_slots;
+  s->n_bases = P.n_bases;
+  s->max_slot = P.max_slot;
+  s->dims = bqsr_dims{P.n_rg, P.max_len};
+  for (int32_t i = 0; i < (int32_t)P.rghist.size(); ++i)
+    if (P.rghist[(size_t)i] > P.rghist[(size_t)s->rg_lo]) s->rg_lo = i;  // as bqsr_batch_create
+  s->q_lo = best_q_lo(P.qhist, 40);
+  for (int q = 0; q < kQBins; ++q) s->qhist[q] = P.qhist[q];
+  *out = s.release();
+  return ok();
+}
+
+void bqsr_staged_destroy(bqsr_staged* s) { delete s; }
+int64_t bqsr_staged_bytes(const bqsr_staged* s) { return s ? (int64_t)s->bytes : 0; }
+int64_t bqsr_staged_reads(const bqsr_staged* s) { return s ? s->n_reads : 0; }
+int64_t bqsr_staged_bases(const bqsr_staged* s) { return s ? s->n_bases : 0; }
+
+bqsr_status bqsr_batch_create_staged(bqsr_context* ctx, const bqsr_staged* S_, bqsr_batch** out) {
+  if (!ctx || !S_ || !out) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_create_staged: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  std::unique_ptr<bqsr_batch> b(new bqsr_batch);
+  b->ctx = ctx;
+  b->owned = true;
+  b->rd.n_reads = S_->n_reads;
+  b->rd.n_slots = S_->n_slots;
+  b->n_slots = S_->n_slots;
+  b->n_bases = S_->n_bases;
+  b->dims = S_->dims;
+  b->rg_lo = S_->rg_lo;
+  b->q_lo = S_->q_lo;
+  b->have_qhist = true;
+  for (int q = 0; q < kQBins; ++q) b->qhist[q] = S_->qhist[q];
+  ReadMeta* meta;
+  ReadAlign* align;
+  uint8_t *qual, *bases, *md;
+  uint32_t* cigar;
+  bqsr_status st;
+  if ((st = dalloc(b->allocs, &meta, S_->cnt[0])) != BQSR_OK || (st = dalloc(b->allocs, &align, S_->cnt[1])) != BQSR_OK ||
+      (st = dalloc(b->allocs, &qual, S_->cnt[2])) != BQSR_OK || (st = dalloc(b->allocs, &bases, S_->cnt[3])) != BQSR_OK ||
+      (st = dalloc(b->allocs, &md, S_->cnt[4])) != BQSR_OK || (st = dalloc(b->allocs, &cigar, S_->cnt[5])) != BQSR_OK)
+    return st;
+  b->rd.meta = meta;
+  b->rd.align = align;
+  b->rd.qual = qual;
+  b->rd.bases = bases;
+  b->rd.md = md;
+  b->rd.cigar = cigar;
+  b->rd.slots_aligned = align_slots();
+  if ((st = finish_batch(b.get(), S_->max_slot)) != BQSR_OK) return st;
+  b->staged_cnt.assign(S_->cnt, S_->cnt + 6);
+  *out = b.release();
+  return ok();
+}
+
+bqsr_status bqsr_batch_upload_async(bqsr_batch* b, const bqsr_staged* S_, void* stream) {
+  if (!b || !S_) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: bad arguments");
+  if (b->staged_cnt.size() != 6 || !std::equal(b->staged_cnt.begin(), b->staged_cnt.end(), S_->cnt) ||
+      b->rd.n_reads != S_->n_reads)
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: batch was not created from a partition of this shape");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  void* dst[6] = {(void*)b->rd.meta, (void*)b->rd.align, (void*)b->rd.qual,
+                  (void*)b->rd.bases, (void*)b->rd.md, (void*)b->rd.cigar};
+  const size_t esz[6] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t)};
+  hipStream_t s = S(stream);
+  for (int i = 0; i < 6; ++i)
+    if (S_->cnt[i]) HIP_TRY(hipMemcpyAsync(dst[i], S_->host + S_->off[i], S_->cnt[i] * esz[i], hipMemcpyHostToDevice, s));
+  b->prepped = false;  // new contents: the next observe / apply re-runs prep
   return ok();
 }
 

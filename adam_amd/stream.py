@@ -1,0 +1,189 @@
+"""Streamed BQSR over host-resident partitions (BASELINE cfg5).
+
+A shard of reads lives on the host as partitions already flattened into the
+device layout in pinned memory (``bqsr_stage_records`` -- what the JNI side
+hands over per Spark partition).  One job (``StreamedShard.run``):
+
+1. observe, partition by partition: the partition's H2D copy on the copy
+   stream, then prep + observe + the exact expectedMismatch fold on the
+   compute stream, which waits on the copy's event -- so partition i+1 moves
+   over PCIe while partition i is on the CUs.  Every partition counts into the
+   one device table (``RecalTable.++`` is an integer sum); its
+   expectedMismatch stays on the device.
+2. ``((0.0 + e_0) + e_1) + ...`` in partition order on the device (Spark's
+   per-partition ``aggregate`` merged in partition order), then
+   on several ranks the int64 all-reduce of the table and the rank-order fold
+   (adam_amd/distributed.py).
+3. finalize on the device, then apply partition by partition from the
+   partitions still resident in HBM, each partition's recalibrated qualities
+   (and per-read start / length) copied back to pinned host memory on the copy
+   stream while the next partition is applied (double-buffered device output).
+
+Reference: RecalibrateBaseQualities.scala:34-76 (computeTable / applyTable over
+an RDD's partitions).  Only the HIP library computes; this module orders
+copies and launches.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+from . import _capi
+from . import distributed as D
+from ._capi import check
+
+
+class StreamedShard:
+    """Partitions of one rank's shard: pinned host copies + device batches."""
+
+    def __init__(self, ctx, parts: Sequence, dims, sites_handle=None, device: int = 0, max_exc: int = 1 << 16,
+                 site_contigs: Optional[Sequence[str]] = None):
+        import torch
+        self.torch = torch
+        self.L = L = _capi.lib()
+        self.ctx = ctx
+        self.dims = dims
+        self.sites = sites_handle
+        self.dev = torch.device("cuda", device)
+        self.staged: List[ctypes.c_void_p] = []
+        self.batches: List[ctypes.c_void_p] = []
+        self.n_reads: List[int] = []
+        self.n_slots: List[int] = []
+        self.n_bases = 0
+        self.staged_bytes = 0
+        self.site_contigs = site_contigs
+        for p in parts:
+            self.add_partition(p)
+        if parts:
+            self.alloc_outputs(max_exc)
+
+    def add_partition(self, part):
+        """Flatten one partition into pinned host memory (device layout) and
+        allocate its device batch; ``part`` may be dropped afterwards."""
+        L = self.L
+        s, keep = part.c_struct(part.contig_ids_for(self.site_contigs))
+        sh = ctypes.c_void_p()
+        check(L.bqsr_stage_records(self.ctx.handle, ctypes.byref(s), ctypes.byref(sh)))
+        del keep
+        bh = ctypes.c_void_p()
+        st = L.bqsr_batch_create_staged(self.ctx.handle, sh, ctypes.byref(bh))
+        if st != _capi.BQSR_OK:
+            L.bqsr_staged_destroy(sh)
+            check(st)
+        self.staged.append(sh)
+        self.batches.append(bh)
+        self.n_reads.append(int(L.bqsr_batch_reads(bh)))
+        self.n_slots.append(int(L.bqsr_batch_slots(bh)))
+        self.n_bases += int(L.bqsr_batch_bases(bh))
+        self.staged_bytes += int(L.bqsr_staged_bytes(sh))
+
+    def alloc_outputs(self, max_exc: int = 1 << 16):
+        torch = self.torch
+        dev = self.dev
+        ms = max(self.n_slots or [1]) + 64
+        mr = max(self.n_reads or [1])
+        self.out_qual = [torch.empty(ms, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.out_start = [torch.empty(max(1, mr), dtype=torch.int32, device=dev) for _ in range(2)]
+        self.out_len = [torch.empty(max(1, mr), dtype=torch.int32, device=dev) for _ in range(2)]
+        # host results, pinned: qualities by packed slot, per-read start / length
+        self.host_qual = [torch.empty(n + 64, dtype=torch.uint8, pin_memory=True) for n in self.n_slots]
+        self.host_start = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
+        self.host_len = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
+        self.exc = torch.empty(max_exc, dtype=torch.int64, device=dev)
+        self.max_exc = max_exc
+        self.em = torch.zeros(max(1, len(self.batches)), dtype=torch.float64, device=dev)
+        self.copy_stream = torch.cuda.Stream(dev)
+        n = len(self.batches)
+        self.ev_up = [torch.cuda.Event() for _ in range(n)]
+        self.ev_ap = [torch.cuda.Event() for _ in range(n)]
+        self.ev_dl = [torch.cuda.Event() for _ in range(2)]
+        self.ev_apply_t = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                           for _ in range(n)]
+        self.lut = ctypes.c_void_p()
+
+    def run(self, table_handle, table_words=None, record_apply: bool = False):
+        """One whole job over the shard; returns the job's expectedMismatch
+        tensor (device).  Results land in host_qual / host_start / host_len
+        once the compute and copy streams are synchronised (``finish``)."""
+        torch, L = self.torch, self.L
+        comp = torch.cuda.current_stream(self.dev)
+        copy = self.copy_stream
+        sp = ctypes.c_void_p(comp.cuda_stream)
+        cp = ctypes.c_void_p(copy.cuda_stream)
+        ctx = self.ctx.handle
+        check(L.bqsr_table_zero_async(table_handle, sp))
+        # (1) stream the partitions in, observing each as it lands
+        for i, bh in enumerate(self.batches):
+            check(L.bqsr_batch_upload_async(bh, self.staged[i], cp))
+            self.ev_up[i].record(copy)
+            comp.wait_event(self.ev_up[i])
+            check(L.bqsr_observe_async(ctx, bh, self.sites, table_handle, sp))
+            check(L.bqsr_batch_em_copy_async(bh, ctypes.c_void_p(self.em.data_ptr() + 8 * i), sp))
+        # (2) partition-order fold of expectedMismatch: ((0.0 + e_0) + e_1) + ...
+        acc = self.em[0:1].clone()
+        for i in range(1, len(self.batches)):
+            acc = acc + self.em[i:i + 1]
+        if table_words is not None:
+            D.allreduce_table(table_words)
+        acc = D.fold_expected_mismatch_device(acc)
+        self._em_keep = acc
+        check(L.bqsr_finalize_device(ctx, table_handle, ctypes.c_void_p(acc.data_ptr()), ctypes.byref(self.lut), sp))
+        # (3) apply from the resident partitions, results streamed back
+        for i, bh in enumerate(self.batches):
+            k = i & 1
+            if i >= 2:
+                comp.wait_event(self.ev_dl[k])  # output buffer k drained to the host
+            if record_apply:
+                self.ev_apply_t[i][0].record(comp)
+            check(L.bqsr_apply_stage(ctx, bh, self.lut, ctypes.c_void_p(self.out_qual[k].data_ptr()),
+                                     ctypes.c_void_p(self.out_start[k].data_ptr()),
+                                     ctypes.c_void_p(self.out_len[k].data_ptr()), ctypes.c_void_p(self.exc.data_ptr()),
+                                     self.max_exc, _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
+            if record_apply:
+                self.ev_apply_t[i][1].record(comp)
+            self.ev_ap[i].record(comp)
+            copy.wait_event(self.ev_ap[i])
+            with torch.cuda.stream(copy):
+                ns, nr = self.n_slots[i], max(1, self.n_reads[i])
+                self.host_qual[i][:ns].copy_(self.out_qual[k][:ns], non_blocking=True)
+                self.host_start[i][:nr].copy_(self.out_start[k][:nr], non_blocking=True)
+                self.host_len[i][:nr].copy_(self.out_len[k][:nr], non_blocking=True)
+            self.ev_dl[k].record(copy)
+        return acc
+
+    def finish(self):
+        """Synchronise, then raise the first error in the reference's order
+        (observe errors partition by partition, finalize, apply)."""
+        L = self.L
+        comp = self.torch.cuda.current_stream(self.dev)
+        sp = ctypes.c_void_p(comp.cuda_stream)
+        em = ctypes.c_double()
+        for bh in self.batches:
+            check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
+        check(L.bqsr_finalize_result(self.lut, sp))
+        nexc = ctypes.c_int64()
+        total = 0
+        for bh in self.batches:
+            check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
+            total += int(nexc.value)
+        self.copy_stream.synchronize()
+        return total
+
+    def apply_ms(self) -> Optional[float]:
+        """Mean apply-kernel time per partition of the last recorded job."""
+        try:
+            t = [a.elapsed_time(b) for a, b in self.ev_apply_t]
+        except RuntimeError:
+            return None
+        return sum(t) / max(1, len(t))
+
+    def close(self):
+        L = self.L
+        if self.lut:
+            L.bqsr_lut_destroy(self.lut)
+            self.lut = ctypes.c_void_p()
+        for bh in self.batches:
+            L.bqsr_batch_destroy(bh)
+        for sh in self.staged:
+            L.bqsr_staged_destroy(sh)
+        self.batches, self.staged = [], []

@@ -30,6 +30,8 @@ WORKLOADS = {
     "cfg2": "cfg2: synthetic 10M x 100 bp reads, 1 read group, no known sites (per GPU)",
     "cfg3": "cfg3: synthetic 60M x 101 bp reads on a 64.4 Mbp contig, ~1.3M known sites (sharded)",
     "cfg4": "cfg4: synthetic 20M reads 150/250 bp, 96 read groups (per GPU)",
+    "cfg5": "cfg5: whole-genome 30x slice, 150 bp reads streamed from pinned host memory in 4M-read partitions, "
+            "H2D/D2H overlapped with compute (600M reads / 8 GPUs = 75M reads per GPU)",
 }
 
 
@@ -43,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-reads", type=int, default=10_000_000, help="oracle baseline sample (reads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--part-reads", type=int, default=4_000_000, help="cfg5: reads per streamed partition")
     return ap.parse_args()
 
 
@@ -68,6 +71,8 @@ def main():
     ctx = bqsr.Context.get(local)
 
     cfg = dict(synth.CONFIGS[args.config])
+    if args.config == "cfg5":
+        return main_stream(args, cfg, world, rank, dev, ctx)
     n_reads = args.reads or cfg["n_reads"]
     if args.config == "cfg3":
         n_reads = args.reads or (cfg["n_reads"] // max(1, world))  # cfg3 is one dataset sharded over the GPUs
@@ -225,6 +230,130 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, cfg, batch, sites)
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_stream(args, cfg, world, rank, dev, ctx):
+    """cfg5: the rank's 1/8 of a 600M x 150 bp whole genome (75M reads), held
+    on the host as pinned 4M-read partitions in the device layout; one step =
+    upload + observe every partition (copy stream overlapped with compute),
+    partition-order expectedMismatch fold, [N > 1: all-reduce + rank fold],
+    finalize, apply every partition with its results copied back to pinned
+    host memory.  PCIe-inclusive, end to end."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from adam_amd import _capi, synth
+    from adam_amd._capi import Dims, check
+    from adam_amd.stream import StreamedShard
+
+    L = _capi.lib()
+    n_reads = args.reads or cfg["n_reads"] // 8
+    pr = max(1, args.part_reads)
+    dims = Dims(cfg["n_rg"], max(cfg["lens"]))
+    t_gen = time.time()
+    sh = StreamedShard(ctx, [], dims, None, dev.index)
+    first = None
+    for i, r0 in enumerate(range(0, n_reads, pr)):
+        part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"],
+                              cfg["seed"] + 1_000_003 * rank + 7919 * i)
+        sh.add_partition(part)
+        if first is None:
+            first = part
+        del part
+        if rank == 0 and i % 4 == 0:
+            print("cfg5: staged %d / %d reads" % (min(n_reads, r0 + pr), n_reads), file=sys.stderr, flush=True)
+    sh.alloc_outputs()
+    t_gen = time.time() - t_gen
+    words = int(L.bqsr_table_words(dims))
+    table_t = torch.zeros(words, dtype=torch.int64, device=dev)
+    th = ctypes.c_void_p()
+    check(L.bqsr_table_create(ctx.handle, dims, ctypes.c_void_p(table_t.data_ptr()), ctypes.byref(th)))
+    torch.cuda.synchronize()
+
+    def step(record):
+        sh.run(th, table_t if world > 1 else None, record_apply=record)
+        sh.finish()
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    apply_ms = []
+    for _ in range(args.steps):
+        step(True)
+        apply_ms.append(sh.apply_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    n_bases = sh.n_bases
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        nb = torch.tensor([n_bases], dtype=torch.int64, device=dev)
+        dist.all_reduce(nb)
+        total_bases = int(nb.item())
+    else:
+        total_bases = n_bases
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        parts_n = len(sh.batches)
+        am = float(np.mean([a for a in apply_ms if a is not None])) if apply_ms else None
+        R_part = n_reads / parts_n
+        alg_part = 2.5 * n_bases / parts_n + 16 * R_part
+        achieved = alg_part / (am * 1e-3) / 1e9 if am else None
+        h2d = sh.staged_bytes
+        d2h = sum(sh.n_slots) + 8 * n_reads
+        line = {
+            "metric": METRIC,
+            "value": args.steps * total_bases / elapsed,
+            "unit": "bases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8 in, int64 counts, f64 recalibration",
+            "data": "synthetic (deterministic generator, SURVEY.md 8d spec), streamed from pinned host memory "
+                    "(PCIe-inclusive: H2D of every partition and D2H of every result inside the timed region)",
+            "config": {
+                "workload": WORKLOADS["cfg5"],
+                "reads_per_gpu": n_reads,
+                "bases_per_gpu": n_bases,
+                "read_len": list(cfg["lens"]),
+                "read_groups": cfg["n_rg"],
+                "known_sites": 0,
+                "partitions_per_gpu": parts_n,
+                "parallelism": "dp%d: read shards per GPU, RCCL int64 table all-reduce" % world,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "bqsr_apply_kernel (per %d-read partition)" % int(R_part),
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                "traffic": None,
+                "alg_bytes_per_launch": alg_part,
+                "kernel_ms": {"apply_per_partition": am},
+            },
+            "pcie": {"h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+                     "achieved_GBps": (h2d + d2h) / (ms_step * 1e-3) / 1e9},
+            "gen_s": t_gen,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            args.cpu_reads = min(args.cpu_reads, 2_000_000)
+            line["cpu_baseline"] = cpu_baseline(args, cfg, first, None)
+        print(json.dumps(line), flush=True)
+    sh.close()
     if world > 1:
         dist.destroy_process_group()
 

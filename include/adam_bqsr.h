@@ -173,6 +173,26 @@ typedef struct bqsr_device_reads {
 } bqsr_device_reads;
 bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* dev, bqsr_batch** out);
 
+/* ---- streamed partitions (BASELINE cfg5: partitions streamed from the host
+ *      with the H2D copy of one overlapping the kernels of another) ---------
+ * Replaces, per Spark task, the hand-over of one partition of
+ * `RecalibrateBaseQualities.computeTable`'s input (RecalibrateBaseQualities.scala:52-64)
+ * when the JNI side streams partitions rather than calling bqsr_batch_create
+ * per partition.  bqsr_stage_records packs the partition once into pinned host
+ * memory in the device layout; bqsr_batch_create_staged allocates matching
+ * device columns (no copy); bqsr_batch_upload_async enqueues the H2D copies on
+ * `stream` without a host sync (the caller orders its compute stream after it
+ * with an event).  A batch may be re-uploaded from the same staged partition
+ * any number of times; each upload invalidates the batch's prep results. */
+typedef struct bqsr_staged bqsr_staged;
+bqsr_status bqsr_stage_records(bqsr_context* ctx, const bqsr_records* recs, bqsr_staged** out);
+void bqsr_staged_destroy(bqsr_staged* s);
+int64_t bqsr_staged_bytes(const bqsr_staged* s);
+int64_t bqsr_staged_reads(const bqsr_staged* s);
+int64_t bqsr_staged_bases(const bqsr_staged* s);
+bqsr_status bqsr_batch_create_staged(bqsr_context* ctx, const bqsr_staged* s, bqsr_batch** out);
+bqsr_status bqsr_batch_upload_async(bqsr_batch* b, const bqsr_staged* s, void* stream);
+
 /* ---- table --------------------------------------------------------------- */
 /* int64 words of a dense table: [touched K][obs K*(C+X)][mm K*(C+X)]. */
 int64_t bqsr_table_words(bqsr_dims d);
