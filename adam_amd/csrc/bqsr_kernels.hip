@@ -1924,20 +1924,37 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
             const bool cok = fast_rd && (unsigned)(wc0 + klo * x.dir) < (unsigned)cw &&
                              (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
             const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
-            const int cx0 = wc0 * kCtxSlots, dx = x.dir * kCtxSlots;
+            const int dx = x.dir * kCtxSlots;
+            // entry of offset k: (q - q_lo) * cw21 + wc0 * 21 + dx * k + xs,
+            // clamped into the table; an offset whose row or cycle cell lies
+            // outside the window reads some other entry and is flagged below
+            // (the per-offset work is two byte extracts, a multiply-add, a
+            // clamp, the LDS byte read and the byte insert)
+            const int eb = wc0 * kCtxSlots - q_lo * cw21, emax = qw * cw21 - 1;
             out[0] = out[1] = out[2] = out[3] = 0;
-            uint32_t goodm = 0;
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
-              const int q = (int)((qd[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-              const int row = q - q_lo;
-              const bool ok = cok && (unsigned)row < (unsigned)qw && ((vmask >> k) & 1u);
-              const int xs = (int)((xo[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-              const uint32_t code = lut[ok ? row * cw21 + cx0 + dx * k + xs : 0];
-              goodm |= (uint32_t)(ok && code != 0u) << k;
-              out[k >> 2] |= code << (8 * (k & 3));
+              const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
+              const int xs = (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8);
+              const int e = min(max(__mul24(q, cw21) + (eb + dx * k) + xs, 0), emax);
+              out[k >> 2] |= (uint32_t)lut[e] << (8 * (k & 3));
             }
-            slow = vmask & ~goodm;
+            // per word: bytes whose qual is outside the window rows (SWAR;
+            // q >= 128 never is in them) or whose entry is 0 (the checked path
+            // decides), gathered to one bit per offset
+            const int hi_lim = min(q_lo + qw, kQBins);
+            const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)hi_lim * 0x01010101u;
+            uint32_t badm = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const uint32_t v = qd[w] & 0x7F7F7F7Fu;
+              const uint32_t ge_lo = (v | 0x80808080u) - lo4;  // byte high bit: v >= q_lo
+              const uint32_t ge_hi = hi_lim < kQBins ? (v | 0x80808080u) - hi4 : 0u;
+              const uint32_t z = ~(((out[w] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | out[w] | 0x7F7F7F7Fu);  // zero bytes
+              const uint32_t bad = ((qd[w] | ~ge_lo | ge_hi) & 0x80808080u) | z;
+              badm |= ((((bad >> 7) & 0x01010101u) * 0x00204081u) >> 21 & 0xFu) << (4 * w);
+            }
+            slow = vmask & (cok ? badm : 0xFFFFu);
           }
           // ---- the checked path, in offset order (the first failing offset wins) ----
           if (__builtin_amdgcn_ballot_w64(slow != 0)) {

@@ -127,6 +127,70 @@ __global__ void __launch_bounds__(1024) copy_eight(const uint8_t* p, uint8_t* o,
   }
 }
 
+// I: plain coalesced copy (16 B per lane, a wavefront's 1 KB contiguous)
+__global__ void __launch_bounds__(1024) copy_coalesced(const uint4* p, uint4* o, int64_t n16) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    uint4 w = p[i];
+    w.x += 1;
+    o[i] = w;
+  }
+}
+
+// J: the apply kernel's store pattern: 112-B (16-aligned) records, 2 lanes per
+// record, each lane four 16-B chunks of its 64-B piece
+constexpr int kRec2 = 112;
+__global__ void __launch_bounds__(1024) copy_two(const uint8_t* p, uint8_t* o, int64_t n_rec) {
+  const int sub = threadIdx.x & 1;
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 1; r < n_rec;
+       r += ((int64_t)gridDim.x * blockDim.x) >> 1) {
+    const uint8_t* q = p + r * kRec2 + 64 * sub;
+    uint8_t* d = o + r * kRec2 + 64 * sub;
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (64 * sub + 16 * i < kRec2) ? *(const uint4*)(q + 16 * i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (64 * sub + 16 * i < kRec2) {
+        v[i].x += 1;
+        *(uint4*)(d + 16 * i) = v[i];
+      }
+  }
+}
+
+// K: as J, but the wavefront's 32 records (3584 contiguous bytes) leave
+// through LDS as coalesced 16-B-per-lane stores
+__global__ void __launch_bounds__(1024) copy_two_lds(const uint8_t* p, uint8_t* o, int64_t n_rec) {
+  __shared__ __align__(16) uint8_t st[16][32 * kRec2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sub = lane & 1, rl = lane >> 1;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; w0 * 32 < n_rec; w0 += nw) {
+    const int64_t r = w0 * 32 + rl;
+    const int nrec = (int)(n_rec - w0 * 32 < 32 ? n_rec - w0 * 32 : 32);
+    if (rl < nrec) {
+      const uint8_t* q = p + r * kRec2 + 64 * sub;
+      uint4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (64 * sub + 16 * i < kRec2) ? *(const uint4*)(q + 16 * i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (64 * sub + 16 * i < kRec2) {
+          v[i].x += 1;
+          *(uint4*)&st[wave][rl * kRec2 + 64 * sub + 16 * i] = v[i];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    uint8_t* d = o + w0 * 32 * kRec2;
+    const int nb = nrec * kRec2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int off = 16 * (lane + 64 * k);
+      if (off < nb) *(uint4*)(d + off) = *(const uint4*)&st[wave][off];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 int main() {
   const int64_t n_rec = 10'000'000;
   const int64_t bytes = n_rec * kRec;
@@ -165,6 +229,10 @@ int main() {
   time("F copy lane/record (x2 B)", [&] { hipLaunchKernelGGL(copy_lane, dim3(grid), dim3(1024), 0, 0, d, o, n_rec); });
   time("G copy 8 lanes/rec (x2 B)", [&] { hipLaunchKernelGGL(copy_eight<false>, dim3(grid), dim3(1024), 0, 0, d, o, perm, n_rec); });
   time("H copy 8 lanes/rec perm (x2)", [&] { hipLaunchKernelGGL(copy_eight<true>, dim3(grid), dim3(1024), 0, 0, d, o, perm, n_rec); });
+  const int64_t n_rec2 = bytes / kRec2;
+  time("I copy coalesced (x2 B)", [&] { hipLaunchKernelGGL(copy_coalesced, dim3(grid), dim3(1024), 0, 0, (const uint4*)d, (uint4*)o, bytes / 16); });
+  time("J copy 2 lanes/112B rec (x2)", [&] { hipLaunchKernelGGL(copy_two, dim3(grid), dim3(1024), 0, 0, d, o, n_rec2); });
+  time("K as J, LDS-staged stores (x2)", [&] { hipLaunchKernelGGL(copy_two_lds, dim3(grid), dim3(1024), 0, 0, d, o, n_rec2); });
   CK(hipGetLastError());
   return 0;
 }
