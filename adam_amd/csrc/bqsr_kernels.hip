@@ -1930,15 +1930,25 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
             // outside the window reads some other entry and is flagged below
             // (the per-offset work is two byte extracts, a multiply-add, a
             // clamp, the LDS byte read and the byte insert)
-            const int eb = wc0 * kCtxSlots - q_lo * cw21, emax = qw * cw21 - 1;
-            out[0] = out[1] = out[2] = out[3] = 0;
+            const uint32_t emax = (uint32_t)(qw * cw21 - 1);
+            // all 16 entry indices first (a running cycle offset, no
+            // multiplies by k; a negative index wraps above emax and clamps),
+            // then the 16 LDS reads back to back, then the byte inserts
+            uint32_t ei[kChunk];
+            int ek = wc0 * kCtxSlots - q_lo * cw21;
 #pragma unroll
             for (int k = 0; k < kChunk; ++k) {
               const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
               const int xs = (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8);
-              const int e = min(max(__mul24(q, cw21) + (eb + dx * k) + xs, 0), emax);
-              out[k >> 2] |= (uint32_t)lut[e] << (8 * (k & 3));
+              ei[k] = min((uint32_t)(__mul24(q, cw21) + ek + xs), emax);
+              ek += dx;
             }
+            uint32_t code[kChunk];
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) code[k] = lut[ei[k]];
+            out[0] = out[1] = out[2] = out[3] = 0;
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) out[k >> 2] |= code[k] << (8 * (k & 3));
             // per word: bytes whose qual is outside the window rows (SWAR;
             // q >= 128 never is in them) or whose entry is 0 (the checked path
             // decides), gathered to one bit per offset
