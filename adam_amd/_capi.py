@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libadam_bqsr.so")
+# ADAM_BQSR_LIB: an instrumented build of the same sources (tools/*.sh profiling)
+LIB_PATH = os.environ.get("ADAM_BQSR_LIB") or os.path.join(_HERE, "libadam_bqsr.so")
 
 BQSR_OK = 0
 STAGE_RESET, STAGE_KERNEL, STAGE_FOLD, STAGE_PREP = 1, 2, 4, 8
@@ -29,7 +30,8 @@ EXPORTS = [
     "bqsr_table_upload", "bqsr_observe", "bqsr_observe_records", "bqsr_table_merge", "bqsr_finalize",
     "bqsr_lut_destroy", "bqsr_lut_stats", "bqsr_lut_shifts", "bqsr_apply", "bqsr_apply_records",
     "bqsr_stage_records", "bqsr_staged_destroy", "bqsr_staged_bytes", "bqsr_staged_reads", "bqsr_staged_bases",
-    "bqsr_batch_create_staged", "bqsr_batch_upload_async",
+    "bqsr_batch_create_staged", "bqsr_batch_upload_async", "bqsr_em_fold_async", "bqsr_batch_em_copy_async",
+    "bqsr_finalize_device", "bqsr_observe_stage", "bqsr_apply_stage",
 ]
 
 
@@ -135,6 +137,7 @@ def lib():
             "bqsr_finalize_result": (ctypes.c_int, [vp, vp]),
             "bqsr_finalize_device": (ctypes.c_int, [vp, vp, vp, pp, vp]),
             "bqsr_batch_em_copy_async": (ctypes.c_int, [vp, vp, vp]),
+            "bqsr_em_fold_async": (ctypes.c_int, [vp, vp, i64, vp, vp]),
             "bqsr_lut_destroy": (None, [vp]),
             "bqsr_lut_stats": (ctypes.c_int, [vp, ctypes.POINTER(FinalStats)]),
             "bqsr_lut_group": (ctypes.c_int, [vp, i32, ctypes.POINTER(i64), ctypes.POINTER(i64)]),

@@ -219,7 +219,10 @@ class FinalizedTable:
 
     def get_read_group_delta(self, qual_by_rg: int) -> float:
         """getReadGroupDelta (RecalTable.scala:128-131)."""
-        r = (qual_by_rg - 1) // MAX_REASONABLE_QSCORE if qual_by_rg >= 1 else 0
+        # (qualByRG - 1) / 60 in Java truncates toward zero: key 0 -> group 0,
+        # keys <= -59 -> group -1 or below, which never exist (MISSING_KEY)
+        num = qual_by_rg - 1
+        r = num // MAX_REASONABLE_QSCORE if num >= 0 else -((-num) // MAX_REASONABLE_QSCORE)
         ec = self.read_group_counts(r)
         if ec is None:
             raise BQSRError(_capi.MISSING_KEY, "read group %d" % r)

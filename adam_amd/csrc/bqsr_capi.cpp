@@ -1147,9 +1147,15 @@ bqsr_status finalize_impl(bqsr_context* ctx, const bqsr_table* t, double em, con
   hipStream_t s = S(stream);
   const TableGeom g = geom(t->dims);
   const int n_rg = t->dims.n_rg;
-  // *out may hold a LUT of the same dims from an earlier job: its buffers are reused
+  // *out is NULL or a LUT from an earlier finalize: one of the same dims and
+  // context is reused (no allocation); any other is destroyed and replaced
   bqsr_lut* L = *out;
   const bool reuse = L && L->ctx == ctx && L->dims.n_rg == t->dims.n_rg && L->dims.max_len == t->dims.max_len;
+  if (L && !reuse) {
+    (void)hipStreamSynchronize(s);  // its buffers may still be read by queued work
+    delete L;
+    *out = nullptr;
+  }
   if (!reuse) L = new bqsr_lut;
   L->ctx = ctx;
   L->dims = t->dims;
@@ -1195,6 +1201,14 @@ bqsr_status bqsr_finalize_device(bqsr_context* ctx, const bqsr_table* t, const d
                                  void* stream) {
   if (!em_device) return fail(BQSR_ERR_INVALID_ARG, "null em_device");
   return finalize_impl(ctx, t, 0.0, em_device, out, stream);
+}
+
+bqsr_status bqsr_em_fold_async(bqsr_context* ctx, const double* ems, int64_t n, double* out, void* stream) {
+  if (!ctx || !out || n < 0 || (n > 0 && !ems)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_em_fold_async: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(bqsr_em_fold, dim3(1), dim3(64), 0, S(stream), ems, n, out);
+  HIP_TRY(hipGetLastError());
+  return ok();
 }
 
 bqsr_status bqsr_batch_em_copy_async(bqsr_batch* b, double* dst, void* stream) {

@@ -2029,6 +2029,16 @@ template __global__ void bqsr_observe_kernel<false, true>(ObserveParams);
 template __global__ void bqsr_apply_kernel<false>(ApplyParams);
 template __global__ void bqsr_apply_kernel<true>(ApplyParams);
 
+// RecalTable.++ over partitions in a declared order (RecalTable.scala:90-108):
+// expectedMismatch = ((0.0 + e_0) + e_1) + ... -- one lane, each `+` one IEEE
+// double addition as on the JVM's driver
+extern "C" __global__ void bqsr_em_fold(const double* ems, int64_t n, double* out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s = s + ems[i];
+  *out = s;
+}
+
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

@@ -10,10 +10,11 @@ hands over per Spark partition).  One job (``StreamedShard.run``):
    over PCIe while partition i is on the CUs.  Every partition counts into the
    one device table (``RecalTable.++`` is an integer sum); its
    expectedMismatch stays on the device.
-2. ``((0.0 + e_0) + e_1) + ...`` in partition order on the device (Spark's
-   per-partition ``aggregate`` merged in partition order), then
-   on several ranks the int64 all-reduce of the table and the rank-order fold
-   (adam_amd/distributed.py).
+2. on several ranks the int64 all-reduce of the table; then
+   ``((0.0 + e_0) + e_1) + ...`` over every partition of the job in global
+   partition order (this rank's partitions after those of lower ranks: Spark's
+   per-partition ``aggregate`` merged in partition order), on
+   the device (adam_amd/distributed.py, ``bqsr_em_fold_async``).
 3. finalize on the device, then apply partition by partition from the
    partitions still resident in HBM, each partition's recalibrated qualities
    (and per-read start / length) copied back to pinned host memory on the copy
@@ -89,8 +90,14 @@ class StreamedShard:
         self.host_qual = [torch.empty(n + 64, dtype=torch.uint8, pin_memory=True) for n in self.n_slots]
         self.host_start = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
         self.host_len = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
-        self.exc = torch.empty(max_exc, dtype=torch.int64, device=dev)
+        # exception lists (chars above 0xFF, Q14): one slice of max_exc entries
+        # per partition, copied back with the partition's qualities
+        n = len(self.batches)
+        self.exc = torch.empty(max(1, n) * max_exc, dtype=torch.int64, device=dev)
+        self.host_exc = torch.empty(max(1, n) * max_exc, dtype=torch.int64, pin_memory=True)
+        self.n_exc = [0] * n
         self.max_exc = max_exc
+        self.counts = None  # every rank's partition count (exchanged on the first multi-rank job)
         self.em = torch.zeros(max(1, len(self.batches)), dtype=torch.float64, device=dev)
         self.copy_stream = torch.cuda.Stream(dev)
         n = len(self.batches)
@@ -119,13 +126,15 @@ class StreamedShard:
             comp.wait_event(self.ev_up[i])
             check(L.bqsr_observe_async(ctx, bh, self.sites, table_handle, sp))
             check(L.bqsr_batch_em_copy_async(bh, ctypes.c_void_p(self.em.data_ptr() + 8 * i), sp))
-        # (2) partition-order fold of expectedMismatch: ((0.0 + e_0) + e_1) + ...
-        acc = self.em[0:1].clone()
-        for i in range(1, len(self.batches)):
-            acc = acc + self.em[i:i + 1]
+        # (2) the table all-reduce across ranks, then the expectedMismatch of
+        # every partition of the job folded in global partition order:
+        # ((0.0 + e_0) + e_1) + ...
+        n = len(self.batches)
         if table_words is not None:
             D.allreduce_table(table_words)
-        acc = D.fold_expected_mismatch_device(acc)
+        if self.counts is None:
+            self.counts = D.partition_counts(n, self.dev)
+        acc = D.fold_partition_ems_device(self.em[:n], self.counts, self.ctx, comp)
         self._em_keep = acc
         check(L.bqsr_finalize_device(ctx, table_handle, ctypes.c_void_p(acc.data_ptr()), ctypes.byref(self.lut), sp))
         # (3) apply from the resident partitions, results streamed back
@@ -135,9 +144,10 @@ class StreamedShard:
                 comp.wait_event(self.ev_dl[k])  # output buffer k drained to the host
             if record_apply:
                 self.ev_apply_t[i][0].record(comp)
+            exc_i = ctypes.c_void_p(self.exc.data_ptr() + 8 * i * self.max_exc)
             check(L.bqsr_apply_stage(ctx, bh, self.lut, ctypes.c_void_p(self.out_qual[k].data_ptr()),
                                      ctypes.c_void_p(self.out_start[k].data_ptr()),
-                                     ctypes.c_void_p(self.out_len[k].data_ptr()), ctypes.c_void_p(self.exc.data_ptr()),
+                                     ctypes.c_void_p(self.out_len[k].data_ptr()), exc_i,
                                      self.max_exc, _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
             if record_apply:
                 self.ev_apply_t[i][1].record(comp)
@@ -153,7 +163,9 @@ class StreamedShard:
 
     def finish(self):
         """Synchronise, then raise the first error in the reference's order
-        (observe errors partition by partition, finalize, apply)."""
+        (observe errors partition by partition, finalize, apply).  Returns the
+        number of recalibrated chars above 0xFF (Q14); their codes are in
+        ``exceptions(i)`` and ``qual_chars`` applies them."""
         L = self.L
         comp = self.torch.cuda.current_stream(self.dev)
         sp = ctypes.c_void_p(comp.cuda_stream)
@@ -163,11 +175,34 @@ class StreamedShard:
         check(L.bqsr_finalize_result(self.lut, sp))
         nexc = ctypes.c_int64()
         total = 0
-        for bh in self.batches:
+        for i, bh in enumerate(self.batches):
             check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
-            total += int(nexc.value)
+            self.n_exc[i] = int(nexc.value)
+            if self.n_exc[i] > self.max_exc:
+                raise _capi.BQSRError(_capi.UNSUPPORTED, "partition %d: %d chars above 0xFF exceed the exception "
+                                      "list (%d)" % (i, self.n_exc[i], self.max_exc))
+            total += self.n_exc[i]
         self.copy_stream.synchronize()
+        if total:  # rare: only then are the exception lists copied back
+            self.host_exc.copy_(self.exc.cpu())
         return total
+
+    def exceptions(self, i: int):
+        """Partition i's chars above 0xFF of the last job: (slot, Java char) pairs."""
+        a = self.host_exc[i * self.max_exc: i * self.max_exc + self.n_exc[i]].numpy()
+        return [(int(v) >> 16, int(v) & 0xFFFF) for v in a]
+
+    def qual_chars(self, i: int, slot: int, r: int):
+        """Read r's recalibrated quality string of partition i as Java chars
+        (uint16), given its packed slot: the u8 output with the partition's
+        exceptions applied."""
+        import numpy as np
+        st, ln = int(self.host_start[i][r]), int(self.host_len[i][r])
+        out = self.host_qual[i][slot + st: slot + st + ln].numpy().astype(np.uint16)
+        for s, code in self.exceptions(i):
+            if slot + st <= s < slot + st + ln:
+                out[s - slot - st] = code
+        return out
 
     def apply_ms(self) -> Optional[float]:
         """Mean apply-kernel time per partition of the last recorded job."""

@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the config's)")
     ap.add_argument("--cpu-reads", type=int, default=10_000_000, help="oracle baseline sample (reads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed job's results")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--part-reads", type=int, default=4_000_000, help="cfg5: reads per streamed partition")
     return ap.parse_args()
@@ -83,81 +84,17 @@ def main():
     t_gen = time.time() - t_gen
     n_bases = batch.n_bases
 
-    stream = torch.cuda.current_stream(dev)
-    sp = ctypes.c_void_p(stream.cuda_stream)
-    s, keep = batch.c_struct(batch.contig_ids_for(snp.contigs if snp else None))
-    bh = ctypes.c_void_p()
-    check(L.bqsr_batch_create(ctx.handle, ctypes.byref(s), sp, ctypes.byref(bh)))
-    del keep
-    n_slots = int(L.bqsr_batch_slots(bh))
-    dims = Dims(cfg["n_rg"], max(cfg["lens"]))
-    words = int(L.bqsr_table_words(dims))
-    table_t = torch.zeros(words, dtype=torch.int64, device=dev)
-    th = ctypes.c_void_p()
-    check(L.bqsr_table_create(ctx.handle, dims, ctypes.c_void_p(table_t.data_ptr()), ctypes.byref(th)))
-    sites_h = snp.handle(ctx) if snp else None
-    out_qual = torch.empty(n_slots + 64, dtype=torch.uint8, device=dev)
-    out_start = torch.empty(max(1, batch.n_reads), dtype=torch.int32, device=dev)
-    out_len = torch.empty(max(1, batch.n_reads), dtype=torch.int32, device=dev)
-    max_exc = 1 << 16
-    exc = torch.empty(max_exc, dtype=torch.int64, device=dev)
-    lut = ctypes.c_void_p()
-    torch.cuda.synchronize()
-
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
-    em_t = torch.zeros(1, dtype=torch.float64, device=dev)
-    keep = {}
-    kt = {"prep": [], "observe": [], "fold": [], "apply": []}
-
-    def step(record: bool):
-        check(L.bqsr_table_zero_async(th, sp))
-        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_RESET, sp))
-        ev[5].record(stream)
-        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_PREP, sp))
-        ev[0].record(stream)
-        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_KERNEL, sp))
-        ev[1].record(stream)
-        check(L.bqsr_observe_stage(ctx.handle, bh, sites_h, th, _capi.STAGE_FOLD, sp))
-        ev[2].record(stream)
-        # RecalTable.++ across ranks: exact int64 all-reduce over xGMI (RCCL),
-        # expectedMismatch all-gathered and folded in rank order on the device
-        # (adam_amd/distributed.py); no host round trip until the job's end
-        if world > 1:
-            check(L.bqsr_batch_em_copy_async(bh, ctypes.c_void_p(em_t.data_ptr()), sp))
-            D.allreduce_table(table_t)
-            keep["em"] = D.fold_expected_mismatch_device(em_t)
-            em_ptr = ctypes.c_void_p(keep["em"].data_ptr())
-        else:
-            em_ptr = ctypes.c_void_p(L.bqsr_batch_em_device_ptr(bh))
-        check(L.bqsr_finalize_device(ctx.handle, th, em_ptr, ctypes.byref(lut), sp))
-        check(L.bqsr_apply_stage(ctx.handle, bh, lut, ctypes.c_void_p(out_qual.data_ptr()),
-                                 ctypes.c_void_p(out_start.data_ptr()), ctypes.c_void_p(out_len.data_ptr()),
-                                 ctypes.c_void_p(exc.data_ptr()), max_exc, _capi.STAGE_RESET, sp))
-        ev[3].record(stream)
-        check(L.bqsr_apply_stage(ctx.handle, bh, lut, ctypes.c_void_p(out_qual.data_ptr()),
-                                 ctypes.c_void_p(out_start.data_ptr()), ctypes.c_void_p(out_len.data_ptr()),
-                                 ctypes.c_void_p(exc.data_ptr()), max_exc, _capi.STAGE_KERNEL, sp))
-        ev[4].record(stream)
-        # the job's results and errors, in the order the reference raises them
-        em = ctypes.c_double()
-        check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
-        check(L.bqsr_finalize_result(lut, sp))
-        nexc = ctypes.c_int64()
-        check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
-        if record:
-            kt["prep"].append(ev[5].elapsed_time(ev[0]))
-            kt["observe"].append(ev[0].elapsed_time(ev[1]))
-            kt["fold"].append(ev[1].elapsed_time(ev[2]))
-            kt["apply"].append(ev[3].elapsed_time(ev[4]))
+    from adam_amd.job import ResidentJob
+    job = ResidentJob(batch, Dims(cfg["n_rg"], max(cfg["lens"])), snp, local)
 
     for _ in range(args.warmup):
-        step(False)
+        job.step(False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        job.step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -171,6 +108,7 @@ def main():
         total_bases = int(nb.item())
     else:
         total_bases = n_bases
+    kt = job.kt
 
     if rank == 0:
         ms = {k: float(np.mean(v)) for k, v in kt.items()}
@@ -228,10 +166,39 @@ def main():
             "gen_s": t_gen,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args, cfg, batch, sites)
+            line["cpu_baseline"], ref = cpu_baseline(args, cfg, batch, sites, whole=not args.no_parity)
+            if ref is not None:
+                line["parity"] = parity_check(job, batch, ref)
+        elif world > 1:
+            line["parity"] = {"checked": False, "reason": "N > 1: the table is the all-reduce over every rank's shard; "
+                                                           "multi-rank parity is tests/test_gpu_multirank.py"}
         print(json.dumps(line), flush=True)
+    job.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def parity_check(job, batch, ref):
+    """The timed job's own results (last step) against the oracle run over the
+    same shard as ONE partition: table words and expectedMismatch bit for bit,
+    every read's recalibrated chars (outside the timed region)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    t = time.perf_counter()
+    words, em, q, st, ln, exc = job.results()
+    rw, rem, rout, rlen = ref
+    table_ok = bool(np.array_equal(words, rw))
+    em_ok = em == rem
+    bad, first = O.compare_device_output(batch, rout, rlen, q, st, ln, exc if len(exc) else None,
+                                         nthreads=max(1, len(os.sched_getaffinity(0))))
+    return {"checked": True, "ok": bool(table_ok and em_ok and bad == 0), "table_words_equal": table_ok,
+            "expected_mismatch_equal": bool(em_ok), "expected_mismatch": float(em).hex(),
+            "reads_checked": batch.n_reads, "reads_differing": bad, "first_differing_read": first,
+            "chars_above_0xff": int(len(exc)),
+            "against": "oracle/ (C++ restatement of ADAM BQSR) on the same shard as one partition, "
+                       "table built by partitions in parallel, expectedMismatch folded sequentially",
+            "check_s": time.perf_counter() - t}
 
 
 def main_stream(args, cfg, world, rank, dev, ctx):
@@ -351,39 +318,62 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         }
         if world == 1 and not args.no_cpu_baseline:
             args.cpu_reads = min(args.cpu_reads, 2_000_000)
-            line["cpu_baseline"] = cpu_baseline(args, cfg, first, None)
+            line["cpu_baseline"] = cpu_baseline(args, cfg, first, None)[0]
         print(json.dumps(line), flush=True)
     sh.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, cfg, batch, sites):
-    """The oracle (C++ restatement of ADAM BQSR, oracle/) timed on this host's
-    cores over a bounded sample of the same workload: the first --cpu-reads
-    reads of the GPU's own shard, observe per partition -> merge in order ->
-    finalize -> apply, one std::thread per partition; plus one thread on an
-    eighth of the sample."""
+def host_cores():
+    """(threads to use, description): every CPU this process may run on (its
+    affinity mask), with the machine's count and any cgroup CPU quota stated."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        quota = None
+    return aff, {"affinity": aff, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(args, cfg, batch, sites, whole=False):
+    """The oracle (oracle/: the C++ restatement of ADAM BQSR; Spark cannot run
+    here) timed on this host's cores over a bounded sample of the same
+    workload: the first --cpu-reads reads of the GPU's own shard, observe per
+    partition -> merge in order -> finalize -> apply, one std::thread per
+    partition; plus one thread on an eighth of the sample.  With `whole` and a
+    sample that is the whole shard, the run is the single-partition form
+    (oracle_bqsr_fold1: expectedMismatch folded over the shard in order by one
+    more thread) and its outputs are returned for the parity check."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, cinfo = host_cores()
     n = min(args.cpu_reads, batch.n_reads)
     sample = batch.slice(0, n) if n < batch.n_reads else batch
+    fold1 = whole and n == batch.n_reads
     osites = O.Sites(sites) if sites else None
     d = O.Dims(cfg["n_rg"], max(cfg["lens"]))
     t = time.perf_counter()
-    O.bqsr(sample, osites, d, n_parts=cores, nthreads=cores)
+    res = O.bqsr(sample, osites, d, n_parts=cores, nthreads=cores, fold1=fold1)
     dt = time.perf_counter() - t
     one = sample.slice(0, max(1, n // 8))
     t1 = time.perf_counter()
     O.bqsr(one, osites, d, n_parts=1, nthreads=1)
     dt1 = time.perf_counter() - t1
-    return {"value": sample.n_bases / dt, "unit": "bases/s", "cores": cores, "kind": "port",
+    line = {"value": sample.n_bases / dt, "unit": "bases/s", "cores": cores, "kind": "port",
+            "label": "C++ restatement of ADAM BQSR (oracle/), not Spark: no JVM on the box",
+            "host": cinfo,
             "sample": "first %d reads (%d bases) of the %s shard, observe+merge+finalize+apply, %d partitions "
-                      "on %d threads (%.1f s); value_1thread on the first %d reads (%.1f s)" %
-                      (n, sample.n_bases, args.config, cores, cores, dt, one.n_reads, dt1),
+                      "on %d threads (%.1f s)%s; value_1thread on the first %d reads (%.1f s)" %
+                      (n, sample.n_bases, args.config, cores, cores, dt,
+                       " + one thread folding expectedMismatch over the shard as one partition" if fold1 else "",
+                       one.n_reads, dt1),
             "value_1thread": one.n_bases / dt1}
-
+    return line, (res if fold1 else None)
 
 if __name__ == "__main__":
     main()

@@ -282,7 +282,9 @@ bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
 bqsr_status bqsr_observe_result(bqsr_batch* b, double* expected_mismatch, void* stream);
 void* bqsr_batch_em_device_ptr(bqsr_batch* b);
 bqsr_status bqsr_table_zero_async(bqsr_table* t, void* stream);
-/* finalize into *out; a non-NULL *out of the same dims is reused (no allocation) */
+/* finalize into *out.  *out must be NULL or a LUT returned by an earlier
+ * finalize: one of the same dims and context is reused (no allocation), any
+ * other is destroyed and replaced. */
 bqsr_status bqsr_finalize_async(bqsr_context* ctx, const bqsr_table* t, double expected_mismatch, bqsr_lut** out,
                                 void* stream);
 bqsr_status bqsr_finalize_result(bqsr_lut* l, void* stream);
@@ -294,6 +296,13 @@ bqsr_status bqsr_finalize_device(bqsr_context* ctx, const bqsr_table* t, const d
                                  void* stream);
 /* copy the batch's expectedMismatch (one double) to a device buffer, on `stream` */
 bqsr_status bqsr_batch_em_copy_async(bqsr_batch* b, double* dst_device, void* stream);
+/* RecalTable.++ of n partitions' expectedMismatch in the given order
+ * (RecalTable.scala:90-108): *out_device = ((0.0 + ems[0]) + ems[1]) + ...,
+ * computed on the device on `stream` (ems_device: n doubles).  The multi-rank
+ * and streamed paths gather every partition's value and fold them in global
+ * partition order with this. */
+bqsr_status bqsr_em_fold_async(bqsr_context* ctx, const double* ems_device, int64_t n, double* out_device,
+                               void* stream);
 /* apply stages: RESET clears the error word and exception count, KERNEL the
  * apply kernel; PREP (re)runs the prep kernel, which also runs by itself when
  * observe has not prepared this batch */

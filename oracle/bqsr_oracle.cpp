@@ -619,8 +619,108 @@ int oracle_apply(const bqsr_records* R, int64_t r0, int64_t r1, const void* fp, 
 // partition order (RecalTable.++, expectedMismatch = acc + part); finalize;
 // apply per partition.  Outputs like oracle_apply.  Returns a status;
 // *err_read = first failing read of the first failing partition.
+// expectedMismatch of reads [r0, r1) as ONE partition's foldLeft from *em
+// (RecalTable.scala:61 over ReadCovariates' trimmed ranges of usable reads,
+// masked bases included, Q15) -- without the covariates: the sequential part
+// of observe, for the single-partition check of the benchmark's job.  Assumes
+// error-free input (observe reports errors).
+void oracle_em_fold(const bqsr_records* R, int64_t r0, int64_t r1, double* em) {
+  const double* p10 = pow10c().v;
+  double acc = *em;
+  for (int64_t r = r0; r < r1; ++r) {
+    const uint32_t f = R->flags[r];
+    if (!usable(f) || !(f & BQSR_F_HAS_QUAL)) continue;
+    const uint8_t* qc = R->qual + R->qual_offset[r];
+    const size_t lq = (size_t)(R->qual_offset[r + 1] - R->qual_offset[r]);
+    auto qs = [&](size_t i) -> int8_t { return (int8_t)(uint8_t)(qc[i] - 33); };
+    size_t st = 0;
+    while (st < lq && qs(st) <= 2) ++st;  // ReadCovariates.scala:31-39
+    size_t tail = 0;
+    while (tail < lq && qs(lq - 1 - tail) <= 2) ++tail;
+    for (size_t o = st; o + tail < lq; ++o) {
+      const int8_t q = qs(o);
+      if (q < 0) break;  // QUAL_RANGE: observe reports it
+      acc = acc + p10[q];
+    }
+  }
+  *em = acc;
+}
+
+static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
+                     bool fold1, uint16_t* out_qual, uint32_t* out_len, int64_t* words_out, double* em_out,
+                     int64_t* err_read);
+
 int oracle_bqsr(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
                 uint16_t* out_qual, uint32_t* out_len, int64_t* words_out, double* em_out, int64_t* err_read) {
+  return bqsr_impl(R, n_parts, sites, dims, nthreads, false, out_qual, out_len, words_out, em_out, err_read);
+}
+
+// The same job as ONE partition (the table -- partition-order free -- still
+// built by n_parts threads; expectedMismatch folded over all reads in order
+// by one more thread running beside them): what one GPU's benchmark job
+// computes over its shard.
+int oracle_bqsr_fold1(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
+                      uint16_t* out_qual, uint32_t* out_len, int64_t* words_out, double* em_out, int64_t* err_read) {
+  return bqsr_impl(R, n_parts, sites, dims, nthreads, true, out_qual, out_len, words_out, em_out, err_read);
+}
+
+// Compare the oracle's output (qual_offset layout, Java chars) with the HIP
+// apply output in the packed device layout: read r's chars at
+// got[slot(r) + got_start[r] ...] (slot = running sum of max(Lq, Ls) rounded
+// up to 16 when `aligned`), chars above 0xFF in the (slot << 16 | code) list.
+// Returns the number of reads that differ; *first_bad = the first one (-1).
+int64_t oracle_compare_device_output(const bqsr_records* R, const uint16_t* ref, const uint32_t* ref_len,
+                                     const uint8_t* got, const uint32_t* got_start, const uint32_t* got_len,
+                                     const uint64_t* exc, int64_t n_exc, int32_t aligned, int32_t nthreads,
+                                     int64_t* first_bad) {
+  const int64_t n = R->n_reads;
+  std::vector<uint64_t> slot((size_t)n + 1, 0);
+  for (int64_t r = 0; r < n; ++r) {
+    const uint32_t f = R->flags[r];
+    const uint64_t lq = (f & BQSR_F_HAS_QUAL) ? R->qual_offset[r + 1] - R->qual_offset[r] : 0;
+    const uint64_t ls = (f & BQSR_F_HAS_SEQ) ? R->seq_offset[r + 1] - R->seq_offset[r] : 0;
+    const uint64_t sl = std::max(lq, ls);
+    slot[(size_t)r + 1] = slot[(size_t)r] + (aligned ? (sl + 15) / 16 * 16 : sl);
+  }
+  std::vector<std::pair<uint64_t, uint16_t>> ex;
+  for (int64_t i = 0; i < n_exc; ++i) ex.push_back({exc[i] >> 16, (uint16_t)(exc[i] & 0xFFFF)});
+  std::sort(ex.begin(), ex.end());
+  std::atomic<int64_t> bad{0}, first{INT64_MAX};
+  const int nt = std::max(1, nthreads);
+  auto work = [&](int t) {
+    int64_t b = 0, fb = INT64_MAX;
+    for (int64_t r = n * t / nt; r < n * (t + 1) / nt; ++r) {
+      bool ok = got_len[r] == ref_len[r];
+      const uint16_t* rq = ref + R->qual_offset[r];
+      const uint64_t s0 = slot[(size_t)r] + got_start[r];
+      for (uint32_t k = 0; ok && k < ref_len[r]; ++k) {
+        uint16_t v = got[s0 + k];
+        if (rq[k] > 0xFF) {
+          auto it = std::lower_bound(ex.begin(), ex.end(), std::make_pair(s0 + k, (uint16_t)0));
+          v = (it != ex.end() && it->first == s0 + k) ? it->second : v;
+        }
+        ok = v == rq[k];
+      }
+      if (!ok) {
+        ++b;
+        fb = std::min(fb, r);
+      }
+    }
+    bad += b;
+    int64_t cur = first.load();
+    while (fb < cur && !first.compare_exchange_weak(cur, fb)) {
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+  for (auto& x : th) x.join();
+  *first_bad = bad.load() ? first.load() : -1;
+  return bad.load();
+}
+
+static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
+                     bool fold1, uint16_t* out_qual, uint32_t* out_len, int64_t* words_out, double* em_out,
+                     int64_t* err_read) {
   if (n_parts < 1 || nthreads < 1) return BQSR_ERR_INVALID_ARG;
   Dims d(dims);
   const int64_t n = R->n_reads;
@@ -639,6 +739,8 @@ int oracle_bqsr(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_
     }
   };
   std::vector<std::thread> th;
+  double em1 = 0.0;
+  if (fold1) th.emplace_back([&]() { oracle_em_fold(R, 0, n, &em1); });
   for (int32_t i = 0; i < nthreads; ++i) th.emplace_back(work_obs);
   for (auto& t : th) t.join();
   th.clear();
@@ -653,6 +755,7 @@ int oracle_bqsr(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_
     for (size_t i = 0; i < acc.size(); ++i) acc[i] += tabs[(size_t)p][i];
     em = em + ems[(size_t)p];
   }
+  if (fold1) em = em1;
   if (words_out) std::memcpy(words_out, acc.data(), acc.size() * sizeof(int64_t));
   if (em_out) *em_out = em;
   int fst;

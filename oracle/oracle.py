@@ -55,6 +55,12 @@ def lib():
         L.oracle_apply.argtypes = [vp, i64, i64, vp, vp, vp, vp]
         L.oracle_bqsr.restype = ctypes.c_int
         L.oracle_bqsr.argtypes = [vp, i32, vp, Dims, i32, vp, vp, vp, vp, vp]
+        L.oracle_bqsr_fold1.restype = ctypes.c_int
+        L.oracle_bqsr_fold1.argtypes = [vp, i32, vp, Dims, i32, vp, vp, vp, vp, vp]
+        L.oracle_em_fold.restype = None
+        L.oracle_em_fold.argtypes = [vp, i64, i64, vp]
+        L.oracle_compare_device_output.restype = i64
+        L.oracle_compare_device_output.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp]
         L.oracle_reference_positions.restype = i64
         L.oracle_reference_positions.argtypes = [vp, ctypes.c_uint64, i64, vp, i64]
         L.oracle_reference_end.restype = i64
@@ -188,9 +194,12 @@ def apply(batch, fin: Final, r0: int = 0, r1: Optional[int] = None, out: Optiona
     return out, out_len
 
 
-def bqsr(batch, sites: Optional[Sites], d: Dims, n_parts: int = 1, nthreads: int = 1):
+def bqsr(batch, sites: Optional[Sites], d: Dims, n_parts: int = 1, nthreads: int = 1, fold1: bool = False):
     """Whole BQSR (observe per partition -> merge in partition order -> finalize
-    -> apply) on nthreads std::threads.  Returns (words, em, out, out_len)."""
+    -> apply) on nthreads std::threads.  Returns (words, em, out, out_len).
+    fold1: expectedMismatch as if the batch were ONE partition (the table is
+    partition-order free; em is folded sequentially over all reads by one more
+    thread) -- the job one GPU runs over its shard."""
     cid = batch.contig_ids_for(sites.contigs if sites else None)
     s, keep = batch.c_struct(cid)
     out = np.zeros(max(1, int(batch.qual_offset[-1])), dtype=np.uint16)
@@ -198,11 +207,42 @@ def bqsr(batch, sites: Optional[Sites], d: Dims, n_parts: int = 1, nthreads: int
     words = np.zeros(table_words(d), dtype=np.int64)
     em = ctypes.c_double(0.0)
     err = ctypes.c_int64(-1)
-    st = lib().oracle_bqsr(ctypes.byref(s), n_parts, sites.handle if sites else None, d, nthreads, _p(out),
+    fn = lib().oracle_bqsr_fold1 if fold1 else lib().oracle_bqsr
+    st = fn(ctypes.byref(s), n_parts, sites.handle if sites else None, d, nthreads, _p(out),
                            _p(out_len), _p(words), ctypes.byref(em), ctypes.byref(err))
     if st != 0:
         raise OracleError(st, err.value)
     return words, em.value, out, out_len
+
+
+def em_fold(batch, r0: int = 0, r1: Optional[int] = None, em: float = 0.0) -> float:
+    """expectedMismatch of reads [r0, r1) folded as one partition (error-free input)."""
+    r1 = batch.n_reads if r1 is None else r1
+    s, keep = batch.c_struct()
+    v = ctypes.c_double(em)
+    lib().oracle_em_fold(ctypes.byref(s), r0, r1, ctypes.byref(v))
+    return v.value
+
+
+def compare_device_output(batch, ref_out: np.ndarray, ref_len: np.ndarray, got_qual: np.ndarray,
+                          got_start: np.ndarray, got_len: np.ndarray, exceptions: Optional[np.ndarray] = None,
+                          aligned: bool = True, nthreads: int = 8) -> Tuple[int, int]:
+    """(number of reads whose recalibrated chars differ, first such read or -1)
+    between the oracle's output and the HIP apply output in the packed device
+    layout (u8 per slot, per-read start/length, exception list for chars > 0xFF)."""
+    s, keep = batch.c_struct()
+    ref_out = np.ascontiguousarray(ref_out, dtype=np.uint16)
+    ref_len = np.ascontiguousarray(ref_len, dtype=np.uint32)
+    got_qual = np.ascontiguousarray(got_qual, dtype=np.uint8)
+    got_start = np.ascontiguousarray(got_start).view(np.uint32)
+    got_len = np.ascontiguousarray(got_len).view(np.uint32)
+    exc = np.ascontiguousarray(exceptions if exceptions is not None else np.zeros(1, np.int64)).view(np.uint64)
+    n_exc = 0 if exceptions is None else len(exceptions)
+    first = ctypes.c_int64(-1)
+    bad = lib().oracle_compare_device_output(ctypes.byref(s), _p(ref_out), _p(ref_len), _p(got_qual), _p(got_start),
+                                             _p(got_len), _p(exc), n_exc, int(aligned), nthreads,
+                                             ctypes.byref(first))
+    return int(bad), int(first.value)
 
 
 def reference_positions(cigar: Sequence[int], start: int):

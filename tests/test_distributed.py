@@ -86,6 +86,68 @@ def test_two_rank_table_allreduce_and_rank_order_fold(tmp_path):
         assert np.array_equal(z["out_len"][r0:r1], ref_len[r0:r1])
 
 
+def _rank_parts_main(rank, port, out_dir):
+    """Several partitions per rank (2 on rank 0, 3 on rank 1): each partition
+    observed from zero, the tables all-reduced, and every partition's
+    expectedMismatch gathered and folded in global partition order."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+    from adam_amd import distributed as D
+    from adam_amd import synth
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        batch = synth.generate(5000, (100,), 1, 78)
+        d = O.Dims(1, 100)
+        cuts = _PART_CUTS[rank]
+        words = np.zeros(O.table_words(d), dtype=np.int64)
+        ems = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            w, e = O.observe(batch, None, d, a, b)
+            words += w
+            ems.append(e)
+        t = torch.from_numpy(words)
+        D.allreduce_table(t)
+        counts = D.partition_counts(len(ems))
+        em = float(D.fold_partition_ems_device(torch.tensor(ems, dtype=torch.float64), counts)[0])
+        np.savez(os.path.join(out_dir, "p%d.npz" % rank), words=t.numpy(), em=np.array([em]),
+                 counts=np.array(counts))
+    finally:
+        dist.destroy_process_group()
+
+
+_PART_CUTS = {0: [0, 1000, 2600], 1: [2600, 3000, 4100, 5000]}
+
+
+def test_two_ranks_several_partitions_each_fold_in_partition_order(tmp_path):
+    import oracle as O
+    from adam_amd import synth
+    mp.start_processes(_rank_parts_main, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    batch = synth.generate(5000, (100,), 1, 78)
+    d = O.Dims(1, 100)
+    words = np.zeros(O.table_words(d), dtype=np.int64)
+    em = 0.0
+    bounds = _PART_CUTS[0] + _PART_CUTS[1][1:]
+    for a, b in zip(bounds[:-1], bounds[1:]):  # partitions 0..4 in order, one driver merge each
+        w, e = O.observe(batch, None, d, a, b)
+        words += w
+        em = em + e
+    for rank in range(WORLD):
+        z = np.load(tmp_path / ("p%d.npz" % rank))
+        assert z["counts"].tolist() == [2, 3]
+        assert np.array_equal(z["words"], words)
+        assert z["em"][0] == em
+
+
 @pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (10, 3), (1001, 8)])
 def test_shard_bounds_cover_in_order(n, world):
     from adam_amd.distributed import shard_bounds

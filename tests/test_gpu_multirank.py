@@ -1,0 +1,148 @@
+"""The multi-rank HIP sequence, two ranks sharing one GPU over gloo.
+
+Each rank is a separate process on cuda:0 running exactly what a rank of
+``bench.py --gpus N`` runs (adam_amd/job.py ResidentJob.step: staged observe ->
+int64 table all-reduce -> expectedMismatch of every rank's partition folded in
+rank order on the device -> finalize from HBM -> apply), and what a rank of the
+streamed path runs (adam_amd/stream.py StreamedShard.run over several
+partitions per rank, the table all-reduced, expectedMismatch folded over every
+partition of the job in global partition order).  The results must equal the
+CPU oracle folding the same partitions in that order as one job
+(RecalibrateBaseQualities.scala:63: aggregate over partitions, merged in
+partition order), bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from _parity import run_oracle
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+N_READS = 24000
+PARTS_PER_RANK = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _data():
+    from adam_amd import synth
+    batch = synth.generate(N_READS, (100, 150), 2, 977)
+    sites = synth.known_sites(300_000, seed=5)
+    return batch, sites
+
+
+def _rank_parts(batch, rank):
+    from adam_amd.distributed import shard_bounds
+    r0, r1 = shard_bounds(batch.n_reads, rank, WORLD)
+    shard = batch.slice(r0, r1)
+    cuts = [shard.n_reads * i // PARTS_PER_RANK for i in range(PARTS_PER_RANK + 1)]
+    return shard, [shard.slice(cuts[i], cuts[i + 1]) for i in range(PARTS_PER_RANK)]
+
+
+def _rank_main(rank, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import ctypes
+
+    import torch
+    import torch.distributed as dist
+
+    from adam_amd import _capi, bqsr
+    from adam_amd.job import ResidentJob
+    from adam_amd.stream import StreamedShard
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.zeros(1, device=dev)  # torch's HIP runtime first, as bench.py does
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        batch, sites = _data()
+        snp = bqsr.SnpTable(sites)
+        dims = bqsr.dims_of([batch])
+        shard, parts = _rank_parts(batch, rank)
+        # ---- bench.py's step: the shard as one partition ----
+        job = ResidentJob(shard, dims, snp, 0)
+        for _ in range(2):  # steady state: the second job reuses every buffer
+            job.step(False)
+        words, em, q, st, ln, exc = job.results()
+        job.close()
+        # ---- the streamed path: PARTS_PER_RANK partitions on this rank ----
+        L = _capi.lib()
+        ctx = bqsr.Context.get(0)
+        words_t = torch.zeros(int(L.bqsr_table_words(dims)), dtype=torch.int64, device=dev)
+        th = ctypes.c_void_p()
+        _capi.check(L.bqsr_table_create(ctx.handle, dims, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
+        sh = StreamedShard(ctx, parts, dims, snp.handle(ctx), 0, site_contigs=snp.contigs)
+        try:
+            for _ in range(2):
+                em_s = sh.run(th, words_t)
+                n_exc = sh.finish()
+            s_words = words_t.cpu().numpy()
+            s_em = float(em_s.cpu()[0])
+            s_q = [sh.host_qual[i].numpy()[:sh.n_slots[i]].copy() for i in range(len(parts))]
+            s_st = [sh.host_start[i].numpy()[:sh.n_reads[i]].copy() for i in range(len(parts))]
+            s_ln = [sh.host_len[i].numpy()[:sh.n_reads[i]].copy() for i in range(len(parts))]
+        finally:
+            sh.close()
+            L.bqsr_table_destroy(th)
+        np.savez(os.path.join(out_dir, "rank%d.npz" % rank), words=words, em=np.array([em]), q=q, st=st, ln=ln,
+                 exc=exc, s_words=s_words, s_em=np.array([s_em]), s_exc=np.array([n_exc]),
+                 **{"s_q%d" % i: s_q[i] for i in range(len(parts))},
+                 **{"s_st%d" % i: s_st[i] for i in range(len(parts))},
+                 **{"s_ln%d" % i: s_ln[i] for i in range(len(parts))})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_two_ranks_one_gpu(tmp_path):
+    import oracle as O
+    ctx = mp.start_processes(_rank_main, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=False,
+                             start_method="spawn")
+    for _ in range(600):  # at most ~10 minutes, normally well under one
+        if ctx.join(timeout=1):
+            break
+    else:
+        for p in ctx.processes:
+            p.kill()
+        pytest.fail("ranks did not finish")
+    batch, sites = _data()
+    shards = [_rank_parts(batch, r) for r in range(WORLD)]
+    # bench.py's job: partitions = the ranks' shards, in rank order
+    o = run_oracle([s for s, _ in shards], sites)
+    assert o.error is None
+    # streamed: partitions = every rank's partitions, rank 0's first
+    all_parts = [p for _, ps in shards for p in ps]
+    os_ = run_oracle(all_parts, sites)
+    assert os_.error is None
+    for rank in range(WORLD):
+        z = np.load(tmp_path / ("rank%d.npz" % rank))
+        shard, parts = shards[rank]
+        assert np.array_equal(z["words"], o.words)
+        assert z["em"][0] == o.em, (z["em"][0], o.em)
+        ref_out, ref_len = o.outs[rank]
+        bad, first = O.compare_device_output(shard, ref_out, ref_len, z["q"], z["st"], z["ln"],
+                                             z["exc"] if len(z["exc"]) else None)
+        assert bad == 0, first
+        # streamed
+        assert np.array_equal(z["s_words"], os_.words)
+        assert z["s_em"][0] == os_.em, (z["s_em"][0], os_.em)
+        assert int(z["s_exc"][0]) == 0
+        for i, p in enumerate(parts):
+            ref_out, ref_len = os_.outs[rank * PARTS_PER_RANK + i]
+            bad, first = O.compare_device_output(p, ref_out, ref_len, z["s_q%d" % i], z["s_st%d" % i],
+                                                 z["s_ln%d" % i])
+            assert bad == 0, (rank, i, first)

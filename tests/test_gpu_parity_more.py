@@ -1,0 +1,159 @@
+"""More HIP-vs-oracle parity cases (bit for bit, through the C ABI):
+
+* quals 60..127 across three read groups: the qualByRG key aliasing of
+  `q + 60 * rg` (rg0/q61 == rg1/q1), q = 0 attributed to group rg - 1 and
+  q >= 61 to rg + 1 by finalize's `(key - 1) / 60` (RecalTable.scala:121,129;
+  StandardCovariate.scala:25-32), and the apply path for quals above the LDS
+  char-table rows;
+* a crafted table (bqsr_table_upload) whose shifts drive apply to Java chars
+  above 0xFF (Q < -33) and to non-ASCII codes 128..255 (Q > 94)
+  (RecalUtil.scala:37-40, quirk Q14);
+* known sites loaded by SnpTable.from_vcf from the reference's own
+  small.vcf (SnpTable.scala:32-47, raw 1-based POS, quirk Q7);
+* a 1M-read partition (1e8 bases): the expectedMismatch fold's block / tile /
+  element descent at scale.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from _parity import check
+from adam_amd import _capi, bqsr, synth
+from adam_amd.records import ADAMRecord, RecordBatch
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_resources")
+
+
+def high_qual_batch(n_reads, n_rg, seed, frac=0.5):
+    """Synthetic reads whose interior quals are redrawn uniformly from 0..127
+    (chars '!'..0xA0) in a fraction of the reads."""
+    b = synth.generate(n_reads, (100,), n_rg, seed)
+    rng = np.random.default_rng(seed)
+    q = b.qual.copy()
+    for r in np.nonzero(rng.random(b.n_reads) < frac)[0]:
+        a, e = int(b.qual_offset[r]), int(b.qual_offset[r + 1])
+        if e - a > 4:
+            q[a + 2:e - 2] = rng.integers(0, 128, e - a - 4) + 33
+    b.qual = q
+    return b
+
+
+def test_quals_60_to_127_three_read_groups():
+    b = high_qual_batch(20000, 3, 41)
+    g, o = check([b.slice(0, 7000), b.slice(7000, 20000)])
+    K = 60 * 2 + 128
+    touched = g.words[:K]
+    assert touched[0] > 0 and touched[61] > 0 and touched[127 + 120] > 0  # q=0, aliased 61, rg2/q127
+
+
+def test_quals_60_to_127_one_read_group_edges():
+    # rg0 keys 0..127: key 0 and keys 1..60 are group 0, keys 61..120 group 1,
+    # 121..127 group 2 -- groups that exist only through aliasing
+    b = high_qual_batch(6000, 1, 43, frac=1.0)
+    check([b])
+
+
+# ---- crafted table: chars above 0xFF and non-ASCII ---------------------------
+
+L10 = 10
+
+
+def crafted_table(seed):
+    """Dense table words (2 read groups, max_len 10) and the quals each read
+    group's reads use.  Read group 1's keys take random bins whose mismatch
+    count may exceed the observations (possible only through the C ABI, not
+    from reads): E = mm/obs far above 1 makes the recalibrated error
+    probability huge, Q very negative, (Q + 33).toChar above 0xFF.  Read group
+    0's 'near-cancel' keys have qualScore error ~= cycle error + context
+    error, so newP is a rounding residue: Q 95..200, chars 128..255 (group 0
+    is kept apart so group 1's huge error rates do not swamp the residue)."""
+    d = O.Dims(2, L10)
+    K, C = 60 + 128, 2 * L10 + 1
+    cells = C + 21
+    w = np.zeros(K + 2 * K * cells, np.int64)
+    t = w[:K]
+    obs = w[K:K + K * cells].reshape(K, cells)
+    mm = w[K + K * cells:].reshape(K, cells)
+    rng = np.random.default_rng(seed)
+    pairs = [(1, 0), (3, 1), (1000, 0), (10 ** 6, 1), (10 ** 9, 2000), (10 ** 6, 2), (1, 10 ** 6), (1000, 10 ** 15),
+             (7, 7)]
+    rand_q = [5, 20, 40, 41, 60]   # read group 1: keys 65..120, group 1
+    near_q = [3, 10, 30, 38, 45, 59]  # read group 0: keys 3..59, group 0
+    for q in rand_q:
+        k = q + 60
+        t[k] = rng.integers(1, 1000)
+        for c in range(cells):
+            if rng.random() < 0.8:
+                obs[k, c], mm[k, c] = pairs[rng.integers(0, len(pairs))]
+    for i, k in enumerate(near_q):
+        t[k] = 5
+        obs[k, :C], mm[k, :C] = 1, 0
+        obs[k, L10 + 1], mm[k, L10 + 1] = 10 ** 9 + 12345 * i, 2000 + i
+        obs[k, C:], mm[k, C:] = 10 ** 6, 1
+    return d, w, {0: near_q, 1: rand_q}
+
+
+def reads_for_keys(quals_by_rg, n, seed):
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        rg = i % 2
+        q = rng.choice(quals_by_rg[rg], L10)
+        seq = "".join(rng.choice(list("ACGTN"), L10, p=[0.24, 0.24, 0.24, 0.24, 0.04]))
+        recs.append(ADAMRecord(record_group_id=rg, read_mapped=True, primary_alignment=True, start=1000 + i,
+                               reference_name="1", cigar="10M", mismatching_positions="10", sequence=seq,
+                               qual="".join(chr(int(v) + 33) for v in q),
+                               read_negative_strand=bool(i & 2), read_paired=bool(i & 4),
+                               second_of_pair=bool(i & 8)))
+    return RecordBatch.from_records(recs)
+
+
+@pytest.mark.parametrize("seed,em", [(7, 0.0), (8, 123.456), (9, 1e5)])
+def test_crafted_table_chars_above_0xff(seed, em):
+    d, w, keys = crafted_table(seed)
+    batch = reads_for_keys(keys, 3000, seed)
+    # oracle
+    fin = O.Final(d, w, em)
+    ref, ref_len = O.apply(batch, fin)
+    # HIP path: upload the same words, finalize with the same expectedMismatch, apply
+    ctx = bqsr.Context.get(0)
+    tab = bqsr.RecalTable(_capi.Dims(2, L10), ctx, expected_mismatch=em)
+    tab.set_words(w)
+    gfin = tab.finalize_table()
+    chars = np.zeros(int(batch.qual_offset[-1]), dtype=np.uint16)
+    out_len = np.zeros(batch.n_reads, dtype=np.uint32)
+    s, keep = batch.c_struct()
+    _capi.check(_capi.lib().bqsr_apply_records(ctx.handle, ctypes.byref(s), gfin.handle, chars.ctypes.data,
+                                               out_len.ctypes.data))
+    assert np.array_equal(out_len, ref_len[:batch.n_reads])
+    n = int(batch.qual_offset[-1])
+    bad = np.nonzero(chars[:n] != ref[:n])[0]
+    assert bad.size == 0, (bad[:10], chars[bad[:10]], ref[bad[:10]])
+    assert (ref[:n] > 0xFF).sum() > 100          # the exception list path
+    assert ((ref[:n] >= 128) & (ref[:n] <= 0xFF)).sum() > 10  # non-ASCII bytes in the fast path
+
+
+# ---- known sites from the reference's VCF -------------------------------------
+
+def test_sites_from_small_vcf():
+    snp = bqsr.SnpTable.from_vcf(os.path.join(GOLD, "small.vcf"))
+    assert "20" in snp.table and 14370 in snp.table["20"].tolist()
+    sites = {k: v.tolist() for k, v in snp.table.items()}
+    # reads on contig "20" around the VCF positions (0-based refPos == raw POS masks, Q7)
+    b = synth.generate(30000, (100,), 1, 51, contig_len=1_300_000, contig="20")
+    g_sites, o_sites = check([b], sites)
+    g_none, _ = check([b], None)
+    assert not np.array_equal(g_sites.words, g_none.words)  # some bases were masked by the VCF sites
+
+
+# ---- the fold at scale --------------------------------------------------------
+
+def test_fold_one_million_reads():
+    b = synth.generate(1_000_000, (100,), 1, 61)
+    g, o = check([b])
+    assert g.em == o.em
