@@ -411,12 +411,110 @@ __device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32
   }
 }
 
+// Known sites of a read whose reference positions are start + o for every
+// offset o (a single-M CIGAR): mask the trimmed offsets [st, en) holding a
+// site (SnpTable.isMaskedAtReadOffset, raw VCF POS vs 0-based refPos, Q7).
+__device__ void mask_sites_linear(const PrepParams& P, int32_t contig, int64_t start, int st, int en, uint64_t rs) {
+  if (contig < 0 || contig >= P.sites.n_contigs) return;
+  const SitesDev& S = P.sites;
+  const int64_t* sp = S.pos + S.off[contig];
+  const int64_t ns = (int64_t)(S.off[contig + 1] - S.off[contig]);
+  if (ns == 0) return;
+  const int64_t lo_p = start + st, hi_p = start + en;
+  const uint32_t* bk = S.bucket + S.bucket_off[contig];
+  const int64_t nb = (int64_t)(S.bucket_off[contig + 1] - S.bucket_off[contig]);
+  const int64_t bi = (lo_p - S.bucket_base[contig]) >> S.shift;
+  int64_t j = bi < 0 ? 0 : (bi >= nb ? ns : (int64_t)bk[bi]);
+  while (j < ns && sp[j] < lo_p) ++j;
+  for (; j < ns && sp[j] < hi_p; ++j) {
+    const uint64_t o = (uint64_t)(sp[j] - start);
+    set_sbits(P.sbits, rs + o, rs + o + 1, 0);
+  }
+}
+
+// The common read, prepared without any per-read loop: eligible, every
+// field present, no low-quality run longer than 15 at either end, a single
+// M CIGAR element covering the trimmed range, and (usable reads) an MD tag
+// that is one number no shorter than the alignment -- so no base is masked
+// by the CIGAR and none mismatches (RichADAMRecord.scala:147-187, MdTag.scala:38-98).
+// Returns false for anything else (the read goes to the worklist of
+// bqsr_prep_complex, which runs prep_one with the full exception order).
+__device__ bool prep_fast(const PrepParams& P, int64_t r) {
+  const ReadMeta m = P.rd.meta[r];
+  const ReadAlign a = P.rd.align[r];
+  const uint16_t f = m.flags;
+  if (!eligible_read(f)) {
+    P.info[r] = ReadInfo{0, 0, kInfoPass, 0};
+    return true;
+  }
+  constexpr uint16_t need = BQSR_F_HAS_QUAL | BQSR_F_HAS_RG | BQSR_F_HAS_SEQ | BQSR_F_HAS_CIGAR | BQSR_F_HAS_START |
+                            BQSR_F_HAS_REFNAME;
+  if ((f & need) != need || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq < 32 || a.n_cigar != 1) return false;
+  const uint8_t* q = P.rd.qual + m.slot;
+  const int lq = m.lq;
+  const uint4 head = *(const uint4*)q, back = *(const uint4*)(q + lq - 16);
+  const uint32_t e = P.rd.cigar[a.cigar_off];
+  const bool usable = usable_read(f);
+  uint4 md4 = make_uint4(0, 0, 0, 0);
+  if (usable && a.md_len <= 10) md4 = *(const uint4*)(P.rd.md + a.md_off);
+  const int st = first_good(head, 16, false), tail = first_good(back, 16, true);
+  if (st == 16 || tail == 16) return false;
+  const int en = lq - tail;
+  const int64_t len = cig_len(e);
+  if (cig_op(e) != BQSR_CIGAR_M || len < en || (int)m.ls < en) return false;
+  const int64_t start = a.start;
+  if (start < 0 || start + 2 * len > 2147483647LL) return false;  // prep_one's Int-range test, unclipped = start
+  if (usable) {
+    // one run of digits, its value >= len: every position of [start, start + len) matches
+    if (a.md_len == 0 || a.md_len > 10) return false;
+    const uint32_t w[4] = {md4.x, md4.y, md4.z, 0u};
+    int64_t v = 0;
+    bool digits = true;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i < a.md_len) {
+        digits &= c >= '0' && c <= '9';
+        v = v * 10 + (int64_t)(c - '0');
+      }
+    }
+    if (!digits || v > 2147483647LL || v < len) return false;
+    mask_sites_linear(P, a.contig, start, st, en, m.slot);
+  }
+  P.info[r] = ReadInfo{(uint16_t)st, (uint16_t)en,
+                       (uint16_t)(kInfoApp | (usable ? kInfoObs : 0) | ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
+                                  (((f & BQSR_F_PAIRED) && (f & BQSR_F_SECOND_OF_PAIR)) ? kInfoSecond : 0)),
+                       0};
+  return true;
+}
+
+// Pass 1: every read; the common ones are finished in lock step, the others
+// appended to the worklist (one atomic per wavefront).
 extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n = P.rd.n_reads;
+  for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x; r0 < n; r0 += stride) {  // wave-uniform trip count
+    const int64_t r = r0 + threadIdx.x;
+    const bool todo = r < n && !prep_fast(P, r);
+    const uint64_t mask = __builtin_amdgcn_ballot_w64(todo);
+    if (mask) {
+      const int lane = threadIdx.x & 63;
+      uint32_t base = 0;
+      if (lane == (int)__builtin_ctzll(mask)) base = atomicAdd(P.n_work, (uint32_t)__popcll(mask));
+      base = __shfl(base, (int)__builtin_ctzll(mask));
+      if (todo) P.work[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)r;
+    }
+  }
+}
+
+// Pass 2: the worklist, one thread per read, the full per-read path.
+extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_complex(PrepParams P) {
   __shared__ uint32_t s_cig[kPrepThreads * kPrepCigStride];
   __shared__ uint32_t s_md[kPrepThreads * kPrepMdStride];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += stride)
-    prep_one(P, r, &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
+  const int64_t n = *P.n_work;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    prep_one(P, (int64_t)P.work[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
 }
 
 // ------------------------------------------------------- lane-per-read ----
