@@ -483,7 +483,8 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_work, (size_t)n + 1)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_work, (size_t)(n + kPrepChunk) + (size_t)(n / kPrepChunk + 1))) != BQSR_OK)
+    return st;
   // read-group buckets (OrderDev): on for several read groups, or when the
   // apply window over all cycle cells would leave more than 0.1% of the bases
   // outside its qual rows (ADAM_BQSR_ORDER=read / group forces either)
@@ -969,13 +970,11 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     P.sbits = b->d_sbits;
     P.err = b->d_err;
     P.work = b->d_work;
-    P.n_work = b->d_work + b->rd.n_reads;
-    HIP_TRY(hipMemsetAsync(P.n_work, 0, 4, s));
+    P.n_work = b->d_work + b->rd.n_reads + kPrepChunk;
     // pass 1: the common reads in lock step; pass 2: the rest, one thread each
-    const int64_t blocks = std::min<int64_t>((b->rd.n_reads + 255) / 256, (int64_t)ctx->n_cu * 32);
-    hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, P);
-    const int64_t cblocks = std::min<int64_t>((b->rd.n_reads + 255) / 256, (int64_t)ctx->n_cu * 8);
-    hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)cblocks), dim3(256), 0, s, P);
+    const int64_t blocks = (b->rd.n_reads + kPrepChunk - 1) / kPrepChunk;
+    hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
+    hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
     HIP_TRY(hipGetLastError());
     if (b->bucketed) {  // counting sort of the reads by read group
       const int64_t n = b->rd.n_reads;

@@ -147,8 +147,8 @@ struct PrepParams {
   ReadInfo* info;      // [n_reads]
   uint64_t* sbits;     // [n_slots / 32 + 2], zeroed before the launch
   unsigned long long* err;  // error words
-  uint32_t* work;      // [n_reads] reads bqsr_prep_kernel left to bqsr_prep_complex
-  uint32_t* n_work;    // their count, zeroed before the launch
+  uint32_t* work;      // [n_reads] reads bqsr_prep_kernel left to bqsr_prep_complex, per workgroup segment
+  uint32_t* n_work;    // [workgroups] their count per segment
 };
 
 // Read order of the per-base passes.  With one read group whose table rows

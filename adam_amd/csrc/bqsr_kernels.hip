@@ -173,6 +173,7 @@ __device__ __forceinline__ int first_good(const uint4 v, int n, bool rev) {
 constexpr int kPrepThreads = 256;
 constexpr int kPrepCig = 4, kPrepCigStride = 5;
 constexpr int kPrepMd = 32, kPrepMdStride = 9;
+constexpr int kPrepChunk = 2048;  // reads per workgroup of bqsr_prep_kernel (8 per thread)
 
 __device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32_t* s_md) {
   const ReadMeta m = P.rd.meta[r];
@@ -488,33 +489,45 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
   return true;
 }
 
-// Pass 1: every read; the common ones are finished in lock step, the others
-// appended to the worklist (one atomic per wavefront).
+// Pass 1: workgroup w takes reads [w * kPrepChunk, (w + 1) * kPrepChunk); the
+// common ones are finished in lock step, the others listed (in read order)
+// in the workgroup's own segment of the worklist -- LDS-compacted, no global
+// atomics (one counter shared by every wavefront serialised at the memory
+// side: measured 1.8 ms for 10M reads).
 extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  __shared__ uint32_t list[kPrepChunk];
+  __shared__ uint32_t cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
   const int64_t n = P.rd.n_reads;
-  for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x; r0 < n; r0 += stride) {  // wave-uniform trip count
-    const int64_t r = r0 + threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
+  const int lane = threadIdx.x & 63;
+  for (int i = 0; i < kPrepChunk; i += kPrepThreads) {
+    const int64_t r = c0 + i + threadIdx.x;
     const bool todo = r < n && !prep_fast(P, r);
     const uint64_t mask = __builtin_amdgcn_ballot_w64(todo);
     if (mask) {
-      const int lane = threadIdx.x & 63;
       uint32_t base = 0;
-      if (lane == (int)__builtin_ctzll(mask)) base = atomicAdd(P.n_work, (uint32_t)__popcll(mask));
+      if (lane == (int)__builtin_ctzll(mask)) base = atomicAdd(&cnt, (uint32_t)__popcll(mask));
       base = __shfl(base, (int)__builtin_ctzll(mask));
-      if (todo) P.work[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)r;
+      if (todo) list[base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))] = (uint32_t)r;
     }
   }
+  __syncthreads();
+  const uint32_t k = cnt;
+  for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads) P.work[c0 + i] = list[i];
+  if (threadIdx.x == 0) P.n_work[blockIdx.x] = k;
 }
 
-// Pass 2: the worklist, one thread per read, the full per-read path.
+// Pass 2: workgroup w takes the reads pass 1's workgroup w listed, one thread
+// per read, the full per-read path (prep_one).
 extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_complex(PrepParams P) {
   __shared__ uint32_t s_cig[kPrepThreads * kPrepCigStride];
   __shared__ uint32_t s_md[kPrepThreads * kPrepMdStride];
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n = *P.n_work;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
-    prep_one(P, (int64_t)P.work[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
+  const uint32_t k = P.n_work[blockIdx.x];
+  const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
+  for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads)
+    prep_one(P, (int64_t)P.work[c0 + i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
 }
 
 // ------------------------------------------------------- lane-per-read ----
