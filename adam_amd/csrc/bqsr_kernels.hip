@@ -412,34 +412,38 @@ __device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32
   }
 }
 
-// Known sites of a read whose reference positions are start + o for every
-// offset o (a single-M CIGAR): mask the trimmed offsets [st, en) holding a
-// site (SnpTable.isMaskedAtReadOffset, raw VCF POS vs 0-based refPos, Q7).
-__device__ void mask_sites_linear(const PrepParams& P, int32_t contig, int64_t start, int st, int en, uint64_t rs) {
+// Known sites of a read whose reference position at offset o is
+// unclipped + o for every offset (CIGAR [S]M[S]): mask the trimmed offsets
+// [st, en) holding a site (SnpTable.isMaskedAtReadOffset, raw VCF POS vs
+// 0-based refPos, Q7).
+__device__ void mask_sites_linear(const PrepParams& P, int32_t contig, int64_t unclipped, int st, int en,
+                                  uint64_t rs) {
   if (contig < 0 || contig >= P.sites.n_contigs) return;
   const SitesDev& S = P.sites;
   const int64_t* sp = S.pos + S.off[contig];
   const int64_t ns = (int64_t)(S.off[contig + 1] - S.off[contig]);
   if (ns == 0) return;
-  const int64_t lo_p = start + st, hi_p = start + en;
+  const int64_t lo_p = unclipped + st, hi_p = unclipped + en;
   const uint32_t* bk = S.bucket + S.bucket_off[contig];
   const int64_t nb = (int64_t)(S.bucket_off[contig + 1] - S.bucket_off[contig]);
   const int64_t bi = (lo_p - S.bucket_base[contig]) >> S.shift;
   int64_t j = bi < 0 ? 0 : (bi >= nb ? ns : (int64_t)bk[bi]);
   while (j < ns && sp[j] < lo_p) ++j;
   for (; j < ns && sp[j] < hi_p; ++j) {
-    const uint64_t o = (uint64_t)(sp[j] - start);
+    const uint64_t o = (uint64_t)(sp[j] - unclipped);
     set_sbits(P.sbits, rs + o, rs + o + 1, 0);
   }
 }
 
-// The common read, prepared without any per-read loop: eligible, every
-// field present, no low-quality run longer than 15 at either end, a single
-// M CIGAR element covering the trimmed range, and (usable reads) an MD tag
-// that is one number no shorter than the alignment -- so no base is masked
-// by the CIGAR and none mismatches (RichADAMRecord.scala:147-187, MdTag.scala:38-98).
-// Returns false for anything else (the read goes to the worklist of
-// bqsr_prep_complex, which runs prep_one with the full exception order).
+// The common read, prepared in lock step (no data-dependent loop): eligible,
+// every field present, no low-quality run longer than 15 at either end, a
+// CIGAR of the form [S]M[S], and (usable reads) an MD tag of at most 16
+// bytes without deletions, parsed in a fixed 16-step loop.  With that CIGAR
+// the reference position of offset o is unclipped + o (RichADAMRecord.scala:
+// 101-109,156-187): the clips fall outside [start, end) and are masked, and
+// MD position p (MdTag.scala:38-98, relative to start) is offset lead + p.
+// Returns false for anything else: the read goes to bqsr_prep_complex, which
+// runs prep_one with the full exception order.
 __device__ bool prep_fast(const PrepParams& P, int64_t r) {
   const ReadMeta m = P.rd.meta[r];
   const ReadAlign a = P.rd.align[r];
@@ -450,37 +454,99 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
   }
   constexpr uint16_t need = BQSR_F_HAS_QUAL | BQSR_F_HAS_RG | BQSR_F_HAS_SEQ | BQSR_F_HAS_CIGAR | BQSR_F_HAS_START |
                             BQSR_F_HAS_REFNAME;
-  if ((f & need) != need || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq < 32 || a.n_cigar != 1) return false;
+  if ((f & need) != need || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq < 32 || a.n_cigar == 0 ||
+      a.n_cigar > 3)
+    return false;
+  const bool usable = usable_read(f);
+  if (usable && (a.md_len == 0 || a.md_len > 16)) return false;
   const uint8_t* q = P.rd.qual + m.slot;
   const int lq = m.lq;
   const uint4 head = *(const uint4*)q, back = *(const uint4*)(q + lq - 16);
-  const uint32_t e = P.rd.cigar[a.cigar_off];
-  const bool usable = usable_read(f);
-  uint4 md4 = make_uint4(0, 0, 0, 0);
-  if (usable && a.md_len <= 10) md4 = *(const uint4*)(P.rd.md + a.md_off);
+  const uint4 c4 = *(const uint4*)(P.rd.cigar + a.cigar_off);  // the column has 32 B of padding
+  const uint4 md4 = usable ? *(const uint4*)(P.rd.md + a.md_off) : make_uint4(0, 0, 0, 0);
   const int st = first_good(head, 16, false), tail = first_good(back, 16, true);
   if (st == 16 || tail == 16) return false;
   const int en = lq - tail;
-  const int64_t len = cig_len(e);
-  if (cig_op(e) != BQSR_CIGAR_M || len < en || (int)m.ls < en) return false;
-  const int64_t start = a.start;
-  if (start < 0 || start + 2 * len > 2147483647LL) return false;  // prep_one's Int-range test, unclipped = start
+  // CIGAR [S]M[S]
+  const uint32_t cw[3] = {c4.x, c4.y, c4.z};
+  const int nc = a.n_cigar;
+  int64_t lead = 0, mlen = 0, trail = 0;
+  {
+    const uint32_t o0 = cig_op(cw[0]), o1 = cig_op(cw[1]), o2 = cig_op(cw[2]);
+    const int64_t l0 = cig_len(cw[0]), l1 = cig_len(cw[1]), l2 = cig_len(cw[2]);
+    if (nc == 1 && o0 == BQSR_CIGAR_M) {
+      mlen = l0;
+    } else if (nc == 2 && o0 == BQSR_CIGAR_S && o1 == BQSR_CIGAR_M) {
+      lead = l0;
+      mlen = l1;
+    } else if (nc == 2 && o0 == BQSR_CIGAR_M && o1 == BQSR_CIGAR_S) {
+      mlen = l0;
+      trail = l1;
+    } else if (nc == 3 && o0 == BQSR_CIGAR_S && o1 == BQSR_CIGAR_M && o2 == BQSR_CIGAR_S) {
+      lead = l0;
+      mlen = l1;
+      trail = l2;
+    } else {
+      return false;
+    }
+    // a zero-length element is prep_one's CIGAR_INVALID
+    if (l0 == 0 || (nc > 1 && l1 == 0) || (nc > 2 && l2 == 0)) return false;
+  }
+  const int64_t rp_len = lead + mlen + trail;
+  if (rp_len < en || (int)m.ls < en) return false;  // CIGAR_SHORT / SEQ_SHORT: prep_one reports them
+  const int64_t start = a.start, unclipped = start - lead;
+  // prep_one's Int-range test (the reference does position arithmetic in Int)
+  if (unclipped < 0 || unclipped + rp_len + mlen > 2147483647LL) return false;
+  const uint64_t rs = m.slot;
   if (usable) {
-    // one run of digits, its value >= len: every position of [start, start + len) matches
-    if (a.md_len == 0 || a.md_len > 10) return false;
-    const uint32_t w[4] = {md4.x, md4.y, md4.z, 0u};
-    int64_t v = 0;
-    bool digits = true;
+    // MD (MdTag.scala:38-98): digits (letters digits)*, no deletion; valid iff
+    // every byte is a digit or a base letter and the first and last are digits
+    const uint32_t w[4] = {md4.x, md4.y, md4.z, md4.w};
+    const int n = a.md_len;
+    int64_t num = 0, pos = 0;
+    bool ok = true;
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < 16; ++i) {  // validity and the tag's span
       const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-      if (i < a.md_len) {
-        digits &= c >= '0' && c <= '9';
-        v = v * 10 + (int64_t)(c - '0');
+      if (i < n) {
+        if (c >= '0' && c <= '9') {
+          num = num * 10 + (int64_t)(c - '0');
+          ok &= num <= 2147483647LL;  // Integer.parseInt
+        } else {
+          ok &= md_base((uint8_t)c) && i > 0 && i + 1 < n;
+          pos += num + 1;
+          num = 0;
+        }
       }
     }
-    if (!digits || v > 2147483647LL || v < len) return false;
-    mask_sites_linear(P, a.contig, start, st, en, m.slot);
+    if (!ok) return false;  // (a letter first or last is invalid: `i > 0 && i + 1 < n`)
+    const int64_t md_total = pos + num;
+    // masked: the clips (reference positions outside [start, start + mlen))
+    if (lead > st) set_sbits(P.sbits, rs + st, rs + min(lead, (int64_t)en), 0);
+    if (lead + mlen < en) set_sbits(P.sbits, rs + max((int64_t)st, lead + mlen), rs + en, 0);
+    // mismatches: each letter's position, then every position past the tag's span
+    num = 0;
+    pos = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i < n) {
+        if (c >= '0' && c <= '9') {
+          num = num * 10 + (int64_t)(c - '0');
+        } else {
+          pos += num;
+          num = 0;
+          const int64_t o = lead + pos;  // reference position start + pos
+          if (pos < mlen && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
+          pos += 1;
+        }
+      }
+    }
+    if (md_total < mlen) {
+      const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
+      if (lo < hi) set_sbits(P.sbits, rs + (uint64_t)lo, rs + (uint64_t)hi, 32);
+    }
+    mask_sites_linear(P, a.contig, unclipped, st, en, rs);
   }
   P.info[r] = ReadInfo{(uint16_t)st, (uint16_t)en,
                        (uint16_t)(kInfoApp | (usable ? kInfoObs : 0) | ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
