@@ -189,7 +189,7 @@ EDGE32 = [
     rec32(cigar="2S30M", mismatching_positions="29C0"), rec32(cigar="30M2S", mismatching_positions="0T29"),
     rec32(cigar="1S30M1S", mismatching_positions="30"), rec32(cigar="5S27M", mismatching_positions="12"),
     rec32(cigar="16S16M", start=15), rec32(cigar="32M", start=0),
-    rec32(cigar="3H29M", sequence=S32[:29], qual=Q32[:29]), rec32(cigar="30M2H"),
+    rec32(cigar="3H29M", sequence=S32[:29], qual=Q32[:29]), rec32(cigar="30M2H", sequence=S32[:30], qual=Q32[:30]),
     rec32(cigar="10M1I21M", mismatching_positions="31"), rec32(cigar="10M2D22M", mismatching_positions="10^AA22"),
     rec32(qual="#" * 16 + "I" * 16), rec32(qual="#" * 15 + "I" * 17), rec32(qual="I" * 17 + "#" * 15),
     rec32(qual="I" * 16 + "#" * 16), rec32(qual="#" * 32),
