@@ -47,6 +47,9 @@ constexpr uint16_t kInfoNeg = 16;       // readNegativeStrand
 constexpr uint16_t kInfoSecond = 32;    // readPaired && secondOfPair (DiscreteCycle negates)
 constexpr uint16_t kInfoPass = 64;      // not eligible: quality string passed through
 constexpr uint16_t kInfoCycNeg = 128;   // (tile record only) cycle cell decreases with the slot
+constexpr uint16_t kInfoTrim = 256;     // st / en not computed yet (prep's lock-step path reads no
+                                        // quals): the first pass over the read's quals trims it
+                                        // (resolve_info), observe writes the result back
 
 // packer-derived flag: the sequence holds a byte outside "ACGTN"
 // (BaseContext.simpleReverseComplement throws on it for reverse reads,
@@ -172,7 +175,7 @@ struct OrderDev {
 struct ObserveParams {
   ReadsDev rd;
   OrderDev ord;
-  const ReadInfo* info;
+  ReadInfo* info;  // read; trimmed ranges left to observe (kInfoTrim) are written back
   const uint64_t* sbits;  // PrepParams::sbits
   TableGeom g;
   Window w;

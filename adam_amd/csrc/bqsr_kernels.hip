@@ -166,6 +166,46 @@ __device__ __forceinline__ int first_good(const uint4 v, int n, bool rev) {
   return first;
 }
 
+// ReadCovariates' quality trimming (ReadCovariates.scala:31-39): st = the
+// number of leading quals <= minQuality (2, Java signed byte), en = lq minus
+// the trailing ones.  The first and last 16 quals come in with one load each.
+__device__ __forceinline__ void trim_quals(const uint8_t* q, int lq, int& st, int& en) {
+  int s = 0, tail = 0;
+  bool more_st = true, more_tail = true;
+  if (lq >= 16) {
+    const uint4 head = *(const uint4*)q, back = *(const uint4*)(q + lq - 16);
+    s = first_good(head, 16, false);
+    tail = first_good(back, 16, true);
+    more_st = s == 16;
+    more_tail = tail == 16;
+  }
+  if (more_st)
+    while (s < lq && (int8_t)q[s] <= 2) ++s;
+  if (more_tail)
+    while (tail < lq && (int8_t)q[lq - 1 - tail] <= 2) ++tail;
+  st = s;
+  en = lq - tail;
+}
+
+// A read's ReadInfo with the trimmed range filled in when prep left it to
+// the first pass over the quals (kInfoTrim); what prep_one writes for the
+// same read: {st, en, flags}, or {st, 0, 0} when no base is left.
+__device__ __forceinline__ ReadInfo resolve_info(const ReadsDev& rd, ReadInfo inf, uint64_t slot, int lq) {
+  if (inf.fl & kInfoTrim) {
+    int st, en;
+    trim_quals(rd.qual + slot, lq, st, en);
+    inf.st = (uint16_t)st;
+    if (st >= en) {
+      inf.en = 0;
+      inf.fl = 0;
+    } else {
+      inf.en = (uint16_t)en;
+      inf.fl &= (uint16_t)~kInfoTrim;
+    }
+  }
+  return inf;
+}
+
 // Per-thread LDS copies of a read's CIGAR (<= kPrepCig ops) and MD (<= kPrepMd
 // bytes): the parsers below then walk LDS instead of issuing one dependent
 // global load per element.  Strides of 5 and 9 dwords keep the 64 lanes'
@@ -195,22 +235,8 @@ __device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32
     P.info[r] = inf;
     return;
   }
-  const uint8_t* q = P.rd.qual + m.slot;
-  const int lq = m.lq;
-  int st = 0, tail = 0;
-  bool more_st = true, more_tail = true;
-  if (lq >= 16) {  // the first and last 16 quals, one load each
-    const uint4 head = *(const uint4*)q, back = *(const uint4*)(q + lq - 16);
-    st = first_good(head, 16, false);
-    tail = first_good(back, 16, true);
-    more_st = st == 16;
-    more_tail = tail == 16;
-  }
-  if (more_st)
-    while (st < lq && (int8_t)q[st] <= 2) ++st;  // isLowQualityBase, minQuality = 2
-  if (more_tail)
-    while (tail < lq && (int8_t)q[lq - 1 - tail] <= 2) ++tail;
-  const int en = lq - tail;
+  int st, en;
+  trim_quals(P.rd.qual + m.slot, m.lq, st, en);  // isLowQualityBase, minQuality = 2
   inf.st = (uint16_t)min(st, 0xFFFF);
   if (!(f & BQSR_F_HAS_RG)) {  // QualByRG: 60 * getRecordGroupId
     fail(err_key(r, 0, kRankCtor, BQSR_ERR_NULL_RG));
@@ -435,13 +461,17 @@ __device__ void mask_sites_linear(const PrepParams& P, int32_t contig, int64_t u
   }
 }
 
-// The common read, prepared in lock step (no data-dependent loop): eligible,
-// every field present, no low-quality run longer than 15 at either end, a
-// CIGAR of the form [S]M[S], and (usable reads) an MD tag of at most 16
-// bytes without deletions, parsed in a fixed 16-step loop.  With that CIGAR
-// the reference position of offset o is unclipped + o (RichADAMRecord.scala:
-// 101-109,156-187): the clips fall outside [start, end) and are masked, and
-// MD position p (MdTag.scala:38-98, relative to start) is offset lead + p.
+// The common read, prepared in lock step (no data-dependent loop) and
+// without touching its quals: eligible, every field present, a CIGAR of the
+// form [S]M[S] covering the whole read (so the trimmed range, whatever it is,
+// has reference positions and no CIGAR_SHORT / SEQ_SHORT can arise), and
+// (usable reads) an MD tag of at most 16 bytes without deletions, parsed in
+// a fixed 16-step loop.  With that CIGAR the reference position of offset o
+// is unclipped + o (RichADAMRecord.scala:101-109,156-187): the clips fall
+// outside [start, end) and are masked, and MD position p (MdTag.scala:38-98,
+// relative to start) is offset lead + p.  Bits are set over the whole read:
+// the per-base passes only read those of the trimmed range.  The trimming
+// itself is left to the first pass over the quals (kInfoTrim, resolve_info).
 // Returns false for anything else: the read goes to bqsr_prep_complex, which
 // runs prep_one with the full exception order.
 __device__ bool prep_fast(const PrepParams& P, int64_t r) {
@@ -454,20 +484,14 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
   }
   constexpr uint16_t need = BQSR_F_HAS_QUAL | BQSR_F_HAS_RG | BQSR_F_HAS_SEQ | BQSR_F_HAS_CIGAR | BQSR_F_HAS_START |
                             BQSR_F_HAS_REFNAME;
-  if ((f & need) != need || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq < 32 || a.n_cigar == 0 ||
+  if ((f & need) != need || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq == 0 || a.n_cigar == 0 ||
       a.n_cigar > 3)
     return false;
   const bool usable = usable_read(f);
   if (usable && (a.md_len == 0 || a.md_len > 16)) return false;
-  const uint8_t* q = P.rd.qual + m.slot;
-  const int lq = m.lq;
-  const uint4 head = *(const uint4*)q, back = *(const uint4*)(q + lq - 16);
   const uint4 c4 = *(const uint4*)(P.rd.cigar + a.cigar_off);  // the column has 32 B of padding
   const uint4 md4 = usable ? *(const uint4*)(P.rd.md + a.md_off) : make_uint4(0, 0, 0, 0);
-  const int st = first_good(head, 16, false), tail = first_good(back, 16, true);
-  if (st == 16 || tail == 16) return false;
-  const int en = lq - tail;
-  // CIGAR [S]M[S]
+  const int st = 0, en = m.lq;  // bits over the whole read (see above)
   const uint32_t cw[3] = {c4.x, c4.y, c4.z};
   const int nc = a.n_cigar;
   int64_t lead = 0, mlen = 0, trail = 0;
@@ -493,7 +517,7 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
     if (l0 == 0 || (nc > 1 && l1 == 0) || (nc > 2 && l2 == 0)) return false;
   }
   const int64_t rp_len = lead + mlen + trail;
-  if (rp_len < en || (int)m.ls < en) return false;  // CIGAR_SHORT / SEQ_SHORT: prep_one reports them
+  if (rp_len < m.lq || m.ls < m.lq) return false;  // else CIGAR_SHORT / SEQ_SHORT may arise: prep_one decides
   const int64_t start = a.start, unclipped = start - lead;
   // prep_one's Int-range test (the reference does position arithmetic in Int)
   if (unclipped < 0 || unclipped + rp_len + mlen > 2147483647LL) return false;
@@ -548,8 +572,9 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
     }
     mask_sites_linear(P, a.contig, unclipped, st, en, rs);
   }
-  P.info[r] = ReadInfo{(uint16_t)st, (uint16_t)en,
-                       (uint16_t)(kInfoApp | (usable ? kInfoObs : 0) | ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
+  P.info[r] = ReadInfo{0, 0,
+                       (uint16_t)(kInfoTrim | kInfoApp | (usable ? kInfoObs : 0) |
+                                  ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
                                   (((f & BQSR_F_PAIRED) && (f & BQSR_F_SECOND_OF_PAIR)) ? kInfoSecond : 0)),
                        0};
   return true;
@@ -657,6 +682,8 @@ struct LaneRead {
   uint64_t slot;  // first base slot
   int st, en;     // visited offsets [st, en)
   int fl;         // kInfo* bits
+  bool trimmed;   // st / en computed here (kInfoTrim): observe writes the ReadInfo back
+  ReadInfo inf;   // the resolved ReadInfo
   int rg;
   int lq, ls;
   int cell0, dir; // cycle cell of offset o = cell0 + dir * o (DiscreteCycle + L)
@@ -671,6 +698,9 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
     m = rd.meta[r];
     inf = info[r];
   }
+  x.trimmed = inf.fl & kInfoTrim;
+  inf = resolve_info(rd, inf, m.slot, m.lq);
+  x.inf = inf;
   x.slot = m.slot;
   x.fl = inf.fl;
   x.rg = m.rg;
@@ -877,6 +907,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     for (int64_t g0 = p0 + (int64_t)rpw * wave; g0 < p1; g0 += (int64_t)rpw * kWaves) {
       const bool live = g0 + rl < p1;
       const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + rl) : 0, live, L);
+      if (x.trimmed && sub == 0) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
       const bool act = x.fl & (kInfoObs | kInfoObsCheck);
       const bool full = x.fl & kInfoObs;
       const int n = act ? x.en - x.st : 0;
@@ -1202,10 +1233,11 @@ extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(Reads
     int n = 0;
     const uint8_t* qp = rd.qual;
     if (r < r1) {
-      const ReadInfo inf = info[r];
+      const ReadMeta m = rd.meta[r];
+      const ReadInfo inf = resolve_info(rd, info[r], m.slot, m.lq);
       if ((inf.fl & kInfoObs) && inf.en > inf.st) {
         n = inf.en - inf.st;
-        qp = rd.qual + rd.meta[r].slot + inf.st;
+        qp = rd.qual + m.slot + inf.st;
       }
     }
     for (int j0 = kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSuper << ls) {
@@ -1313,10 +1345,11 @@ __device__ int fold_stream(const ReadsDev& rd, const ReadInfo* info, int64_t til
   const int64_t r0 = tile * (int64_t)rd.reads_per_tile;
   const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
   if (tid < nr) {
-    const ReadInfo inf = info[r0 + tid];
+    const ReadMeta m = rd.meta[r0 + tid];
+    const ReadInfo inf = resolve_info(rd, info[r0 + tid], m.slot, m.lq);
     const bool on = (inf.fl & kInfoObs) && inf.en > inf.st;
     F.lens[tid] = on ? inf.en - inf.st : 0;
-    F.rbase[tid] = rd.meta[r0 + tid].slot + inf.st;
+    F.rbase[tid] = m.slot + inf.st;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1758,7 +1791,7 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, co
     ReadInfo inf{0, 0, 0, 0};
     if (lane < nr) {
       m = rd.meta[r0 + lane];
-      inf = info[r0 + lane];
+      inf = resolve_info(rd, info[r0 + lane], m.slot, m.lq);
     }
     const uint64_t ts0 = __shfl(m.slot, 0);
     const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
