@@ -23,6 +23,7 @@ using namespace bqsr;
 
 // the kernels are compiled in this translation unit (one HIP module)
 #include "bqsr_kernels.hip"
+#include "bqsr_fold.hip"
 
 // ------------------------------------------------------------- errors -----
 
@@ -260,13 +261,8 @@ struct bqsr_batch {
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
   // per-call scratch
-  uint16_t* d_h2 = nullptr;
-  uint32_t* d_hq = nullptr;
-  uint8_t* d_cand = nullptr;       // [n_blocks] fold candidates
-  double* d_dblk = nullptr;        // FoldParams::dblk / dtile / elo
-  double* d_dtile = nullptr;
-  int16_t* d_elo = nullptr;
-  int32_t* d_cand_list = nullptr;  // [n_blocks + 1]: list, then count
+  uint32_t* d_hq = nullptr;        // [n_blocks][128] fold blocks' qual histograms
+  FoldParams fold{};               // the fold's device buffers (FoldParams)
   uint32_t* d_part = nullptr;      // per-block window counts
   size_t part_words = 0;
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
@@ -368,6 +364,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_fold_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain_lds());
   if (e != hipSuccess) {
     bqsr_context_destroy(c);
     return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
@@ -471,13 +469,21 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   b->rd.n_tiles = (n + b->rd.reads_per_tile - 1) / b->rd.reads_per_tile;
   b->n_blocks = std::min(b->ctx->n_cu, kMaxFoldBlocks);
   bqsr_status st;
-  if ((st = dalloc(b->allocs, &b->d_h2, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kQBins)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_hq, (size_t)b->n_blocks * kQBins)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_cand, (size_t)b->n_blocks)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_dblk, (size_t)b->n_blocks * kFoldE)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_elo, (size_t)b->n_blocks)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_dtile, (size_t)std::max<int64_t>(1, b->rd.n_tiles) * kFoldE)) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_cand_list, (size_t)b->n_blocks + 1)) != BQSR_OK) return st;
+  {  // the fold's buffers (bqsr_fold.hip)
+    FoldParams& F = b->fold;
+    const size_t nt = (size_t)std::max<int64_t>(1, b->rd.n_tiles), nbk = (size_t)b->n_blocks;
+    F.stream_cap = std::max<int64_t>(1 << 20, std::min<int64_t>(16 << 20, b->rd.n_slots));
+    if ((st = dalloc(b->allocs, &F.blk, nbk)) != BQSR_OK || (st = dalloc(b->allocs, &F.cand_list, nbk)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.n_cand, 1)) != BQSR_OK || (st = dalloc(b->allocs, &F.delta, 1)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.rtile, nt)) != BQSR_OK || (st = dalloc(b->allocs, &F.ntile, nt)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.dtile, nt * kFoldE)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.seg, nbk * kFoldMaxSegs)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.nseg, nbk)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.streams, (size_t)F.stream_cap + 64)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.stream_used, 1)) != BQSR_OK)
+      return st;
+  }
   if ((st = dalloc(b->allocs, &b->d_err, kErrWords)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_info, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
   b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
@@ -1063,28 +1069,18 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
                          b->n_blocks, lane_shift(b), b->d_hq);
       HIP_TRY(hipGetLastError());
     }
-    int32_t* n_cand = b->d_cand_list + b->n_blocks;
-    hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(256), 0, s, (const uint32_t*)b->d_hq, (const double*)ctx->d_pow10,
-                       b->n_blocks, b->d_cand, b->d_cand_list, n_cand, b->d_dblk, b->d_elo);
-    HIP_TRY(hipGetLastError());
-    const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
-    hipLaunchKernelGGL(bqsr_tile_hist, dim3(ctx->n_cu * 4), dim3(256), 0, s, b->rd, (const ReadInfo*)b->d_info,
-                       (const int32_t*)b->d_cand_list, (const int32_t*)n_cand, b->n_blocks, max_tpb, b->d_h2,
-                       (const int16_t*)b->d_elo, (const double*)ctx->d_pow10, b->d_dtile);
-    HIP_TRY(hipGetLastError());
-    FoldParams F{};
+    FoldParams F = b->fold;
     F.rd = b->rd;
     F.info = b->d_info;
     F.hq_block = b->d_hq;
-    F.h2 = b->d_h2;
-    F.cand = b->d_cand;
-    F.dblk = b->d_dblk;
-    F.dtile = b->d_dtile;
-    F.elo = b->d_elo;
     F.pow10 = ctx->d_pow10;
     F.n_blocks = b->n_blocks;
     F.em_out = b->d_em;
-    hipLaunchKernelGGL(bqsr_fold_kernel, dim3(1), dim3(1024), 0, s, F);
+    hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(1024), 0, s, F);
+    const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
+    hipLaunchKernelGGL(bqsr_fold_tiles, dim3(ctx->n_cu * 4), dim3(kFtWaves * 64), 0, s, F, max_tpb);
+    hipLaunchKernelGGL(bqsr_fold_segs, dim3(b->n_blocks), dim3(1024), 0, s, F);
+    hipLaunchKernelGGL(bqsr_fold_chain, dim3(1), dim3(1024), chain_lds(), s, F);
     HIP_TRY(hipGetLastError());
   }
   return ok();

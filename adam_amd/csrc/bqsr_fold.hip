@@ -1,0 +1,654 @@
+// bqsr_fold.hip -- the partition's expectedMismatch, replayed exactly.
+//
+// The reference folds expectedMismatch += pow10cache[q] sequentially over the
+// partition's folded bases (every trimmed base of every usable read, masked
+// ones included: RecalTable.scala:61), and the low bits of
+// that double decide Q59 vs Q60 in apply: the fold is replayed
+// bit for bit, not approximated.
+//
+// While the running sum S stays inside one binade [2^e, 2^(e+1)),
+//   fl(S + t) = S + u * round(t / u),   u = 2^(e - 52),
+// unless t / u is exactly a half-integer (a tie: the result then depends on
+// the parity of S / u).  So a run of additions inside a binade is an exact
+// integer sum of per-qual increments, and only the additions that leave the
+// binade (about log2 of the sum's growth: ~22 for 1e9 bases), the ties, and
+// the first ones while S < 1/16 (the binade changes every few additions) are
+// performed one at a time in double arithmetic, as the JVM performs them.
+//
+// Where can an event be?  The exact S_k stays within a relative
+// k * 2^-53 of the real sum R_k (each rounding error is at most half an ulp of
+// a partial sum <= S_k), so the real sum, widened by
+// delta = (N + 64) * 2^-52, bounds S everywhere.  The work is split so that
+// everything but a short chain of dependent steps runs across the GPU:
+//
+//   bqsr_fold_plan    1 workgroup: per fold block (one observe workgroup's
+//                     reads) the real sum and count from the block's qual
+//                     histogram, their prefix, and either "no event in this
+//                     block" (then the block's exact increment at its binade)
+//                     or "candidate";
+//   bqsr_fold_tiles   candidate blocks' tiles (<= 64 reads) across the GPU,
+//                     one wavefront each: real sum, count, and the exact
+//                     increment at the four binades the block may be in;
+//   bqsr_fold_segs    one workgroup per candidate block: the tiles' real
+//                     prefix, then runs of tiles that surely stay in one
+//                     binade (their summed increment) and the tiles that may
+//                     hold an event, whose quals are copied, in fold order,
+//                     into a compact stream;
+//   bqsr_fold_chain   one workgroup: prefetches blocks, segments and streams
+//                     into LDS, then one wavefront walks the job in order:
+//                     whole blocks and runs by one integer addition each,
+//                     event streams by a wavefront-parallel search for the
+//                     next binade crossing or tie and one IEEE addition there.
+//
+// Every shortcut is verified where it is taken (S in the expected binade, no
+// crossing): should a bound ever fail, the chain folds those tiles element by
+// element from the read columns instead.  The result is exact either way.
+
+namespace bqsr {
+
+constexpr double kFoldSeqLimit = 0.0625;  // below, binade mode is not worth it: sequential
+constexpr double kTwo53 = 9007199254740992.0;
+constexpr int kChainLdsSegs = 384;         // segments prefetched into the chain's LDS
+constexpr int kChainLdsStream = 104 * 1024;  // stream bytes prefetched into the chain's LDS
+constexpr size_t chain_lds() {
+  return (size_t)kMaxFoldBlocks * sizeof(FoldBlock) + (size_t)kChainLdsSegs * sizeof(FoldSeg) + kChainLdsStream;
+}
+
+// 2^k as a double from its exponent bits (k in the normal range)
+__device__ __forceinline__ double pow2i(int k) { return __longlong_as_double((long long)(1023 + k) << 52); }
+
+// round(t / u) at binade e and whether it is a tie; t / u = t * 2^(52 - e) is exact
+__device__ __forceinline__ double fold_inc(double t, int e, bool* tie) {
+  const double x = t * pow2i(52 - e);
+  const double r = rint(x);  // round half to even, as the IEEE addition does
+  *tie = (x - floor(x)) == 0.5;
+  return r;
+}
+// the lowest binade a unit starting at real partial sum lo can be in
+__device__ __forceinline__ int fold_elo(double lo) { return lo >= 0x1p-60 ? ilogb(lo) : -60; }
+
+// ---------------------------------------------------------------- plan ----
+// One workgroup of 1024 threads (n_blocks <= kMaxFoldBlocks): per block the
+// real sum and count (4 threads x 32 histogram bins), their prefix in block
+// order, the classification, the increment of each event-free block at its
+// binade, and the candidate list in block order.
+extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) {
+  __shared__ double t[kQBins];
+  __shared__ double sre[kMaxFoldBlocks];
+  __shared__ int64_t scn[kMaxFoldBlocks];
+  __shared__ double pre[kMaxFoldBlocks];
+  __shared__ int32_t cnd[kMaxFoldBlocks];
+  __shared__ double wsum[16];
+  __shared__ int64_t wcnt[16];
+  __shared__ int32_t wc[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int q = tid; q < kQBins; q += 1024) t[q] = P.pow10[q];
+  __syncthreads();
+  const int nb = P.n_blocks;
+  // (1) per block: real sum and count
+  for (int b0 = 0; b0 < nb; b0 += 256) {
+    const int b = b0 + (tid >> 2), part = tid & 3;
+    double re = 0.0;
+    int64_t n = 0;
+    if (b < nb) {
+      const uint4* row = (const uint4*)(P.hq_block + (int64_t)b * kQBins + part * 32);
+      uint4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = row[i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t h[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          re += (double)h[j] * t[part * 32 + i * 4 + j];
+          n += h[j];
+        }
+      }
+    }
+    re += __shfl_xor(re, 1);
+    re += __shfl_xor(re, 2);
+    n += __shfl_xor(n, 1);
+    n += __shfl_xor(n, 2);
+    if (b < nb && part == 0) {
+      sre[b] = re;
+      scn[b] = n;
+    }
+  }
+  __syncthreads();
+  // (2) exclusive prefix of the real sums in block order (thread = block)
+  {
+    const double v0 = tid < nb ? sre[tid] : 0.0;
+    const int64_t c0 = tid < nb ? scn[tid] : 0;
+    double v = v0;
+    int64_t c = c0;
+    for (int off = 1; off < 64; off <<= 1) {
+      const double x = __shfl_up(v, off);
+      const int64_t y = __shfl_up(c, off);
+      if (lane >= off) {
+        v += x;
+        c += y;
+      }
+    }
+    if (lane == 63) {
+      wsum[wave] = v;
+      wcnt[wave] = c;
+    }
+    __syncthreads();
+    double base = 0.0;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    if (tid < nb) pre[tid] = base + (v - v0);
+  }
+  double total_n = 0.0;
+  for (int w = 0; w < 16; ++w) total_n += (double)wcnt[w];
+  const double delta = (total_n + 64.0) * 0x1p-52 + 1e-12;
+  __syncthreads();
+  // (3) classify, 4 threads per block: a block holds no event if its widened
+  // real span lies in one binade at or above kFoldSeqLimit and no present
+  // qual ties there; then its exact increment at that binade
+  for (int b0 = 0; b0 < nb; b0 += 256) {
+    const int b = b0 + (tid >> 2), part = tid & 3;
+    const bool live = b < nb && scn[min(b, nb - 1)] > 0;
+    const double R0 = b < nb ? pre[b] : 0.0, R1 = b < nb ? pre[b] + sre[b] : 0.0;
+    const double lo = R0 * (1.0 - delta), hi = R1 * (1.0 + delta);
+    bool cand = live && (lo < kFoldSeqLimit * (1.0 + delta) || ilogb(lo) != ilogb(hi));
+    const int e = (live && !cand) ? ilogb(lo) : 0;
+    double inc = 0.0;
+    bool tie = false;
+    if (live && !cand) {
+      const uint32_t* row = P.hq_block + (int64_t)b * kQBins + part * 32;
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t h = row[i];
+        bool tq;
+        const double d = fold_inc(t[part * 32 + i], e, &tq);
+        if (h) {
+          inc += (double)h * d;
+          tie |= tq;
+        }
+      }
+    }
+    inc += __shfl_xor(inc, 1);
+    inc += __shfl_xor(inc, 2);
+    tie |= __shfl_xor((int)tie, 1) != 0;
+    tie |= __shfl_xor((int)tie, 2) != 0;
+    if (live && !cand && (tie || !(inc < 0x1p52))) cand = true;  // below 2^52 every partial sum was exact
+    if (b < nb && part == 0) {
+      cnd[b] = cand;
+      if (!live) P.blk[b] = FoldBlock{R0, 0.0, kFoldNoBase, -1};
+      else if (!cand) P.blk[b] = FoldBlock{R0, inc, e, -1};
+      else P.blk[b] = FoldBlock{R0, 0.0, fold_elo(lo), 0};  // cidx set below
+    }
+  }
+  __syncthreads();
+  // (4) candidate list in block order (thread = block)
+  const int cand = tid < nb ? cnd[tid] : 0;
+  const uint64_t m = __builtin_amdgcn_ballot_w64(cand != 0);
+  if (lane == 0) wc[wave] = __popcll(m);
+  __syncthreads();
+  int cb = 0, ctot = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wave) cb += wc[w];
+    ctot += wc[w];
+  }
+  if (cand) {
+    const int ci = cb + __popcll(m & ((1ull << lane) - 1ull));
+    P.cand_list[ci] = tid;
+    P.blk[tid].cidx = ci;
+  }
+  if (tid == 0) {
+    *P.n_cand = ctot;
+    *P.delta = delta;
+    *P.stream_used = 0ull;
+  }
+}
+
+// ----------------------------------------------------------- tile sums ----
+// Candidate blocks' tiles, one wavefront each: the folded bases (usable
+// valid reads, trimmed ranges) become an LDS slot bitmap, then every folded
+// slot adds its qual's real value and its increments at the block's four
+// binades elo .. elo + 3 (per-wavefront tables, rebuilt when the block changes).
+constexpr int kFtWaves = 4;
+extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(FoldParams P, int64_t max_tpb) {
+  __shared__ double t[kQBins];
+  __shared__ double inc[kFtWaves][kFoldE][kQBins];
+  __shared__ uint8_t tiem[kFtWaves][kQBins];
+  __shared__ uint32_t bm[kFtWaves][kTileSlots / 32];
+  for (int q = threadIdx.x; q < kQBins; q += blockDim.x) t[q] = P.pow10[q];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const ReadsDev& rd = P.rd;
+  const int64_t nt = rd.n_tiles;
+  const int64_t total = (int64_t)(*P.n_cand) * max_tpb;
+  int cur_elo = -100000;
+  for (int64_t v = (int64_t)blockIdx.x * kFtWaves + wv; v < total; v += (int64_t)gridDim.x * kFtWaves) {
+    const int64_t b = P.cand_list[v / max_tpb];
+    const int64_t tl = nt * b / P.n_blocks + v % max_tpb;
+    if (tl >= nt * (b + 1) / P.n_blocks) continue;
+    const int elo = P.blk[b].e;
+    if (elo != cur_elo) {  // this block's increment tables
+      for (int q = lane; q < kQBins; q += 64) {
+        uint8_t tm = 0;
+        for (int k = 0; k < kFoldE; ++k) {
+          bool tq;
+          inc[wv][k][q] = fold_inc(t[q], elo + k, &tq);
+          tm |= (uint8_t)(tq << k);
+        }
+        tiem[wv][q] = tm;
+      }
+      cur_elo = elo;
+    }
+    const int64_t r0 = tl * (int64_t)rd.reads_per_tile;
+    const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
+    ReadMeta m{0, 0, 0, 0, 0};
+    ReadInfo inf{0, 0, 0, 0};
+    if (lane < nr) {
+      m = rd.meta[r0 + lane];
+      inf = resolve_info(rd, P.info[r0 + lane], m.slot, m.lq);
+    }
+    const uint64_t ts0 = __shfl(m.slot, 0);
+    const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
+    for (int i = lane; i < kTileSlots / 32; i += 64) bm[wv][i] = 0;
+    wave_sync();
+    if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
+      int lo = (int)(m.slot - ts0) + inf.st;
+      const int hi = (int)(m.slot - ts0) + inf.en;
+      while (lo < hi) {
+        const int n = min(32 - (lo & 31), hi - lo);
+        atomicOr(&bm[wv][lo >> 5], (n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (lo & 31));
+        lo += n;
+      }
+    }
+    wave_sync();
+    double re = 0.0, d[kFoldE] = {0.0, 0.0, 0.0, 0.0};
+    uint32_t cnt = 0, tm = 0;
+    const uint8_t* qt = rd.qual + ts0;
+    for (int s0 = lane * 4; s0 < nslots; s0 += 256) {  // 4 slots per lane and step
+      const uint32_t qw4 = *(const uint32_t*)(qt + s0);  // (the qual column has 32 B of padding)
+      const uint32_t bits = (bm[wv][s0 >> 5] >> (s0 & 31)) & 0xFu;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (((bits >> k) & 1u) && s0 + k < nslots) {
+          const int q = (int)((qw4 >> (8 * k)) & 0x7Fu);  // folded quals are 0..127 (q < 0 fails observe)
+          re += t[q];
+          ++cnt;
+          tm |= tiem[wv][q];
+#pragma unroll
+          for (int e = 0; e < kFoldE; ++e) d[e] = fmin(d[e] + inc[wv][e][q], 0x1p53);  // saturating: exact below
+        }
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      re += __shfl_xor(re, off);
+      cnt += __shfl_xor(cnt, off);
+      tm |= __shfl_xor(tm, off);
+#pragma unroll
+      for (int e = 0; e < kFoldE; ++e) d[e] = fmin(d[e] + __shfl_xor(d[e], off), 0x1p53);
+    }
+    if (lane == 0) {
+      P.rtile[tl] = re;
+      P.ntile[tl] = (int32_t)cnt;
+#pragma unroll
+      for (int e = 0; e < kFoldE; ++e)
+        P.dtile[tl * kFoldE + e] = ((tm >> e) & 1u) ? kFoldTie : (d[e] < 0x1p52 ? d[e] : kFoldUnknown);
+    }
+    wave_sync();
+  }
+}
+
+// ------------------------------------------------------------ segments ----
+// One workgroup per candidate block (blockIdx.x < n_cand).  Tiles in chunks
+// of 1024 (one per thread), carried across chunks: the real prefix, the
+// current segment, its summed increment and the stream offsets.
+
+// copy the folded quals of tile tl, in fold order, to dst (one wavefront)
+__device__ void fold_copy_tile(const FoldParams& P, int64_t tl, uint8_t* dst, int lane) {
+  const ReadsDev& rd = P.rd;
+  const int64_t r0 = tl * (int64_t)rd.reads_per_tile;
+  const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
+  int len = 0;
+  uint64_t src = 0;
+  if (lane < nr) {
+    const ReadMeta m = rd.meta[r0 + lane];
+    const ReadInfo inf = resolve_info(rd, P.info[r0 + lane], m.slot, m.lq);
+    if ((inf.fl & kInfoObs) && inf.en > inf.st) {
+      len = inf.en - inf.st;
+      src = m.slot + inf.st;
+    }
+  }
+  int pre = len;  // inclusive prefix over the tile's reads
+  for (int off = 1; off < 64; off <<= 1) {
+    const int x = __shfl_up(pre, off);
+    if (lane >= off) pre += x;
+  }
+  uint8_t* d = dst + (pre - len);
+  for (int i = 0; i < len; ++i) d[i] = rd.qual[src + i];
+}
+
+extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) {
+  const int c = blockIdx.x;
+  if (c >= *P.n_cand) return;
+  __shared__ double wsum[16];
+  __shared__ int32_t wcount[16];
+  __shared__ int32_t keys[1024];
+  __shared__ unsigned long long s_inc[kFoldMaxSegs];
+  __shared__ int32_t s_n[kFoldMaxSegs], s_t0[kFoldMaxSegs], s_t1[kFoldMaxSegs], s_key[kFoldMaxSegs];
+  __shared__ int32_t carry_sid, carry_key;
+  __shared__ double carry_r;
+  __shared__ int32_t ev_tile[1024], ev_pos[1024];
+  __shared__ int32_t n_ev;
+  __shared__ FoldSeg out[kFoldMaxSegs];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = P.cand_list[c];
+  const FoldBlock B = P.blk[b];
+  const double delta = *P.delta;
+  const int64_t nt = P.rd.n_tiles;
+  const int64_t c0 = nt * b / P.n_blocks, c1 = nt * (b + 1) / P.n_blocks;
+  constexpr int kEvent = INT32_MIN + 1;  // the key of tiles that may hold an event
+  constexpr int kLast = kFoldMaxSegs - 1;  // segment index absorbing any overflow (folded from the columns)
+  if (tid < kFoldMaxSegs) {
+    s_inc[tid] = 0;
+    s_n[tid] = 0;
+    s_t0[tid] = INT32_MAX;
+    s_t1[tid] = -1;
+    s_key[tid] = kEvent;
+  }
+  if (tid == 0) {
+    carry_sid = -1;
+    carry_key = INT32_MIN;
+    carry_r = B.r0;
+  }
+  __syncthreads();
+  for (int64_t k0 = c0; k0 < c1; k0 += 1024) {
+    const int64_t tl = k0 + tid;
+    const bool live = tl < c1;
+    const double re = live ? P.rtile[tl] : 0.0;
+    const int32_t cnt = live ? P.ntile[tl] : 0;
+    // real prefix at the tile's start and end
+    double v = re;
+    for (int off = 1; off < 64; off <<= 1) {
+      const double x = __shfl_up(v, off);
+      if (lane >= off) v += x;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    double base = carry_r;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    const double Rt = base + (v - re), Re = base + v;
+    // a tile that surely stays in binade e >= kFoldSeqLimit, with a tabulated,
+    // tie-free increment there, has key e; any other has key kEvent
+    int key = kEvent;
+    int64_t inc = 0;
+    if (live) {
+      const double lo = Rt * (1.0 - delta), hi = Re * (1.0 + delta);
+      if (lo >= kFoldSeqLimit * (1.0 + delta) && ilogb(lo) == ilogb(hi)) {
+        const int e = ilogb(lo), kk = e - B.e;
+        const double d = (kk >= 0 && kk < kFoldE) ? P.dtile[tl * kFoldE + kk] : kFoldUnknown;
+        if (d >= 0.0) {
+          key = e;
+          inc = (int64_t)d;
+        }
+      }
+    }
+    keys[tid] = live ? key : INT32_MIN;
+    __syncthreads();
+    // a segment starts where the key changes (event tiles of a run form one segment)
+    const int prev = tid > 0 ? keys[tid - 1] : carry_key;
+    const bool start = live && key != prev;
+    const uint64_t sm = __builtin_amdgcn_ballot_w64(start);
+    if (lane == 0) wcount[wave] = __popcll(sm);
+    __syncthreads();
+    int sid = carry_sid;
+    for (int w = 0; w < wave; ++w) sid += wcount[w];
+    sid += __popcll(sm & ((2ull << lane) - 1ull));  // inclusive: this tile's segment
+    if (live) {
+      const int s = min(sid, kLast);
+      atomicMin(&s_t0[s], (int32_t)tl);
+      atomicMax(&s_t1[s], (int32_t)tl);
+      if (sid >= kLast) {
+        s_key[kLast] = INT32_MAX;  // overflow: folded from the read columns
+      } else {
+        if (start) s_key[s] = key;
+        if (key == kEvent) atomicAdd(&s_n[s], cnt);
+        else atomicAdd(&s_inc[s], (unsigned long long)inc);
+      }
+    }
+    __syncthreads();
+    const int last = (int)(min(c1, k0 + 1024) - k0) - 1;  // the chunk's last tile
+    if (tid == last) {
+      carry_sid = sid;
+      carry_key = key;
+      carry_r = Re;
+    }
+    __syncthreads();
+  }
+  const int ns = min(carry_sid + 1, kFoldMaxSegs);
+  // the segments; event segments get their stream space
+  if (tid < ns) {
+    FoldSeg g;
+    g.t0 = s_t0[tid];
+    g.t1 = s_t1[tid];
+    g.e = 0;
+    g.off = 0;
+    const int key = s_key[tid];
+    if (key == INT32_MAX) {
+      g.kind = kSegGlobal;
+      g.inc = 0;
+    } else if (key == kEvent) {
+      g.kind = kSegEvent;
+      g.inc = s_n[tid];  // element count
+      const unsigned long long o = atomicAdd(P.stream_used, (unsigned long long)s_n[tid]);
+      if (o + (unsigned long long)s_n[tid] <= (unsigned long long)P.stream_cap) g.off = (int64_t)o;
+      else g.kind = kSegGlobal;  // no stream room: folded from the read columns
+    } else {
+      g.kind = kSegRun;
+      g.e = key;
+      g.inc = (int64_t)s_inc[tid];
+    }
+    out[tid] = g;
+    P.seg[(int64_t)c * kFoldMaxSegs + tid] = g;
+  }
+  if (tid == 0) P.nseg[c] = ns;
+  __syncthreads();
+  // copy the event segments' tiles, one wavefront per tile, each at its
+  // element offset in its segment's stream
+  for (int s = 0; s < ns; ++s) {
+    const FoldSeg g = out[s];
+    if (g.kind != kSegEvent) continue;
+    for (int64_t k0 = g.t0; k0 <= g.t1; k0 += 1024) {
+      if (tid == 0) {
+        int64_t acc = 0;
+        for (int64_t tl = g.t0; tl < k0; ++tl) acc += P.ntile[tl];
+        int k = 0;
+        for (int64_t tl = k0; tl <= g.t1 && k < 1024; ++tl, ++k) {
+          ev_tile[k] = (int32_t)tl;
+          ev_pos[k] = (int32_t)acc;
+          acc += P.ntile[tl];
+        }
+        n_ev = k;
+      }
+      __syncthreads();
+      for (int k = wave; k < n_ev; k += 16) fold_copy_tile(P, ev_tile[k], P.streams + g.off + ev_pos[k], lane);
+      __syncthreads();
+    }
+  }
+}
+
+// --------------------------------------------------------------- chain ----
+
+// Fold elements [0, n) of `q` (LDS or global bytes) into S exactly, one
+// wavefront.  inc / tie: LDS tables of the current binade cur_e.
+__device__ double wave_fold(double S, const uint8_t* q, int64_t n, const double* t, double* inc, uint8_t* tie,
+                            int& cur_e, int lane) {
+  int64_t pos = 0;
+  while (pos < n) {
+    if (S < kFoldSeqLimit) {
+      // small S: the binade changes every few additions -- lane 0 adds in order
+      int64_t p = pos;
+      double s = S;
+      if (lane == 0) {
+        while (p < n && s < kFoldSeqLimit) {
+          s = s + t[q[p]];
+          ++p;
+        }
+      }
+      S = __shfl(s, 0);
+      pos = __shfl(p, 0);
+      continue;
+    }
+    const int e = ilogb(S);
+    if (e != cur_e) {
+      for (int k = lane; k < kQBins; k += 64) {
+        bool tq;
+        inc[k] = fold_inc(t[k], e, &tq);
+        tie[k] = tq;
+      }
+      cur_e = e;
+      wave_sync();
+    }
+    const double N0 = S * pow2i(52 - e);  // S / u, an integer < 2^53
+    const double head = kTwo53 - N0;     // increments left before the binade ends
+    // lane l takes elements [pos + 64 l, pos + 64 l + 64)
+    const int64_t a = pos + 64 * (int64_t)lane, bnd = min(a + 64, n);
+    double sum = 0.0;
+    bool th = false;
+    for (int64_t k = a; k < bnd; ++k) {
+      const int qq = q[k];
+      sum = fmin(sum + inc[qq], 0x1p53);  // saturating: exact while it matters
+      th |= tie[qq] != 0;
+    }
+    double incl = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+      const double x = __shfl_up(incl, off);
+      if (lane >= off) incl = fmin(incl + x, 0x1p54);
+    }
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(a < bnd && (incl >= head || th));
+    if (!hit) {  // the whole window stays in the binade
+      const double tot = __shfl(incl, 63);
+      S = (N0 + tot) * pow2i(e - 52);
+      pos = min(n, pos + 64 * 64);
+      continue;
+    }
+    const int L = (int)__builtin_ctzll(hit);
+    const double excl = L > 0 ? __shfl(incl, L - 1) : 0.0;  // < head: exact
+    const int64_t aL = pos + 64 * (int64_t)L, bL = min(aL + 64, n);
+    int64_t p = bL;
+    double s = 0.0;
+    if (lane == 0) {  // the first event inside lane L's elements
+      double N = N0 + excl;
+      bool found = false;
+      for (int64_t k = aL; k < bL; ++k) {
+        const int qq = q[k];
+        if (tie[qq] || N + inc[qq] >= kTwo53) {
+          s = N * pow2i(e - 52) + t[qq];  // the exact IEEE addition the JVM performs
+          p = k + 1;
+          found = true;
+          break;
+        }
+        N += inc[qq];
+      }
+      if (!found) s = N * pow2i(e - 52);  // (cannot happen: the lane's sum signalled an event)
+    }
+    S = __shfl(s, 0);
+    pos = __shfl(p, 0);
+  }
+  return S;
+}
+
+// one tile's folded quals into LDS scratch (the fallback path), then fold
+__device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, uint8_t* scratch, const double* t,
+                                   double* inc, uint8_t* tie, int& cur_e, int lane) {
+  const ReadsDev& rd = P.rd;
+  const int64_t r0 = tl * (int64_t)rd.reads_per_tile;
+  const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
+  int len = 0;
+  if (lane < nr) {
+    const ReadMeta m = rd.meta[r0 + lane];
+    const ReadInfo inf = resolve_info(rd, P.info[r0 + lane], m.slot, m.lq);
+    if ((inf.fl & kInfoObs) && inf.en > inf.st) len = inf.en - inf.st;
+  }
+  int tot = len;
+  for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
+  fold_copy_tile(P, tl, scratch, lane);
+  wave_sync();
+  return wave_fold(S, scratch, tot, t, inc, tie, cur_e, lane);
+}
+
+extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P) {
+  extern __shared__ __align__(16) unsigned char chain_smem[];
+  __shared__ double t[kQBins];
+  __shared__ double inc[kQBins];
+  __shared__ uint8_t tie[kQBins];
+  __shared__ uint8_t scratch[kTileSlots];
+  __shared__ int32_t nseg_l[kMaxFoldBlocks];
+  FoldBlock* blk = (FoldBlock*)chain_smem;                    // [n_blocks]
+  FoldSeg* segs = (FoldSeg*)(blk + kMaxFoldBlocks);           // [kChainLdsSegs]
+  uint8_t* streams = (uint8_t*)(segs + kChainLdsSegs);        // [kChainLdsStream]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int nb = P.n_blocks, nc = *P.n_cand;
+  const int64_t used = (int64_t)*P.stream_used;
+  const int64_t sl = min(used, (int64_t)kChainLdsStream);
+  const int nsl = min(nc * kFoldMaxSegs, kChainLdsSegs);
+  // prefetch: every thread issues its loads before any is used
+  for (int q = tid; q < kQBins; q += 1024) t[q] = P.pow10[q];
+  for (int i = tid; i < nc; i += 1024) nseg_l[i] = P.nseg[i];
+  {
+    const uint64_t* src = (const uint64_t*)P.blk;
+    uint64_t* dst = (uint64_t*)blk;
+    const int nw = nb * (int)(sizeof(FoldBlock) / 8);
+    for (int i = tid; i < nw; i += 1024) dst[i] = src[i];
+    const uint64_t* ss = (const uint64_t*)P.seg;
+    uint64_t* sd = (uint64_t*)segs;
+    const int sw = nsl * (int)(sizeof(FoldSeg) / 8);
+    for (int i = tid; i < sw; i += 1024) sd[i] = ss[i];
+    const uint4* s4 = (const uint4*)P.streams;
+    uint4* d4 = (uint4*)streams;
+    const int64_t n16 = (sl + 15) / 16;
+#pragma unroll 4
+    for (int64_t i = tid; i < n16; i += 1024) d4[i] = s4[i];
+  }
+  __syncthreads();
+  if (tid >= 64) return;  // one wavefront walks the job
+  double S = 0.0;
+  int cur_e = INT32_MIN;
+  const int64_t nt = P.rd.n_tiles;
+  for (int b = 0; b < nb; ++b) {
+    const FoldBlock B = blk[b];
+    if (B.cidx < 0) {  // no event expected: one integer addition
+      if (B.e == kFoldNoBase) continue;
+      if (S >= kFoldSeqLimit && ilogb(S) == B.e) {
+        const double N0 = S * pow2i(52 - B.e);
+        if (N0 + B.inc < kTwo53) {
+          S = (N0 + B.inc) * pow2i(B.e - 52);
+          continue;
+        }
+      }
+      // the bound failed (not expected): fold the block's tiles element by element
+      for (int64_t tl = nt * b / nb; tl < nt * (b + 1) / nb; ++tl)
+        S = fold_tile_global(P, S, tl, scratch, t, inc, tie, cur_e, lane);
+      continue;
+    }
+    const int c = B.cidx;
+    const int ns = nseg_l[c];
+    for (int s = 0; s < ns; ++s) {
+      const int64_t si = (int64_t)c * kFoldMaxSegs + s;
+      const FoldSeg G = si < nsl ? segs[si] : P.seg[si];
+      if (G.kind == kSegRun) {
+        if (S >= kFoldSeqLimit && ilogb(S) == G.e) {
+          const double N0 = S * pow2i(52 - G.e);
+          if (N0 + (double)G.inc < kTwo53) {
+            S = (N0 + (double)G.inc) * pow2i(G.e - 52);
+            continue;
+          }
+        }
+      } else if (G.kind == kSegEvent) {
+        const uint8_t* q = G.off + G.inc <= sl ? streams + G.off : P.streams + G.off;
+        S = wave_fold(S, q, G.inc, t, inc, tie, cur_e, lane);
+        continue;
+      }
+      // kSegGlobal, or a run whose bound failed: element by element
+      for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, scratch, t, inc, tie, cur_e, lane);
+    }
+  }
+  if (lane == 0) P.em_out[0] = S;
+}
+
+}  // namespace bqsr

@@ -192,25 +192,51 @@ struct ObserveParams {
   int32_t lane_shift;  // lane-per-chunk kernels: log2(lanes per read)
 };
 
-constexpr int kFoldE = 4;
-constexpr double kFoldTie = -1.0, kFoldUnknown = -2.0;
+// ---- expectedMismatch fold (bqsr_fold.hip) ----
+constexpr int kFoldE = 4;  // binades a candidate block's tiles are tabulated at: elo .. elo + 3
+constexpr double kFoldTie = -1.0, kFoldUnknown = -2.0;  // increment sentinels: a tie / not exact
+constexpr int32_t kFoldNoBase = INT32_MIN;              // FoldBlock::e of a block without folded bases
+constexpr int kFoldMaxSegs = 16;                        // segments per candidate block
+enum : int32_t { kSegRun = 0, kSegEvent = 1, kSegGlobal = 2 };
+
+// per fold block (one observe workgroup's range of tiles), bqsr_fold_plan
+struct FoldBlock {
+  double r0;     // real sum of the folded quals before the block (approximate)
+  double inc;    // event-free block: its exact increment at binade e, in units 2^(e-52)
+  int32_t e;     // event-free: the binade the whole block stays in; candidate: the lowest it may start in
+  int32_t cidx;  // candidate index (bqsr_fold_segs workgroup), -1 when event-free
+};
+static_assert(sizeof(FoldBlock) == 24, "FoldBlock is 3 words");
+
+// a run of tiles of a candidate block, bqsr_fold_segs
+struct FoldSeg {
+  int64_t inc;         // kSegRun: exact increment at binade e; kSegEvent: element count
+  int32_t t0, t1;      // tiles t0 .. t1
+  int32_t e;           // kSegRun: the binade
+  int32_t kind;        // kSegRun / kSegEvent (quals at streams + off) / kSegGlobal (folded from the columns)
+  int64_t off;
+};
+static_assert(sizeof(FoldSeg) == 32, "FoldSeg is 4 words");
+
 struct FoldParams {
   ReadsDev rd;
   const ReadInfo* info;
-  const uint32_t* hq_block;
-  const uint16_t* h2;     // [n_tiles][128] per-tile histograms (candidate blocks only)
-  const uint8_t* cand;    // [n_blocks] bqsr_fold_plan's candidate blocks
-  // increments of a unit (block / candidate block's tile) at binades
-  // e_lo .. e_lo + kFoldE - 1, e_lo = elo[block] (bqsr_fold_plan,
-  // bqsr_tile_hist): the fold's unit scans read one double instead of a
-  // 128-bin histogram row.  kFoldTie: the unit holds a tie at that binade;
-  // kFoldUnknown: not tabulated (scan the row).
-  const double* dblk;     // [n_blocks][kFoldE]
-  const double* dtile;    // [n_tiles][kFoldE] (candidate blocks' tiles)
-  const int16_t* elo;     // [n_blocks]
-  const double* pow10;  // phredToErrorProbabilityCache[0..127]
+  const uint32_t* hq_block;  // [n_blocks][128] qual histograms of the folded bases, read order
+  const double* pow10;       // phredToErrorProbabilityCache[0..127]
   int32_t n_blocks;
-  double* em_out;      // [1]
+  FoldBlock* blk;            // [n_blocks]
+  int32_t* cand_list;        // [n_blocks] candidate blocks in block order
+  int32_t* n_cand;
+  double* delta;             // relative bound of |exact - real| partial sums
+  double* rtile;             // [n_tiles] candidate blocks' tiles: real sum
+  int32_t* ntile;            //           folded bases
+  double* dtile;             //           [kFoldE] increments at elo .. elo + 3 (or a sentinel)
+  FoldSeg* seg;              // [n_blocks][kFoldMaxSegs]
+  int32_t* nseg;             // [n_blocks]
+  uint8_t* streams;          // event segments' quals in fold order
+  int64_t stream_cap;
+  unsigned long long* stream_used;
+  double* em_out;            // [1]
 };
 
 // errorProbabilityToPhred by buckets: p's binade (unbiased exponent

@@ -1263,582 +1263,6 @@ extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(Reads
   }
 }
 
-// ------------------------------------------------------ expectedMismatch --
-//
-// The reference folds expectedMismatch += pow10cache[q] sequentially over the
-// partition (RecalTable.scala:61) and the low bits of that double decide
-// Q59 vs Q60, so the fold is replayed exactly.  While the sum
-// S stays inside one binade [2^e, 2^(e+1)), fl(S + t) = S + u*round(t/u)
-// with u = 2^(e-52) (no ties), so a run of additions is an integer sum of
-// per-qual increments: the per-block and per-tile qual histograms written by
-// the observe kernel give that sum for whole blocks / tiles at once.  Only the
-// additions that leave the binade (about log2(S_end/S_0) of them) or hit a
-// rounding tie are done one by one, in double arithmetic, exactly as the JVM
-// does.  One workgroup of 1024 threads.
-
-constexpr int kFoldThreads = 1024;
-constexpr double kFoldSeqLimit = 0.0625;
-constexpr int kFoldWaves = kFoldThreads / 64;
-
-struct FoldShared {
-  double t[kQBins];     // phredToErrorProbabilityCache
-  double inc[kQBins];   // round(t / u) at the current binade
-  uint8_t tie[kQBins];  // t / u is exactly a half-integer at the current binade
-  double wsum[kFoldWaves];
-  uint8_t stream[kTileSlots];
-  double tv[kTileSlots];  // t[stream[k]]: the sequential fold's operands, one LDS read each
-  int32_t lens[kMaxTileReads + 1];
-  uint64_t rbase[kMaxTileReads];
-  double S;
-  int32_t e;
-  int32_t found;
-  int32_t ntot;
-  double cut_sum;
-#ifdef BQSR_FOLD_PROFILE
-  long long p_stream, p_seq, p_bin, n_bin, n_seq;
-#endif
-};
-
-// (re)derive the binade state of S and the increment table
-__device__ void fold_set_binade(FoldShared& F, int tid, double Sv) {
-  __syncthreads();
-  if (tid == 0) {
-    F.S = Sv;
-    F.e = ilogb(Sv);
-  }
-  __syncthreads();
-  const int e = F.e;
-  for (int q = tid; q < kQBins; q += kFoldThreads) {
-    const double x = ldexp(F.t[q], 52 - e);
-    F.tie[q] = (x - floor(x)) == 0.5;
-    F.inc[q] = rint(x);
-  }
-  __syncthreads();
-}
-
-// block-wide inclusive scan of doubles (exact for integer values < 2^53)
-__device__ double block_scan(FoldShared& F, int tid, double v) {
-  const int lane = tid & 63, wave = tid >> 6;
-  for (int off = 1; off < 64; off <<= 1) {
-    const double x = __shfl_up(v, off);
-    if (lane >= off) v += x;
-  }
-  if (lane == 63) F.wsum[wave] = v;
-  __syncthreads();
-  if (wave == 0) {
-    double w = lane < kFoldWaves ? F.wsum[lane] : 0.0;
-    for (int off = 1; off < kFoldWaves; off <<= 1) {
-      const double x = __shfl_up(w, off);
-      if (lane >= off) w += x;
-    }
-    if (lane < kFoldWaves) F.wsum[lane] = w;
-  }
-  __syncthreads();
-  if (wave > 0) v += F.wsum[wave - 1];
-  __syncthreads();
-  return v;
-}
-
-// Materialise a tile's fold-order qual stream (usable valid reads, trimmed
-// bases) into LDS; returns its length.
-__device__ int fold_stream(const ReadsDev& rd, const ReadInfo* info, int64_t tile, FoldShared& F, int tid) {
-  const int64_t r0 = tile * (int64_t)rd.reads_per_tile;
-  const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
-  if (tid < nr) {
-    const ReadMeta m = rd.meta[r0 + tid];
-    const ReadInfo inf = resolve_info(rd, info[r0 + tid], m.slot, m.lq);
-    const bool on = (inf.fl & kInfoObs) && inf.en > inf.st;
-    F.lens[tid] = on ? inf.en - inf.st : 0;
-    F.rbase[tid] = m.slot + inf.st;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int i = 0; i < nr; ++i) {
-      const int l = F.lens[i];
-      F.lens[i] = acc;
-      acc += l;
-    }
-    F.lens[nr] = acc;
-    F.ntot = acc;
-  }
-  __syncthreads();
-  const int ntot = F.ntot;
-  for (int k = tid; k < ntot; k += kFoldThreads) {  // element k: the last read starting at or before it
-    int lo = 0, hi = nr;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (F.lens[mid] <= k) lo = mid; else hi = mid;
-    }
-    const uint8_t q = rd.qual[F.rbase[lo] + (uint64_t)(k - F.lens[lo])];
-    F.stream[k] = q;
-    F.tv[k] = F.t[q];
-  }
-  __syncthreads();
-  return ntot;
-}
-
-// Fold one tile's stream exactly, starting from F.S.
-__device__ void fold_tile_exact(const ReadsDev& rd, const ReadInfo* info, int64_t tile, FoldShared& F, int tid,
-                                double seq_limit) {
-#ifdef BQSR_FOLD_PROFILE
-  long long c0 = clock64();
-#endif
-  const int n = fold_stream(rd, info, tile, F, tid);
-#ifdef BQSR_FOLD_PROFILE
-  if (tid == 0) F.p_stream += clock64() - c0;
-#endif
-  int pos = 0;
-  while (pos < n) {
-#ifdef BQSR_FOLD_PROFILE
-    c0 = clock64();
-    const bool was_seq = F.S < seq_limit;
-#endif
-    if (F.S < seq_limit) {
-      // small S: the binade changes every few additions -- plain sequential fold
-      if (tid == 0) {
-        // batches of eight operands, the next batch's LDS reads in flight
-        // while the current one is added; the additions stay in stream order
-        // (a sequential fold is exact at any S, seq_limit only decides when
-        // the binade mode takes over)
-        double S = F.S;
-        int p = pos;
-        double a[8], b[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = p + i < n ? F.tv[p + i] : 0.0;
-        while (p < n && S < seq_limit) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) b[i] = p + 8 + i < n ? F.tv[p + 8 + i] : 0.0;
-          const int m = min(8, n - p);
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (i < m) S = S + a[i];
-          p += m;
-          if (p >= n || S >= seq_limit) break;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) a[i] = p + 8 + i < n ? F.tv[p + 8 + i] : 0.0;
-          const int m2 = min(8, n - p);
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (i < m2) S = S + b[i];
-          p += m2;
-        }
-        F.S = S;
-        F.ntot = p;
-      }
-      __syncthreads();
-      pos = F.ntot;
-      if (F.S >= seq_limit) fold_set_binade(F, tid, F.S);
-#ifdef BQSR_FOLD_PROFILE
-      if (tid == 0) {
-        F.p_seq += clock64() - c0;
-        F.n_seq++;
-      }
-#endif
-      continue;
-    }
-    // binade mode: per-thread contiguous runs of the remaining stream
-    const double N0 = ldexp(F.S, 52 - F.e);       // S / u, an integer < 2^53
-    const double head = 9007199254740992.0 - N0;  // increments allowed before leaving the binade
-    const int rem = n - pos;
-    const int per = (rem + kFoldThreads - 1) / kFoldThreads;
-    const int a = pos + tid * per, b = min(a + per, n);
-    double mine = 0.0;
-    bool stop = false;
-    for (int k = a; k < b; ++k) {
-      const int q = F.stream[k];
-      if (F.tie[q]) {
-        stop = true;
-        break;
-      }
-      mine += F.inc[q];
-    }
-    const double incl = block_scan(F, tid, mine);
-    const double excl = incl - mine;
-    if (tid == 0) F.found = 0x7FFFFFFF;
-    __syncthreads();
-    if (a < b && (incl >= head || stop)) {  // the first event is in this run
-      double run = excl;
-      for (int k = a; k < b; ++k) {
-        const int q = F.stream[k];
-        if (F.tie[q] || run + F.inc[q] >= head) {
-          atomicMin(&F.found, k);
-          break;
-        }
-        run += F.inc[q];
-      }
-    }
-    __syncthreads();
-    const int found = F.found;
-    if (found == 0x7FFFFFFF) {
-      // the whole remainder stays in the binade
-      if (tid == kFoldThreads - 1) F.cut_sum = incl;
-      __syncthreads();
-      if (tid == 0) F.S = ldexp(N0 + F.cut_sum, F.e - 52);
-      __syncthreads();
-      break;
-    }
-    // sum of increments strictly before `found`
-    double part = 0.0;
-    for (int k = a; k < min(b, found); ++k) part += F.inc[F.stream[k]];
-    const double tot = block_scan(F, tid, part);
-    if (tid == kFoldThreads - 1) F.cut_sum = tot;
-    __syncthreads();
-    if (tid == 0) {
-      double S = ldexp(N0 + F.cut_sum, F.e - 52);
-      S = S + F.t[F.stream[found]];  // the exact IEEE addition the JVM performs
-      F.S = S;
-    }
-    __syncthreads();
-    pos = found + 1;
-    fold_set_binade(F, tid, F.S);
-#ifdef BQSR_FOLD_PROFILE
-    if (tid == 0) {
-      F.p_bin += clock64() - c0;
-      F.n_bin++;
-    }
-#endif
-  }
-}
-
-// histogram row of a unit: 128 counters as 16-B vectors
-template <class T>
-__device__ __forceinline__ void unit_delta(const T* row, const FoldShared& F, double* d, bool* tie) {
-  constexpr int per = 16 / sizeof(T);   // counters per 16-B vector
-  constexpr int nv = kQBins / per;       // vectors per row
-  constexpr int chunk = 8;               // loads in flight per thread
-  const uint4* v = (const uint4*)row;
-  double acc = 0.0;
-  bool tt = false;
-#pragma unroll
-  for (int i0 = 0; i0 < nv; i0 += chunk) {
-    uint4 buf[chunk];
-#pragma unroll
-    for (int i = 0; i < chunk; ++i) buf[i] = v[i0 + i];
-#pragma unroll
-    for (int i = 0; i < chunk; ++i) {
-      const uint32_t w[4] = {buf[i].x, buf[i].y, buf[i].z, buf[i].w};
-#pragma unroll
-      for (int j = 0; j < per; ++j) {
-        const uint32_t h = (sizeof(T) == 4) ? w[j] : ((w[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu);
-        const int q = (i0 + i) * per + j;
-        if (h) {
-          acc += (double)h * F.inc[q];
-          tt |= F.tie[q] != 0;
-        }
-      }
-    }
-  }
-  *d = acc;
-  *tie = tt;
-}
-
-// Advance over `count` consecutive units (blocks or tiles) while none leaves
-// the binade; returns the index (relative to first) of the first unit that
-// would, or count.
-// dtab[unit][k]: the unit's increment at binade elo + k (FoldParams::dblk);
-// elo is read at elo_p[unit * elo_stride].
-template <class T>
-__device__ int64_t fold_units(FoldShared& F, int tid, const T* rows, int64_t first, int64_t count, const double* dtab,
-                              const int16_t* elo_p, int elo_stride) {
-  int64_t u = 0;
-  while (u < count) {
-    const bool have = (u + tid) < count;
-    double d = 0.0;
-    bool tie = false;
-    if (have) {
-      const int64_t unit = first + u + tid;
-      const int k = F.e - (int)elo_p[(u + tid) * elo_stride];
-      const double v = (k >= 0 && k < kFoldE) ? dtab[unit * kFoldE + k] : kFoldUnknown;
-      if (v >= 0.0) d = v;
-      else if (v == kFoldTie) tie = true;
-      else unit_delta(rows + unit * kQBins, F, &d, &tie);
-    }
-    const double N0 = ldexp(F.S, 52 - F.e);
-    const double head = 9007199254740992.0 - N0;
-    if (d >= head) d = head;  // saturate: it crosses anyway
-    const double incl = block_scan(F, tid, d);
-    if (tid == 0) F.found = 0x7FFFFFFF;
-    __syncthreads();
-    if (have && (tie || incl >= head)) atomicMin(&F.found, tid);
-    __syncthreads();
-    const int found = F.found;
-    const int take = (found == 0x7FFFFFFF) ? (int)min((int64_t)kFoldThreads, count - u) : found;
-    if (take > 0) {  // commit the units before `found`
-      if (tid == take - 1) F.cut_sum = incl;
-      __syncthreads();
-      if (tid == 0) F.S = ldexp(N0 + F.cut_sum, F.e - 52);
-      __syncthreads();
-    }
-    u += take;
-    if (found != 0x7FFFFFFF) return u;
-  }
-  return count;
-}
-
-extern "C" __global__ void __launch_bounds__(kFoldThreads) bqsr_fold_kernel(FoldParams P) {
-  __shared__ FoldShared F;
-  const int tid = threadIdx.x;
-  for (int q = tid; q < kQBins; q += kFoldThreads) F.t[q] = P.pow10[q];
-  if (tid == 0) {
-    F.S = 0.0;
-    F.e = 0;
-#ifdef BQSR_FOLD_PROFILE
-    F.p_stream = F.p_seq = F.p_bin = F.n_bin = F.n_seq = 0;
-#endif
-  }
-  __syncthreads();
-  // Binade mode starts at S >= 1/16 (it is exact for any S > 0 as long as the
-  // sum stays in the binade; below, crossings come every few additions and
-  // the plain sequential fold is cheaper).  Ties are detected and added one
-  // by one.
-  const double seq_limit = kFoldSeqLimit;
-  const int64_t nt = P.rd.n_tiles;
-#ifdef BQSR_FOLD_PROFILE
-  long long tb = 0, tt = 0, te = 0, ne = 0, nbk = 0, ntu = 0, c;
-#define FP_T0 c = clock64();
-#define FP_T1(acc) acc += clock64() - c;
-#else
-#define FP_T0
-#define FP_T1(acc)
-#endif
-  for (int64_t b = 0; b < P.n_blocks; ++b) {
-    if (F.S >= seq_limit) {
-      FP_T0
-      b += fold_units(F, tid, P.hq_block, b, P.n_blocks - b, P.dblk, P.elo + b, 1);  // whole blocks at once
-      FP_T1(tb)
-#ifdef BQSR_FOLD_PROFILE
-      ++nbk;
-#endif
-      if (b >= P.n_blocks) break;
-    }
-    // block b leaves the binade somewhere (or S is still small): tile level
-    const int64_t c0 = nt * b / P.n_blocks, c1 = nt * (b + 1) / P.n_blocks;
-    if (!P.cand[b]) {
-      // bqsr_fold_plan's bound said no event here, so it built no tile
-      // histograms for this block: fold every tile exactly (correct, slow)
-      for (int64_t t = c0; t < c1; ++t) fold_tile_exact(P.rd, P.info, t, F, tid, seq_limit);
-      continue;
-    }
-    int64_t t = c0;
-    while (t < c1) {
-      if (F.S >= seq_limit) {
-        FP_T0
-        t += fold_units(F, tid, P.h2, t, c1 - t, P.dtile, P.elo + b, 0);
-        FP_T1(tt)
-#ifdef BQSR_FOLD_PROFILE
-        ++ntu;
-#endif
-        if (t >= c1) break;
-      }
-      FP_T0
-      fold_tile_exact(P.rd, P.info, t, F, tid, seq_limit);
-      FP_T1(te)
-#ifdef BQSR_FOLD_PROFILE
-      ++ne;
-#endif
-      ++t;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) P.em_out[0] = F.S;
-#ifdef BQSR_FOLD_PROFILE
-  if (tid == 0)
-    printf("FOLDPROF blocks_calls %lld cyc %lld tiles_calls %lld cyc %lld exact_tiles %lld cyc %lld | stream %lld seq %lld "
-           "(%lld) bin %lld (%lld)\n",
-           nbk, tb, ntu, tt, ne, te, F.p_stream, F.p_seq, F.n_seq, F.p_bin, F.n_bin);
-#endif
-}
-
-// Which blocks may hold a fold event (a binade crossing, a rounding tie, or
-// the sequential start S < kFoldSeqLimit)?  The exact fold S_k stays within a
-// relative k * 2^-53 of the real sum R_k of the increments (every rounding
-// error is at most half an ulp of a partial sum <= S_k), so a block whose
-// real-sum span [R_b, R_b+1], widened by delta = (N + 64) * 2^-52, lies inside
-// one binade at or above kFoldSeqLimit and has no tie there holds no event.
-// Only candidate blocks get per-tile histograms (bqsr_tile_hist).
-// A unit's increment at binade e from its histogram: the sum of h[q] *
-// round(t[q] / 2^(e-52)), kFoldTie when a present qual ties there,
-// kFoldUnknown when the sum may be inexact (>= 2^52: such a unit crosses).
-template <class H>
-__device__ double unit_inc(const H* h, const double* t, int e) {
-  // 2^(52 - e) built from its exponent bits (ldexp is a library call here);
-  // outside the normal range the unit is left to the row scan
-  const int be = 1023 + 52 - e;
-  if (be < 1 || be > 2046) return kFoldUnknown;
-  const double scale = __longlong_as_double((long long)be << 52);
-  double acc = 0.0;
-  bool tie = false;
-  for (int q = 0; q < kQBins; ++q) {
-    const double c = (double)h[q];
-    const double x = t[q] * scale;  // exact: a power-of-two scaling of a normal double
-    const double r = rint(x);
-    tie |= c != 0.0 && x - floor(x) == 0.5;
-    acc += c * r;
-  }
-  if (tie) return kFoldTie;
-  return acc < 0x1p51 ? acc : kFoldUnknown;  // below 2^51 every partial sum was exact
-}
-// the same, one wavefront over one histogram (two bins per lane)
-template <class H>
-__device__ double unit_inc_wave(const H* h, const double* t, int e, int lane) {
-  const int be = 1023 + 52 - e;
-  if (be < 1 || be > 2046) return kFoldUnknown;
-  const double scale = __longlong_as_double((long long)be << 52);
-  double acc = 0.0;
-  bool tie = false;
-  for (int q = lane; q < kQBins; q += 64) {
-    const double c = (double)h[q];
-    const double x = t[q] * scale;
-    tie |= c != 0.0 && x - floor(x) == 0.5;
-    acc += c * rint(x);
-  }
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if (__builtin_amdgcn_ballot_w64(tie)) return kFoldTie;
-  return acc < 0x1p51 ? acc : kFoldUnknown;
-}
-// the lowest binade of a unit that starts at real partial sum lo (see bqsr_fold_plan)
-__device__ __forceinline__ int unit_elo(double lo) { return lo >= 0x1p-60 ? ilogb(lo) : -60; }
-
-extern "C" __global__ void __launch_bounds__(256) bqsr_fold_plan(const uint32_t* hq_block, const double* pow10,
-                                                                   int32_t n_blocks, uint8_t* cand, int32_t* cand_list,
-                                                                   int32_t* n_cand, double* dblk, int16_t* elo) {
-  __shared__ double t[kQBins];
-  __shared__ double bsum[kMaxFoldBlocks + 1];
-  __shared__ uint64_t bcnt[kMaxFoldBlocks];
-  __shared__ double delta;
-  __shared__ int32_t nc;
-  const int tid = threadIdx.x;
-  for (int q = tid; q < kQBins; q += blockDim.x) t[q] = pow10[q];
-  if (tid == 0) nc = 0;
-  __syncthreads();
-  for (int b = tid; b < n_blocks; b += blockDim.x) {
-    double v = 0.0;
-    uint64_t n = 0;
-    for (int q = 0; q < kQBins; ++q) {
-      const uint32_t h = hq_block[(int64_t)b * kQBins + q];
-      v += (double)h * t[q];
-      n += h;
-    }
-    bsum[b + 1] = v;
-    bcnt[b] = n;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    bsum[0] = 0.0;
-    uint64_t n = 0;
-    for (int b = 0; b < n_blocks; ++b) {
-      bsum[b + 1] += bsum[b];
-      n += bcnt[b];
-    }
-    delta = ((double)n + 64.0) * 0x1p-52 + 1e-12;
-  }
-  __syncthreads();
-  for (int b = tid; b < n_blocks; b += blockDim.x) {
-    bool c = false;
-    if (bcnt[b]) {
-      const double lo = bsum[b] * (1.0 - delta), hi = bsum[b + 1] * (1.0 + delta);
-      if (lo < kFoldSeqLimit * (1.0 + delta) || ilogb(lo) != ilogb(hi)) {
-        c = true;
-      } else {
-        const int e = ilogb(lo);
-        for (int q = 0; q < kQBins && !c; ++q) {
-          if (!hq_block[(int64_t)b * kQBins + q]) continue;
-          const double x = ldexp(t[q], 52 - e);
-          c = (x - floor(x)) == 0.5;
-        }
-      }
-    }
-    cand[b] = c;
-    if (c) cand_list[atomicAdd(&nc, 1)] = b;
-    const int e0 = unit_elo(bsum[b] * (1.0 - delta));
-    elo[b] = (int16_t)e0;
-    for (int k = 0; k < kFoldE; ++k)
-      dblk[(int64_t)b * kFoldE + k] = bcnt[b] ? unit_inc(hq_block + (int64_t)b * kQBins, t, e0 + k) : 0.0;
-  }
-  __syncthreads();
-  if (tid == 0) *n_cand = nc;
-}
-
-constexpr int kUnroll = 4;
-constexpr int kThCopies = 8;
-constexpr int kThStride = kQBins + 1;
-
-// Per-tile qual histograms of the folded bases of the candidate blocks' tiles
-// (one wavefront per tile: the folded ranges of the tile's reads become an LDS
-// slot bitmap, then every slot's qual is counted if its bit is set).
-extern "C" __global__ void __launch_bounds__(256) bqsr_tile_hist(ReadsDev rd, const ReadInfo* info,
-                                                                   const int32_t* cand_list, const int32_t* n_cand,
-                                                                   int32_t n_blocks, int64_t max_tpb, uint16_t* h2,
-                                                                   const int16_t* elo, const double* pow10,
-                                                                   double* dtile) {
-  __shared__ double tq[kQBins];
-  __shared__ uint32_t hsum[4][kQBins];
-  for (int q = threadIdx.x; q < kQBins; q += blockDim.x) tq[q] = pow10[q];
-  __syncthreads();
-  __shared__ uint32_t hist[4][kThCopies * kThStride];  // copies by lane & 7, rows one word apart in banks
-  __shared__ uint32_t bm[4][kTileSlots / 32];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t nt = rd.n_tiles;
-  const int64_t total = (int64_t)(*n_cand) * max_tpb;
-  for (int64_t v = (int64_t)blockIdx.x * 4 + wv; v < total; v += (int64_t)gridDim.x * 4) {
-    const int64_t b = cand_list[v / max_tpb];
-    const int64_t t = nt * b / n_blocks + v % max_tpb;
-    if (t >= nt * (b + 1) / n_blocks) continue;
-    const int64_t r0 = t * (int64_t)rd.reads_per_tile;
-    const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
-    ReadMeta m{0, 0, 0, 0, 0};
-    ReadInfo inf{0, 0, 0, 0};
-    if (lane < nr) {
-      m = rd.meta[r0 + lane];
-      inf = resolve_info(rd, info[r0 + lane], m.slot, m.lq);
-    }
-    const uint64_t ts0 = __shfl(m.slot, 0);
-    const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
-    for (int q = lane; q < kThCopies * kThStride; q += 64) hist[wv][q] = 0;
-    for (int i = lane; i < kTileSlots / 32; i += 64) bm[wv][i] = 0;
-    wave_sync();
-    if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
-      int lo = (int)(m.slot - ts0) + inf.st;
-      const int hi = (int)(m.slot - ts0) + inf.en;
-      while (lo < hi) {
-        const int n = min(32 - (lo & 31), hi - lo);
-        atomicOr(&bm[wv][lo >> 5], (n == 32 ? 0xFFFFFFFFu : ((1u << n) - 1u)) << (lo & 31));
-        lo += n;
-      }
-    }
-    wave_sync();
-    const uint8_t* qt = rd.qual + ts0;
-    for (int s0 = lane; s0 < nslots; s0 += 64 * kUnroll) {
-      int qv[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int s = s0 + 64 * u;
-        qv[u] = s < nslots ? (int)(int8_t)qt[s] : -1;
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int s = s0 + 64 * u;
-        if (qv[u] >= 0 && ((bm[wv][s >> 5] >> (s & 31)) & 1u))
-          atomicAdd(&hist[wv][(lane & (kThCopies - 1)) * kThStride + qv[u]], 1u);
-      }
-    }
-    wave_sync();
-    for (int q = lane; q < kQBins; q += 64) {
-      uint32_t v = 0;
-      for (int c = 0; c < kThCopies; ++c) v += hist[wv][c * kThStride + q];
-      h2[t * kQBins + q] = (uint16_t)v;
-      hsum[wv][q] = v;
-    }
-    wave_sync();
-    for (int k = 0; k < kFoldE; ++k) {
-      const double v = unit_inc_wave(hsum[wv], tq, (int)elo[b] + k, lane);
-      if (lane == 0) dtile[t * kFoldE + k] = v;
-    }
-    wave_sync();
-  }
-}
-
 // -------------------------------------------------------------- finalize ----
 //
 // RecalTable.finalizeTable (RecalTable.scala:117-126) and the per-(rg, q)
