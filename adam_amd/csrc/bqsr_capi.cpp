@@ -477,9 +477,10 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
     if ((st = dalloc(b->allocs, &F.blk, nbk)) != BQSR_OK || (st = dalloc(b->allocs, &F.cand_list, nbk)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.n_cand, 1)) != BQSR_OK || (st = dalloc(b->allocs, &F.delta, 1)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.rtile, nt)) != BQSR_OK || (st = dalloc(b->allocs, &F.ntile, nt)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &F.dtile, nt * kFoldE)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.h2, nt * kQBins)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.seg, nbk * kFoldMaxSegs)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &F.nseg, nbk)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.seg_base, nbk)) != BQSR_OK || (st = dalloc(b->allocs, &F.nseg, nbk)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.seg_used, 1)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.streams, (size_t)F.stream_cap + 64)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.stream_used, 1)) != BQSR_OK)
       return st;

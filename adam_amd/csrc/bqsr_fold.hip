@@ -49,7 +49,8 @@ namespace bqsr {
 constexpr double kFoldSeqLimit = 0.0625;  // below, binade mode is not worth it: sequential
 constexpr double kTwo53 = 9007199254740992.0;
 constexpr int kChainLdsSegs = 384;         // segments prefetched into the chain's LDS
-constexpr int kChainLdsStream = 104 * 1024;  // stream bytes prefetched into the chain's LDS
+constexpr int kSegBinades = 24;            // binades tabulated per candidate block (more: computed inline)
+constexpr int kChainLdsStream = 96 * 1024;  // stream bytes prefetched into the chain's LDS
 constexpr size_t chain_lds() {
   return (size_t)kMaxFoldBlocks * sizeof(FoldBlock) + (size_t)kChainLdsSegs * sizeof(FoldSeg) + kChainLdsStream;
 }
@@ -64,8 +65,6 @@ __device__ __forceinline__ double fold_inc(double t, int e, bool* tie) {
   *tie = (x - floor(x)) == 0.5;
   return r;
 }
-// the lowest binade a unit starting at real partial sum lo can be in
-__device__ __forceinline__ int fold_elo(double lo) { return lo >= 0x1p-60 ? ilogb(lo) : -60; }
 
 // ---------------------------------------------------------------- plan ----
 // One workgroup of 1024 threads (n_blocks <= kMaxFoldBlocks): per block the
@@ -173,9 +172,9 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
     if (live && !cand && (tie || !(inc < 0x1p52))) cand = true;  // below 2^52 every partial sum was exact
     if (b < nb && part == 0) {
       cnd[b] = cand;
-      if (!live) P.blk[b] = FoldBlock{R0, 0.0, kFoldNoBase, -1};
-      else if (!cand) P.blk[b] = FoldBlock{R0, inc, e, -1};
-      else P.blk[b] = FoldBlock{R0, 0.0, fold_elo(lo), 0};  // cidx set below
+      if (!live) P.blk[b] = FoldBlock{R0, R1, 0.0, kFoldNoBase, -1};
+      else if (!cand) P.blk[b] = FoldBlock{R0, R1, inc, e, -1};
+      else P.blk[b] = FoldBlock{R0, R1, 0.0, 0, 0};  // cidx set below
     }
   }
   __syncthreads();
@@ -198,19 +197,20 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
     *P.n_cand = ctot;
     *P.delta = delta;
     *P.stream_used = 0ull;
+    *P.seg_used = 0u;
   }
 }
 
 // ----------------------------------------------------------- tile sums ----
 // Candidate blocks' tiles, one wavefront each: the folded bases (usable
 // valid reads, trimmed ranges) become an LDS slot bitmap, then every folded
-// slot adds its qual's real value and its increments at the block's four
-// binades elo .. elo + 3 (per-wavefront tables, rebuilt when the block changes).
-constexpr int kFtWaves = 4;
+// slot counts its qual into the wavefront's histogram (8 copies by lane & 7
+// against same-bin conflicts, rows 129 words apart); out: the tile's
+// histogram, real sum and count.
+constexpr int kFtWaves = 4, kFtCopies = 8, kFtStride = kQBins + 1;
 extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(FoldParams P, int64_t max_tpb) {
   __shared__ double t[kQBins];
-  __shared__ double inc[kFtWaves][kFoldE][kQBins];
-  __shared__ uint8_t tiem[kFtWaves][kQBins];
+  __shared__ uint32_t hist[kFtWaves][kFtCopies * kFtStride];
   __shared__ uint32_t bm[kFtWaves][kTileSlots / 32];
   for (int q = threadIdx.x; q < kQBins; q += blockDim.x) t[q] = P.pow10[q];
   __syncthreads();
@@ -218,24 +218,11 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
   const ReadsDev& rd = P.rd;
   const int64_t nt = rd.n_tiles;
   const int64_t total = (int64_t)(*P.n_cand) * max_tpb;
-  int cur_elo = -100000;
+  uint32_t* hw = &hist[wv][(lane & (kFtCopies - 1)) * kFtStride];
   for (int64_t v = (int64_t)blockIdx.x * kFtWaves + wv; v < total; v += (int64_t)gridDim.x * kFtWaves) {
     const int64_t b = P.cand_list[v / max_tpb];
     const int64_t tl = nt * b / P.n_blocks + v % max_tpb;
     if (tl >= nt * (b + 1) / P.n_blocks) continue;
-    const int elo = P.blk[b].e;
-    if (elo != cur_elo) {  // this block's increment tables
-      for (int q = lane; q < kQBins; q += 64) {
-        uint8_t tm = 0;
-        for (int k = 0; k < kFoldE; ++k) {
-          bool tq;
-          inc[wv][k][q] = fold_inc(t[q], elo + k, &tq);
-          tm |= (uint8_t)(tq << k);
-        }
-        tiem[wv][q] = tm;
-      }
-      cur_elo = elo;
-    }
     const int64_t r0 = tl * (int64_t)rd.reads_per_tile;
     const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
     ReadMeta m{0, 0, 0, 0, 0};
@@ -247,6 +234,7 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
     const uint64_t ts0 = __shfl(m.slot, 0);
     const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
     for (int i = lane; i < kTileSlots / 32; i += 64) bm[wv][i] = 0;
+    for (int i = lane; i < kFtCopies * kFtStride; i += 64) hist[wv][i] = 0;
     wave_sync();
     if (lane < nr && (inf.fl & kInfoObs) && inf.en > inf.st) {
       int lo = (int)(m.slot - ts0) + inf.st;
@@ -258,37 +246,32 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
       }
     }
     wave_sync();
-    double re = 0.0, d[kFoldE] = {0.0, 0.0, 0.0, 0.0};
-    uint32_t cnt = 0, tm = 0;
     const uint8_t* qt = rd.qual + ts0;
     for (int s0 = lane * 4; s0 < nslots; s0 += 256) {  // 4 slots per lane and step
       const uint32_t qw4 = *(const uint32_t*)(qt + s0);  // (the qual column has 32 B of padding)
       const uint32_t bits = (bm[wv][s0 >> 5] >> (s0 & 31)) & 0xFu;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (((bits >> k) & 1u) && s0 + k < nslots) {
-          const int q = (int)((qw4 >> (8 * k)) & 0x7Fu);  // folded quals are 0..127 (q < 0 fails observe)
-          re += t[q];
-          ++cnt;
-          tm |= tiem[wv][q];
+      for (int k = 0; k < 4; ++k)
+        if (((bits >> k) & 1u) && s0 + k < nslots) atomicAdd(&hw[(qw4 >> (8 * k)) & 0x7Fu], 1u);
+    }
+    wave_sync();
+    double re = 0.0;
+    uint32_t cnt = 0;
+    for (int q = lane; q < kQBins; q += 64) {
+      uint32_t h = 0;
 #pragma unroll
-          for (int e = 0; e < kFoldE; ++e) d[e] = fmin(d[e] + inc[wv][e][q], 0x1p53);  // saturating: exact below
-        }
-      }
+      for (int c = 0; c < kFtCopies; ++c) h += hist[wv][c * kFtStride + q];
+      P.h2[tl * kQBins + q] = (uint16_t)h;  // <= kTileSlots
+      re += (double)h * t[q];
+      cnt += h;
     }
     for (int off = 32; off > 0; off >>= 1) {
       re += __shfl_xor(re, off);
       cnt += __shfl_xor(cnt, off);
-      tm |= __shfl_xor(tm, off);
-#pragma unroll
-      for (int e = 0; e < kFoldE; ++e) d[e] = fmin(d[e] + __shfl_xor(d[e], off), 0x1p53);
     }
     if (lane == 0) {
       P.rtile[tl] = re;
       P.ntile[tl] = (int32_t)cnt;
-#pragma unroll
-      for (int e = 0; e < kFoldE; ++e)
-        P.dtile[tl * kFoldE + e] = ((tm >> e) & 1u) ? kFoldTie : (d[e] < 0x1p52 ? d[e] : kFoldUnknown);
     }
     wave_sync();
   }
@@ -336,10 +319,23 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
   __shared__ int32_t ev_tile[1024], ev_pos[1024];
   __shared__ int32_t n_ev;
   __shared__ FoldSeg out[kFoldMaxSegs];
+  __shared__ double itab[kSegBinades][kQBins];  // increments at the block's binades eb0 ..
+  __shared__ uint8_t ttab[kSegBinades][kQBins];  // and ties
+  __shared__ int32_t seg0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = P.cand_list[c];
   const FoldBlock B = P.blk[b];
   const double delta = *P.delta;
+  // the binades the block's tiles may stay in: from where the real sum
+  // reaches kFoldSeqLimit (or the block's start) to the block's end
+  const int eb0 = ilogb(fmax(B.r0 * (1.0 - delta), kFoldSeqLimit)), eb1 = ilogb(fmax(B.r1 * (1.0 + delta), kFoldSeqLimit));
+  const int nbin = min(eb1 - eb0 + 1, kSegBinades);
+  for (int i = tid; i < nbin * kQBins; i += 1024) {
+    const int k = i / kQBins, q = i - k * kQBins;
+    bool tq;
+    itab[k][q] = fold_inc(P.pow10[q], eb0 + k, &tq);
+    ttab[k][q] = tq;
+  }
   const int64_t nt = P.rd.n_tiles;
   const int64_t c0 = nt * b / P.n_blocks, c1 = nt * (b + 1) / P.n_blocks;
   constexpr int kEvent = INT32_MIN + 1;  // the key of tiles that may hold an event
@@ -380,9 +376,28 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
     if (live) {
       const double lo = Rt * (1.0 - delta), hi = Re * (1.0 + delta);
       if (lo >= kFoldSeqLimit * (1.0 + delta) && ilogb(lo) == ilogb(hi)) {
-        const int e = ilogb(lo), kk = e - B.e;
-        const double d = (kk >= 0 && kk < kFoldE) ? P.dtile[tl * kFoldE + kk] : kFoldUnknown;
-        if (d >= 0.0) {
+        const int e = ilogb(lo), k = e - eb0;
+        // the tile's exact increment at binade e from its histogram
+        const uint4* hr = (const uint4*)(P.h2 + tl * kQBins);
+        double d = 0.0;
+        bool tie = false;
+        for (int i = 0; i < kQBins / 8; ++i) {
+          const uint4 hv = hr[i];
+          const uint32_t w[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+            if (h) {
+              const int q = i * 8 + j;
+              bool tq;
+              const double iq = (k >= 0 && k < nbin) ? itab[k][q] : fold_inc(P.pow10[q], e, &tq);
+              if (k >= 0 && k < nbin) tq = ttab[k][q];
+              d += (double)h * iq;
+              tie |= tq;
+            }
+          }
+        }
+        if (!tie && d < 0x1p52) {  // below 2^52 every partial sum was exact
           key = e;
           inc = (int64_t)d;
         }
@@ -421,6 +436,12 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
     __syncthreads();
   }
   const int ns = min(carry_sid + 1, kFoldMaxSegs);
+  if (tid == 0) {
+    seg0 = (int32_t)atomicAdd(P.seg_used, (uint32_t)ns);  // this block's place in the compact list
+    P.seg_base[c] = seg0;
+    P.nseg[c] = ns;
+  }
+  __syncthreads();
   // the segments; event segments get their stream space
   if (tid < ns) {
     FoldSeg g;
@@ -444,9 +465,8 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
       g.inc = (int64_t)s_inc[tid];
     }
     out[tid] = g;
-    P.seg[(int64_t)c * kFoldMaxSegs + tid] = g;
+    P.seg[seg0 + tid] = g;
   }
-  if (tid == 0) P.nseg[c] = ns;
   __syncthreads();
   // copy the event segments' tiles, one wavefront per tile, each at its
   // element offset in its segment's stream
@@ -578,7 +598,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   __shared__ double inc[kQBins];
   __shared__ uint8_t tie[kQBins];
   __shared__ uint8_t scratch[kTileSlots];
-  __shared__ int32_t nseg_l[kMaxFoldBlocks];
+  __shared__ int32_t nseg_l[kMaxFoldBlocks], sbase_l[kMaxFoldBlocks];
   FoldBlock* blk = (FoldBlock*)chain_smem;                    // [n_blocks]
   FoldSeg* segs = (FoldSeg*)(blk + kMaxFoldBlocks);           // [kChainLdsSegs]
   uint8_t* streams = (uint8_t*)(segs + kChainLdsSegs);        // [kChainLdsStream]
@@ -586,10 +606,13 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   const int nb = P.n_blocks, nc = *P.n_cand;
   const int64_t used = (int64_t)*P.stream_used;
   const int64_t sl = min(used, (int64_t)kChainLdsStream);
-  const int nsl = min(nc * kFoldMaxSegs, kChainLdsSegs);
+  const int nsl = min((int)*P.seg_used, kChainLdsSegs);
   // prefetch: every thread issues its loads before any is used
   for (int q = tid; q < kQBins; q += 1024) t[q] = P.pow10[q];
-  for (int i = tid; i < nc; i += 1024) nseg_l[i] = P.nseg[i];
+  for (int i = tid; i < nc; i += 1024) {
+    nseg_l[i] = P.nseg[i];
+    sbase_l[i] = P.seg_base[i];
+  }
   {
     const uint64_t* src = (const uint64_t*)P.blk;
     uint64_t* dst = (uint64_t*)blk;
@@ -610,6 +633,13 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   double S = 0.0;
   int cur_e = INT32_MIN;
   const int64_t nt = P.rd.n_tiles;
+#ifdef BQSR_FOLD_PROFILE
+  long long pf_blk = 0, pf_blk_fb = 0, pf_run = 0, pf_run_fb = 0, pf_ev = 0, pf_ev_el = 0, pf_glob = 0,
+            pf_glob_tiles = 0, pf_c0 = clock64();
+#define PF(x) x
+#else
+#define PF(x)
+#endif
   for (int b = 0; b < nb; ++b) {
     const FoldBlock B = blk[b];
     if (B.cidx < 0) {  // no event expected: one integer addition
@@ -618,9 +648,11 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
         const double N0 = S * pow2i(52 - B.e);
         if (N0 + B.inc < kTwo53) {
           S = (N0 + B.inc) * pow2i(B.e - 52);
+          PF(++pf_blk);
           continue;
         }
       }
+      PF(++pf_blk_fb);
       // the bound failed (not expected): fold the block's tiles element by element
       for (int64_t tl = nt * b / nb; tl < nt * (b + 1) / nb; ++tl)
         S = fold_tile_global(P, S, tl, scratch, t, inc, tie, cur_e, lane);
@@ -629,26 +661,37 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
     const int c = B.cidx;
     const int ns = nseg_l[c];
     for (int s = 0; s < ns; ++s) {
-      const int64_t si = (int64_t)c * kFoldMaxSegs + s;
+      const int64_t si = (int64_t)sbase_l[c] + s;
       const FoldSeg G = si < nsl ? segs[si] : P.seg[si];
       if (G.kind == kSegRun) {
         if (S >= kFoldSeqLimit && ilogb(S) == G.e) {
           const double N0 = S * pow2i(52 - G.e);
           if (N0 + (double)G.inc < kTwo53) {
             S = (N0 + (double)G.inc) * pow2i(G.e - 52);
+            PF(++pf_run);
             continue;
           }
         }
+        PF(++pf_run_fb);
       } else if (G.kind == kSegEvent) {
         const uint8_t* q = G.off + G.inc <= sl ? streams + G.off : P.streams + G.off;
         S = wave_fold(S, q, G.inc, t, inc, tie, cur_e, lane);
+        PF(++pf_ev; pf_ev_el += G.inc);
         continue;
       }
+      PF(++pf_glob; pf_glob_tiles += G.t1 - G.t0 + 1);
       // kSegGlobal, or a run whose bound failed: element by element
       for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, scratch, t, inc, tie, cur_e, lane);
     }
   }
   if (lane == 0) P.em_out[0] = S;
+#ifdef BQSR_FOLD_PROFILE
+  if (lane == 0)
+    printf("FOLD2 cand %d stream_used %lld | blocks %lld fallback %lld | runs %lld fallback %lld | events %lld elems %lld | "
+           "global %lld tiles %lld | cycles %lld\n",
+           nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles,
+           clock64() - pf_c0);
+#endif
 }
 
 }  // namespace bqsr

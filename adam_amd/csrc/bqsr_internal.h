@@ -193,20 +193,18 @@ struct ObserveParams {
 };
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----
-constexpr int kFoldE = 4;  // binades a candidate block's tiles are tabulated at: elo .. elo + 3
-constexpr double kFoldTie = -1.0, kFoldUnknown = -2.0;  // increment sentinels: a tie / not exact
-constexpr int32_t kFoldNoBase = INT32_MIN;              // FoldBlock::e of a block without folded bases
-constexpr int kFoldMaxSegs = 16;                        // segments per candidate block
+constexpr int32_t kFoldNoBase = INT32_MIN;  // FoldBlock::e of a block without folded bases
+constexpr int kFoldMaxSegs = 64;            // segments per candidate block (the rest: one fallback segment)
 enum : int32_t { kSegRun = 0, kSegEvent = 1, kSegGlobal = 2 };
 
 // per fold block (one observe workgroup's range of tiles), bqsr_fold_plan
 struct FoldBlock {
-  double r0;     // real sum of the folded quals before the block (approximate)
-  double inc;    // event-free block: its exact increment at binade e, in units 2^(e-52)
-  int32_t e;     // event-free: the binade the whole block stays in; candidate: the lowest it may start in
-  int32_t cidx;  // candidate index (bqsr_fold_segs workgroup), -1 when event-free
+  double r0, r1;  // real sum of the folded quals before / after the block (approximate)
+  double inc;     // event-free block: its exact increment at binade e, in units 2^(e-52)
+  int32_t e;      // event-free: the binade the whole block stays in
+  int32_t cidx;   // candidate index (bqsr_fold_segs workgroup), -1 when event-free
 };
-static_assert(sizeof(FoldBlock) == 24, "FoldBlock is 3 words");
+static_assert(sizeof(FoldBlock) == 32, "FoldBlock is 4 words");
 
 // a run of tiles of a candidate block, bqsr_fold_segs
 struct FoldSeg {
@@ -230,9 +228,11 @@ struct FoldParams {
   double* delta;             // relative bound of |exact - real| partial sums
   double* rtile;             // [n_tiles] candidate blocks' tiles: real sum
   int32_t* ntile;            //           folded bases
-  double* dtile;             //           [kFoldE] increments at elo .. elo + 3 (or a sentinel)
-  FoldSeg* seg;              // [n_blocks][kFoldMaxSegs]
-  int32_t* nseg;             // [n_blocks]
+  uint16_t* h2;              //           [128] qual histogram of the folded bases
+  FoldSeg* seg;              // segments of all candidate blocks, each block's consecutive
+  int32_t* seg_base;         // [n_blocks] candidate c's first segment
+  int32_t* nseg;             // [n_blocks] and count
+  uint32_t* seg_used;
   uint8_t* streams;          // event segments' quals in fold order
   int64_t stream_cap;
   unsigned long long* stream_used;
