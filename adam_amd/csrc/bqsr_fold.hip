@@ -46,7 +46,7 @@
 
 namespace bqsr {
 
-constexpr double kFoldSeqLimit = 0.0625;  // below, binade mode is not worth it: sequential
+constexpr double kFoldSeqLimit = 0.0625;  // below, binades change every few additions: events only
 constexpr double kTwo53 = 9007199254740992.0;
 constexpr int kChainLdsSegs = 384;         // segments prefetched into the chain's LDS
 constexpr int kSegBinades = 24;            // binades tabulated per candidate block (more: computed inline)
@@ -302,8 +302,21 @@ __device__ void fold_copy_tile(const FoldParams& P, int64_t tl, uint8_t* dst, in
     const int x = __shfl_up(pre, off);
     if (lane >= off) pre += x;
   }
+  // 16-B pieces (unaligned global loads and stores are fine on gfx950), the
+  // read's last < 16 bytes one by one: lanes never write each other's bytes
   uint8_t* d = dst + (pre - len);
-  for (int i = 0; i < len; ++i) d[i] = rd.qual[src + i];
+  const uint8_t* sp = rd.qual + src;
+  const int full = len & ~15;
+  for (int i0 = 0; i0 < full; i0 += 64) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + 16 * k < full) v[k] = *(const uint4*)(sp + i0 + 16 * k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + 16 * k < full) *(uint4*)(d + i0 + 16 * k) = v[k];
+  }
+  for (int i = full; i < len; ++i) d[i] = sp[i];
 }
 
 extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) {
@@ -494,24 +507,19 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
 
 // --------------------------------------------------------------- chain ----
 
-// Fold elements [0, n) of `q` (LDS or global bytes) into S exactly, one
-// wavefront.  inc / tie: LDS tables of the current binade cur_e.
-__device__ double wave_fold(double S, const uint8_t* q, int64_t n, const double* t, double* inc, uint8_t* tie,
-                            int& cur_e, int lane) {
-  int64_t pos = 0;
+// Fold elements [0, n) of q (LDS) into S exactly, one wavefront, no serial
+// loop: lane l sums the increments of elements pos + 64 l .. + 63 at the
+// current binade, a wavefront scan finds the first lane whose elements leave
+// the binade or hold a tie, a second scan over that lane's 64 elements finds
+// the element, and that element is added in IEEE double arithmetic.
+// inc / tie: LDS tables of binade cur_e (rebuilt when S changes binade).
+__device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, const double* t, double* inc,
+                                            uint8_t* tie, int& cur_e, int lane) {
+  int pos = 0;
   while (pos < n) {
-    if (S < kFoldSeqLimit) {
-      // small S: the binade changes every few additions -- lane 0 adds in order
-      int64_t p = pos;
-      double s = S;
-      if (lane == 0) {
-        while (p < n && s < kFoldSeqLimit) {
-          s = s + t[q[p]];
-          ++p;
-        }
-      }
-      S = __shfl(s, 0);
-      pos = __shfl(p, 0);
+    if (S == 0.0) {  // 0.0 + t is exact
+      S = t[q[pos]];
+      ++pos;
       continue;
     }
     const int e = ilogb(S);
@@ -526,14 +534,19 @@ __device__ double wave_fold(double S, const uint8_t* q, int64_t n, const double*
     }
     const double N0 = S * pow2i(52 - e);  // S / u, an integer < 2^53
     const double head = kTwo53 - N0;     // increments left before the binade ends
-    // lane l takes elements [pos + 64 l, pos + 64 l + 64)
-    const int64_t a = pos + 64 * (int64_t)lane, bnd = min(a + 64, n);
+    const int a = pos + 64 * lane, bnd = min(a + 64, n);
     double sum = 0.0;
     bool th = false;
-    for (int64_t k = a; k < bnd; ++k) {
-      const int qq = q[k];
-      sum = fmin(sum + inc[qq], 0x1p53);  // saturating: exact while it matters
-      th |= tie[qq] != 0;
+    for (int k0 = a; k0 < bnd; k0 += 16) {
+      int qq[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) qq[j] = k0 + j < bnd ? (int)q[k0 + j] : -1;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (qq[j] >= 0) {
+          sum = fmin(sum + inc[qq[j]], 0x1p53);  // saturating: exact while it matters
+          th |= tie[qq[j]] != 0;
+        }
     }
     double incl = sum;
     for (int off = 1; off < 64; off <<= 1) {
@@ -542,33 +555,30 @@ __device__ double wave_fold(double S, const uint8_t* q, int64_t n, const double*
     }
     const uint64_t hit = __builtin_amdgcn_ballot_w64(a < bnd && (incl >= head || th));
     if (!hit) {  // the whole window stays in the binade
-      const double tot = __shfl(incl, 63);
-      S = (N0 + tot) * pow2i(e - 52);
+      S = (N0 + __shfl(incl, 63)) * pow2i(e - 52);
       pos = min(n, pos + 64 * 64);
       continue;
     }
     const int L = (int)__builtin_ctzll(hit);
     const double excl = L > 0 ? __shfl(incl, L - 1) : 0.0;  // < head: exact
-    const int64_t aL = pos + 64 * (int64_t)L, bL = min(aL + 64, n);
-    int64_t p = bL;
-    double s = 0.0;
-    if (lane == 0) {  // the first event inside lane L's elements
-      double N = N0 + excl;
-      bool found = false;
-      for (int64_t k = aL; k < bL; ++k) {
-        const int qq = q[k];
-        if (tie[qq] || N + inc[qq] >= kTwo53) {
-          s = N * pow2i(e - 52) + t[qq];  // the exact IEEE addition the JVM performs
-          p = k + 1;
-          found = true;
-          break;
-        }
-        N += inc[qq];
-      }
-      if (!found) s = N * pow2i(e - 52);  // (cannot happen: the lane's sum signalled an event)
+    // lane L's elements, one per lane
+    const int k = pos + 64 * L + lane;
+    const bool valid = k < min(pos + 64 * L + 64, n);
+    const int qk = valid ? (int)q[k] : 0;
+    const double v = valid ? inc[qk] : 0.0;
+    const bool tk = valid && tie[qk] != 0;
+    double sc = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const double x = __shfl_up(sc, off);
+      if (lane >= off) sc = fmin(sc + x, 0x1p54);
     }
-    S = __shfl(s, 0);
-    pos = __shfl(p, 0);
+    double scx = __shfl_up(sc, 1);  // exclusive prefix (not sc - v: sc may have saturated)
+    if (lane == 0) scx = 0.0;
+    const uint64_t ev = __builtin_amdgcn_ballot_w64(valid && (tk || excl + sc >= head));
+    const int j = ev ? (int)__builtin_ctzll(ev) : 63;  // (an event exists: lane L signalled one)
+    const double before = N0 + excl + __shfl(scx, j);  // exact: below head <= 2^52
+    S = before * pow2i(e - 52) + t[__shfl(qk, j)];  // the exact IEEE addition the JVM performs
+    pos = pos + 64 * L + j + 1;
   }
   return S;
 }
@@ -589,7 +599,9 @@ __device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, ui
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
   fold_copy_tile(P, tl, scratch, lane);
   wave_sync();
-  return wave_fold(S, scratch, tot, t, inc, tie, cur_e, lane);
+  S = wave_fold(S, scratch, tot, t, inc, tie, cur_e, lane);
+  wave_sync();  // the scratch is free again
+  return S;
 }
 
 extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P) {
@@ -674,8 +686,17 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
         }
         PF(++pf_run_fb);
       } else if (G.kind == kSegEvent) {
-        const uint8_t* q = G.off + G.inc <= sl ? streams + G.off : P.streams + G.off;
-        S = wave_fold(S, q, G.inc, t, inc, tie, cur_e, lane);
+        if (G.off + G.inc <= sl) {
+          S = wave_fold(S, streams + G.off, (int)G.inc, t, inc, tie, cur_e, lane);
+        } else {  // beyond the prefetched bytes: through the scratch buffer, 4 KB at a time
+          for (int64_t o = 0; o < G.inc; o += kTileSlots) {
+            const int m = (int)min((int64_t)kTileSlots, G.inc - o);
+            for (int i = lane; i < m; i += 64) scratch[i] = P.streams[G.off + o + i];
+            wave_sync();
+            S = wave_fold(S, scratch, m, t, inc, tie, cur_e, lane);
+            wave_sync();
+          }
+        }
         PF(++pf_ev; pf_ev_el += G.inc);
         continue;
       }
