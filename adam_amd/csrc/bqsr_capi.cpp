@@ -477,7 +477,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
     if ((st = dalloc(b->allocs, &F.blk, nbk)) != BQSR_OK || (st = dalloc(b->allocs, &F.cand_list, nbk)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.n_cand, 1)) != BQSR_OK || (st = dalloc(b->allocs, &F.delta, 1)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.rtile, nt)) != BQSR_OK || (st = dalloc(b->allocs, &F.ntile, nt)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &F.h2, nt * kQBins)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.dtile, nt * kSegBinades)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.seg, nbk * kFoldMaxSegs)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.seg_base, nbk)) != BQSR_OK || (st = dalloc(b->allocs, &F.nseg, nbk)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.seg_used, 1)) != BQSR_OK ||
@@ -1080,7 +1080,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(1024), 0, s, F);
     const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
     hipLaunchKernelGGL(bqsr_fold_tiles, dim3(ctx->n_cu * 4), dim3(kFtWaves * 64), 0, s, F, max_tpb);
-    hipLaunchKernelGGL(bqsr_fold_segs, dim3(b->n_blocks), dim3(1024), 0, s, F);
+    hipLaunchKernelGGL(bqsr_fold_segs, dim3(b->n_blocks), dim3(kSegThreads), 0, s, F);
     hipLaunchKernelGGL(bqsr_fold_chain, dim3(1), dim3(1024), chain_lds(), s, F);
     HIP_TRY(hipGetLastError());
   }

@@ -49,10 +49,10 @@ namespace bqsr {
 constexpr double kFoldSeqLimit = 0.0625;  // below, binades change every few additions: events only
 constexpr double kTwo53 = 9007199254740992.0;
 constexpr int kChainLdsSegs = 384;         // segments prefetched into the chain's LDS
-constexpr int kSegBinades = 24;            // binades tabulated per candidate block (more: computed inline)
+constexpr int kSegThreads = 512, kSegWaves = kSegThreads / 64;  // bqsr_fold_segs workgroup
 constexpr int kChainLdsStream = 96 * 1024;  // stream bytes prefetched into the chain's LDS
 constexpr size_t chain_lds() {
-  return (size_t)kMaxFoldBlocks * sizeof(FoldBlock) + (size_t)kChainLdsSegs * sizeof(FoldSeg) + kChainLdsStream;
+  return (size_t)kMaxFoldBlocks * sizeof(FoldBlock) + (size_t)kChainLdsSegs * sizeof(FoldSeg) + kChainLdsStream + 64;
 }
 
 // 2^k as a double from its exponent bits (k in the normal range)
@@ -64,6 +64,15 @@ __device__ __forceinline__ double fold_inc(double t, int e, bool* tie) {
   const double r = rint(x);  // round half to even, as the IEEE addition does
   *tie = (x - floor(x)) == 0.5;
   return r;
+}
+
+// the binades a candidate block's tiles may stay in: from where its widened
+// real span reaches kFoldSeqLimit (or its start) to its end; eb0 and count
+__device__ __forceinline__ int block_eb0(const FoldBlock& B, double delta) {
+  return ilogb(fmax(B.r0 * (1.0 - delta), kFoldSeqLimit));
+}
+__device__ __forceinline__ int block_nbin(const FoldBlock& B, double delta) {
+  return min(ilogb(fmax(B.r1 * (1.0 + delta), kFoldSeqLimit)) - block_eb0(B, delta) + 1, kSegBinades);
 }
 
 // ---------------------------------------------------------------- plan ----
@@ -256,12 +265,14 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
     }
     wave_sync();
     double re = 0.0;
-    uint32_t cnt = 0;
-    for (int q = lane; q < kQBins; q += 64) {
+    uint32_t cnt = 0, h2[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = lane + 64 * i;
       uint32_t h = 0;
 #pragma unroll
       for (int c = 0; c < kFtCopies; ++c) h += hist[wv][c * kFtStride + q];
-      P.h2[tl * kQBins + q] = (uint16_t)h;  // <= kTileSlots
+      h2[i] = h;
       re += (double)h * t[q];
       cnt += h;
     }
@@ -272,6 +283,23 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
     if (lane == 0) {
       P.rtile[tl] = re;
       P.ntile[tl] = (int32_t)cnt;
+    }
+    // exact increments at every binade the block may be in (from the histogram)
+    const FoldBlock B = P.blk[b];
+    const int eb0 = block_eb0(B, *P.delta), nbin = block_nbin(B, *P.delta);
+    for (int k = 0; k < nbin; ++k) {
+      double d = 0.0;
+      bool tie = false;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        bool tq;
+        const double iq = fold_inc(t[lane + 64 * i], eb0 + k, &tq);
+        d += (double)h2[i] * iq;  // integers: exact while below 2^53
+        tie |= h2[i] != 0 && tq;
+      }
+      for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+      const bool anytie = __builtin_amdgcn_ballot_w64(tie) != 0;
+      if (lane == 0) P.dtile[tl * kSegBinades + k] = anytie ? kFoldTie : (d < 0x1p52 ? d : kFoldUnknown);
     }
     wave_sync();
   }
@@ -304,54 +332,43 @@ __device__ void fold_copy_tile(const FoldParams& P, int64_t tl, uint8_t* dst, in
   }
   // 16-B pieces (unaligned global loads and stores are fine on gfx950), the
   // read's last < 16 bytes one by one: lanes never write each other's bytes
-  uint8_t* d = dst + (pre - len);
-  const uint8_t* sp = rd.qual + src;
+  uint8_t* __restrict__ d = dst + (pre - len);
+  const uint8_t* __restrict__ sp = rd.qual + src;
   const int full = len & ~15;
-  for (int i0 = 0; i0 < full; i0 += 64) {
-    uint4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (i0 + 16 * k < full) v[k] = *(const uint4*)(sp + i0 + 16 * k);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (i0 + 16 * k < full) *(uint4*)(d + i0 + 16 * k) = v[k];
-  }
+#pragma unroll 4
+  for (int i = 0; i < full; i += 16) *(uint4*)(d + i) = *(const uint4*)(sp + i);
   for (int i = full; i < len; ++i) d[i] = sp[i];
 }
 
-extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) {
+extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldParams P) {
   const int c = blockIdx.x;
   if (c >= *P.n_cand) return;
   __shared__ double wsum[16];
-  __shared__ int32_t wcount[16];
-  __shared__ int32_t keys[1024];
+  __shared__ int32_t wcount[16], wev[16];
+  __shared__ int32_t keys[kSegThreads];
   __shared__ unsigned long long s_inc[kFoldMaxSegs];
   __shared__ int32_t s_n[kFoldMaxSegs], s_t0[kFoldMaxSegs], s_t1[kFoldMaxSegs], s_key[kFoldMaxSegs];
-  __shared__ int32_t carry_sid, carry_key;
+  __shared__ int64_t s_off[kFoldMaxSegs];
+  __shared__ int32_t carry_sid;
   __shared__ double carry_r;
-  __shared__ int32_t ev_tile[1024], ev_pos[1024];
-  __shared__ int32_t n_ev;
+  __shared__ int64_t chunk_off;
+  __shared__ int32_t ev_tile[kSegThreads];
+  __shared__ int64_t ev_dst[kSegThreads];
   __shared__ FoldSeg out[kFoldMaxSegs];
-  __shared__ double itab[kSegBinades][kQBins];  // increments at the block's binades eb0 ..
-  __shared__ uint8_t ttab[kSegBinades][kQBins];  // and ties
   __shared__ int32_t seg0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef BQSR_FOLD_PROFILE
+  const long long pf_t0 = clock64();
+#endif
   const int b = P.cand_list[c];
   const FoldBlock B = P.blk[b];
   const double delta = *P.delta;
   // the binades the block's tiles may stay in: from where the real sum
   // reaches kFoldSeqLimit (or the block's start) to the block's end
-  const int eb0 = ilogb(fmax(B.r0 * (1.0 - delta), kFoldSeqLimit)), eb1 = ilogb(fmax(B.r1 * (1.0 + delta), kFoldSeqLimit));
-  const int nbin = min(eb1 - eb0 + 1, kSegBinades);
-  for (int i = tid; i < nbin * kQBins; i += 1024) {
-    const int k = i / kQBins, q = i - k * kQBins;
-    bool tq;
-    itab[k][q] = fold_inc(P.pow10[q], eb0 + k, &tq);
-    ttab[k][q] = tq;
-  }
+  const int eb0 = block_eb0(B, delta), nbin = block_nbin(B, delta);
   const int64_t nt = P.rd.n_tiles;
   const int64_t c0 = nt * b / P.n_blocks, c1 = nt * (b + 1) / P.n_blocks;
-  constexpr int kEvent = INT32_MIN + 1;  // the key of tiles that may hold an event
+  constexpr int kEvent = INT32_MIN + 1;    // the key of tiles that may hold an event
   constexpr int kLast = kFoldMaxSegs - 1;  // segment index absorbing any overflow (folded from the columns)
   if (tid < kFoldMaxSegs) {
     s_inc[tid] = 0;
@@ -359,14 +376,14 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
     s_t0[tid] = INT32_MAX;
     s_t1[tid] = -1;
     s_key[tid] = kEvent;
+    s_off[tid] = -1;
   }
   if (tid == 0) {
     carry_sid = -1;
-    carry_key = INT32_MIN;
     carry_r = B.r0;
   }
   __syncthreads();
-  for (int64_t k0 = c0; k0 < c1; k0 += 1024) {
+  for (int64_t k0 = c0; k0 < c1; k0 += kSegThreads) {
     const int64_t tl = k0 + tid;
     const bool live = tl < c1;
     const double re = live ? P.rtile[tl] : 0.0;
@@ -382,35 +399,16 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
     double base = carry_r;
     for (int w = 0; w < wave; ++w) base += wsum[w];
     const double Rt = base + (v - re), Re = base + v;
-    // a tile that surely stays in binade e >= kFoldSeqLimit, with a tabulated,
+    // a tile that surely stays in binade e >= kFoldSeqLimit, with a
     // tie-free increment there, has key e; any other has key kEvent
     int key = kEvent;
     int64_t inc = 0;
     if (live) {
       const double lo = Rt * (1.0 - delta), hi = Re * (1.0 + delta);
-      if (lo >= kFoldSeqLimit * (1.0 + delta) && ilogb(lo) == ilogb(hi)) {
-        const int e = ilogb(lo), k = e - eb0;
-        // the tile's exact increment at binade e from its histogram
-        const uint4* hr = (const uint4*)(P.h2 + tl * kQBins);
-        double d = 0.0;
-        bool tie = false;
-        for (int i = 0; i < kQBins / 8; ++i) {
-          const uint4 hv = hr[i];
-          const uint32_t w[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-            if (h) {
-              const int q = i * 8 + j;
-              bool tq;
-              const double iq = (k >= 0 && k < nbin) ? itab[k][q] : fold_inc(P.pow10[q], e, &tq);
-              if (k >= 0 && k < nbin) tq = ttab[k][q];
-              d += (double)h * iq;
-              tie |= tq;
-            }
-          }
-        }
-        if (!tie && d < 0x1p52) {  // below 2^52 every partial sum was exact
+      const int e = ilogb(lo), k = e - eb0;
+      if (lo >= kFoldSeqLimit * (1.0 + delta) && ilogb(lo) == ilogb(hi) && k >= 0 && k < nbin) {
+        const double d = P.dtile[tl * kSegBinades + k];
+        if (d >= 0.0) {
           key = e;
           inc = (int64_t)d;
         }
@@ -418,15 +416,38 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
     }
     keys[tid] = live ? key : INT32_MIN;
     __syncthreads();
-    // a segment starts where the key changes (event tiles of a run form one segment)
-    const int prev = tid > 0 ? keys[tid - 1] : carry_key;
+    // a segment starts where the key changes, and at every chunk's first tile
+    // (event tiles of a run form one segment; segments never span chunks)
+    const int prev = tid > 0 ? keys[tid - 1] : INT32_MIN;
     const bool start = live && key != prev;
+    const bool ev = live && key == kEvent;
     const uint64_t sm = __builtin_amdgcn_ballot_w64(start);
+    // event elements of the chunk: exclusive prefix
+    int ecnt = ev ? cnt : 0;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int x = __shfl_up(ecnt, off);
+      if (lane >= off) ecnt += x;
+    }
     if (lane == 0) wcount[wave] = __popcll(sm);
+    if (lane == 63) wev[wave] = ecnt;
     __syncthreads();
-    int sid = carry_sid;
-    for (int w = 0; w < wave; ++w) sid += wcount[w];
+    int sid = carry_sid, ebase = 0, etot = 0;
+    for (int w = 0; w < kSegWaves; ++w) {
+      if (w < wave) {
+        sid += wcount[w];
+        ebase += wev[w];
+      }
+      etot += wev[w];
+    }
     sid += __popcll(sm & ((2ull << lane) - 1ull));  // inclusive: this tile's segment
+    const int64_t epos = ebase + ecnt - (ev ? cnt : 0);  // this tile's first element in the chunk's events
+    if (tid == 0) {
+      // the chunk's event quals, 16-B aligned, or none when the stream is full
+      const unsigned long long need = ((unsigned long long)etot + 15ull) & ~15ull;
+      const unsigned long long o = need ? atomicAdd(P.stream_used, need) : 0ull;
+      chunk_off = (o + need <= (unsigned long long)P.stream_cap) ? (int64_t)o : -1;
+    }
+    __syncthreads();
     if (live) {
       const int s = min(sid, kLast);
       atomicMin(&s_t0[s], (int32_t)tl);
@@ -434,20 +455,42 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
       if (sid >= kLast) {
         s_key[kLast] = INT32_MAX;  // overflow: folded from the read columns
       } else {
-        if (start) s_key[s] = key;
-        if (key == kEvent) atomicAdd(&s_n[s], cnt);
+        if (start) {
+          s_key[s] = key;
+          if (ev) s_off[s] = chunk_off < 0 ? -1 : chunk_off + epos;
+        }
+        if (ev) atomicAdd(&s_n[s], cnt);
         else atomicAdd(&s_inc[s], (unsigned long long)inc);
       }
     }
+    // copy the chunk's event tiles (those of regular segments), one wavefront per tile
+    const bool cp = ev && sid < kLast && chunk_off >= 0;
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(cp);
     __syncthreads();
-    const int last = (int)(min(c1, k0 + 1024) - k0) - 1;  // the chunk's last tile
+    if (lane == 0) wcount[wave] = __popcll(cm);
+    __syncthreads();
+    int cb = 0, ctot = 0;
+    for (int w = 0; w < kSegWaves; ++w) {
+      if (w < wave) cb += wcount[w];
+      ctot += wcount[w];
+    }
+    if (cp) {
+      const int i = cb + __popcll(cm & ((1ull << lane) - 1ull));
+      ev_tile[i] = (int32_t)tl;
+      ev_dst[i] = chunk_off + epos;
+    }
+    __syncthreads();
+    for (int k = wave; k < ctot; k += kSegWaves) fold_copy_tile(P, ev_tile[k], P.streams + ev_dst[k], lane);
+    const int last = (int)(min(c1, k0 + kSegThreads) - k0) - 1;  // the chunk's last tile
     if (tid == last) {
       carry_sid = sid;
-      carry_key = key;
       carry_r = Re;
     }
     __syncthreads();
   }
+#ifdef BQSR_FOLD_PROFILE
+  const long long pf_t1 = clock64();
+#endif
   const int ns = min(carry_sid + 1, kFoldMaxSegs);
   if (tid == 0) {
     seg0 = (int32_t)atomicAdd(P.seg_used, (uint32_t)ns);  // this block's place in the compact list
@@ -455,7 +498,6 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
     P.nseg[c] = ns;
   }
   __syncthreads();
-  // the segments; event segments get their stream space
   if (tid < ns) {
     FoldSeg g;
     g.t0 = s_t0[tid];
@@ -467,42 +509,20 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
       g.kind = kSegGlobal;
       g.inc = 0;
     } else if (key == kEvent) {
-      g.kind = kSegEvent;
       g.inc = s_n[tid];  // element count
-      const unsigned long long o = atomicAdd(P.stream_used, (unsigned long long)s_n[tid]);
-      if (o + (unsigned long long)s_n[tid] <= (unsigned long long)P.stream_cap) g.off = (int64_t)o;
-      else g.kind = kSegGlobal;  // no stream room: folded from the read columns
+      g.off = s_off[tid];
+      g.kind = g.off >= 0 ? kSegEvent : kSegGlobal;  // no stream room: folded from the read columns
     } else {
       g.kind = kSegRun;
       g.e = key;
       g.inc = (int64_t)s_inc[tid];
     }
-    out[tid] = g;
     P.seg[seg0 + tid] = g;
   }
-  __syncthreads();
-  // copy the event segments' tiles, one wavefront per tile, each at its
-  // element offset in its segment's stream
-  for (int s = 0; s < ns; ++s) {
-    const FoldSeg g = out[s];
-    if (g.kind != kSegEvent) continue;
-    for (int64_t k0 = g.t0; k0 <= g.t1; k0 += 1024) {
-      if (tid == 0) {
-        int64_t acc = 0;
-        for (int64_t tl = g.t0; tl < k0; ++tl) acc += P.ntile[tl];
-        int k = 0;
-        for (int64_t tl = k0; tl <= g.t1 && k < 1024; ++tl, ++k) {
-          ev_tile[k] = (int32_t)tl;
-          ev_pos[k] = (int32_t)acc;
-          acc += P.ntile[tl];
-        }
-        n_ev = k;
-      }
-      __syncthreads();
-      for (int k = wave; k < n_ev; k += 16) fold_copy_tile(P, ev_tile[k], P.streams + g.off + ev_pos[k], lane);
-      __syncthreads();
-    }
-  }
+#ifdef BQSR_FOLD_PROFILE
+  if (tid == 0)
+    printf("FOLDSEGS c %d tiles %lld segs %d cycles %lld\n", c, (long long)(c1 - c0), ns, pf_t1 - pf_t0);
+#endif
 }
 
 // --------------------------------------------------------------- chain ----
@@ -513,79 +533,114 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_segs(FoldParams P) 
 // the binade or hold a tie, a second scan over that lane's 64 elements finds
 // the element, and that element is added in IEEE double arithmetic.
 // inc / tie: LDS tables of binade cur_e (rebuilt when S changes binade).
+#ifdef BQSR_FOLD_PROFILE
+__device__ long long g_fold_pf[8];  // seq adds, seq cycles, windows, window cycles, events, event cycles, tables
+#define FPF(i, v) (lane == 0 ? (void)atomicAdd((unsigned long long*)&g_fold_pf[i], (unsigned long long)(v)) : (void)0)
+#else
+#define FPF(i, v) (void)0
+#endif
 __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, const double* t, double* inc,
-                                            uint8_t* tie, int& cur_e, int lane) {
+                                            int& cur_e, int lane) {
   int pos = 0;
   while (pos < n) {
-    if (S == 0.0) {  // 0.0 + t is exact
-      S = t[q[pos]];
-      ++pos;
+#ifdef BQSR_FOLD_PROFILE
+    const long long c0 = clock64();
+#endif
+    if (S < kFoldSeqLimit) {
+      // small S: binades change every few additions and ties are common --
+      // add one by one (every lane the same chain), 64 operands per load round
+      const int k = pos + lane;
+      const double x = k < n ? t[q[k] & 0x7F] : 0.0;
+      const int m = min(64, n - pos);
+      int j = 0;
+      for (; j < m && S < kFoldSeqLimit; ++j) {
+        const uint64_t xb = (uint64_t)__double_as_longlong(x);
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)xb, j), hi = __builtin_amdgcn_readlane((uint32_t)(xb >> 32), j);
+        S = S + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+      }
+      pos += j;
+      FPF(0, j);
+      FPF(1, clock64() - c0);
       continue;
     }
     const int e = ilogb(S);
     if (e != cur_e) {
+      FPF(6, 1);
       for (int k = lane; k < kQBins; k += 64) {
         bool tq;
-        inc[k] = fold_inc(t[k], e, &tq);
-        tie[k] = tq;
+        const double d = fold_inc(t[k], e, &tq);
+        inc[k] = tq ? -1.0 : d;  // a tie is flagged by a negative increment
       }
       cur_e = e;
       wave_sync();
     }
     const double N0 = S * pow2i(52 - e);  // S / u, an integer < 2^53
     const double head = kTwo53 - N0;     // increments left before the binade ends
-    const int a = pos + 64 * lane, bnd = min(a + 64, n);
-    double sum = 0.0;
+    // lane l: elements pos + 64 l .. + 63; loads and lookups without branches
+    // (a sum only needs to be exact below head <= 2^52: rounding above it
+    // cannot bring it back below)
+    const int a = pos + 64 * lane;
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
     bool th = false;
-    for (int k0 = a; k0 < bnd; k0 += 16) {
-      int qq[16];
+    if (a < n) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) qq[j] = k0 + j < bnd ? (int)q[k0 + j] : -1;
+      for (int i0 = 0; i0 < 64; i0 += 16) {
+        int qq[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (qq[j] >= 0) {
-          sum = fmin(sum + inc[qq[j]], 0x1p53);  // saturating: exact while it matters
-          th |= tie[qq[j]] != 0;
+        for (int j = 0; j < 16; ++j) qq[j] = q[a + i0 + j];  // (buffers have 64 B of slack)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const double d = inc[qq[j] & 0x7F];
+          const bool ok = a + i0 + j < n;
+          th |= ok && d < 0.0;
+          s4[j & 3] += ok ? fmax(d, 0.0) : 0.0;
         }
+      }
     }
+    const double sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     double incl = sum;
     for (int off = 1; off < 64; off <<= 1) {
       const double x = __shfl_up(incl, off);
-      if (lane >= off) incl = fmin(incl + x, 0x1p54);
+      if (lane >= off) incl += x;
     }
-    const uint64_t hit = __builtin_amdgcn_ballot_w64(a < bnd && (incl >= head || th));
+    const uint64_t hit = __builtin_amdgcn_ballot_w64(a < n && (incl >= head || th));
     if (!hit) {  // the whole window stays in the binade
       S = (N0 + __shfl(incl, 63)) * pow2i(e - 52);
       pos = min(n, pos + 64 * 64);
+      FPF(2, 1);
+      FPF(3, clock64() - c0);
       continue;
     }
     const int L = (int)__builtin_ctzll(hit);
     const double excl = L > 0 ? __shfl(incl, L - 1) : 0.0;  // < head: exact
     // lane L's elements, one per lane
     const int k = pos + 64 * L + lane;
-    const bool valid = k < min(pos + 64 * L + 64, n);
-    const int qk = valid ? (int)q[k] : 0;
-    const double v = valid ? inc[qk] : 0.0;
-    const bool tk = valid && tie[qk] != 0;
+    const bool valid = k < n;
+    const int qk = (int)q[k] & 0x7F;
+    const double d = inc[qk];
+    const bool tk = valid && d < 0.0;
+    const double v = valid ? fmax(d, 0.0) : 0.0;
     double sc = v;
     for (int off = 1; off < 64; off <<= 1) {
       const double x = __shfl_up(sc, off);
-      if (lane >= off) sc = fmin(sc + x, 0x1p54);
+      if (lane >= off) sc += x;
     }
-    double scx = __shfl_up(sc, 1);  // exclusive prefix (not sc - v: sc may have saturated)
+    double scx = __shfl_up(sc, 1);  // exclusive prefix
     if (lane == 0) scx = 0.0;
-    const uint64_t ev = __builtin_amdgcn_ballot_w64(valid && (tk || excl + sc >= head));
-    const int j = ev ? (int)__builtin_ctzll(ev) : 63;  // (an event exists: lane L signalled one)
-    const double before = N0 + excl + __shfl(scx, j);  // exact: below head <= 2^52
-    S = before * pow2i(e - 52) + t[__shfl(qk, j)];  // the exact IEEE addition the JVM performs
+    const uint64_t evm = __builtin_amdgcn_ballot_w64(valid && (tk || excl + sc >= head));
+    const int j = evm ? (int)__builtin_ctzll(evm) : 63;  // (an event exists: lane L signalled one)
+    const double before = N0 + excl + __shfl(scx, j);    // exact: below head <= 2^52
+    S = before * pow2i(e - 52) + t[__shfl(qk, j)];       // the exact IEEE addition the JVM performs
     pos = pos + 64 * L + j + 1;
+    FPF(4, 1);
+    FPF(5, clock64() - c0);
   }
   return S;
 }
 
 // one tile's folded quals into LDS scratch (the fallback path), then fold
 __device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, uint8_t* scratch, const double* t,
-                                   double* inc, uint8_t* tie, int& cur_e, int lane) {
+                                   double* inc, int& cur_e, int lane) {
   const ReadsDev& rd = P.rd;
   const int64_t r0 = tl * (int64_t)rd.reads_per_tile;
   const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
@@ -599,7 +654,7 @@ __device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, ui
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
   fold_copy_tile(P, tl, scratch, lane);
   wave_sync();
-  S = wave_fold(S, scratch, tot, t, inc, tie, cur_e, lane);
+  S = wave_fold(S, scratch, tot, t, inc, cur_e, lane);
   wave_sync();  // the scratch is free again
   return S;
 }
@@ -608,8 +663,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   extern __shared__ __align__(16) unsigned char chain_smem[];
   __shared__ double t[kQBins];
   __shared__ double inc[kQBins];
-  __shared__ uint8_t tie[kQBins];
-  __shared__ uint8_t scratch[kTileSlots];
+  __shared__ __align__(16) uint8_t scratch[kTileSlots + 64];
   __shared__ int32_t nseg_l[kMaxFoldBlocks], sbase_l[kMaxFoldBlocks];
   FoldBlock* blk = (FoldBlock*)chain_smem;                    // [n_blocks]
   FoldSeg* segs = (FoldSeg*)(blk + kMaxFoldBlocks);           // [kChainLdsSegs]
@@ -642,6 +696,10 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   }
   __syncthreads();
   if (tid >= 64) return;  // one wavefront walks the job
+#ifdef BQSR_FOLD_PROFILE
+  if (lane < 8) g_fold_pf[lane] = 0;
+  const long long pf_pre = clock64();
+#endif
   double S = 0.0;
   int cur_e = INT32_MIN;
   const int64_t nt = P.rd.n_tiles;
@@ -667,7 +725,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
       PF(++pf_blk_fb);
       // the bound failed (not expected): fold the block's tiles element by element
       for (int64_t tl = nt * b / nb; tl < nt * (b + 1) / nb; ++tl)
-        S = fold_tile_global(P, S, tl, scratch, t, inc, tie, cur_e, lane);
+        S = fold_tile_global(P, S, tl, scratch, t, inc, cur_e, lane);
       continue;
     }
     const int c = B.cidx;
@@ -686,14 +744,14 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
         }
         PF(++pf_run_fb);
       } else if (G.kind == kSegEvent) {
-        if (G.off + G.inc <= sl) {
-          S = wave_fold(S, streams + G.off, (int)G.inc, t, inc, tie, cur_e, lane);
+        if (G.off + G.inc <= sl) {  // (the LDS copy has 64 B of slack past sl)
+          S = wave_fold(S, streams + G.off, (int)G.inc, t, inc, cur_e, lane);
         } else {  // beyond the prefetched bytes: through the scratch buffer, 4 KB at a time
           for (int64_t o = 0; o < G.inc; o += kTileSlots) {
             const int m = (int)min((int64_t)kTileSlots, G.inc - o);
             for (int i = lane; i < m; i += 64) scratch[i] = P.streams[G.off + o + i];
             wave_sync();
-            S = wave_fold(S, scratch, m, t, inc, tie, cur_e, lane);
+            S = wave_fold(S, scratch, m, t, inc, cur_e, lane);
             wave_sync();
           }
         }
@@ -702,16 +760,18 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
       }
       PF(++pf_glob; pf_glob_tiles += G.t1 - G.t0 + 1);
       // kSegGlobal, or a run whose bound failed: element by element
-      for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, scratch, t, inc, tie, cur_e, lane);
+      for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, scratch, t, inc, cur_e, lane);
     }
   }
   if (lane == 0) P.em_out[0] = S;
 #ifdef BQSR_FOLD_PROFILE
   if (lane == 0)
     printf("FOLD2 cand %d stream_used %lld | blocks %lld fallback %lld | runs %lld fallback %lld | events %lld elems %lld | "
-           "global %lld tiles %lld | cycles %lld\n",
+           "global %lld tiles %lld | cycles %lld | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld cyc) "
+           "tables %lld\n",
            nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles,
-           clock64() - pf_c0);
+           clock64() - pf_c0, g_fold_pf[0], g_fold_pf[1], g_fold_pf[2], g_fold_pf[3], g_fold_pf[4], g_fold_pf[5],
+           g_fold_pf[6]);
 #endif
 }
 

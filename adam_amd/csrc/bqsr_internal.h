@@ -194,6 +194,8 @@ struct ObserveParams {
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----
 constexpr int32_t kFoldNoBase = INT32_MIN;  // FoldBlock::e of a block without folded bases
+constexpr int kSegBinades = 32;             // binades a candidate block's tiles are tabulated at
+constexpr double kFoldTie = -1.0, kFoldUnknown = -2.0;
 constexpr int kFoldMaxSegs = 64;            // segments per candidate block (the rest: one fallback segment)
 enum : int32_t { kSegRun = 0, kSegEvent = 1, kSegGlobal = 2 };
 
@@ -228,7 +230,8 @@ struct FoldParams {
   double* delta;             // relative bound of |exact - real| partial sums
   double* rtile;             // [n_tiles] candidate blocks' tiles: real sum
   int32_t* ntile;            //           folded bases
-  uint16_t* h2;              //           [128] qual histogram of the folded bases
+  double* dtile;             //           [kSegBinades] exact increments at the block's binades eb0 ..
+                             //           (kFoldTie / kFoldUnknown when a qual ties / not exact)
   FoldSeg* seg;              // segments of all candidate blocks, each block's consecutive
   int32_t* seg_base;         // [n_blocks] candidate c's first segment
   int32_t* nseg;             // [n_blocks] and count
