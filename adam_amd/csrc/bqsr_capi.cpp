@@ -365,7 +365,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
   if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_fold_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chain_lds());
+    e = hipFuncSetAttribute((const void*)bqsr_fold_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)chain_lds(kMaxFoldBlocks));
   if (e != hipSuccess) {
     bqsr_context_destroy(c);
     return fail(BQSR_ERR_DEVICE, std::string("context: ") + hipGetErrorString(e));
@@ -482,6 +483,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
         (st = dalloc(b->allocs, &F.seg_base, nbk)) != BQSR_OK || (st = dalloc(b->allocs, &F.nseg, nbk)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.seg_used, 1)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.streams, (size_t)F.stream_cap + 64)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &F.csum, (size_t)F.stream_cap / 64 * 2 + 2)) != BQSR_OK ||
         (st = dalloc(b->allocs, &F.stream_used, 1)) != BQSR_OK)
       return st;
   }
@@ -1081,7 +1083,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
     hipLaunchKernelGGL(bqsr_fold_tiles, dim3(ctx->n_cu * 4), dim3(kFtWaves * 64), 0, s, F, max_tpb);
     hipLaunchKernelGGL(bqsr_fold_segs, dim3(b->n_blocks), dim3(kSegThreads), 0, s, F);
-    hipLaunchKernelGGL(bqsr_fold_chain, dim3(1), dim3(1024), chain_lds(), s, F);
+    hipLaunchKernelGGL(bqsr_fold_chain, dim3(1), dim3(1024), chain_lds(b->n_blocks), s, F);
     HIP_TRY(hipGetLastError());
   }
   return ok();

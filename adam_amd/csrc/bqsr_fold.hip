@@ -50,11 +50,16 @@ constexpr double kFoldSeqLimit = 0.0625;  // below, binades change every few add
 constexpr double kTwo53 = 9007199254740992.0;
 constexpr int kChainLdsSegs = 384;         // segments prefetched into the chain's LDS
 constexpr int kSegThreads = 512, kSegWaves = kSegThreads / 64;  // bqsr_fold_segs workgroup
-constexpr int kChainLdsStream = 96 * 1024;  // stream bytes prefetched into the chain's LDS
-constexpr size_t chain_lds() {
-  return (size_t)kMaxFoldBlocks * sizeof(FoldBlock) + (size_t)kChainLdsSegs * sizeof(FoldSeg) + kChainLdsStream + 64;
+constexpr int kChainLdsStream = 80 * 1024;  // stream bytes prefetched into the chain's LDS
+constexpr size_t chain_lds(int n_blocks) {
+  return kChainLdsStream + 64 + (size_t)kChainLdsStream / 64 * 2 * sizeof(double) + (size_t)kChainLdsSegs * sizeof(FoldSeg) +
+         (size_t)n_blocks * sizeof(FoldBlock);
 }
 
+// the binade of a positive normal double (its unbiased exponent); 0 -> -1023
+__device__ __forceinline__ int expo(double x) {
+  return (int)(((uint64_t)__double_as_longlong(x) >> 52) & 0x7FF) - 1023;
+}
 // 2^k as a double from its exponent bits (k in the normal range)
 __device__ __forceinline__ double pow2i(int k) { return __longlong_as_double((long long)(1023 + k) << 52); }
 
@@ -69,10 +74,10 @@ __device__ __forceinline__ double fold_inc(double t, int e, bool* tie) {
 // the binades a candidate block's tiles may stay in: from where its widened
 // real span reaches kFoldSeqLimit (or its start) to its end; eb0 and count
 __device__ __forceinline__ int block_eb0(const FoldBlock& B, double delta) {
-  return ilogb(fmax(B.r0 * (1.0 - delta), kFoldSeqLimit));
+  return expo(fmax(B.r0 * (1.0 - delta), kFoldSeqLimit));
 }
 __device__ __forceinline__ int block_nbin(const FoldBlock& B, double delta) {
-  return min(ilogb(fmax(B.r1 * (1.0 + delta), kFoldSeqLimit)) - block_eb0(B, delta) + 1, kSegBinades);
+  return min(expo(fmax(B.r1 * (1.0 + delta), kFoldSeqLimit)) - block_eb0(B, delta) + 1, kSegBinades);
 }
 
 // ---------------------------------------------------------------- plan ----
@@ -158,8 +163,8 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
     const bool live = b < nb && scn[min(b, nb - 1)] > 0;
     const double R0 = b < nb ? pre[b] : 0.0, R1 = b < nb ? pre[b] + sre[b] : 0.0;
     const double lo = R0 * (1.0 - delta), hi = R1 * (1.0 + delta);
-    bool cand = live && (lo < kFoldSeqLimit * (1.0 + delta) || ilogb(lo) != ilogb(hi));
-    const int e = (live && !cand) ? ilogb(lo) : 0;
+    bool cand = live && (lo < kFoldSeqLimit * (1.0 + delta) || expo(lo) != expo(hi));
+    const int e = (live && !cand) ? expo(lo) : 0;
     double inc = 0.0;
     bool tie = false;
     if (live && !cand) {
@@ -343,28 +348,27 @@ __device__ void fold_copy_tile(const FoldParams& P, int64_t tl, uint8_t* dst, in
 extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldParams P) {
   const int c = blockIdx.x;
   if (c >= *P.n_cand) return;
-  __shared__ double wsum[16];
-  __shared__ int32_t wcount[16], wev[16];
+  __shared__ double t[kQBins];
+  __shared__ double wsum[kSegWaves];
+  __shared__ int32_t wcount[kSegWaves], wev[kSegWaves];
   __shared__ int32_t keys[kSegThreads];
   __shared__ unsigned long long s_inc[kFoldMaxSegs];
   __shared__ int32_t s_n[kFoldMaxSegs], s_t0[kFoldMaxSegs], s_t1[kFoldMaxSegs], s_key[kFoldMaxSegs];
+  __shared__ int32_t s_e0[kFoldMaxSegs], s_epos0[kFoldMaxSegs];
   __shared__ int64_t s_off[kFoldMaxSegs];
-  __shared__ int32_t carry_sid;
+  __shared__ int32_t carry_sid, chunk_sid0;
   __shared__ double carry_r;
-  __shared__ int64_t chunk_off;
   __shared__ int32_t ev_tile[kSegThreads];
   __shared__ int64_t ev_dst[kSegThreads];
-  __shared__ FoldSeg out[kFoldMaxSegs];
   __shared__ int32_t seg0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef BQSR_FOLD_PROFILE
   const long long pf_t0 = clock64();
 #endif
+  for (int q = tid; q < kQBins; q += kSegThreads) t[q] = P.pow10[q];
   const int b = P.cand_list[c];
   const FoldBlock B = P.blk[b];
   const double delta = *P.delta;
-  // the binades the block's tiles may stay in: from where the real sum
-  // reaches kFoldSeqLimit (or the block's start) to the block's end
   const int eb0 = block_eb0(B, delta), nbin = block_nbin(B, delta);
   const int64_t nt = P.rd.n_tiles;
   const int64_t c0 = nt * b / P.n_blocks, c1 = nt * (b + 1) / P.n_blocks;
@@ -405,8 +409,8 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     int64_t inc = 0;
     if (live) {
       const double lo = Rt * (1.0 - delta), hi = Re * (1.0 + delta);
-      const int e = ilogb(lo), k = e - eb0;
-      if (lo >= kFoldSeqLimit * (1.0 + delta) && ilogb(lo) == ilogb(hi) && k >= 0 && k < nbin) {
+      const int e = expo(lo), k = e - eb0;
+      if (lo >= kFoldSeqLimit * (1.0 + delta) && e == expo(hi) && k >= 0 && k < nbin) {
         const double d = P.dtile[tl * kSegBinades + k];
         if (d >= 0.0) {
           key = e;
@@ -422,8 +426,7 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     const bool start = live && key != prev;
     const bool ev = live && key == kEvent;
     const uint64_t sm = __builtin_amdgcn_ballot_w64(start);
-    // event elements of the chunk: exclusive prefix
-    int ecnt = ev ? cnt : 0;
+    int ecnt = ev ? cnt : 0;  // event elements of the chunk: inclusive prefix
     for (int off = 1; off < 64; off <<= 1) {
       const int x = __shfl_up(ecnt, off);
       if (lane >= off) ecnt += x;
@@ -431,23 +434,14 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     if (lane == 0) wcount[wave] = __popcll(sm);
     if (lane == 63) wev[wave] = ecnt;
     __syncthreads();
-    int sid = carry_sid, ebase = 0, etot = 0;
-    for (int w = 0; w < kSegWaves; ++w) {
-      if (w < wave) {
-        sid += wcount[w];
-        ebase += wev[w];
-      }
-      etot += wev[w];
+    int sid = carry_sid, ebase = 0;
+    for (int w = 0; w < wave; ++w) {
+      sid += wcount[w];
+      ebase += wev[w];
     }
-    sid += __popcll(sm & ((2ull << lane) - 1ull));  // inclusive: this tile's segment
-    const int64_t epos = ebase + ecnt - (ev ? cnt : 0);  // this tile's first element in the chunk's events
-    if (tid == 0) {
-      // the chunk's event quals, 16-B aligned, or none when the stream is full
-      const unsigned long long need = ((unsigned long long)etot + 15ull) & ~15ull;
-      const unsigned long long o = need ? atomicAdd(P.stream_used, need) : 0ull;
-      chunk_off = (o + need <= (unsigned long long)P.stream_cap) ? (int64_t)o : -1;
-    }
-    __syncthreads();
+    sid += __popcll(sm & ((2ull << lane) - 1ull));      // inclusive: this tile's segment
+    const int epos = ebase + ecnt - (ev ? cnt : 0);    // this tile's first element among the chunk's events
+    if (tid == 0) chunk_sid0 = carry_sid + 1;           // the first segment starting in this chunk
     if (live) {
       const int s = min(sid, kLast);
       atomicMin(&s_t0[s], (int32_t)tl);
@@ -457,16 +451,31 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
       } else {
         if (start) {
           s_key[s] = key;
-          if (ev) s_off[s] = chunk_off < 0 ? -1 : chunk_off + epos;
+          s_epos0[s] = epos;
+          s_e0[s] = expo(fmax(Rt * (1.0 - delta), kFoldSeqLimit));
         }
         if (ev) atomicAdd(&s_n[s], cnt);
         else atomicAdd(&s_inc[s], (unsigned long long)inc);
       }
     }
-    // copy the chunk's event tiles (those of regular segments), one wavefront per tile
-    const bool cp = ev && sid < kLast && chunk_off >= 0;
-    const uint64_t cm = __builtin_amdgcn_ballot_w64(cp);
+    const int last = (int)(min(c1, k0 + kSegThreads) - k0) - 1;  // the chunk's last tile
     __syncthreads();
+    // the chunk's event segments (complete now): 64-B aligned stream space
+    if (tid == last) carry_sid = sid;
+    __syncthreads();
+    const int s_lo = chunk_sid0, s_hi = min(carry_sid, kLast - 1);
+    if (tid <= s_hi - s_lo) {
+      const int s = s_lo + tid;
+      if (s_key[s] == kEvent) {
+        const unsigned long long need = ((unsigned long long)s_n[s] + 63ull) & ~63ull;
+        const unsigned long long o = atomicAdd(P.stream_used, need);
+        s_off[s] = (o + need <= (unsigned long long)P.stream_cap) ? (int64_t)o : -1;
+      }
+    }
+    __syncthreads();
+    // copy the chunk's event tiles, one wavefront per tile
+    const bool cp = ev && sid < kLast && s_off[min(sid, kLast)] >= 0;
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(cp);
     if (lane == 0) wcount[wave] = __popcll(cm);
     __syncthreads();
     int cb = 0, ctot = 0;
@@ -477,15 +486,42 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     if (cp) {
       const int i = cb + __popcll(cm & ((1ull << lane) - 1ull));
       ev_tile[i] = (int32_t)tl;
-      ev_dst[i] = chunk_off + epos;
+      ev_dst[i] = s_off[sid] + (epos - s_epos0[sid]);
     }
     __syncthreads();
     for (int k = wave; k < ctot; k += kSegWaves) fold_copy_tile(P, ev_tile[k], P.streams + ev_dst[k], lane);
-    const int last = (int)(min(c1, k0 + kSegThreads) - k0) - 1;  // the chunk's last tile
-    if (tid == last) {
-      carry_sid = sid;
-      carry_r = Re;
+    __syncthreads();  // (the copies are visible to the workgroup)
+    // per 64 quals of the chunk's event streams: exact increments at the
+    // segment's binades e0, e0 + 1, one thread per 64 quals
+    int64_t tot = 0;
+    for (int s = s_lo; s <= s_hi; ++s)
+      if (s_key[s] == kEvent && s_off[s] >= 0) tot += (s_n[s] + 63) / 64;
+    for (int64_t f = tid; f < tot; f += kSegThreads) {
+      int s = s_lo;
+      int64_t j = f;
+      for (; s <= s_hi; ++s) {
+        if (!(s_key[s] == kEvent && s_off[s] >= 0)) continue;
+        const int64_t nch = (s_n[s] + 63) / 64;
+        if (j < nch) break;
+        j -= nch;
+      }
+      const int64_t o = s_off[s] + 64 * j;
+      const int m = (int)min((int64_t)64, (int64_t)s_n[s] - 64 * j);
+      const int e0 = s_e0[s];
+      double d0 = 0.0, d1 = 0.0;
+      bool t0 = false, t1 = false;
+      for (int i = 0; i < m; ++i) {
+        const int q = P.streams[o + i] & 0x7F;
+        bool a0, a1;
+        d0 += fold_inc(t[q], e0, &a0);
+        d1 += fold_inc(t[q], e0 + 1, &a1);
+        t0 |= a0;
+        t1 |= a1;
+      }
+      P.csum[(o / 64) * 2] = t0 ? kFoldTie : (d0 < 0x1p52 ? d0 : kFoldUnknown);
+      P.csum[(o / 64) * 2 + 1] = t1 ? kFoldTie : (d1 < 0x1p52 ? d1 : kFoldUnknown);
     }
+    if (tid == last) carry_r = Re;
     __syncthreads();
   }
 #ifdef BQSR_FOLD_PROFILE
@@ -511,6 +547,7 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     } else if (key == kEvent) {
       g.inc = s_n[tid];  // element count
       g.off = s_off[tid];
+      g.e = s_e0[tid];
       g.kind = g.off >= 0 ? kSegEvent : kSegGlobal;  // no stream room: folded from the read columns
     } else {
       g.kind = kSegRun;
@@ -528,19 +565,25 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
 // --------------------------------------------------------------- chain ----
 
 // Fold elements [0, n) of q (LDS) into S exactly, one wavefront, no serial
-// loop: lane l sums the increments of elements pos + 64 l .. + 63 at the
-// current binade, a wavefront scan finds the first lane whose elements leave
-// the binade or hold a tie, a second scan over that lane's 64 elements finds
-// the element, and that element is added in IEEE double arithmetic.
-// inc / tie: LDS tables of binade cur_e (rebuilt when S changes binade).
+// loop over elements:
+//  * S < kFoldSeqLimit: one addition at a time, 64 operands per load round;
+//  * at a 64-element boundary, in binade e0 or e0 + 1 of the precomputed
+//    per-64 increments cs (kSegEvent streams): lane l takes the sum of the
+//    l-th next 64 elements, a wavefront scan finds the first group that leaves
+//    the binade or holds a tie;
+//  * otherwise lane l sums the increments of elements pos + 64 l .. + 63;
+//  * inside the group found (or the rest of a partial group) lane j takes
+//    element j, a second scan finds the element, which is added in IEEE
+//    double arithmetic.
+// inc: LDS table of binade cur_e (a tie is a negative increment).
 #ifdef BQSR_FOLD_PROFILE
-__device__ long long g_fold_pf[8];  // seq adds, seq cycles, windows, window cycles, events, event cycles, tables
+__device__ long long g_fold_pf[8];  // seq adds, seq cycles, windows, window cycles, events, event cycles, tables, chunk windows
 #define FPF(i, v) (lane == 0 ? (void)atomicAdd((unsigned long long*)&g_fold_pf[i], (unsigned long long)(v)) : (void)0)
 #else
 #define FPF(i, v) (void)0
 #endif
-__device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, const double* t, double* inc,
-                                            int& cur_e, int lane) {
+__device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, const double* cs, int e0,
+                                            const double* t, double* inc, int& cur_e, int lane) {
   int pos = 0;
   while (pos < n) {
 #ifdef BQSR_FOLD_PROFILE
@@ -563,7 +606,7 @@ __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, c
       FPF(1, clock64() - c0);
       continue;
     }
-    const int e = ilogb(S);
+    const int e = expo(S);
     if (e != cur_e) {
       FPF(6, 1);
       for (int k = lane; k < kQBins; k += 64) {
@@ -576,64 +619,89 @@ __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, c
     }
     const double N0 = S * pow2i(52 - e);  // S / u, an integer < 2^53
     const double head = kTwo53 - N0;     // increments left before the binade ends
-    // lane l: elements pos + 64 l .. + 63; loads and lookups without branches
-    // (a sum only needs to be exact below head <= 2^52: rounding above it
-    // cannot bring it back below)
-    const int a = pos + 64 * lane;
-    double s4[4] = {0.0, 0.0, 0.0, 0.0};
-    bool th = false;
-    if (a < n) {
-#pragma unroll
-      for (int i0 = 0; i0 < 64; i0 += 16) {
-        int qq[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) qq[j] = q[a + i0 + j];  // (buffers have 64 B of slack)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const double d = inc[qq[j] & 0x7F];
-          const bool ok = a + i0 + j < n;
-          th |= ok && d < 0.0;
-          s4[j & 3] += ok ? fmax(d, 0.0) : 0.0;
+    // (a sum only needs to be exact below head <= 2^52: rounding above it cannot bring it back below)
+    int g0 = pos;    // start of the group the element step examines
+    int gn = 64;     // its length
+    double excl = 0.0;
+    bool element_step = false;
+    if ((pos & 63) != 0) {  // the rest of a partial group first
+      gn = 64 - (pos & 63);
+      element_step = true;
+    } else {
+      double sum = 0.0;
+      bool bad = false;
+      const int a = pos + 64 * lane;
+      if (cs && (e == e0 || e == e0 + 1)) {
+        if (a < n) {
+          const double d = cs[(a >> 6) * 2 + (e - e0)];
+          bad = d < 0.0;  // a tie, or not exact (then it surely leaves the binade)
+          sum = bad ? 0.0 : d;
         }
+        FPF(7, 1);
+      } else if (a < n) {
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i0 = 0; i0 < 64; i0 += 16) {
+          int qq[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) qq[j] = q[a + i0 + j];  // (buffers have 64 B of slack)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const double d = inc[qq[j] & 0x7F];
+            const bool ok = a + i0 + j < n;
+            bad |= ok && d < 0.0;
+            s4[j & 3] += ok ? fmax(d, 0.0) : 0.0;
+          }
+        }
+        sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
       }
+      double incl = sum;
+      for (int off = 1; off < 64; off <<= 1) {
+        const double x = __shfl_up(incl, off);
+        if (lane >= off) incl += x;
+      }
+      const uint64_t hit = __builtin_amdgcn_ballot_w64(a < n && (incl >= head || bad));
+      if (!hit) {  // the whole window stays in the binade
+        S = (N0 + __shfl(incl, 63)) * pow2i(e - 52);
+        pos = min(n, pos + 64 * 64);
+        FPF(2, 1);
+        FPF(3, clock64() - c0);
+        continue;
+      }
+      const int L = (int)__builtin_ctzll(hit);
+      excl = L > 0 ? __shfl(incl, L - 1) : 0.0;  // < head: exact
+      g0 = pos + 64 * L;
+      element_step = true;
     }
-    const double sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-    double incl = sum;
-    for (int off = 1; off < 64; off <<= 1) {
-      const double x = __shfl_up(incl, off);
-      if (lane >= off) incl += x;
+    if (element_step) {
+      // elements g0 .. g0 + gn - 1, one per lane
+      const int k = g0 + lane;
+      const bool valid = lane < gn && k < n;
+      const int qk = (int)q[k] & 0x7F;
+      const double d = inc[qk];
+      const bool tk = valid && d < 0.0;
+      const double v = valid ? fmax(d, 0.0) : 0.0;
+      double sc = v;
+      for (int off = 1; off < 64; off <<= 1) {
+        const double x = __shfl_up(sc, off);
+        if (lane >= off) sc += x;
+      }
+      double scx = __shfl_up(sc, 1);  // exclusive prefix
+      if (lane == 0) scx = 0.0;
+      const uint64_t evm = __builtin_amdgcn_ballot_w64(valid && (tk || excl + sc >= head));
+      if (!evm) {  // (only a partial group can have none): it stays in the binade
+        S = (N0 + excl + __shfl(sc, 63)) * pow2i(e - 52);
+        pos = min(n, g0 + gn);
+        FPF(5, clock64() - c0);
+        continue;
+      }
+      const int j = (int)__builtin_ctzll(evm);
+      const double before = N0 + excl + __shfl(scx, j);  // exact: below head <= 2^52
+      S = before * pow2i(e - 52) + t[__shfl(qk, j)];     // the exact IEEE addition the JVM performs
+      pos = g0 + j + 1;
+      FPF(4, 1);
+      FPF(5, clock64() - c0);
     }
-    const uint64_t hit = __builtin_amdgcn_ballot_w64(a < n && (incl >= head || th));
-    if (!hit) {  // the whole window stays in the binade
-      S = (N0 + __shfl(incl, 63)) * pow2i(e - 52);
-      pos = min(n, pos + 64 * 64);
-      FPF(2, 1);
-      FPF(3, clock64() - c0);
-      continue;
-    }
-    const int L = (int)__builtin_ctzll(hit);
-    const double excl = L > 0 ? __shfl(incl, L - 1) : 0.0;  // < head: exact
-    // lane L's elements, one per lane
-    const int k = pos + 64 * L + lane;
-    const bool valid = k < n;
-    const int qk = (int)q[k] & 0x7F;
-    const double d = inc[qk];
-    const bool tk = valid && d < 0.0;
-    const double v = valid ? fmax(d, 0.0) : 0.0;
-    double sc = v;
-    for (int off = 1; off < 64; off <<= 1) {
-      const double x = __shfl_up(sc, off);
-      if (lane >= off) sc += x;
-    }
-    double scx = __shfl_up(sc, 1);  // exclusive prefix
-    if (lane == 0) scx = 0.0;
-    const uint64_t evm = __builtin_amdgcn_ballot_w64(valid && (tk || excl + sc >= head));
-    const int j = evm ? (int)__builtin_ctzll(evm) : 63;  // (an event exists: lane L signalled one)
-    const double before = N0 + excl + __shfl(scx, j);    // exact: below head <= 2^52
-    S = before * pow2i(e - 52) + t[__shfl(qk, j)];       // the exact IEEE addition the JVM performs
-    pos = pos + 64 * L + j + 1;
-    FPF(4, 1);
-    FPF(5, clock64() - c0);
   }
   return S;
 }
@@ -654,7 +722,7 @@ __device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, ui
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
   fold_copy_tile(P, tl, scratch, lane);
   wave_sync();
-  S = wave_fold(S, scratch, tot, t, inc, cur_e, lane);
+  S = wave_fold(S, scratch, tot, nullptr, 0, t, inc, cur_e, lane);
   wave_sync();  // the scratch is free again
   return S;
 }
@@ -665,11 +733,16 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   __shared__ double inc[kQBins];
   __shared__ __align__(16) uint8_t scratch[kTileSlots + 64];
   __shared__ int32_t nseg_l[kMaxFoldBlocks], sbase_l[kMaxFoldBlocks];
-  FoldBlock* blk = (FoldBlock*)chain_smem;                    // [n_blocks]
-  FoldSeg* segs = (FoldSeg*)(blk + kMaxFoldBlocks);           // [kChainLdsSegs]
-  uint8_t* streams = (uint8_t*)(segs + kChainLdsSegs);        // [kChainLdsStream]
+#ifdef BQSR_FOLD_PROFILE
+  const long long pf_k0 = clock64();
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int nb = P.n_blocks, nc = *P.n_cand;
+  // dynamic LDS (chain_lds): streams | per-64 increments | segments | blocks
+  uint8_t* streams = chain_smem;                                             // [kChainLdsStream + 64]
+  double* csum = (double*)(chain_smem + kChainLdsStream + 64);               // [kChainLdsStream / 64][2]
+  FoldSeg* segs = (FoldSeg*)(csum + kChainLdsStream / 64 * 2);               // [kChainLdsSegs]
+  FoldBlock* blk = (FoldBlock*)(segs + kChainLdsSegs);                       // [n_blocks]
   const int64_t used = (int64_t)*P.stream_used;
   const int64_t sl = min(used, (int64_t)kChainLdsStream);
   const int nsl = min((int)*P.seg_used, kChainLdsSegs);
@@ -693,12 +766,14 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
     const int64_t n16 = (sl + 15) / 16;
 #pragma unroll 4
     for (int64_t i = tid; i < n16; i += 1024) d4[i] = s4[i];
+    const int64_t nc2 = sl / 64 * 2;
+#pragma unroll 2
+    for (int64_t i = tid; i < nc2; i += 1024) csum[i] = P.csum[i];
   }
   __syncthreads();
   if (tid >= 64) return;  // one wavefront walks the job
 #ifdef BQSR_FOLD_PROFILE
   if (lane < 8) g_fold_pf[lane] = 0;
-  const long long pf_pre = clock64();
 #endif
   double S = 0.0;
   int cur_e = INT32_MIN;
@@ -714,7 +789,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
     const FoldBlock B = blk[b];
     if (B.cidx < 0) {  // no event expected: one integer addition
       if (B.e == kFoldNoBase) continue;
-      if (S >= kFoldSeqLimit && ilogb(S) == B.e) {
+      if (S >= kFoldSeqLimit && expo(S) == B.e) {
         const double N0 = S * pow2i(52 - B.e);
         if (N0 + B.inc < kTwo53) {
           S = (N0 + B.inc) * pow2i(B.e - 52);
@@ -734,7 +809,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
       const int64_t si = (int64_t)sbase_l[c] + s;
       const FoldSeg G = si < nsl ? segs[si] : P.seg[si];
       if (G.kind == kSegRun) {
-        if (S >= kFoldSeqLimit && ilogb(S) == G.e) {
+        if (S >= kFoldSeqLimit && expo(S) == G.e) {
           const double N0 = S * pow2i(52 - G.e);
           if (N0 + (double)G.inc < kTwo53) {
             S = (N0 + (double)G.inc) * pow2i(G.e - 52);
@@ -745,13 +820,13 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
         PF(++pf_run_fb);
       } else if (G.kind == kSegEvent) {
         if (G.off + G.inc <= sl) {  // (the LDS copy has 64 B of slack past sl)
-          S = wave_fold(S, streams + G.off, (int)G.inc, t, inc, cur_e, lane);
+          S = wave_fold(S, streams + G.off, (int)G.inc, csum + G.off / 64 * 2, G.e, t, inc, cur_e, lane);
         } else {  // beyond the prefetched bytes: through the scratch buffer, 4 KB at a time
           for (int64_t o = 0; o < G.inc; o += kTileSlots) {
             const int m = (int)min((int64_t)kTileSlots, G.inc - o);
             for (int i = lane; i < m; i += 64) scratch[i] = P.streams[G.off + o + i];
             wave_sync();
-            S = wave_fold(S, scratch, m, t, inc, cur_e, lane);
+            S = wave_fold(S, scratch, m, P.csum + (G.off + o) / 64 * 2, G.e, t, inc, cur_e, lane);
             wave_sync();
           }
         }
@@ -767,11 +842,11 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
 #ifdef BQSR_FOLD_PROFILE
   if (lane == 0)
     printf("FOLD2 cand %d stream_used %lld | blocks %lld fallback %lld | runs %lld fallback %lld | events %lld elems %lld | "
-           "global %lld tiles %lld | cycles %lld | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld cyc) "
-           "tables %lld\n",
+           "global %lld tiles %lld | cycles %lld (prefetch %lld) | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld "
+           "cyc) tables %lld chunkwin %lld\n",
            nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles,
-           clock64() - pf_c0, g_fold_pf[0], g_fold_pf[1], g_fold_pf[2], g_fold_pf[3], g_fold_pf[4], g_fold_pf[5],
-           g_fold_pf[6]);
+           clock64() - pf_c0, pf_c0 - pf_k0, g_fold_pf[0], g_fold_pf[1], g_fold_pf[2], g_fold_pf[3], g_fold_pf[4],
+           g_fold_pf[5], g_fold_pf[6], g_fold_pf[7]);
 #endif
 }
 

@@ -212,7 +212,7 @@ static_assert(sizeof(FoldBlock) == 32, "FoldBlock is 4 words");
 struct FoldSeg {
   int64_t inc;         // kSegRun: exact increment at binade e; kSegEvent: element count
   int32_t t0, t1;      // tiles t0 .. t1
-  int32_t e;           // kSegRun: the binade
+  int32_t e;           // kSegRun: the binade; kSegEvent: the lowest binade >= kFoldSeqLimit it may start in
   int32_t kind;        // kSegRun / kSegEvent (quals at streams + off) / kSegGlobal (folded from the columns)
   int64_t off;
 };
@@ -236,7 +236,9 @@ struct FoldParams {
   int32_t* seg_base;         // [n_blocks] candidate c's first segment
   int32_t* nseg;             // [n_blocks] and count
   uint32_t* seg_used;
-  uint8_t* streams;          // event segments' quals in fold order
+  uint8_t* streams;          // event segments' quals in fold order, each segment 64-B aligned
+  double* csum;              // [stream_cap / 64][2] per 64 quals of a stream: exact increment at the
+                             // segment's binades e, e + 1 (kFoldTie / kFoldUnknown sentinels)
   int64_t stream_cap;
   unsigned long long* stream_used;
   double* em_out;            // [1]
