@@ -505,18 +505,27 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
         if (j < nch) break;
         j -= nch;
       }
-      const int64_t o = s_off[s] + 64 * j;
+      const int64_t o = s_off[s] + 64 * j;  // 64-B aligned
       const int m = (int)min((int64_t)64, (int64_t)s_n[s] - 64 * j);
       const int e0 = s_e0[s];
+      uint4 w4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w4[i] = *(const uint4*)(P.streams + o + 16 * i);  // (the stream has 64 B of slack)
       double d0 = 0.0, d1 = 0.0;
       bool t0 = false, t1 = false;
-      for (int i = 0; i < m; ++i) {
-        const int q = P.streams[o + i] & 0x7F;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint4 v4 = w4[i >> 4];
+        const uint32_t word = ((i >> 2) & 3) == 0 ? v4.x : ((i >> 2) & 3) == 1 ? v4.y : ((i >> 2) & 3) == 2 ? v4.z : v4.w;
+        const int q = (int)((word >> (8 * (i & 3))) & 0x7Fu);
         bool a0, a1;
-        d0 += fold_inc(t[q], e0, &a0);
-        d1 += fold_inc(t[q], e0 + 1, &a1);
-        t0 |= a0;
-        t1 |= a1;
+        const double i0 = fold_inc(t[q], e0, &a0), i1 = fold_inc(t[q], e0 + 1, &a1);
+        if (i < m) {
+          d0 += i0;
+          d1 += i1;
+          t0 |= a0;
+          t1 |= a1;
+        }
       }
       P.csum[(o / 64) * 2] = t0 ? kFoldTie : (d0 < 0x1p52 ? d0 : kFoldUnknown);
       P.csum[(o / 64) * 2 + 1] = t1 ? kFoldTie : (d1 < 0x1p52 ? d1 : kFoldUnknown);
@@ -807,7 +816,9 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
     const int ns = nseg_l[c];
     for (int s = 0; s < ns; ++s) {
       const int64_t si = (int64_t)sbase_l[c] + s;
-      const FoldSeg G = si < nsl ? segs[si] : P.seg[si];
+      FoldSeg G;
+      if (si < nsl) G = segs[si];  // (two branches: a select of the pointers would make it a flat load)
+      else G = P.seg[si];
       if (G.kind == kSegRun) {
         if (S >= kFoldSeqLimit && expo(S) == G.e) {
           const double N0 = S * pow2i(52 - G.e);
