@@ -585,6 +585,33 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
 //    element j, a second scan finds the element, which is added in IEEE
 //    double arithmetic.
 // inc: LDS table of binade cur_e (a tie is a negative increment).
+// Wavefront scans and broadcasts without LDS (DPP / readlane): the chain is
+// one wavefront on one CU, its cost is the latency of these steps.
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, kCtrl, kRowMask, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), kCtrl, kRowMask, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));  // 0.0 where no source lane
+}
+// inclusive prefix sum over the 64 lanes (row_shr 1, 2, 4, 8, then row_bcast 15 / 31)
+__device__ __forceinline__ double wave_incl_scan(double x) {
+  x += dpp_f64<0x111>(x);
+  x += dpp_f64<0x112>(x);
+  x += dpp_f64<0x114>(x);
+  x += dpp_f64<0x118>(x);
+  x += dpp_f64<0x142, 0xA>(x);
+  x += dpp_f64<0x143, 0xC>(x);
+  return x;
+}
+// the value of the previous lane (0.0 in lane 0): wave_shr 1
+__device__ __forceinline__ double wave_shr1(double x) { return dpp_f64<0x138>(x); }
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 #ifdef BQSR_FOLD_PROFILE
 __device__ long long g_fold_pf[8];  // seq adds, seq cycles, windows, window cycles, events, event cycles, tables, chunk windows
 #define FPF(i, v) (lane == 0 ? (void)atomicAdd((unsigned long long*)&g_fold_pf[i], (unsigned long long)(v)) : (void)0)
@@ -605,11 +632,7 @@ __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, c
       const double x = k < n ? t[q[k] & 0x7F] : 0.0;
       const int m = min(64, n - pos);
       int j = 0;
-      for (; j < m && S < kFoldSeqLimit; ++j) {
-        const uint64_t xb = (uint64_t)__double_as_longlong(x);
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)xb, j), hi = __builtin_amdgcn_readlane((uint32_t)(xb >> 32), j);
-        S = S + __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-      }
+      for (; j < m && S < kFoldSeqLimit; ++j) S = S + readlane_f64(x, j);
       pos += j;
       FPF(0, j);
       FPF(1, clock64() - c0);
@@ -664,21 +687,17 @@ __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, c
         }
         sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
       }
-      double incl = sum;
-      for (int off = 1; off < 64; off <<= 1) {
-        const double x = __shfl_up(incl, off);
-        if (lane >= off) incl += x;
-      }
+      const double incl = wave_incl_scan(sum);
       const uint64_t hit = __builtin_amdgcn_ballot_w64(a < n && (incl >= head || bad));
       if (!hit) {  // the whole window stays in the binade
-        S = (N0 + __shfl(incl, 63)) * pow2i(e - 52);
+        S = (N0 + readlane_f64(incl, 63)) * pow2i(e - 52);
         pos = min(n, pos + 64 * 64);
         FPF(2, 1);
         FPF(3, clock64() - c0);
         continue;
       }
       const int L = (int)__builtin_ctzll(hit);
-      excl = L > 0 ? __shfl(incl, L - 1) : 0.0;  // < head: exact
+      excl = L > 0 ? readlane_f64(incl, L - 1) : 0.0;  // < head: exact
       g0 = pos + 64 * L;
       element_step = true;
     }
@@ -690,23 +709,18 @@ __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, c
       const double d = inc[qk];
       const bool tk = valid && d < 0.0;
       const double v = valid ? fmax(d, 0.0) : 0.0;
-      double sc = v;
-      for (int off = 1; off < 64; off <<= 1) {
-        const double x = __shfl_up(sc, off);
-        if (lane >= off) sc += x;
-      }
-      double scx = __shfl_up(sc, 1);  // exclusive prefix
-      if (lane == 0) scx = 0.0;
+      const double sc = wave_incl_scan(v);
+      const double scx = wave_shr1(sc);  // exclusive prefix
       const uint64_t evm = __builtin_amdgcn_ballot_w64(valid && (tk || excl + sc >= head));
       if (!evm) {  // (only a partial group can have none): it stays in the binade
-        S = (N0 + excl + __shfl(sc, 63)) * pow2i(e - 52);
+        S = (N0 + excl + readlane_f64(sc, 63)) * pow2i(e - 52);
         pos = min(n, g0 + gn);
         FPF(5, clock64() - c0);
         continue;
       }
       const int j = (int)__builtin_ctzll(evm);
-      const double before = N0 + excl + __shfl(scx, j);  // exact: below head <= 2^52
-      S = before * pow2i(e - 52) + t[__shfl(qk, j)];     // the exact IEEE addition the JVM performs
+      const double before = N0 + excl + readlane_f64(scx, j);                // exact: below head <= 2^52
+      S = before * pow2i(e - 52) + t[__builtin_amdgcn_readlane((uint32_t)qk, j)];  // the exact IEEE addition
       pos = g0 + j + 1;
       FPF(4, 1);
       FPF(5, clock64() - c0);
