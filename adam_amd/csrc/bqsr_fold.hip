@@ -618,8 +618,13 @@ __device__ long long g_fold_pf[8];  // seq adds, seq cycles, windows, window cyc
 #else
 #define FPF(i, v) (void)0
 #endif
-__device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, const double* cs, int e0,
-                                            const double* t, double* inc, int& cur_e, int lane) {
+#define LDS __attribute__((address_space(3)))
+// one copy (noinline: the chain is a single wavefront whose time goes to
+// latency, and a kernel this size also misses in the instruction cache);
+// every buffer is LDS, cur_e included
+__device__ __noinline__ double wave_fold(double S, const LDS uint8_t* q, int n, const LDS double* cs, int e0,
+                                         const LDS double* t, LDS double* inc, LDS int* cur_ep, int lane) {
+  int cur_e = *cur_ep;
   int pos = 0;
   while (pos < n) {
 #ifdef BQSR_FOLD_PROFILE
@@ -726,12 +731,13 @@ __device__ __forceinline__ double wave_fold(double S, const uint8_t* q, int n, c
       FPF(5, clock64() - c0);
     }
   }
+  *cur_ep = cur_e;
   return S;
 }
 
 // one tile's folded quals into LDS scratch (the fallback path), then fold
-__device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, uint8_t* scratch, const double* t,
-                                   double* inc, int& cur_e, int lane) {
+__device__ __noinline__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, LDS uint8_t* scratch,
+                                                const LDS double* t, LDS double* inc, LDS int* cur_e, int lane) {
   const ReadsDev& rd = P.rd;
   const int64_t r0 = tl * (int64_t)rd.reads_per_tile;
   const int nr = (int)min((int64_t)rd.reads_per_tile, rd.n_reads - r0);
@@ -743,7 +749,7 @@ __device__ double fold_tile_global(const FoldParams& P, double S, int64_t tl, ui
   }
   int tot = len;
   for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
-  fold_copy_tile(P, tl, scratch, lane);
+  fold_copy_tile(P, tl, (uint8_t*)scratch, lane);
   wave_sync();
   S = wave_fold(S, scratch, tot, nullptr, 0, t, inc, cur_e, lane);
   wave_sync();  // the scratch is free again
@@ -799,7 +805,15 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   if (lane < 8) g_fold_pf[lane] = 0;
 #endif
   double S = 0.0;
-  int cur_e = INT32_MIN;
+  __shared__ int cur_e_s;
+  if (lane == 0) cur_e_s = INT32_MIN;
+  wave_sync();
+  LDS int* cur_e = (LDS int*)&cur_e_s;
+  const LDS uint8_t* lstreams = (const LDS uint8_t*)streams;
+  const LDS double* lcsum = (const LDS double*)csum;
+  const LDS double* lt = (const LDS double*)t;
+  LDS double* linc = (LDS double*)inc;
+  LDS uint8_t* lscratch = (LDS uint8_t*)scratch;
   const int64_t nt = P.rd.n_tiles;
 #ifdef BQSR_FOLD_PROFILE
   long long pf_blk = 0, pf_blk_fb = 0, pf_run = 0, pf_run_fb = 0, pf_ev = 0, pf_ev_el = 0, pf_glob = 0,
@@ -823,7 +837,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
       PF(++pf_blk_fb);
       // the bound failed (not expected): fold the block's tiles element by element
       for (int64_t tl = nt * b / nb; tl < nt * (b + 1) / nb; ++tl)
-        S = fold_tile_global(P, S, tl, scratch, t, inc, cur_e, lane);
+        S = fold_tile_global(P, S, tl, lscratch, lt, linc, cur_e, lane);
       continue;
     }
     const int c = B.cidx;
@@ -845,29 +859,33 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
         PF(++pf_run_fb);
       } else if (G.kind == kSegEvent) {
         if (G.off + G.inc <= sl) {  // (the LDS copy has 64 B of slack past sl)
-          S = wave_fold(S, streams + G.off, (int)G.inc, csum + G.off / 64 * 2, G.e, t, inc, cur_e, lane);
+#ifdef BQSR_FOLD_PROFILE
+          const long long w0 = clock64();
+#endif
+          S = wave_fold(S, lstreams + G.off, (int)G.inc, lcsum + G.off / 64 * 2, G.e, lt, linc, cur_e, lane);
+          PF(pf_glob_tiles += clock64() - w0);
         } else {  // beyond the prefetched bytes: through the scratch buffer, 4 KB at a time
           for (int64_t o = 0; o < G.inc; o += kTileSlots) {
             const int m = (int)min((int64_t)kTileSlots, G.inc - o);
             for (int i = lane; i < m; i += 64) scratch[i] = P.streams[G.off + o + i];
             wave_sync();
-            S = wave_fold(S, scratch, m, P.csum + (G.off + o) / 64 * 2, G.e, t, inc, cur_e, lane);
+            S = wave_fold(S, lscratch, m, nullptr, 0, lt, linc, cur_e, lane);
             wave_sync();
           }
         }
         PF(++pf_ev; pf_ev_el += G.inc);
         continue;
       }
-      PF(++pf_glob; pf_glob_tiles += G.t1 - G.t0 + 1);
+      PF(++pf_glob);
       // kSegGlobal, or a run whose bound failed: element by element
-      for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, scratch, t, inc, cur_e, lane);
+      for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, lscratch, lt, linc, cur_e, lane);
     }
   }
   if (lane == 0) P.em_out[0] = S;
 #ifdef BQSR_FOLD_PROFILE
   if (lane == 0)
     printf("FOLD2 cand %d stream_used %lld | blocks %lld fallback %lld | runs %lld fallback %lld | events %lld elems %lld | "
-           "global %lld tiles %lld | cycles %lld (prefetch %lld) | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld "
+           "global %lld wavefold-cyc %lld | cycles %lld (prefetch %lld) | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld "
            "cyc) tables %lld chunkwin %lld\n",
            nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles,
            clock64() - pf_c0, pf_c0 - pf_k0, g_fold_pf[0], g_fold_pf[1], g_fold_pf[2], g_fold_pf[3], g_fold_pf[4],
