@@ -213,6 +213,37 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
     *P.stream_used = 0ull;
     *P.seg_used = 0u;
   }
+  // (5) runs of event-free blocks of one binade become one addition: the
+  // run's first block holds the summed increment and cidx = -(run length)
+  // (a run adds less than 2^53 units: its integer sum is exact)
+  __shared__ unsigned long long rsum[kMaxFoldBlocks];
+  __shared__ int32_t rkey[kMaxFoldBlocks], rfirst[kMaxFoldBlocks], rlen[kMaxFoldBlocks];
+  __syncthreads();
+  const bool blive = tid < nb;
+  FoldBlock mine{};
+  if (blive) mine = P.blk[tid];
+  const int key = !blive ? INT32_MIN : (mine.cidx >= 0 ? INT32_MIN + 1 : (mine.e == kFoldNoBase ? INT32_MIN + 2 : mine.e));
+  rkey[tid] = key;
+  rsum[tid] = 0ull;
+  rlen[tid] = 0;
+  __syncthreads();
+  const bool evfree = blive && mine.cidx < 0 && mine.e != kFoldNoBase;
+  const bool rstart = evfree && (tid == 0 || rkey[tid - 1] != key);
+  // the run's first block: the last start at or before this block (a max-scan of start indices)
+  int f = rstart ? tid : -1;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int x = __shfl_up(f, off);
+    if (lane >= off) f = max(f, x);
+  }
+  if (lane == 63) wc[wave] = f;
+  __syncthreads();
+  for (int w = 0; w < wave; ++w) f = max(f, wc[w]);
+  if (evfree) {
+    atomicAdd(&rsum[f], (unsigned long long)mine.inc);
+    atomicAdd(&rlen[f], 1);
+  }
+  __syncthreads();
+  if (rstart) P.blk[tid] = FoldBlock{mine.r0, mine.r1, (double)rsum[tid], mine.e, -rlen[tid]};
 }
 
 // ----------------------------------------------------------- tile sums ----
@@ -822,22 +853,31 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
 #else
 #define PF(x)
 #endif
+#ifdef BQSR_FOLD_PROFILE
+  long long pf_nc = 0, pf_cb = 0;
+#endif
   for (int b = 0; b < nb; ++b) {
+#ifdef BQSR_FOLD_PROFILE
+    const long long bt0 = clock64();
+#endif
     const FoldBlock B = blk[b];
-    if (B.cidx < 0) {  // no event expected: one integer addition
+    if (B.cidx < 0) {  // a run of -cidx event-free blocks in binade e: one integer addition
       if (B.e == kFoldNoBase) continue;
+      const int nrun = -B.cidx;
       if (S >= kFoldSeqLimit && expo(S) == B.e) {
         const double N0 = S * pow2i(52 - B.e);
         if (N0 + B.inc < kTwo53) {
           S = (N0 + B.inc) * pow2i(B.e - 52);
-          PF(++pf_blk);
+          b += nrun - 1;
+          PF(++pf_blk; pf_nc += clock64() - bt0);
           continue;
         }
       }
       PF(++pf_blk_fb);
-      // the bound failed (not expected): fold the block's tiles element by element
-      for (int64_t tl = nt * b / nb; tl < nt * (b + 1) / nb; ++tl)
+      // the bound failed (not expected): fold the run's tiles element by element
+      for (int64_t tl = nt * b / nb; tl < nt * (b + nrun) / nb; ++tl)
         S = fold_tile_global(P, S, tl, lscratch, lt, linc, cur_e, lane);
+      b += nrun - 1;
       continue;
     }
     const int c = B.cidx;
@@ -880,14 +920,15 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
       // kSegGlobal, or a run whose bound failed: element by element
       for (int64_t tl = G.t0; tl <= G.t1; ++tl) S = fold_tile_global(P, S, tl, lscratch, lt, linc, cur_e, lane);
     }
+    PF(pf_cb += clock64() - bt0);
   }
   if (lane == 0) P.em_out[0] = S;
 #ifdef BQSR_FOLD_PROFILE
   if (lane == 0)
     printf("FOLD2 cand %d stream_used %lld | blocks %lld fallback %lld | runs %lld fallback %lld | events %lld elems %lld | "
-           "global %lld wavefold-cyc %lld | cycles %lld (prefetch %lld) | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld "
+           "global %lld wavefold-cyc %lld noncand-cyc %lld cand-cyc %lld | cycles %lld (prefetch %lld) | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld "
            "cyc) tables %lld chunkwin %lld\n",
-           nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles,
+           nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles, pf_nc, pf_cb,
            clock64() - pf_c0, pf_c0 - pf_k0, g_fold_pf[0], g_fold_pf[1], g_fold_pf[2], g_fold_pf[3], g_fold_pf[4],
            g_fold_pf[5], g_fold_pf[6], g_fold_pf[7]);
 #endif
