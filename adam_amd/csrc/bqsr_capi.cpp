@@ -173,7 +173,7 @@ constexpr size_t kLdsMax = 163840;
 // LDS of the per-base passes: observe's u32 window [qw][wcells] x {obs, mm}
 // + masked counts + block histogram; apply's char table [qw][cw][21]
 size_t observe_lds(int qw, int wcells) { return (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4; }
-size_t apply_lds(int qw, int cw) { return (size_t)qw * cw * kCtxSlots; }
+size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + (size_t)qw * cw * kCtxSlots; }
 int observe_rows(int wcells) {
   int qw = kQBins;
   while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;
@@ -359,8 +359,7 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   for (const void* f : {(const void*)bqsr_observe_kernel<false, false>, (const void*)bqsr_observe_kernel<true, false>,
-                        (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel<false>,
-                        (const void*)bqsr_apply_kernel<true>})
+                        (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -1389,11 +1388,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
   const size_t lds = apply_lds(P.w.qw, cw);
-  P.lane_shift = lane_shift(b);
-  if (chunk_lanes(true))
-    hipLaunchKernelGGL(bqsr_apply_kernel<true>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
-  else
-    hipLaunchKernelGGL(bqsr_apply_kernel<false>, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
   return ok();
 }

@@ -72,6 +72,7 @@ constexpr int kMaxTileReads = 64;
 constexpr int kMaxFoldBlocks = 1024;  // workgroups of the per-base passes (one per CU)
 constexpr int kWaves = 16;  // waves per workgroup of the per-base passes (1024 threads)
 constexpr int kBlockThreads = 64 * kWaves;
+constexpr int kMkWords = kWaves * 64;  // LDS of the lane-per-chunk walk: one marker word per lane
 constexpr int kMaxReadLen = 4096;  // longest read the device path takes
 constexpr int kColumnPad = 32;     // readable bytes past the end of the qual / bases columns
 constexpr int kRedSlabs = 16;      // slabs one bqsr_window_reduce thread sums (grid y splits the rest)

@@ -853,6 +853,115 @@ __device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
   w[3] = __builtin_amdgcn_alignbyte(u0, u3, b);
 }
 
+// ------------------------------------------------------- lane per chunk ----
+//
+// The per-base passes' wavefront walk: every lane takes one 16-offset chunk
+// per step, the chunks of consecutive reads laid end to end over the 64
+// lanes, so a step's loads and stores are consecutive 16-B pieces of the
+// columns (read order, 16-aligned slots: one contiguous kilobyte) and no lane
+// idles while another finishes a longer read.
+//
+// Windows of 64 sorted positions: lane j first decodes the window's read j
+// (`read lane`: lane_read, the per-read callback), and a scan of the reads'
+// chunk counts gives read j its first chunk ps_j.  The window's chunks are
+// then taken 64 at a time: lane l takes chunk g0 + l, whose read is the last
+// read with a chunk and ps <= g0 + l -- a per-wavefront LDS word per lane
+// takes the largest such read starting at each lane (LDS max), a DPP max-scan
+// carries it to the lanes after it -- and fetches that read's packed fields
+// from its read lane with ds_bpermute.
+
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, kRowMask, 0xF, false);  // 0 where no source lane
+}
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+  x += dpp_u32<0x111>(x);
+  x += dpp_u32<0x112>(x);
+  x += dpp_u32<0x114>(x);
+  x += dpp_u32<0x118>(x);
+  x += dpp_u32<0x142, 0xA>(x);
+  x += dpp_u32<0x143, 0xC>(x);
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = max(x, dpp_u32<0x111>(x));
+  x = max(x, dpp_u32<0x112>(x));
+  x = max(x, dpp_u32<0x114>(x));
+  x = max(x, dpp_u32<0x118>(x));
+  x = max(x, dpp_u32<0x142, 0xA>(x));
+  x = max(x, dpp_u32<0x143, 0xC>(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+constexpr uint32_t kPkRev = 0x8000u;  // packed flags: cycle direction -1
+
+// kAct: the kInfo bits of reads whose [st, en) the pass visits.  Chunk k of a
+// read covers offsets st + jb + 16k .. +15 (jb = -(st & 15) in the aligned
+// layout, else 0).  fread(x, live) runs once per read (on its read lane).  A
+// step takes kU groups of 64 chunks: every group's chunk is mapped and its
+// loads issued (fload(x, j, on) -> LD) before the first is used
+// (fchunk(x, j, n, on, ld)), so a lane has kU chunks' loads in flight; x
+// holds r, slot, st, en, fl, rg, cell0 and dir of the chunk's read, j = jb +
+// 16k, n = en - st.
+template <uint32_t kAct, int kU, class LD, class FRead, class FLoad, class FChunk>
+__device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* info, const OrderDev& ord, int64_t q0,
+                                           int64_t q1, int64_t qstep, int L, int lane, uint32_t* mk, FRead&& fread,
+                                           FLoad&& fload, FChunk&& fchunk) {
+  for (int64_t wb = q0; wb < q1; wb += qstep) {
+    const bool live = wb + lane < q1;
+    const LaneRead x = lane_read(rd, info, live ? order_read(ord, wb + lane) : 0, live, L);
+    fread(x, live);
+    const int n = (live && (x.fl & kAct)) ? x.en - x.st : 0;
+    const int jb = rd.slots_aligned ? -(x.st & 15) : 0;
+    const uint32_t nch = n > 0 ? (uint32_t)((n - jb + 15) >> 4) : 0u;
+    const uint32_t pe = wave_incl_add(nch), ps = pe - nch;
+    const uint32_t total = __builtin_amdgcn_readlane(pe, 63);
+    const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
+    const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
+    const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
+    const uint32_t p_rg = (uint32_t)x.rg;
+    for (uint32_t g00 = 0; g00 < total; g00 += 64 * kU) {
+      LaneRead c[kU];
+      int jj[kU];
+      bool on[kU];
+      LD ld[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint32_t g0 = g00 + 64 * u;
+        mk[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        if (nch && ps > g0 && ps < g0 + 64) atomicMax(&mk[ps - g0], (uint32_t)lane);
+        __builtin_amdgcn_wave_barrier();
+        // chunk g0's read: the last read with chunks whose first is <= g0
+        const uint64_t below = __builtin_amdgcn_ballot_w64(nch && ps <= g0);
+        uint32_t v = mk[lane];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) v = 63u - (uint32_t)__builtin_clzll(below);
+        const int ri = (int)wave_incl_max(v);
+        c[u].r = bperm(ri, p_r);
+        c[u].slot = ((uint64_t)bperm(ri, p_shi) << 32) | bperm(ri, p_slo);
+        const uint32_t se = bperm(ri, p_se), fl = bperm(ri, p_fl);
+        c[u].st = (int)(se & 0xFFFFu);
+        c[u].en = (int)(se >> 16);
+        c[u].fl = (int)(fl & 0x7FFFu);
+        c[u].dir = (fl & kPkRev) ? -1 : 1;
+        c[u].cell0 = (int)(fl >> 16);
+        c[u].rg = (int)bperm(ri, p_rg);
+        const uint32_t ps_c = bperm(ri, ps);
+        const int jb_c = rd.slots_aligned ? -(c[u].st & 15) : 0;
+        jj[u] = jb_c + 16 * (int)(g0 + lane - ps_c);
+        on[u] = g0 + lane < total;
+        ld[u] = fload(c[u], jj[u], on[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) fchunk(c[u], jj[u], c[u].en - c[u].st, on[u], ld[u]);
+    }
+  }
+}
+
 // ------------------------------------------------------------ observe ------
 
 // LDS: [obs window qw*wcells u32][mm window qw*wcells u32][masked qw u32][block hist 128 u32]
@@ -1436,39 +1545,203 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
   return (int32_t)0x80000000;          // log10(inf) = inf
 }
 
-// LDS: the piece's char table [qw rows][cw cycle cells][21 contexts] u8.
-// Built once per piece (bqsr_apply_kernel's prologue) from the exact LUT:
-// char = (errorProbabilityToPhred(s1[c] + d2[x]) + 33) for every (qual row,
-// cycle cell, context) of the piece's read group, 0 where the checked path
-// must decide (key not in the table, a char above 0xFF, or a genuine 0).
-// Lane per read as in observe; per offset the fast path is one LDS byte
-// read.  Offsets it cannot finish (qual outside the rows, entry 0, the read
-// only being checked) set a bit of `slow` and are redone after the chunk by
-// the exact checked path.  A super-chunk's chars leave as 16-B stores (a
-// read's last chunk byte-wise).
-template <bool kCL>
+// LDS: the wavefronts' chunk-walk markers (kMkWords u32), then the piece's
+// char table [qw rows][cw cycle cells][21 contexts] u8, built once per piece
+// from the exact LUT: char = (errorProbabilityToPhred(s1[c] + d2[x]) + 33)
+// for every (qual row, cycle cell, context) of the piece's read group, 0
+// where the checked path must decide (key not in the table, a char above
+// 0xFF, or a genuine 0).  A lane per chunk (chunk_walk); per offset the fast
+// path is one LDS byte read.  Offsets it cannot finish (qual outside the
+// rows, entry 0, the read only being checked) set a bit of `slow` and are
+// redone after the chunk by the exact checked path.  Chunks leave as 16-B
+// stores (an unaligned layout's last chunk of a read byte-wise).
+struct ApplyPiece {
+  const uint8_t* lut;
+  int rg_lo, c_lo, cw, cw21, q_lo, qw;
+};
+
+struct ChunkLoads {
+  uint4 qs, cr;
+};
+__device__ __forceinline__ ChunkLoads apply_load(const ApplyParams& P, const LaneRead& x, int j, bool on) {
+  ChunkLoads v{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  if (on) {
+    const int o0 = x.st + j;
+    v.qs = *(const uint4*)(P.rd.qual + x.slot + o0);
+    if (!(x.fl & kInfoPass)) v.cr = chunk_raw(P.rd, chunk_n0(x, o0));
+  }
+  return v;
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const uint8_t* LdsBytes;
+
+// The checked path of a chunk's flagged offsets (RecalUtil.recalibrate with
+// the table's key checks), out of line: its table pointers stay out of the
+// fast path's registers.
+__device__ __forceinline__ uint4 apply_slow(const ApplyParams* Pp, LaneRead x, int o0, uint32_t slow, uint64_t x01,
+                                         uint64_t x23, uint4 outv) {
+  const ApplyParams& P = *Pp;
+  const bool app = x.fl & kInfoApp;
+  const uint8_t* qp = P.rd.qual + x.slot;
+  uint64_t lo = ((uint64_t)outv.y << 32) | outv.x, hi = ((uint64_t)outv.w << 32) | outv.z;
+  while (slow) {
+    const int k = __builtin_ctz(slow);
+    slow &= slow - 1;
+    const int o = o0 + k;
+    const int q = (int)(int8_t)qp[o];
+    const int xs = (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
+    // key validity as getReadGroupDelta / getQualScoreDelta see it
+    const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
+    const int64_t gr = (key - 1) / kMaxQ;
+    const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
+    const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
+    if (!grp || !kok) {
+      report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
+      continue;
+    }
+    if (q < 0) {
+      report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+      continue;
+    }
+    if (!app) continue;
+    const int64_t rq = (int64_t)x.rg * kQBins + q;
+    const int ccell = x.cell0 + x.dir * o;
+    const double p = P.s1[rq * P.g.C + ccell] + P.d2[rq * kCtxSlots + xs];
+    const int32_t Q = phred_q(p, P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
+    const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+    if (code > 0xFFu) {
+      const unsigned long long e = atomicAdd(P.n_exc, 1ull);
+      if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
+    }
+    // byte k := code
+    const uint64_t m = 0xFFull << (8 * (k & 7)), v = (uint64_t)(code & 0xFFu) << (8 * (k & 7));
+    if (k < 8) lo = (lo & ~m) | v; else hi = (hi & ~m) | v;
+  }
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+__device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyParams* Pp, const ApplyPiece& pc,
+                                            const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
+  if (!on) return;
+  const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
+  const int o0 = x.st + j;
+  const uint4 qs = ld.qs;
+  const uint32_t qd[4] = {qs.x, qs.y, qs.z, qs.w};
+  uint32_t out[4];
+  uint32_t slow = 0;
+  uint32_t xo[4] = {4u, 4u, 4u, 4u};
+  if (pass) {  // the original chars: (qual + 33) byte-wise
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
+  } else {
+    uint64_t clo = 0;
+    uint32_t chi = 0;
+    chunk_finish(P.rd, x, chunk_n0(x, o0), ld.cr, clo, chi);
+    ctx_slots(clo, chi, xo);
+    {  // the read's first visited offset (chunk offset -j when j <= 0): context 0
+      const uint32_t kf = (uint32_t)(-j) & 15u;
+      const uint32_t bm = j <= 0 ? 0xFFu << (8 * (kf & 3)) : 0u;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t m = (kf >> 2) == (uint32_t)w ? bm : 0u;
+        xo[w] = (xo[w] & ~m) | (0x04040404u & m);
+      }
+    }
+    const int wc0 = x.cell0 + __mul24(x.dir, o0) - pc.c_lo;  // window cycle cell of offset k: wc0 + dir * k
+    // the cycle cells of the chunk's valid offsets inside the table
+    // (monotone in k: both ends)
+    const uint32_t nv = (uint32_t)min(kChunk, n - j);
+    const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
+    const bool cok = app && x.rg == pc.rg_lo && (unsigned)(wc0 + klo * x.dir) < (unsigned)pc.cw &&
+                     (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)pc.cw;
+    const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
+    const int dx = x.dir * kCtxSlots;
+    // LDS address of offset k: lut + (q - q_lo) * cw21 + wc0 * 21 + dx * k +
+    // xs, clamped to the table's last byte; an offset whose row or cycle
+    // cell lies outside the window reads some other entry and is flagged
+    // below.  The 16 addresses first (a negative table index wraps far above
+    // the table and clamps), then the 16 byte reads into 16-bit halves, two
+    // halves per register, merged by byte permutes.
+    const uint32_t lbase = (uint32_t)(uintptr_t)(LdsBytes)pc.lut;
+    const uint32_t amax = lbase + (uint32_t)(pc.qw * pc.cw21 - 1);
+    uint32_t ei[kChunk];
+    uint32_t ek = lbase + (uint32_t)(wc0 * kCtxSlots - pc.q_lo * pc.cw21);
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const uint32_t q = __builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
+      const uint32_t xs = __builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8);
+      ei[k] = min((uint32_t)__mul24((int)q, pc.cw21) + ek + xs, amax);
+      ek += (uint32_t)dx;
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      u16x2 a, b;  // a: bytes 0 and 2 of the word, b: bytes 1 and 3
+      a.x = *(LdsBytes)(uintptr_t)ei[4 * w];
+      b.x = *(LdsBytes)(uintptr_t)ei[4 * w + 1];
+      a.y = *(LdsBytes)(uintptr_t)ei[4 * w + 2];
+      b.y = *(LdsBytes)(uintptr_t)ei[4 * w + 3];
+      out[w] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
+    }
+    // per word: bytes whose qual is outside the window rows (SWAR; q >= 128
+    // never is in them) or whose entry is 0 (the checked path decides),
+    // gathered to one bit per offset
+    const int hi_lim = min(pc.q_lo + pc.qw, kQBins);
+    const uint32_t lo4 = (uint32_t)pc.q_lo * 0x01010101u, hi4 = (uint32_t)hi_lim * 0x01010101u;
+    uint32_t badm = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t v = qd[w] & 0x7F7F7F7Fu;
+      const uint32_t ge_lo = (v | 0x80808080u) - lo4;  // byte high bit: v >= q_lo
+      const uint32_t ge_hi = hi_lim < kQBins ? (v | 0x80808080u) - hi4 : 0u;
+      const uint32_t z = ~(((out[w] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | out[w] | 0x7F7F7F7Fu);  // zero bytes
+      const uint32_t bad = (((qd[w] | ~ge_lo | ge_hi) & 0x80808080u) | z) >> 7;  // bit 8i: byte i
+      badm |= (bad | (bad >> 7) | (bad >> 14) | (bad >> 21)) << (4 * w);  // bits 0..3 (higher bits: masked below)
+    }
+    slow = vmask & (cok ? badm : 0xFFFFu);
+  }
+  // ---- the checked path ----
+  if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+    if (slow) {
+      const uint4 r = apply_slow(Pp, x, o0, slow, ((uint64_t)xo[1] << 32) | xo[0], ((uint64_t)xo[3] << 32) | xo[2],
+                                 make_uint4(out[0], out[1], out[2], out[3]));
+      out[0] = r.x;
+      out[1] = r.y;
+      out[2] = r.z;
+      out[3] = r.w;
+    }
+  }
+  if (app || pass) {
+    uint8_t* op = P.out_qual + x.slot;
+    if (j + kChunk <= n || P.rd.slots_aligned) {  // aligned: the chunk's other bytes are this read's scratch
+      *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kChunk; ++k)
+        if (k < n - j) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+
+#ifndef BQSR_APPLY_U
+#define BQSR_APPLY_U 4
+#endif
+constexpr int kApplyU = BQSR_APPLY_U;  // chunks in flight per lane
+
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
-  uint8_t* lut = smem;
+  uint32_t* mk_all = (uint32_t*)smem;
+  uint8_t* lut = smem + kMkWords * 4;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
+  uint32_t* mk = mk_all + wave * 64;
   const int q_lo = P.w.q_lo;
   const int G = gridDim.x;
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
-  // kCL (lane per super-chunk): a wavefront step takes 64 >> ls reads with
-  // 2^ls lanes each, lane `sub` of a read taking its super-chunks (kSub
-  // chunks, 64 offsets) sub, sub + 2^ls, ...: the lanes of a read cover
-  // neighbouring 64-B pieces of its columns, so a wavefront's loads and
-  // stores fill whole cache lines at once.  Otherwise a lane per read walks
-  // all its super-chunks.
-  const int ls = kCL ? P.lane_shift : 6;
-  const int sub = kCL ? lane & ((1 << ls) - 1) : 0, rl = kCL ? lane >> ls : lane, rpw = kCL ? 64 >> ls : 64;
-  constexpr int NS = kSub;
-  const int jstep = kSuper << (kCL ? ls : 0);
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -1477,13 +1750,13 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     if (p0 >= p1) continue;
     const int rg_lo = key_rg(P.ord, key, P.w.rg_lo);
     const WinGeom gm = win_geom(P.ord, P.g, key);
-    const int c_lo = gm.c_lo, cw = gm.cw, cw21 = cw * kCtxSlots;
+    const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw};
     const bool win_ok = rg_lo < P.n_rg;
     const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
     __syncthreads();  // the previous piece is done with the table
     // ---- the piece's char table: one thread per (row, cycle cell), 21 contexts each ----
-    for (int i = tid; i < qw * cw; i += blockDim.x) {
-      const int row = i / cw, c = i - row * cw;
+    for (int i = tid; i < qw * pc.cw; i += blockDim.x) {
+      const int row = i / pc.cw, c = i - row * pc.cw;
       const int64_t rq = rq0 + row;
       const bool ok = win_ok && q_lo + row < kQBins && P.rq_ok[rq];
       uint8_t* dst = lut + (int64_t)i * kCtxSlots;
@@ -1491,7 +1764,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
         for (int x = 0; x < kCtxSlots; ++x) dst[x] = 0;
         continue;
       }
-      const double s1 = P.s1[rq * C + c_lo + c];
+      const double s1 = P.s1[rq * C + pc.c_lo + c];
       const double* d2 = P.d2 + rq * kCtxSlots;
       for (int x = 0; x < kCtxSlots; ++x) {
         // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
@@ -1501,167 +1774,26 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
       }
     }
     __syncthreads();
-
-    for (int64_t g0 = p0 + (int64_t)rpw * wave; g0 < p1; g0 += (int64_t)rpw * kWaves) {
-      const bool live = g0 + rl < p1;
-      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + rl) : 0, live, L);
-      if (live && sub == 0) {
-        if (x.fl & kInfoPass) {  // quality string passed through
-          P.out_start[x.r] = 0;
-          P.out_len[x.r] = (uint32_t)x.en;
-        } else {
-          P.out_start[x.r] = (uint32_t)x.st;
-          P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
-        }
-      }
-      const bool app = x.fl & kInfoApp, pass = x.fl & kInfoPass;
-      const int n = (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) ? x.en - x.st : 0;
-      const bool fast_rd = app && x.rg == rg_lo;
-      const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;  // as in observe
-      const uint8_t* qp = P.rd.qual + x.slot;
-      uint8_t* op = P.out_qual + x.slot;
-      for (int j0 = jb + kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += jstep) {
-        if (j0 >= n) continue;
-        // issue every load of the super-chunk first
-        uint4 qs[NS], cr[NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-          const bool lv = j0 + kChunk * i < n;
-          const int o0 = x.st + j0 + kChunk * i;
-          qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
-          cr[i] = (lv && !pass) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
-        }
-#pragma clang loop unroll(full)
-        for (int i = 0; i < NS; ++i) {
-          const int j = j0 + kChunk * i;
-          if (j >= n) continue;
-          const int o0 = x.st + j;
-          const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
-          uint32_t out[4];
-          uint32_t slow = 0;
-          uint32_t xo[4] = {4u, 4u, 4u, 4u};
-          if (pass) {  // the original chars: (qual + 33) byte-wise
-#pragma unroll
-            for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
+    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads>(
+        P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk,
+        [&](const LaneRead& x, bool live) {
+          if (!live) return;
+          if (x.fl & kInfoPass) {  // quality string passed through
+            P.out_start[x.r] = 0;
+            P.out_len[x.r] = (uint32_t)x.en;
           } else {
-            uint64_t clo = 0;
-            uint32_t chi = 0;
-            chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
-            ctx_slots(clo, chi, xo);
-            if (j <= 0) ctx_first(xo, -j);  // the read's first visited offset: context 0
-            const int wc0 = x.cell0 + __mul24(x.dir, o0) - c_lo;  // window cycle cell of offset k: wc0 + dir * k
-            // the cycle cells of the chunk's valid offsets inside the table
-            // (monotone in k: both ends); invalid offsets may index past the
-            // table's rows: their reads are masked to entry 0
-            const uint32_t nv = (uint32_t)min(kChunk, n - j);
-            const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
-            const bool cok = fast_rd && (unsigned)(wc0 + klo * x.dir) < (unsigned)cw &&
-                             (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
-            const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
-            const int dx = x.dir * kCtxSlots;
-            // entry of offset k: (q - q_lo) * cw21 + wc0 * 21 + dx * k + xs,
-            // clamped into the table; an offset whose row or cycle cell lies
-            // outside the window reads some other entry and is flagged below
-            // (the per-offset work is two byte extracts, a multiply-add, a
-            // clamp, the LDS byte read and the byte insert)
-            const uint32_t emax = (uint32_t)(qw * cw21 - 1);
-            // all 16 entry indices first (a running cycle offset, no
-            // multiplies by k; a negative index wraps above emax and clamps),
-            // then the 16 LDS reads back to back, then the byte inserts
-            uint32_t ei[kChunk];
-            int ek = wc0 * kCtxSlots - q_lo * cw21;
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-              const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
-              const int xs = (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8);
-              ei[k] = min((uint32_t)(__mul24(q, cw21) + ek + xs), emax);
-              ek += dx;
-            }
-            uint32_t code[kChunk];
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) code[k] = lut[ei[k]];
-            out[0] = out[1] = out[2] = out[3] = 0;
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) out[k >> 2] |= code[k] << (8 * (k & 3));
-            // per word: bytes whose qual is outside the window rows (SWAR;
-            // q >= 128 never is in them) or whose entry is 0 (the checked path
-            // decides), gathered to one bit per offset
-            const int hi_lim = min(q_lo + qw, kQBins);
-            const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)hi_lim * 0x01010101u;
-            uint32_t badm = 0;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              const uint32_t v = qd[w] & 0x7F7F7F7Fu;
-              const uint32_t ge_lo = (v | 0x80808080u) - lo4;  // byte high bit: v >= q_lo
-              const uint32_t ge_hi = hi_lim < kQBins ? (v | 0x80808080u) - hi4 : 0u;
-              const uint32_t z = ~(((out[w] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | out[w] | 0x7F7F7F7Fu);  // zero bytes
-              const uint32_t bad = ((qd[w] | ~ge_lo | ge_hi) & 0x80808080u) | z;
-              badm |= ((((bad >> 7) & 0x01010101u) * 0x00204081u) >> 21 & 0xFu) << (4 * w);
-            }
-            slow = vmask & (cok ? badm : 0xFFFFu);
+            P.out_start[x.r] = (uint32_t)x.st;
+            P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
           }
-          // ---- the checked path, in offset order (the first failing offset wins) ----
-          if (__builtin_amdgcn_ballot_w64(slow != 0)) {
-            const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-            while (slow) {
-              const int k = __builtin_ctz(slow);
-              slow &= slow - 1;
-              const int o = o0 + k;
-              const int q = (int)(int8_t)qp[o];
-              const int xs = (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
-              // key validity as getReadGroupDelta / getQualScoreDelta see it
-              const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
-              const int64_t gr = (key - 1) / kMaxQ;
-              const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
-              const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
-              if (!grp || !kok) {
-                report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
-                continue;
-              }
-              if (q < 0) {
-                report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
-                continue;
-              }
-              if (!app) continue;
-              const int64_t rq = (int64_t)x.rg * kQBins + q;
-              const int ccell = x.cell0 + x.dir * o;
-              const double p = P.s1[rq * C + ccell] + P.d2[rq * kCtxSlots + xs];
-              const int32_t Q = phred_q(p, P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
-              const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-              if (code > 0xFFu) {
-                const unsigned long long e = atomicAdd(P.n_exc, 1ull);
-                if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
-              }
-              // byte k of out[] := code (u64 halves: no dynamically indexed array)
-              const uint64_t m = 0xFFull << (8 * (k & 7)), v = (uint64_t)(code & 0xFFu) << (8 * (k & 7));
-              uint64_t lo = ((uint64_t)out[1] << 32) | out[0], hi = ((uint64_t)out[3] << 32) | out[2];
-              if (k < 8) lo = (lo & ~m) | v; else hi = (hi & ~m) | v;
-              out[0] = (uint32_t)lo;
-              out[1] = (uint32_t)(lo >> 32);
-              out[2] = (uint32_t)hi;
-              out[3] = (uint32_t)(hi >> 32);
-            }
-          }
-          if (app || pass) {
-            if (j + kChunk <= n || P.rd.slots_aligned) {  // aligned: the chunk's other bytes are this read's scratch
-              *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
-            } else {
-#pragma unroll
-              for (int k = 0; k < kChunk; ++k)
-                if (k < n - j) op[o0 + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
-            }
-          }
-        }
-      }
-    }
+        },
+        [&](const LaneRead& x, int j, bool on) { return apply_load(P, x, j, on); },
+        [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) { apply_chunk(P, &P, pc, x, j, n, on, ld); });
   }  // pieces
 }
 
 template __global__ void bqsr_observe_kernel<false, false>(ObserveParams);
 template __global__ void bqsr_observe_kernel<true, false>(ObserveParams);
 template __global__ void bqsr_observe_kernel<false, true>(ObserveParams);
-template __global__ void bqsr_apply_kernel<false>(ApplyParams);
-template __global__ void bqsr_apply_kernel<true>(ApplyParams);
 
 // RecalTable.++ over partitions in a declared order (RecalTable.scala:90-108):
 // expectedMismatch = ((0.0 + e_0) + e_1) + ... -- one lane, each `+` one IEEE
