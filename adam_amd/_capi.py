@@ -17,9 +17,10 @@ LIB_PATH = os.environ.get("ADAM_BQSR_LIB") or os.path.join(_HERE, "libadam_bqsr.
 BQSR_OK = 0
 STAGE_RESET, STAGE_KERNEL, STAGE_FOLD, STAGE_PREP = 1, 2, 4, 8
 STATUS_NAMES = ["OK", "NULL_RG", "MD_PARSE", "CIGAR_SHORT", "BAD_REVCOMP_BASE", "EMPTY_TABLE", "MISSING_KEY",
-                "QUAL_RANGE", "NULL_FIELD", "SEQ_SHORT", "CIGAR_INVALID", "INVALID_ARG", "DEVICE", "UNSUPPORTED"]
+                "QUAL_RANGE", "NULL_FIELD", "SEQ_SHORT", "CIGAR_INVALID", "INVALID_ARG", "DEVICE", "UNSUPPORTED",
+                "SAM_PARSE"]
 (NULL_RG, MD_PARSE, CIGAR_SHORT, BAD_REVCOMP_BASE, EMPTY_TABLE, MISSING_KEY, QUAL_RANGE, NULL_FIELD, SEQ_SHORT,
- CIGAR_INVALID, INVALID_ARG, DEVICE, UNSUPPORTED) = range(1, 14)
+ CIGAR_INVALID, INVALID_ARG, DEVICE, UNSUPPORTED, SAM_PARSE) = range(1, 15)
 
 # every symbol include/adam_bqsr.h declares
 EXPORTS = [

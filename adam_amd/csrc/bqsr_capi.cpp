@@ -53,7 +53,7 @@ hipStream_t S(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
 
 const char* kStatusNames[] = {"OK",          "NULL_RG",      "MD_PARSE",       "CIGAR_SHORT", "BAD_REVCOMP_BASE",
                               "EMPTY_TABLE", "MISSING_KEY",  "QUAL_RANGE",     "NULL_FIELD",  "SEQ_SHORT",
-                              "CIGAR_INVALID", "INVALID_ARG", "DEVICE",        "UNSUPPORTED"};
+                              "CIGAR_INVALID", "INVALID_ARG", "DEVICE",        "UNSUPPORTED", "SAM_PARSE"};
 
 // map a device error key to (status, read) and record the message
 bqsr_status from_err_key(unsigned long long k, int64_t read_base) {
@@ -236,9 +236,12 @@ struct bqsr_sites {
   uint32_t* bucket = nullptr;
   uint64_t* bucket_off = nullptr;
   int64_t* bucket_base = nullptr;
+  uint64_t* bm = nullptr;
+  uint64_t* bm_off = nullptr;
+  int64_t* bm_base = nullptr;
   int32_t n = 0;
   int32_t shift = 8;
-  SitesDev dev() const { return SitesDev{pos, off, bucket, bucket_off, bucket_base, n, shift}; }
+  SitesDev dev() const { return SitesDev{pos, off, bucket, bucket_off, bucket_base, bm, bm_off, bm_base, n, shift}; }
 };
 
 struct bqsr_batch {
@@ -338,7 +341,7 @@ int bqsr_abi_version(void) { return BQSR_ABI_VERSION; }
 const char* bqsr_last_error(void) { return g_err.c_str(); }
 int64_t bqsr_last_error_read(void) { return g_err_read; }
 const char* bqsr_status_name(bqsr_status s) {
-  if ((int)s < 0 || (int)s > 13) return "UNKNOWN";
+  if ((int)s < 0 || (int)s > 14) return "UNKNOWN";
   return kStatusNames[(int)s];
 }
 
@@ -398,6 +401,8 @@ bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, con
   std::vector<uint32_t> bucket;
   std::vector<uint64_t> boff(1, 0);
   std::vector<int64_t> bbase;
+  std::vector<uint64_t> bm, bmoff(1, 0);
+  std::vector<int64_t> bmbase;
   for (int32_t c = 0; c < n_contigs; ++c) {
     s->names.emplace_back(contigs[c] ? contigs[c] : "");
     std::vector<int64_t> v(pos[c], pos[c] + n[c]);  // SnpTable: Set[Long] per contig
@@ -413,6 +418,18 @@ bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, con
     }
     bbase.push_back(base);
     boff.push_back(bucket.size());
+    // the position bitmap (a 16-24 B read per read in the prep kernel's
+    // common path), unless it would hold over 64 words per site
+    const int64_t b0 = v.empty() ? 0 : (int64_t)((uint64_t)base & ~(uint64_t)63);  // floor to 64
+    const int64_t nw = v.empty() ? 0 : ((v.back() - b0) >> 6) + 1;
+    const bool dense = nw > 0 && nw <= 64 * (int64_t)v.size() + 64 && nw <= (int64_t(1) << 28);
+    if (dense) {
+      const size_t w0 = bm.size();
+      bm.resize(w0 + (size_t)nw, 0ull);
+      for (const int64_t p : v) bm[w0 + (size_t)((p - b0) >> 6)] |= 1ull << ((p - b0) & 63);
+    }
+    bmbase.push_back(dense ? b0 : 0);
+    bmoff.push_back(bm.size());
     all.insert(all.end(), v.begin(), v.end());
     off.push_back(all.size());
   }
@@ -429,6 +446,9 @@ bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, con
   if (e == hipSuccess) e = up(&s->bucket, bucket);
   if (e == hipSuccess) e = up(&s->bucket_off, boff);
   if (e == hipSuccess) e = up(&s->bucket_base, bbase);
+  if (e == hipSuccess) e = up(&s->bm, bm);
+  if (e == hipSuccess) e = up(&s->bm_off, bmoff);
+  if (e == hipSuccess) e = up(&s->bm_base, bmbase);
   if (e != hipSuccess) {
     bqsr_sites_destroy(s);
     return fail(BQSR_ERR_DEVICE, std::string("sites upload: ") + hipGetErrorString(e));
@@ -439,7 +459,8 @@ bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, con
 
 void bqsr_sites_destroy(bqsr_sites* s) {
   if (!s) return;
-  for (void* p : {(void*)s->pos, (void*)s->off, (void*)s->bucket, (void*)s->bucket_off, (void*)s->bucket_base})
+  for (void* p : {(void*)s->pos, (void*)s->off, (void*)s->bucket, (void*)s->bucket_off, (void*)s->bucket_base,
+                  (void*)s->bm, (void*)s->bm_off, (void*)s->bm_base})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -1483,3 +1504,7 @@ bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* R, const b
 }
 
 }  // extern "C"
+
+// ---- SAM ingest / output (include/adam_sam.h) ----
+#include "sam_ingest.hip"
+#include "mark_duplicates.cpp"

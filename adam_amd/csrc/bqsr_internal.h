@@ -104,6 +104,11 @@ struct SitesDev {
   const uint32_t* bucket;      // per contig: first site index (relative) with pos >= base + (b << shift)
   const uint64_t* bucket_off;  // [n_contigs + 1] into bucket
   const int64_t* bucket_base;  // [n_contigs] position of bucket 0 (min pos)
+  // per contig a bitmap of site positions (bit p - bm_base = a site at raw POS
+  // p); a contig whose bitmap would be too sparse has none (bm_off equal)
+  const uint64_t* bm;
+  const uint64_t* bm_off;      // [n_contigs + 1] words into bm
+  const int64_t* bm_base;      // [n_contigs] position of bit 0 (a multiple of 64)
   int32_t n_contigs;
   int32_t shift;
 };

@@ -461,6 +461,40 @@ __device__ void mask_sites_linear(const PrepParams& P, int32_t contig, int64_t u
   }
 }
 
+// The same from the contig's position bitmap: 64 offsets per step, one
+// funnel shift of two bitmap words (the next step reuses the second), an
+// atomic OR per sbits word only where a site falls.  False when the contig
+// has no bitmap.
+__device__ __forceinline__ bool mask_sites_bitmap(const PrepParams& P, int32_t contig, int64_t unclipped, int lq,
+                                                  uint64_t rs) {
+  const SitesDev& S = P.sites;
+  const int64_t nw = (int64_t)(S.bm_off[contig + 1] - S.bm_off[contig]);
+  if (nw == 0) return false;
+  const uint64_t* w = S.bm + S.bm_off[contig];
+  const int64_t b0 = unclipped - S.bm_base[contig];  // bit of offset 0
+  int64_t wi = b0 >> 6;                               // floor
+  const uint32_t sh = (uint32_t)(b0 & 63);
+  uint64_t lo = (wi >= 0 && wi < nw) ? w[wi] : 0ull;
+  for (int o = 0; o < lq; o += 64) {
+    ++wi;
+    const uint64_t hi = (wi >= 0 && wi < nw) ? w[wi] : 0ull;
+    uint64_t m = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;  // bits of offsets o .. o + 63
+    lo = hi;
+    if (lq - o < 64) m &= (1ull << (lq - o)) - 1ull;
+    if (!m) continue;
+    // slots s .. s + 63 span sbits words s >> 5 .. (s >> 5) + 2 (masked half: the low 32 bits)
+    const uint64_t s = rs + (uint64_t)o;
+    const uint32_t sb = (uint32_t)(s & 31);
+    const uint64_t lo64 = m << sb, hi64 = sb ? m >> (64 - sb) : 0ull;  // bit k of (hi64:lo64): slot (s & ~31) + k
+    const uint32_t p0 = (uint32_t)lo64, p1 = (uint32_t)(lo64 >> 32), p2 = (uint32_t)hi64;
+    unsigned long long* sw = (unsigned long long*)&P.sbits[s >> 5];
+    if (p0) atomicOr(sw, (unsigned long long)p0);
+    if (p1) atomicOr(sw + 1, (unsigned long long)p1);
+    if (p2) atomicOr(sw + 2, (unsigned long long)p2);
+  }
+  return true;
+}
+
 // The common read, prepared in lock step (no data-dependent loop) and
 // without touching its quals: eligible, every field present, a CIGAR of the
 // form [S]M[S] covering the whole read (so the trimmed range, whatever it is,
@@ -570,7 +604,8 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
       const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
       if (lo < hi) set_sbits(P.sbits, rs + (uint64_t)lo, rs + (uint64_t)hi, 32);
     }
-    mask_sites_linear(P, a.contig, unclipped, st, en, rs);
+    if (a.contig >= 0 && a.contig < P.sites.n_contigs && !mask_sites_bitmap(P, a.contig, unclipped, en, rs))
+      mask_sites_linear(P, a.contig, unclipped, st, en, rs);
   }
   P.info[r] = ReadInfo{0, 0,
                        (uint16_t)(kInfoTrim | kInfoApp | (usable ? kInfoObs : 0) |

@@ -59,7 +59,8 @@ typedef enum bqsr_status {
   BQSR_ERR_CIGAR_INVALID = 10,   /* NoSuchElementException: zero-length M/X/=/S element (Range.last)     */
   BQSR_ERR_INVALID_ARG = 11,     /* bad call: null pointer, inconsistent sizes, dims mismatch            */
   BQSR_ERR_DEVICE = 12,          /* HIP runtime failure                                                  */
-  BQSR_ERR_UNSUPPORTED = 13      /* input outside what the device path handles          */
+  BQSR_ERR_UNSUPPORTED = 13,     /* input outside what the device path handles          */
+  BQSR_ERR_SAM_PARSE = 14        /* malformed SAM text where read_sam / SAMRecordConverter throws (adam_sam.h) */
 } bqsr_status;
 
 /* ADAMRecord boolean fields (adam-format/.../adam.avdl:28-38) and null-ness

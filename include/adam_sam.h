@@ -1,0 +1,135 @@
+/*
+ * adam_sam.h -- SAM text into and out of the device around the BQSR path
+ * (SURVEY.md §8 rows f1, f2, f3), part of libadam_bqsr.so.
+ *
+ *   ingest  : sc.adamLoad of a SAM file          adam-core/.../rdd/AdamContext.scala:122-137
+ *             SAMRecordConverter.convert         adam-core/.../converters/SAMRecordConverter.scala:26-144
+ *             RecordGroupDictionary (sorted ids) adam-core/.../models/RecordGroupDictionary.scala:36-43
+ *             with the BQSR column projection    adam-core/.../projections/ADAMRecordField.scala:28-71
+ *   output  : the recalibrated records written back (adamSave,
+ *             adam-core/.../rdd/AdamRDDFunctions.scala:37-56) -- here as SAM
+ *             text: every record's QUAL field replaced by the string
+ *             RecalUtil.recalibrate built (trimmed length, Q13; Java chars
+ *             as UTF-8, Q14), every other byte of the record kept
+ *   dedup   : MarkDuplicates (adam-core/.../rdd/MarkDuplicates.scala:24-111),
+ *             the `-mark_duplicate_reads` step `transform` runs before BQSR
+ *             (adam-cli/.../cli/Transform.scala:73-76)
+ *
+ * Same conventions as adam_bqsr.h (bqsr_status results, bqsr_last_error(),
+ * library-owned handles with *_destroy, `stream` = hipStream_t as void*).
+ */
+#ifndef ADAM_SAM_H
+#define ADAM_SAM_H
+
+#include "adam_bqsr.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A parsed SAM file: the text and the record columns, in device memory. */
+typedef struct bqsr_sam bqsr_sam;
+
+/* Parse a whole SAM file (header + records) as read_sam does
+ * (adam_amd/records.py, the SAMRecordConverter semantics): start = POS - 1
+ * when RNAME is a header @SQ name and POS != 0; flag bits only when the flag
+ * word is non-zero (quirk Q2); MD:Z -> mismatchingPositions; RG:Z -> the
+ * index of the name among the sorted @RG IDs; referenceName ids in order of
+ * first appearance.  Header lines are parsed on the host, records on the
+ * device (line split, field split, CIGAR text -> BAM u32 elements).
+ * `text` is host memory (pinned or not).  BQSR_ERR_SAM_PARSE where the
+ * reference's parser throws (fewer than 11 fields, a tag without two ':', a
+ * malformed CIGAR or FLAG / POS); BQSR_ERR_UNSUPPORTED for header lines after
+ * the first record and lone '\r' bytes. */
+bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n_bytes, void* stream, bqsr_sam** out);
+void bqsr_sam_destroy(bqsr_sam* s);
+
+typedef struct bqsr_sam_counts {
+  int64_t n_reads;     /* records (empty lines skipped)   */
+  int64_t seq_bytes;   /* Σ SEQ field lengths            */
+  int64_t qual_bytes;  /* Σ QUAL field lengths           */
+  int64_t cigar_ops;   /* Σ CIGAR elements               */
+  int64_t md_bytes;    /* Σ MD:Z value lengths           */
+  int64_t text_bytes;  /* the SAM text (input, or the rewritten text after bqsr_sam_rewrite_quals) */
+  int32_t n_ref_names; /* distinct referenceNames used    */
+  int32_t n_read_groups;
+} bqsr_sam_counts;
+bqsr_status bqsr_sam_get_counts(const bqsr_sam* s, bqsr_sam_counts* out);
+/* referenceName i (ref_index order: first appearance in the records) */
+const char* bqsr_sam_ref_name(const bqsr_sam* s, int32_t i);
+
+/* The record columns (bqsr_records layout; ref_index as RecordBatch keeps it:
+ * index into the bqsr_sam_ref_name list, -1 when referenceName is null). */
+typedef struct bqsr_sam_columns {
+  uint32_t* flags;
+  int32_t* rg_id;
+  int32_t* ref_index;
+  int64_t* start;
+  uint64_t* seq_offset;
+  uint8_t* seq;
+  uint64_t* qual_offset;
+  uint8_t* qual;
+  uint64_t* cigar_offset;
+  uint32_t* cigar;
+  uint64_t* md_offset;
+  uint8_t* md;
+} bqsr_sam_columns;
+/* device pointers of the columns (valid while `s` lives) */
+bqsr_status bqsr_sam_device_columns(const bqsr_sam* s, bqsr_sam_columns* out);
+/* copy the columns to caller-allocated host arrays sized by bqsr_sam_get_counts */
+bqsr_status bqsr_sam_download(const bqsr_sam* s, const bqsr_sam_columns* dst);
+
+/* Output (§8 f2): replace every record's QUAL field by its recalibrated
+ * string.  out_qual / out_start / out_len / exceptions are the device
+ * buffers bqsr_apply_async wrote for batch `b`, built from this parse's
+ * records in read order (b's slot of read r = its qual chars' base).
+ * Recalibrated reads get the chars of [out_start, out_start + out_len) as
+ * UTF-8 (chars above 0xFF from the exception list); pass-through reads keep
+ * their QUAL bytes; with b == NULL every QUAL field is kept.  After
+ * bqsr_sam_mark_duplicates the FLAG fields are rewritten too (0x400 = the
+ * duplicateRead MarkDuplicates gave the read).  The header is kept, empty
+ * lines are dropped and every record ends with '\n'.  The new text
+ * replaces the parse's on the device. */
+bqsr_status bqsr_sam_rewrite_quals(bqsr_context* ctx, bqsr_sam* s, const bqsr_batch* b, const uint8_t* out_qual,
+                                   const uint32_t* out_start, const uint32_t* out_len, const uint64_t* exceptions,
+                                   int64_t n_exceptions, void* stream);
+/* copy the (rewritten) SAM text to host memory of at least counts.text_bytes */
+bqsr_status bqsr_sam_text_download(const bqsr_sam* s, char* dst);
+
+/* MarkDuplicates (§8 f3): adam-core/.../rdd/MarkDuplicates.scala:24-111 over
+ * SingleReadBucket (models/SingleReadBucket.scala:27-37: reads grouped by
+ * (recordGroupId, readName)) and ReferencePositionPair
+ * (models/ReferencePositionPair.scala:27-63: the buckets' 5' positions,
+ * RichADAMRecord.scala:77-118).  Buckets grouped by (left position,
+ * library), then by right position; the best-scoring bucket of a group
+ * (score = Σ quals >= 15 of its primary reads, :37-39) keeps its primary
+ * reads, every other mapped read of the group is a duplicate, unmapped reads
+ * never are.  Ties go to the bucket seen first (Spark leaves their order to
+ * its shuffle).  Host C++: a grouping step in front of the device passes. */
+typedef struct bqsr_dup_reads {
+  int64_t n_reads;
+  const char* const* read_name; /* [n] readName (NULL = null)                      */
+  const char* const* library;   /* [n] recordGroupLibrary (NULL = null)            */
+  const uint32_t* flags;        /* [n] BQSR_F_* (PAIRED, MAPPED, NEG_STRAND, PRIMARY, HAS_RG) */
+  const uint8_t* mate_mapped;   /* [n] mateMapped                                  */
+  const int32_t* rg_id;         /* [n] recordGroupId (when BQSR_F_HAS_RG)          */
+  const int32_t* reference_id;  /* [n] referenceId                                 */
+  const int64_t* start;         /* [n] 0-based start                               */
+  const uint64_t* qual_offset;  /* [n+1] */
+  const uint8_t* qual;          /* phred+33 chars                                  */
+  const uint64_t* cigar_offset; /* [n+1] */
+  const uint32_t* cigar;        /* BAM-encoded elements                            */
+} bqsr_dup_reads;
+/* dup[r] = the duplicateRead value MarkDuplicates gives read r */
+bqsr_status bqsr_mark_duplicates(const bqsr_dup_reads* reads, uint8_t* dup);
+/* The same over a parse (readName = QNAME, referenceId = the @SQ index,
+ * mateMapped from FLAG 0x8, library = the read group's LB); the parse's
+ * flags column gets BQSR_F_DUPLICATE set or cleared accordingly, as
+ * `transform -mark_duplicate_reads` does before BQSR. */
+bqsr_status bqsr_sam_mark_duplicates(bqsr_sam* s, int64_t* n_duplicates);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADAM_SAM_H */

@@ -159,6 +159,22 @@ def test_sites_from_small_vcf():
     assert not np.array_equal(g_sites.words, g_none.words)  # some bases were masked by the VCF sites
 
 
+@pytest.mark.parametrize("lens", [(101,), (150, 250)])
+def test_sites_bitmap_dense(lens):
+    """Dense sites (the prep kernel's position bitmap): runs where every
+    position is a site, so reads of 101-250 bases take several 64-offset
+    steps with bits in all three sbits words of a step, plus a sparse contig
+    (no bitmap: the linear scan) on the same batch."""
+    rng = np.random.default_rng(7)
+    dense = np.unique(np.concatenate([np.arange(5_000, 9_000), np.arange(40_001, 40_600, 3),
+                                      rng.integers(1, 200_000, size=20_000)]))
+    b = synth.generate(20000, lens, 1, 71, contig_len=200_000, contig="chr20")
+    sites = {"chr20": dense.tolist(), "chr7": [5, 90_000_000]}
+    g_sites, o_sites = check([b], sites)
+    g_none, _ = check([b], None)
+    assert not np.array_equal(g_sites.words, g_none.words)
+
+
 # ---- the fold at scale --------------------------------------------------------
 
 def test_fold_one_million_reads():

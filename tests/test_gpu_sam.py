@@ -1,0 +1,266 @@
+"""SAM ingest (§8 f1), the output path (§8 f2) and the transform harness on
+the device, against records.read_sam (the SAMRecordConverter restatement) and
+the CPU oracle."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import markdup as M  # oracle/markdup.py
+import oracle as O
+from _parity import run_oracle
+from adam_amd import _capi, bqsr, synth
+from adam_amd import records as R
+from adam_amd.records import read_sam
+from adam_amd.sam import SamText
+from adam_amd.samgen import sam_text
+from adam_amd.transform import transform
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_resources")
+FIXTURES = ["artificial.realigned.sam", "artificial.sam", "reads12.sam", "small.sam",
+            "small_realignment_targets.sam", "unmapped.sam"]
+COLS = ["flags", "rg_id", "ref_index", "start", "seq_offset", "seq", "qual_offset", "qual", "cigar_offset", "cigar",
+        "md_offset", "md"]
+
+
+def assert_same_columns(a: R.RecordBatch, b: R.RecordBatch):
+    assert a.n_reads == b.n_reads
+    assert a.ref_names == b.ref_names
+    for c in COLS:
+        x, y = getattr(a, c), getattr(b, c)
+        assert x.dtype == y.dtype and np.array_equal(x, y), c
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_parse_reference_fixtures(name):
+    path = os.path.join(GOLD, name)
+    assert_same_columns(SamText.read(path).batch(), read_sam(path))
+
+
+EDGE = (b"@HD\tVN:1.4\r\n"
+        b"@SQ\tSN:chrA\tLN:1000\n@SQ\tSN:chrB\tLN:1000\n\n"
+        b"@RG\tID:zeta\tLB:l1\n@RG\tID:alpha\n@RG\tID:mid\tLB:l2\n"
+        b"q1\t0\tchrA\t10\t60\t5M\t*\t0\t0\tACGTN\tIIIII\tMD:Z:5\tRG:Z:mid\r\n"
+        b"\n"
+        b"q2\t16\tchrB\t0\t60\t2S3M\t*\t0\t0\tAC\xe9GT\t#\xa0I!~\tMD:Z:1A1\tMD:i:3\tXX:Z:a:b:c\n"
+        b"q3\t4\t*\t0\t0\t*\t*\t0\t0\t*\t*\n"
+        b"q4\t1107\tchrZ\t77\t60\t1M1I1D1N1S1H1P1=1X\t*\t0\t0\tAAAAAAA\tBBBBBBB\tRG:Z:nope\tRG:Z:alpha\n"
+        b"q5\t+3\tchrA\t 5 \t60\t4M\t*\t0\t0\tGGGG\t????\n"
+        b"q6\t-1\tchrB\t1\t60\t3M\t*\t0\t0\tTTT\t@@@\tMD:Z:\n"
+        b"q7\t256\tchrA\t99\t60\t2M\t*\t0\t0\tCC\tDD")  # no final newline
+
+
+def test_parse_edge_cases(tmp_path):
+    p = tmp_path / "edge.sam"
+    p.write_bytes(EDGE)
+    got = SamText(EDGE).batch()
+    want = read_sam(str(p))
+    assert got.n_reads == 7
+    assert_same_columns(got, want)
+
+
+@pytest.mark.parametrize("line,status", [
+    (b"q\t0\tchrA\t1\t60\t3M\t*\t0\t0\tAAA\n", "SAM_PARSE"),                      # 10 fields
+    (b"q\t0\tchrA\t1\t60\t3M\t*\t0\t0\tAAA\tIII\tMD5\n", "SAM_PARSE"),            # tag without two ':'
+    (b"q\t0\tchrA\t1\t60\t3M\t*\t0\t0\tAAA\tIII\t\n", "SAM_PARSE"),               # empty optional field
+    (b"q\tx1\tchrA\t1\t60\t3M\t*\t0\t0\tAAA\tIII\n", "SAM_PARSE"),                # FLAG
+    (b"q\t0\tchrA\tx\t60\t3M\t*\t0\t0\tAAA\tIII\n", "SAM_PARSE"),                 # POS of a known RNAME
+    (b"q\t0\tchrA\t1\t60\t3Q\t*\t0\t0\tAAA\tIII\n", "SAM_PARSE"),                 # CIGAR op
+    (b"q\t0\tchrA\t1\t60\tM\t*\t0\t0\tAAA\tIII\n", "SAM_PARSE"),                  # CIGAR without length
+    (b"q\t0\tchrA\t1\t60\t3\t*\t0\t0\tAAA\tIII\n", "SAM_PARSE"),                  # trailing number
+    (b"q\t0\tchrA\t1\t60\t3M\t*\t0\t0\tAAA\tIII\n@CO\tlate\n", "UNSUPPORTED"),  # header after a record
+])
+def test_parse_errors(tmp_path, line, status):
+    text = b"@SQ\tSN:chrA\tLN:10\n" + line
+    with pytest.raises(_capi.BQSRError) as e:
+        SamText(text)
+    assert e.value.name == status
+    if status == "SAM_PARSE":  # the Python restatement throws on the same text
+        p = tmp_path / "bad.sam"
+        p.write_bytes(text)
+        with pytest.raises(Exception):
+            read_sam(str(p))
+
+
+def test_parse_unknown_rname_ignores_pos(tmp_path):
+    # int(pos) is only evaluated for a header RNAME (records.py:331-335)
+    text = b"@SQ\tSN:chrA\tLN:10\nq\t0\tchrQ\tx\t60\t3M\t*\t0\t0\tAAA\tIII\n"
+    p = tmp_path / "u.sam"
+    p.write_bytes(text)
+    assert_same_columns(SamText(text).batch(), read_sam(str(p)))
+
+
+def test_parse_synthetic_reads(tmp_path):
+    b = synth.generate(60000, (100, 150), 3, 97, contig_len=2_000_000)
+    text = sam_text(b, n_rg=3)
+    p = tmp_path / "syn.sam"
+    p.write_bytes(text)
+    t0 = time.perf_counter()
+    s = SamText(text)
+    dt = time.perf_counter() - t0
+    got = s.batch()
+    assert_same_columns(got, read_sam(str(p)))
+    print("ingest: %d reads, %.1f MB in %.3f s (incl. H2D)" % (got.n_reads, len(text) / 1e6, dt))
+
+
+def _oracle_quals(batch, sites):
+    o = run_oracle([batch], sites)
+    assert o.error is None, o.error
+    chars, out_len = o.outs[0]
+    return o, [chars[int(batch.qual_offset[r]):int(batch.qual_offset[r]) + int(out_len[r])]
+               for r in range(batch.n_reads)]
+
+
+def _records(text: bytes):
+    return [l.split(b"\t") for l in text.split(b"\n") if l and not l.startswith(b"@")]
+
+
+def test_transform_recalibrate_round_trip(tmp_path):
+    src = os.path.join(GOLD, "artificial.realigned.sam")
+    vcf = os.path.join(GOLD, "small.vcf")
+    out = tmp_path / "out.sam"
+    transform(src, str(out), recalibrate=True, dbsnp=vcf)
+    batch = read_sam(src)
+    snp = bqsr.SnpTable.from_vcf(vcf)
+    o, quals = _oracle_quals(batch, {k: v.tolist() for k, v in snp.table.items()})
+    before, after = _records(open(src, "rb").read()), _records(out.read_bytes())
+    assert len(before) == len(after) == batch.n_reads
+    eligible = 0
+    for r, (a, b) in enumerate(zip(before, after)):
+        assert a[:10] == b[:10] and a[11:] == b[11:]  # every field but QUAL kept
+        f = int(batch.flags[r])
+        if (f & R.F_MAPPED) and (f & R.F_PRIMARY) and not (f & R.F_DUPLICATE):
+            eligible += 1
+            assert b[10] == "".join(map(chr, quals[r])).encode("utf-8"), r
+        else:
+            assert b[10] == a[10]
+    assert eligible > 0
+
+
+def test_transform_empty_table_and_null_rg(tmp_path):
+    with pytest.raises(_capi.BQSRError) as e:
+        transform(os.path.join(GOLD, "small.sam"), str(tmp_path / "o.sam"), recalibrate=True)
+    assert e.value.name == "EMPTY_TABLE"
+    with pytest.raises(_capi.BQSRError) as e:
+        transform(os.path.join(GOLD, "artificial.sam"), str(tmp_path / "o.sam"), recalibrate=True)
+    assert e.value.name == "NULL_RG"
+
+
+def test_transform_synthetic_reads(tmp_path):
+    b = synth.generate(20000, (100,), 2, 5, contig_len=500_000)
+    text = sam_text(b, n_rg=2)
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    sites = synth.known_sites(5000, contig_len=500_000)
+    vcf = tmp_path / "s.vcf"
+    vcf.write_text("".join("chr20\t%d\t.\tA\tC\n" % p for p in sites["chr20"]))
+    transform(str(src), str(out), recalibrate=True, dbsnp=str(vcf))
+    batch = read_sam(str(src))
+    o, quals = _oracle_quals(batch, {"chr20": sites["chr20"].tolist()})
+    before, after = _records(text), _records(out.read_bytes())
+    for r, (a, c) in enumerate(zip(before, after)):
+        f = int(batch.flags[r])
+        assert a[:10] == c[:10] and a[11:] == c[11:]
+        if (f & R.F_MAPPED) and (f & R.F_PRIMARY) and not (f & R.F_DUPLICATE):
+            assert c[10] == "".join(map(chr, quals[r])).encode("utf-8"), r
+        else:
+            assert c[10] == a[10]
+
+
+def test_rewrite_java_chars_as_utf8():
+    # the output path's encoding (Q14): the apply buffers of a job, overwritten
+    # with chars of every UTF-8 length (u8 slots plus exceptions above 0xFF)
+    from adam_amd.job import ResidentJob
+    import torch
+    src = os.path.join(GOLD, "artificial.realigned.sam")
+    sam = SamText.read(src)
+    batch = sam.batch()
+    job = ResidentJob(batch, bqsr.dims_of([batch]), None, 0)
+    try:
+        job.step()
+        L = _capi.lib()
+        n = batch.n_reads
+        slots = np.zeros(n, np.int64)
+        # the batch's slot of each read: consecutive 16-aligned spans (bqsr_capi.cpp slot_span)
+        lq = np.diff(batch.qual_offset.astype(np.int64))
+        ls = np.diff(batch.seq_offset.astype(np.int64))
+        span = ((np.maximum(lq, ls) + 15) // 16) * 16
+        slots[1:] = np.cumsum(span)[:-1]
+        assert int(L.bqsr_batch_slots(job.bh)) == int(span.sum())
+        oq = np.zeros(job.out_qual.numel(), np.uint8)
+        ost = np.zeros(n, np.int32)
+        oln = np.zeros(n, np.int32)
+        exc = []
+        want = {}
+        for r in range(n):
+            k = int(min(lq[r], 12))
+            chars = [0x41 + ((r * 7 + j * 29) % 0xBE) for j in range(k)]
+            if k > 3:
+                chars[2] = 0x100 + r * 97
+                chars[3] = 0x7FF + r
+            for j, c in enumerate(chars):
+                oq[slots[r] + 1 + j] = c & 0xFF
+                if c > 0xFF:
+                    exc.append(((int(slots[r]) + 1 + j) << 16) | c)
+            ost[r], oln[r] = 1, k
+            want[r] = "".join(map(chr, chars)).encode("utf-8")
+        job.out_qual.copy_(torch.from_numpy(oq))
+        job.out_start[:n].copy_(torch.from_numpy(ost))
+        job.out_len[:n].copy_(torch.from_numpy(oln))
+        job.exc[:len(exc)].copy_(torch.from_numpy(np.asarray(exc[::-1], np.int64)))
+        job.n_exc = len(exc)
+        torch.cuda.synchronize()
+        sam.rewrite(job)
+        after = _records(sam.text())
+        before = _records(open(src, "rb").read())
+        for r in range(n):
+            f = int(batch.flags[r])
+            if (f & R.F_MAPPED) and (f & R.F_PRIMARY) and not (f & R.F_DUPLICATE):
+                assert after[r][10] == want[r], r
+            else:
+                assert after[r][10] == before[r][10]
+    finally:
+        job.close()
+        sam.close()
+
+
+def test_transform_mark_duplicates(tmp_path):
+    # pairs and fragments stacked on few positions, flags then BQSR's eligibility
+    b = synth.generate(4000, (60,), 2, 11, contig_len=3000, p_duplicate=0.0)
+    text = sam_text(b, n_rg=2, qname="p")
+    lines = text.split(b"\n")
+    # mates share a QNAME: pair read 2k+1 with read 2k
+    body = [l for l in lines if l and not l.startswith(b"@")]
+    for k in range(1, len(body), 2):
+        f = body[k].split(b"\t")
+        f[0] = body[k - 1].split(b"\t")[0]
+        body[k] = b"\t".join(f)
+    text = b"\n".join([l for l in lines if l.startswith(b"@")] + body) + b"\n"
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    st = transform(str(src), str(out), mark_duplicates=True)
+    # the restatement over the same records
+    batch = read_sam(str(src))
+    recs = _records(text)
+    rg_lib = {i: "lib%d" % (i % 2) for i in range(2)}
+    reads = []
+    for r, f in enumerate(recs):
+        fl = int(batch.flags[r])
+        flag = int(f[1])
+        cig = R.parse_cigar(f[5].decode())
+        reads.append(dict(name=f[0].decode(), library=rg_lib[int(batch.rg_id[r])] if fl & R.F_HAS_RG else None,
+                          rg=int(batch.rg_id[r]) if fl & R.F_HAS_RG else None, mapped=bool(fl & R.F_MAPPED),
+                          primary=bool(fl & R.F_PRIMARY), paired=bool(fl & R.F_PAIRED),
+                          mate_mapped=flag != 0 and bool(flag & 1) and not flag & 8, neg=bool(fl & R.F_NEG_STRAND),
+                          ref=0, start=int(batch.start[r]), qual=f[10].decode("latin-1"),
+                          cigar=[(int(e) >> 4, "MIDNSHP=X"[int(e) & 15]) for e in cig]))
+    want = M.mark_duplicates(reads)
+    assert st["duplicates"] == sum(want) > 0
+    after = _records(out.read_bytes())
+    for r, (a, c) in enumerate(zip(recs, after)):
+        flag = int(a[1])
+        assert int(c[1]) == ((flag | 0x400) if want[r] else (flag & ~0x400)), r
+        assert a[2:] == c[2:]

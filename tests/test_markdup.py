@@ -1,0 +1,141 @@
+"""MarkDuplicates (§8 f3): the library's bqsr_mark_duplicates (host C++, no
+device) against the cases of core/.../rdd/MarkDuplicatesSuite.scala:27-166 and
+against the plain-Python restatement in oracle/markdup.py on random read sets."""
+
+import numpy as np
+import pytest
+
+from adam_amd import records as R
+from adam_amd.sam import mark_duplicates
+import markdup as M  # oracle/markdup.py (tests/conftest.py puts oracle/ on sys.path)
+
+_uid = [0]
+
+
+def _name():
+    _uid[0] += 1
+    return "uuid-%d" % _uid[0]
+
+
+def mapped(ref, pos, name=None, phred=20, clipped=0, primary=True, neg=False):
+    """MarkDuplicatesSuite.createMappedRead (:27-48)."""
+    cigar = [(clipped, "S"), (100 - clipped, "M")] if clipped else [(100, "M")]
+    return dict(name=name or _name(), library="library bar", rg=0, mapped=True, primary=primary, paired=False,
+                mate_mapped=False, neg=neg, ref=ref, start=pos, qual=chr(phred + 33) * 100, cigar=cigar)
+
+
+def unmapped():
+    """createUnmappedRead (:23-25): only readMapped = false is set."""
+    return dict(name=None, library=None, rg=None, mapped=False, primary=False, paired=False, mate_mapped=False,
+                neg=False, ref=0, start=0, qual="", cigar=[])
+
+
+def pair(ref1, pos1, ref2, pos2, name=None, phred=20):
+    """createPair (:50-72)."""
+    name = name or _name()
+    a = mapped(ref1, pos1, name=name, phred=phred)
+    b = mapped(ref2, pos2, name=name, phred=phred, neg=True)
+    for r in (a, b):
+        r["paired"] = True
+        r["mate_mapped"] = True
+    return [a, b]
+
+
+def run(reads):
+    ops = "MIDNSHP=X"
+    flags, quals, cigs = [], [], []
+    for r in reads:
+        f = 0
+        f |= R.F_MAPPED if r["mapped"] else 0
+        f |= R.F_PRIMARY if r["primary"] else 0
+        f |= R.F_PAIRED if r["paired"] else 0
+        f |= R.F_NEG_STRAND if r["neg"] else 0
+        f |= R.F_HAS_RG if r["rg"] is not None else 0
+        flags.append(f)
+        quals.append(r["qual"].encode("latin-1"))
+        cigs.append([(n << 4) | ops.index(op) for n, op in r["cigar"]])
+    qo = np.zeros(len(reads) + 1, np.uint64)
+    np.cumsum([len(q) for q in quals], out=qo[1:])
+    co = np.zeros(len(reads) + 1, np.uint64)
+    np.cumsum([len(c) for c in cigs], out=co[1:])
+    got = mark_duplicates([r["name"] for r in reads], [r["library"] for r in reads], flags,
+                          [r["mate_mapped"] for r in reads], [r["rg"] or 0 for r in reads],
+                          [r["ref"] for r in reads], [r["start"] for r in reads], qo,
+                          np.frombuffer(b"".join(quals), np.uint8), co,
+                          np.asarray([e for c in cigs for e in c], np.uint32))
+    want = M.mark_duplicates(reads)
+    assert list(got) == want
+    return got
+
+
+def test_single_read():
+    assert not run([mapped(0, 100)]).any()
+
+
+def test_reads_at_different_positions():
+    assert not run([mapped(0, 42), mapped(0, 43)]).any()
+
+
+def test_reads_at_the_same_position():
+    reads = [mapped(1, 42, phred=30, name="best")] + [mapped(1, 42, name="poor%d" % i) for i in range(10)]
+    d = run(reads)
+    assert not d[0] and d[1:].all()
+
+
+def test_reads_at_the_same_position_with_clipping():
+    reads = ([mapped(1, 42, phred=30, name="best")] +
+             [mapped(1, 44, clipped=2, name="poorClipped%d" % i) for i in range(5)] +
+             [mapped(1, 42, name="poorUnclipped%d" % i) for i in range(5)])
+    d = run(reads)
+    assert not d[0] and d[1:].all()
+
+
+def test_reads_on_reverse_strand():
+    reads = [mapped(10, 42, neg=True, phred=30, name="best")] + \
+            [mapped(10, 42, neg=True, name="poor%d" % i) for i in range(7)]
+    d = run(reads)
+    assert not d[0] and d[1:].all()
+
+
+def test_unmapped_reads():
+    assert not run([unmapped() for _ in range(10)]).any()
+
+
+def test_read_pairs():
+    reads = pair(0, 10, 0, 210, name="best", phred=30)
+    for i in range(10):
+        reads += pair(0, 10, 0, 210, name="poor%d" % i)
+    d = run(reads)
+    assert not d[:2].any() and d[2:].all()
+
+
+def test_read_pairs_with_fragments():
+    reads = [mapped(2, 33, phred=40, name="fragment%d" % i) for i in range(10)] + pair(2, 33, 2, 200, name="pair")
+    d = run(reads)
+    assert d[:10].all() and not d[10:].any()
+
+
+def test_quality_score():
+    assert M.score(dict(qual=chr(53) * 100)) == 2000
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_reads_against_restatement(seed):
+    rng = np.random.default_rng(seed)
+    reads = []
+    for k in range(400):
+        kind = rng.integers(0, 10)
+        name = "q%d" % rng.integers(0, 150)
+        lib = [None, "libA", "libB"][rng.integers(0, 3)]
+        rg = [None, 0, 1][rng.integers(0, 3)]
+        clip = int(rng.integers(0, 3)) * int(rng.integers(0, 6))
+        cig = ([(clip, "S")] if clip else []) + [(int(rng.integers(20, 60)), "M")]
+        if rng.integers(0, 4) == 0:
+            cig += [(int(rng.integers(1, 4)), "D"), (int(rng.integers(5, 20)), "M"), (int(rng.integers(1, 5)), "H")]
+        r = dict(name=name, library=lib, rg=rg, mapped=kind != 0, primary=kind != 1, paired=bool(rng.integers(0, 2)),
+                 mate_mapped=bool(rng.integers(0, 2)), neg=bool(rng.integers(0, 2)), ref=int(rng.integers(0, 2)),
+                 start=int(rng.integers(0, 30)),
+                 qual="".join(chr(33 + int(q)) for q in rng.integers(0, 45, size=int(rng.integers(0, 40)))),
+                 cigar=cig)
+        reads.append(r)
+    run(reads)

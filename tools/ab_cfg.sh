@@ -1,0 +1,20 @@
+#!/bin/bash
+# A/B kernel stats of one config: tools/ab_cfg.sh TAG CONFIG lib1 lib2 ... ("-" = default library)
+set -e
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=$1
+CFG=$2
+shift 2
+O="$R/gpurun_out/$TAG"
+mkdir -p "$O"
+export TMPDIR=/tmp
+i=0
+for lib in "$@"; do
+  i=$((i+1))
+  if [ "$lib" = "-" ]; then unset ADAM_BQSR_LIB; else export ADAM_BQSR_LIB="$R/$lib"; fi
+  cd /tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/s$i" -o run --output-format csv -- \
+    python3 "$R/bench.py" --config "$CFG" --no-cpu-baseline --no-parity --steps 5 --warmup 1 > "$O/s$i.log" 2>&1
+  echo "== $lib"
+  find "$O/s$i" -name "*kernel_stats.csv" -exec grep -E "prep|observe|apply" {} \; | cut -d, -f1,4
+done
