@@ -264,3 +264,14 @@ def test_transform_mark_duplicates(tmp_path):
         flag = int(a[1])
         assert int(c[1]) == ((flag | 0x400) if want[r] else (flag & ~0x400)), r
         assert a[2:] == c[2:]
+
+
+def test_compare_baseqs_transform_output(tmp_path):
+    # compare -baseqs (§8 f4) between the input and its recalibrated output
+    from adam_amd.compare import compare_baseqs
+    src = os.path.join(GOLD, "small_realignment_targets.sam")
+    out = tmp_path / "out.sam"
+    transform(src, str(out), recalibrate=True)
+    r = compare_baseqs(src, str(out), "latin-1", "utf-8")
+    assert r["unique1"] == r["unique2"] == 0
+    assert r["count"] > 0 and r["identity"] < r["count"]
