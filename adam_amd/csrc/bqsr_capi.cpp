@@ -172,7 +172,9 @@ TableGeom geom(const bqsr_dims& d) {
 constexpr size_t kLdsMax = 163840;
 // LDS of the per-base passes: observe's u32 window [qw][wcells] x {obs, mm}
 // + masked counts + block histogram; apply's char table [qw][cw][21]
-size_t observe_lds(int qw, int wcells) { return (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4; }
+size_t observe_lds(int qw, int wcells) {
+  return (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 + (size_t)kMkWords * 4;
+}
 size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + (size_t)qw * cw * kCtxSlots; }
 int observe_rows(int wcells) {
   int qw = kQBins;
@@ -201,6 +203,16 @@ bool chunk_lanes(bool dflt) {
 // lanes per read of the lane-per-super-chunk passes: 2^s >= the super-chunks
 // (64 offsets) of the batch's longest read (at most 64; longer reads loop)
 int lane_shift(const bqsr_batch* b);
+// observe's form: ADAM_BQSR_OBSERVE=chunk (bqsr_observe_chunks, the lane-per-chunk walk), read
+// (bqsr_observe_kernel: lane per read, or lanes per super-chunk when bucketed), superchunk; unset:
+// chunk for bucketed batches, read otherwise (-1)
+int observe_form() {
+  static const int v = [] {
+    const char* e = getenv("ADAM_BQSR_OBSERVE");
+    return !e ? -1 : strcmp(e, "read") == 0 ? 1 : strcmp(e, "superchunk") == 0 ? 2 : 0;
+  }();
+  return v;
+}
 // observe's rotated fast path (bqsr_observe_kernel<true, false>); ADAM_BQSR_OBSERVE_ROTATE=0/1 overrides
 bool observe_rotate() {
   static const bool v = [] {
@@ -362,7 +374,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   for (const void* f : {(const void*)bqsr_observe_kernel<false, false>, (const void*)bqsr_observe_kernel<true, false>,
-                        (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel})
+                        (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel,
+                        (const void*)bqsr_observe_chunks})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -1003,7 +1016,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     // pass 1: the common reads in lock step; pass 2: the rest, one thread each
     const int64_t blocks = (b->rd.n_reads + kPrepChunk - 1) / kPrepChunk;
     hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
-    hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
+    hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)blocks), dim3(kComplexThreads), 0, s, P);
     HIP_TRY(hipGetLastError());
     if (b->bucketed) {  // counting sort of the reads by read group
       const int64_t n = b->rd.n_reads;
@@ -1072,7 +1085,12 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.n_blocks = b->n_blocks;
     const size_t lds = observe_lds(P.w.qw, P.wcells);
     P.lane_shift = lane_shift(b);
-    if (chunk_lanes(b->bucketed))
+    // measured (cfg2 / cfg4 / cfg3): the chunk walk wins on bucketed batches (4.63 vs 5.03 ms),
+    // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
+    const int form = observe_form() >= 0 ? observe_form() : (b->bucketed ? 0 : 1);
+    if (form == 0)
+      hipLaunchKernelGGL(bqsr_observe_chunks, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    else if (form == 2 || chunk_lanes(b->bucketed))
       hipLaunchKernelGGL((bqsr_observe_kernel<false, true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else if (observe_rotate())
       hipLaunchKernelGGL((bqsr_observe_kernel<true, false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);

@@ -211,6 +211,7 @@ __device__ __forceinline__ ReadInfo resolve_info(const ReadsDev& rd, ReadInfo in
 // global load per element.  Strides of 5 and 9 dwords keep the 64 lanes'
 // slots in distinct banks.
 constexpr int kPrepThreads = 256;
+constexpr int kComplexThreads = 128;  // bqsr_prep_complex: a segment holds a few % of its 2048 reads
 constexpr int kPrepCig = 4, kPrepCigStride = 5;
 constexpr int kPrepMd = 32, kPrepMdStride = 9;
 constexpr int kPrepChunk = 2048;  // reads per workgroup of bqsr_prep_kernel (8 per thread)
@@ -495,6 +496,60 @@ __device__ __forceinline__ bool mask_sites_bitmap(const PrepParams& P, int32_t c
   return true;
 }
 
+// A read's sbits words in registers (prep_fast, reads whose bits fit in
+// kAccWords words): bit b of the accumulator = slot (rs & ~31) + b; static
+// indices only (a dynamic one would put the array in scratch).
+constexpr int kAccWords = 5;
+__device__ __forceinline__ void acc_range(uint64_t acc[kAccWords], uint32_t lo, uint32_t hi, int half) {
+#pragma unroll
+  for (int j = 0; j < kAccWords; ++j) {
+    const uint32_t a = max(lo, 32u * j), b = min(hi, 32u * j + 32u);
+    const uint32_t n = b > a ? b - a : 0u;
+    const uint32_t m = n >= 32u ? 0xFFFFFFFFu : (((1u << n) - 1u) << (a - 32u * j));
+    acc[j] |= n ? (uint64_t)m << half : 0ull;
+  }
+}
+__device__ __forceinline__ void acc_bit(uint64_t acc[kAccWords], uint32_t b, int half) {
+#pragma unroll
+  for (int j = 0; j < kAccWords; ++j) acc[j] |= (b >> 5) == (uint32_t)j ? 1ull << ((b & 31) + half) : 0ull;
+}
+// mask_sites_bitmap into the accumulator (offsets 0 .. lq-1 at bits r0 + o)
+__device__ __forceinline__ bool sites_bitmap_acc(const PrepParams& P, int32_t contig, int64_t unclipped, int lq,
+                                                 uint32_t r0, uint64_t acc[kAccWords]) {
+  const SitesDev& S = P.sites;
+  const int64_t nw = (int64_t)(S.bm_off[contig + 1] - S.bm_off[contig]);
+  if (nw == 0) return false;
+  const uint64_t* w = S.bm + S.bm_off[contig];
+  const int64_t b0 = unclipped - S.bm_base[contig];
+  int64_t wi = b0 >> 6;
+  const uint32_t sh = (uint32_t)(b0 & 63);
+  uint64_t lo = (wi >= 0 && wi < nw) ? w[wi] : 0ull;
+#pragma unroll
+  for (int step = 0; step < 2; ++step) {  // offsets 64 step .. 64 step + 63 (lq <= 160 - r0 <= 160)
+    const int o = 64 * step;
+    if (o >= lq) break;
+    ++wi;
+    const uint64_t hi = (wi >= 0 && wi < nw) ? w[wi] : 0ull;
+    uint64_t m = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    lo = hi;
+    if (lq - o < 64) m &= (1ull << (lq - o)) - 1ull;
+    // bits r0 + o .. : word 2 step + ((r0 + o) >> 5 - 2 step) = 2 step, at bit r0
+    const uint64_t lo64 = m << r0, hi64 = r0 ? m >> (64 - r0) : 0ull;
+    acc[2 * step] |= (uint64_t)(uint32_t)lo64;
+    acc[2 * step + 1] |= (uint64_t)(uint32_t)(lo64 >> 32);
+    if (2 * step + 2 < kAccWords) acc[2 * step + 2] |= (uint64_t)(uint32_t)hi64;
+  }
+  if (lq > 128) {  // offsets 128 .. lq-1 (lq <= 160 - r0 <= 160: at most 32 more)
+    ++wi;
+    const uint64_t hi = (wi >= 0 && wi < nw) ? w[wi] : 0ull;
+    uint64_t m = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    m &= (1ull << (lq - 128)) - 1ull;
+    const uint64_t lo64 = m << r0;
+    acc[4] |= (uint64_t)(uint32_t)lo64;
+  }
+  return true;
+}
+
 // The common read, prepared in lock step (no data-dependent loop) and
 // without touching its quals: eligible, every field present, a CIGAR of the
 // form [S]M[S] covering the whole read (so the trimmed range, whatever it is,
@@ -579,33 +634,79 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
     }
     if (!ok) return false;  // (a letter first or last is invalid: `i > 0 && i + 1 < n`)
     const int64_t md_total = pos + num;
-    // masked: the clips (reference positions outside [start, start + mlen))
-    if (lead > st) set_sbits(P.sbits, rs + st, rs + min(lead, (int64_t)en), 0);
-    if (lead + mlen < en) set_sbits(P.sbits, rs + max((int64_t)st, lead + mlen), rs + en, 0);
-    // mismatches: each letter's position, then every position past the tag's span
-    num = 0;
-    pos = 0;
+    // with known sites (several bits per read, from three sources) the bits
+    // are gathered per word first; without, the few bits go straight out
+    // (measured: the gathering costs more than it saves on cfg2's reads)
+    if (P.sites.n_contigs > 0 && (int64_t)(rs & 31) + en <= 32 * kAccWords) {
+      // the read's sbits words in registers, one atomic OR per word with bits
+      // (measured: plain stores of the words a read owns alone, mixed with
+      // the neighbours' atomics on the same lines, were 2x slower)
+      uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
+      const uint32_t r0 = (uint32_t)(rs & 31);  // bit of offset 0 in acc
+      if (lead > st) acc_range(acc, r0 + st, r0 + (uint32_t)min(lead, (int64_t)en), 0);
+      if (lead + mlen < en) acc_range(acc, r0 + (uint32_t)max((int64_t)st, lead + mlen), r0 + en, 0);
+      num = 0;
+      pos = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-      if (i < n) {
-        if (c >= '0' && c <= '9') {
-          num = num * 10 + (int64_t)(c - '0');
-        } else {
-          pos += num;
-          num = 0;
-          const int64_t o = lead + pos;  // reference position start + pos
-          if (pos < mlen && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
-          pos += 1;
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        if (i < n) {
+          if (c >= '0' && c <= '9') {
+            num = num * 10 + (int64_t)(c - '0');
+          } else {
+            pos += num;
+            num = 0;
+            const int64_t o = lead + pos;
+            if (pos < mlen && o >= st && o < en) acc_bit(acc, r0 + (uint32_t)o, 32);
+            pos += 1;
+          }
         }
       }
+      if (md_total < mlen) {
+        const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
+        if (lo < hi) acc_range(acc, r0 + (uint32_t)lo, r0 + (uint32_t)hi, 32);
+      }
+      bool linear = false;
+      if (a.contig >= 0 && a.contig < P.sites.n_contigs) {
+        if (!sites_bitmap_acc(P, a.contig, unclipped, en, r0, acc)) linear = true;
+      }
+      const uint64_t wb = rs >> 5;
+#pragma unroll
+      for (int j = 0; j < kAccWords; ++j) {
+        if (!acc[j]) continue;
+        const uint64_t wi = wb + (uint64_t)j;
+        atomicOr((unsigned long long*)&P.sbits[wi], (unsigned long long)acc[j]);
+      }
+      if (linear) mask_sites_linear(P, a.contig, unclipped, st, en, rs);
+    } else {
+      // masked: the clips (reference positions outside [start, start + mlen))
+      if (lead > st) set_sbits(P.sbits, rs + st, rs + min(lead, (int64_t)en), 0);
+      if (lead + mlen < en) set_sbits(P.sbits, rs + max((int64_t)st, lead + mlen), rs + en, 0);
+      // mismatches: each letter's position, then every position past the tag's span
+      num = 0;
+      pos = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        if (i < n) {
+          if (c >= '0' && c <= '9') {
+            num = num * 10 + (int64_t)(c - '0');
+          } else {
+            pos += num;
+            num = 0;
+            const int64_t o = lead + pos;  // reference position start + pos
+            if (pos < mlen && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
+            pos += 1;
+          }
+        }
+      }
+      if (md_total < mlen) {
+        const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
+        if (lo < hi) set_sbits(P.sbits, rs + (uint64_t)lo, rs + (uint64_t)hi, 32);
+      }
+      if (a.contig >= 0 && a.contig < P.sites.n_contigs && !mask_sites_bitmap(P, a.contig, unclipped, en, rs))
+        mask_sites_linear(P, a.contig, unclipped, st, en, rs);
     }
-    if (md_total < mlen) {
-      const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
-      if (lo < hi) set_sbits(P.sbits, rs + (uint64_t)lo, rs + (uint64_t)hi, 32);
-    }
-    if (a.contig >= 0 && a.contig < P.sites.n_contigs && !mask_sites_bitmap(P, a.contig, unclipped, en, rs))
-      mask_sites_linear(P, a.contig, unclipped, st, en, rs);
   }
   P.info[r] = ReadInfo{0, 0,
                        (uint16_t)(kInfoTrim | kInfoApp | (usable ? kInfoObs : 0) |
@@ -647,12 +748,12 @@ extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(Prep
 
 // Pass 2: workgroup w takes the reads pass 1's workgroup w listed, one thread
 // per read, the full per-read path (prep_one).
-extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_complex(PrepParams P) {
-  __shared__ uint32_t s_cig[kPrepThreads * kPrepCigStride];
-  __shared__ uint32_t s_md[kPrepThreads * kPrepMdStride];
+extern "C" __global__ void __launch_bounds__(kComplexThreads) bqsr_prep_complex(PrepParams P) {
+  __shared__ uint32_t s_cig[kComplexThreads * kPrepCigStride];
+  __shared__ uint32_t s_md[kComplexThreads * kPrepMdStride];
   const uint32_t k = P.n_work[blockIdx.x];
   const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
-  for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads)
+  for (uint32_t i = threadIdx.x; i < k; i += kComplexThreads)
     prep_one(P, (int64_t)P.work[c0 + i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
 }
 
@@ -1184,6 +1285,174 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
         const uint32_t tot = v + w_masked[slot];
         pb[2 * qw * wcells + slot] = tot;
         if (ident && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+      }
+    }
+    __syncthreads();
+  }
+  if (ident)
+    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
+}
+
+// Lane per chunk (chunk_walk): the same counts, each lane one 16-offset
+// chunk of the wavefront's reads laid end to end.  LDS: the window as in
+// bqsr_observe_kernel, then the walk's kMkWords markers.
+struct ObsChunkLoads {
+  uint4 qs, cr;
+  uint64_t bw0, bw1;  // sbits words of the chunk's first slot and the next
+};
+
+__device__ __forceinline__ ObsChunkLoads observe_load(const ObserveParams& P, const LaneRead& x, int j, bool on) {
+  ObsChunkLoads v{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0, 0};
+  if (!on) return v;
+  const int o0 = x.st + j;
+  v.qs = *(const uint4*)(P.rd.qual + x.slot + o0);
+  if (x.fl & kInfoObs) {
+    v.cr = chunk_raw(P.rd, chunk_n0(x, o0));
+    const uint64_t s0 = x.slot + (uint64_t)o0;
+    v.bw0 = P.sbits[s0 >> 5];
+    if ((s0 & 31) > 16) v.bw1 = P.sbits[(s0 >> 5) + 1];  // an unaligned layout's chunk across two words
+  }
+  return v;
+}
+
+struct ObsPiece {
+  uint32_t *w_obs, *w_mm, *w_masked, *blk_hist;
+  int rg_w, c_lo, cw, q_lo, qw, wcells;
+  bool ident;
+};
+
+__device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsPiece& pc, const LaneRead& x, int j,
+                                              int n, bool on, const ObsChunkLoads& ld) {
+  if (!on) return;
+  const bool full = x.fl & kInfoObs;
+  const int o0 = x.st + j;
+  const int C = P.g.C, cells = P.g.cells;
+  const uint32_t qd[4] = {ld.qs.x, ld.qs.y, ld.qs.z, ld.qs.w};
+  uint32_t bm = 0, bx = 0;
+  uint32_t xo[4] = {4u, 4u, 4u, 4u};
+  if (full) {
+    const uint32_t sb = (uint32_t)((x.slot + (uint64_t)o0) & 31);
+    bm = __builtin_amdgcn_alignbit((uint32_t)ld.bw1, (uint32_t)ld.bw0, sb);
+    bx = __builtin_amdgcn_alignbit((uint32_t)(ld.bw1 >> 32), (uint32_t)(ld.bw0 >> 32), sb);
+    uint64_t clo;
+    uint32_t chi;
+    chunk_finish(P.rd, x, chunk_n0(x, o0), ld.cr, clo, chi);
+    ctx_slots(clo, chi, xo);
+    if (j <= 0) ctx_first(xo, -j);  // the read's first visited offset: context 0
+  }
+  const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
+  const int wc0 = cc0 - pc.c_lo;                 // ... and window cycle cell
+  const uint32_t nv = (uint32_t)min(kChunk, n - j);
+  const int klo = j < 0 ? -j : 0;
+  const bool cok = full && x.rg == pc.rg_w && (unsigned)(wc0 + klo * x.dir) < (unsigned)pc.cw &&
+                   (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)pc.cw;
+  const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
+  uint32_t fastm = 0;
+  if (cok) {
+#pragma unroll
+    for (int k = 0; k < kChunk; ++k) {
+      const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
+      const int row = q - pc.q_lo;
+      const bool f = (unsigned)row < (unsigned)pc.qw && ((vmask >> k) & 1u);
+      const bool m = (bm >> k) & 1u;
+      const int base = row * pc.wcells;
+      if (f) {
+        atomicAdd(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k], 1u);
+        if (!m) atomicAdd(&pc.w_obs[base + pc.cw + (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)], 1u);
+      }
+      fastm |= (uint32_t)f << k;
+    }
+  }
+  uint32_t slow = vmask & ~fastm;
+  uint32_t mmk = fastm & ~bm & bx;
+  if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
+    const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+    while (mmk) {
+      const int k = __builtin_ctz(mmk);
+      mmk &= mmk - 1;
+      const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
+      const int base = (q - pc.q_lo) * pc.wcells;
+      atomicAdd(&pc.w_mm[base + wc0 + x.dir * k], 1u);
+      atomicAdd(&pc.w_mm[base + pc.cw + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+    const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+    while (slow) {
+      const int k = __builtin_ctz(slow);
+      slow &= slow - 1;
+      const int o = o0 + k;
+      const int q = (int)(int8_t)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
+      if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+        report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+      } else if (full) {  // outside the LDS window: straight to the int64 table
+        const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
+        const int ccell = cc0 + x.dir * k;
+        const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
+        if (pc.ident) atomicAdd(&pc.blk_hist[q], 1u);
+        const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
+        atomicAdd((unsigned long long*)&P.touched[key], 1ull);
+        if (!masked) {
+          atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
+          atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
+          if (mism) {
+            atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
+            atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+          }
+        }
+      }
+    }
+  }
+}
+
+constexpr int kObserveU = 2;  // chunks in flight per lane
+
+__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObserveParams P) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int qw = P.w.qw, L = P.g.L;
+  const int wcells = P.wcells;
+  uint32_t* w_obs = (uint32_t*)smem;
+  uint32_t* w_mm = w_obs + qw * wcells;
+  uint32_t* w_masked = w_mm + qw * wcells;
+  uint32_t* blk_hist = w_masked + qw;
+  uint32_t* mk_all = blk_hist + kQBins;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* mk = mk_all + wave * 64;
+  const int G = P.n_blocks;
+  const bool ident = P.ord.perm == nullptr;
+  for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+  const int nk = order_keys(P.ord);
+  for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
+    const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
+    const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
+    if (p0 >= wb) break;
+    if (p0 >= p1) continue;
+    const WinGeom gm = win_geom(P.ord, P.g, key);
+    const ObsPiece pc{w_obs, w_mm, w_masked, blk_hist, key_rg(P.ord, key, P.w.rg_lo), gm.c_lo, gm.cw, P.w.q_lo, qw,
+                      wcells, ident};
+    for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
+    __syncthreads();
+    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads>(
+        P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk,
+        [&](const LaneRead& x, bool live) {
+          if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+        },
+        [&](const LaneRead& x, int j, bool on) { return observe_load(P, x, j, on); },
+        [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) { observe_chunk(P, pc, x, j, n, on, ld); });
+    __syncthreads();
+    // ---- the piece's window -> its slab; window rows into the block histogram ----
+    uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
+    for (int i = tid; i < 2 * qw * wcells; i += blockDim.x) pb[i] = w_obs[i];
+    for (int slot = wave; slot < qw; slot += kWaves) {
+      uint32_t v = 0;
+      for (int c = lane; c < gm.cw; c += 64) v += w_obs[slot * wcells + c];  // every unmasked base hits one cycle cell
+      v = wave_sum(v);
+      if (lane == 0) {
+        const uint32_t tot = v + w_masked[slot];
+        pb[2 * qw * wcells + slot] = tot;
+        if (ident && tot && P.w.q_lo + slot < kQBins) atomicAdd(&blk_hist[P.w.q_lo + slot], tot);
       }
     }
     __syncthreads();
@@ -1758,10 +2027,7 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
   }
 }
 
-#ifndef BQSR_APPLY_U
-#define BQSR_APPLY_U 4
-#endif
-constexpr int kApplyU = BQSR_APPLY_U;  // chunks in flight per lane
+constexpr int kApplyU = 4;  // chunks in flight per lane
 
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
