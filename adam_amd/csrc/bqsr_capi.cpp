@@ -294,8 +294,10 @@ struct bqsr_batch {
   OrderDev order() const {
     return bucketed ? OrderDev{d_perm, d_key_off, n_keys} : OrderDev{nullptr, nullptr, 1};
   }
+  uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
   ~bqsr_batch() {
     if (d_part) (void)hipFree(d_part);
+    if (h_status) (void)hipHostFree(h_status);
     for (void* p : allocs) (void)hipFree(p);
   }
 };
@@ -324,6 +326,7 @@ struct bqsr_lut {
   double *a2 = nullptr, *s1 = nullptr, *d2 = nullptr;
   FinalOut* d_out = nullptr;
   FinalOut out{};
+  bool out_pending = false;  // bqsr_finalize_device: `out` not copied back yet (bqsr_job_result / lut_out)
   // host mirror for stats / shifts queries (filled lazily)
   bool host_ready = false;
   std::vector<int64_t> h_words, h_qk_obs, h_qk_mm, h_grp_obs, h_grp_mm;
@@ -1227,7 +1230,10 @@ bqsr_status finalize_impl(bqsr_context* ctx, const bqsr_table* t, double em, con
   hipLaunchKernelGGL(bqsr_final_tables, dim3((unsigned)std::min<int64_t>(8192, (ncell + 255) / 256)), dim3(256), 0, s,
                      t->obs(), t->mm(), g, n_rg, L->a2, L->rq_ok, pow10tab().v[kMaxQ], L->s1, L->d2);
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpyAsync(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost, s);
+  // the device path (em in HBM) leaves `out` on the device: bqsr_job_result
+  // fetches it with the job's other status words in one transfer
+  L->out_pending = em_dev != nullptr;
+  if (e == hipSuccess && !em_dev) e = hipMemcpyAsync(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost, s);
   if (e != hipSuccess) {
     if (!reuse) delete L;
     return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
@@ -1265,6 +1271,10 @@ bqsr_status bqsr_batch_em_copy_async(bqsr_batch* b, double* dst, void* stream) {
 bqsr_status bqsr_finalize_result(bqsr_lut* L, void* stream) {
   HIP_TRY(hipSetDevice(L->ctx->device));
   HIP_TRY(hipStreamSynchronize(S(stream)));
+  if (L->out_pending) {
+    HIP_TRY(hipMemcpy(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost));
+    L->out_pending = false;
+  }
   if (!L->out.any_key)  // readGroupCounts.values.reduce on an empty map (RecalTable.scala:123)
     return fail(BQSR_ERR_EMPTY_TABLE, "empty.reduceLeft: no usable base was observed");
   return ok();
@@ -1290,6 +1300,11 @@ namespace {
 bqsr_status lut_host(bqsr_lut* L) {
   if (L->host_ready) return BQSR_OK;
   HIP_TRY(hipSetDevice(L->ctx->device));
+  if (L->out_pending) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost));
+    L->out_pending = false;
+  }
   const TableGeom g = geom(L->dims);
   L->h_words.resize((size_t)table_words(L->dims));
   L->h_qk_obs.resize((size_t)g.K);
@@ -1317,6 +1332,11 @@ bool eprob(int64_t obs, int64_t mm, double* v) {
 bqsr_status bqsr_lut_stats(const bqsr_lut* lc, bqsr_final_stats* out) {
   bqsr_lut* L = const_cast<bqsr_lut*>(lc);
   if (!L || !out) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (L->out_pending) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&L->out, L->d_out, sizeof(FinalOut), hipMemcpyDeviceToHost));
+    L->out_pending = false;
+  }
   out->average_reported_error = L->out.avg;
   out->global_error = L->out.global_error;
   out->global_obs = L->out.g_obs;
@@ -1519,6 +1539,44 @@ bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* R, const b
   for (void* p : tmp) (void)hipFree(p);
   bqsr_batch_destroy(b);
   return st;
+}
+
+
+// ---- one job's launches with the fewest host round trips (adam_amd/job.py) ----
+// bqsr_job_reset_async: the count table zeroed and the batch's error words /
+// exception count reset in one kernel (bqsr_table_zero_async + the RESET
+// stages).  bqsr_job_result: the batch's error words, expectedMismatch and
+// the LUT's finalize status in one kernel writing pinned host memory, one
+// stream sync, then the job's errors in the order the reference raises them
+// (observe, EMPTY_TABLE at finalize, apply).
+bqsr_status bqsr_job_reset_async(bqsr_batch* b, bqsr_table* t, void* stream) {
+  if (!b || !t) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  const int64_t n = table_words(t->dims);
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 255) / 256), (int64_t)b->ctx->n_cu * 8);
+  hipLaunchKernelGGL(bqsr_job_reset_kernel, dim3(g), dim3(256), 0, S(stream), t->words, n, b->d_err);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_exceptions, void* stream) {
+  if (!b || !L) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipStream_t s = S(stream);
+  if (!b->h_status) HIP_TRY(hipHostMalloc((void**)&b->h_status, kJobStatusWords * 8, hipHostMallocDefault));
+  hipLaunchKernelGGL(bqsr_job_status_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)b->d_err,
+                     (const double*)b->d_em, (const FinalOut*)L->d_out, b->h_status);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint64_t* h = b->h_status;
+  std::memcpy(&L->out, h + 5, sizeof(FinalOut));
+  L->out_pending = false;
+  if (em) std::memcpy(em, h + 4, 8);
+  if (n_exceptions) *n_exceptions = (int64_t)h[kNExc];
+  bqsr_status st = from_err_key(h[kErrObs], 0);
+  if (st != BQSR_OK) return st;
+  if (!L->out.any_key) return fail(BQSR_ERR_EMPTY_TABLE, "empty.reduceLeft: no usable base was observed");
+  return from_err_key(std::min(h[kErrAppPrep], h[kErrAppKern]), 0);
 }
 
 }  // extern "C"

@@ -2106,6 +2106,21 @@ extern "C" __global__ void bqsr_em_fold(const double* ems, int64_t n, double* ou
   *out = s;
 }
 
+// ------------------------------------------------------- job reset / status --
+extern "C" __global__ void bqsr_job_reset_kernel(int64_t* words, int64_t n, unsigned long long* err) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    words[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < kErrWords) err[threadIdx.x] = threadIdx.x == kNExc ? 0ull : ~0ull;
+}
+// [0, kErrWords) error words, [4] expectedMismatch bits, [5, 10) FinalOut
+extern "C" __global__ void bqsr_job_status_kernel(const unsigned long long* err, const double* em, const FinalOut* fo,
+                                                  uint64_t* host) {
+  const int t = threadIdx.x;
+  if (t < kErrWords) host[t] = err[t];
+  else if (t == kErrWords) host[t] = (uint64_t)__double_as_longlong(*em);
+  else if (t < kErrWords + 1 + (int)(sizeof(FinalOut) / 8)) host[t] = ((const uint64_t*)fo)[t - kErrWords - 1];
+}
+
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

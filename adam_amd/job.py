@@ -5,7 +5,7 @@ ranks sharing one GPU over gloo): the rank's shard is one partition of the
 job (RecalibrateBaseQualities.scala:52-76 over an RDD whose partitions are the
 ranks' shards, in rank order).  One ``step``:
 
-1. zero the count table (``new RecalTable``);
+1. zero the count table (``new RecalTable``) and the job's error words (one kernel);
 2. observe: prep (trimming, CIGAR / MD / known-site masks), the observe kernel
    (+ window reduce), the exact expectedMismatch fold -- all on one HIP stream;
 3. N > 1: the int64 table all-reduce and the expectedMismatch of every
@@ -13,7 +13,7 @@ ranks' shards, in rank order).  One ``step``:
 4. finalize on the device (expectedMismatch read from HBM: no host round trip);
 5. apply into device outputs (u8 chars per packed slot, per-read start and
    length, exception list for chars above 0xFF);
-6. the job's errors, in the order the reference raises them.
+6. the job's errors, in the order the reference raises them (one transfer, one sync).
 
 Only the HIP library computes; this module orders launches.
 """
@@ -75,16 +75,18 @@ class ResidentJob:
         return ctypes.c_void_p(t.data_ptr())
 
     def step(self, record: bool = False):
+        """One job.  record: bracket the stages with timing events (each event
+        record costs the stream ~30 us on this runtime, so callers sample)."""
         L, ctx, bh, th, sp, ev, stream = self.L, self.ctx.handle, self.bh, self.th, self.sp, self.ev, self.stream
-        check(L.bqsr_table_zero_async(th, sp))
-        check(L.bqsr_observe_stage(ctx, bh, self.sites_h, th, _capi.STAGE_RESET, sp))
-        ev[5].record(stream)
+        check(L.bqsr_job_reset_async(bh, th, sp))  # new RecalTable; the job's error words reset
+        mark = (lambda i: ev[i].record(stream)) if record else (lambda i: None)
+        mark(5)
         check(L.bqsr_observe_stage(ctx, bh, self.sites_h, th, _capi.STAGE_PREP, sp))
-        ev[0].record(stream)
+        mark(0)
         check(L.bqsr_observe_stage(ctx, bh, self.sites_h, th, _capi.STAGE_KERNEL, sp))
-        ev[1].record(stream)
+        mark(1)
         check(L.bqsr_observe_stage(ctx, bh, self.sites_h, th, _capi.STAGE_FOLD, sp))
-        ev[2].record(stream)
+        mark(2)
         if self.world > 1:
             # RecalTable.++ across ranks: exact int64 all-reduce (RCCL over
             # xGMI), expectedMismatch of every rank's partition folded in rank
@@ -99,16 +101,14 @@ class ResidentJob:
         check(L.bqsr_finalize_device(ctx, th, em_ptr, ctypes.byref(self.lut), sp))
         args = (ctx, bh, self.lut, self._ptr(self.out_qual), self._ptr(self.out_start), self._ptr(self.out_len),
                 self._ptr(self.exc), self.max_exc)
-        check(L.bqsr_apply_stage(*args, _capi.STAGE_RESET, sp))
-        ev[3].record(stream)
+        mark(3)
         check(L.bqsr_apply_stage(*args, _capi.STAGE_KERNEL, sp))
-        ev[4].record(stream)
+        mark(4)
         # the job's results and errors, in the order the reference raises them
+        # (one transfer and one sync)
         em = ctypes.c_double()
-        check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
-        check(L.bqsr_finalize_result(self.lut, sp))
         nexc = ctypes.c_int64()
-        check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
+        check(L.bqsr_job_result(bh, self.lut, ctypes.byref(em), ctypes.byref(nexc), sp))
         self.n_exc = int(nexc.value)
         if self.n_exc > self.max_exc:
             raise _capi.BQSRError(_capi.UNSUPPORTED, "%d chars above 0xFF exceed the exception list" % self.n_exc)

@@ -329,6 +329,16 @@ int bqsr_lut_group(const bqsr_lut* l, int32_t r, int64_t* obs, int64_t* mm);
  * out[i] = largest p with phred(p) >= qmin + i; returns the entry count */
 int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin);
 
+/* One job's launches with the fewest host round trips (what bench.py's step
+ * runs): the table zeroed and the batch's error words reset in one kernel
+ * (replaces bqsr_table_zero_async and the BQSR_STAGE_RESET stages), and, after
+ * the stages, every status of the job fetched in one transfer: the observe
+ * error, expectedMismatch, finalize's EMPTY_TABLE, the apply error and the
+ * exception count, raised in the reference's order. */
+bqsr_status bqsr_job_reset_async(bqsr_batch* b, bqsr_table* t, void* stream);
+bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* l, double* expected_mismatch, int64_t* n_exceptions,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif
