@@ -928,14 +928,20 @@ __device__ __forceinline__ void chunk_finish(const ReadsDev& rd, const LaneRead&
 // instead of once per chunk.
 constexpr int kSub = 4;
 constexpr int kSuper = kSub * kChunk;
+constexpr int kObsSub = 8;  // observe, lane per read: chunks per step
 
-// 16 masked / mismatch bits of sub-chunk i from the super-chunk's three
-// bitmap words (w[0] holds the slot of the super-chunk's first offset at bit b0)
-__device__ __forceinline__ void sub_bits(const uint64_t w[3], uint32_t b0, int i, uint32_t& masked, uint32_t& mism) {
+// 16 masked / mismatch bits of sub-chunk i from a step's NW bitmap words
+// (w[0] holds the slot of the step's first offset at bit b0)
+template <int NW>
+__device__ __forceinline__ void sub_bits(const uint64_t* w, uint32_t b0, int i, uint32_t& masked, uint32_t& mism) {
   const uint32_t b = b0 + 16u * (uint32_t)i;
   const uint32_t wi = b >> 5, sh = b & 31;
-  const uint64_t lo = wi == 0 ? w[0] : (wi == 1 ? w[1] : w[2]);
-  const uint64_t hi = wi == 0 ? w[1] : w[2];
+  uint64_t lo = w[0], hi = w[1];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) {  // a chunk starting in the last word ends in it
+    lo = wi == (uint32_t)k ? w[k] : lo;
+    hi = wi == (uint32_t)k ? w[k + 1 < NW ? k + 1 : k] : hi;
+  }
   masked = __builtin_amdgcn_alignbit((uint32_t)hi, (uint32_t)lo, sh);
   mism = __builtin_amdgcn_alignbit((uint32_t)(hi >> 32), (uint32_t)(lo >> 32), sh);
 }
@@ -1135,8 +1141,14 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   // all its super-chunks.
   const int ls = kCL ? P.lane_shift : 6;
   const int sub = kCL ? lane & ((1 << ls) - 1) : 0, rl = kCL ? lane >> ls : lane, rpw = kCL ? 64 >> ls : 64;
-  constexpr int NS = kSub;
-  const int jstep = kSuper << (kCL ? ls : 0);
+  // lane per read: a read's 8 chunks (128 offsets) per step, so all its
+  // cache lines are fetched while hot (with 4 chunks a step, half of a
+  // 100-bp read's lines were fetched again a step later: PMC FETCH 2.0x ->
+  // 1.25x the algorithmic bytes); lane per super-chunk: 4
+  constexpr int NS = kCL ? kSub : kObsSub;
+  constexpr int kSup = NS * kChunk;
+  constexpr int NW = (kSup + 31) / 32 + 1;  // sbits words of a step (first slot at bit 0..31)
+  const int jstep = kSup << (kCL ? ls : 0);
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -1161,11 +1173,11 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
       // layout (then the first chunk's offsets below st are not visited)
       const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;
       const uint8_t* qp = P.rd.qual + x.slot;
-      for (int j0 = jb + kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += jstep) {
+      for (int j0 = jb + kSup * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += jstep) {
         if (j0 >= n) continue;
         // issue every load of the super-chunk first
         uint4 qs[NS], cr[NS];
-        uint64_t bw[3] = {0, 0, 0};
+        uint64_t bw[NW];
         const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
@@ -1174,11 +1186,9 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
           cr[i] = (lv && full) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
         }
-        if (full) {
-          bw[0] = P.sbits[s0 >> 5];
-          bw[1] = P.sbits[(s0 >> 5) + 1];
-          bw[2] = P.sbits[(s0 >> 5) + 2];
-        }
+        // word w holds slots from bit 32 w - (s0 & 31) on: needed while that is below n - j0
+#pragma unroll
+        for (int w = 0; w < NW; ++w) bw[w] = (full && (w == 0 || 32 * w - 32 < n - j0)) ? P.sbits[(s0 >> 5) + w] : 0ull;
 #pragma clang loop unroll(full)
         for (int i = 0; i < NS; ++i) {
           const int j = j0 + kChunk * i;
@@ -1188,7 +1198,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           uint32_t bm = 0, bx = 0;
           uint32_t xo[4] = {4u, 4u, 4u, 4u};
           if (full) {
-            sub_bits(bw, (uint32_t)(s0 & 31), i, bm, bx);
+            sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
             uint64_t clo;
             uint32_t chi;
             chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
