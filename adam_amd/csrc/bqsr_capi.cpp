@@ -213,6 +213,14 @@ int observe_form() {
   }();
   return v;
 }
+// prep's word stores (PrepParams::store_words); ADAM_BQSR_PREP_ATOMIC=1 turns them off (A/B)
+bool store_words_off() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_PREP_ATOMIC");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 // observe's rotated fast path (bqsr_observe_kernel<true, false>); ADAM_BQSR_OBSERVE_ROTATE=0/1 overrides
 bool observe_rotate() {
   static const bool v = [] {
@@ -272,6 +280,7 @@ struct bqsr_batch {
   ReadInfo* d_info = nullptr;
   uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
   uint32_t* d_work = nullptr;   // prep worklist (PrepParams::work), count at d_work[n_reads]
+  uint64_t* d_bnd = nullptr;    // prep pass 1 wavefront-boundary shares (PrepParams::bnd)
   int64_t sbits_words = 0;
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
@@ -528,6 +537,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_bnd, (size_t)2 * (size_t)(n / 64 + kPrepChunk / 64 + 1))) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_work, (size_t)(n + kPrepChunk) + (size_t)(n / kPrepChunk + 1))) != BQSR_OK)
     return st;
   // read-group buckets (OrderDev): on for several read groups, or when the
@@ -1007,10 +1017,16 @@ namespace {
 bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
   HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
   if (b->rd.n_reads > 0) {
-    HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
     PrepParams P{};
     P.rd = b->rd;
     if (sites) P.sites = sites->dev();
+    // with known sites and reads of <= 128 bases, pass 1 stores every bitmap
+    // word (no zeroing pass, no read-modify-write atomics: cfg3 prep 3.0 ->
+    // 2.2 ms); without sites the few mismatch bits as atomics onto a zeroed
+    // bitmap cost less (cfg2: 0.25 + 0.03 ms against 0.30)
+    P.store_words = b->dims.max_len <= 128 && P.sites.n_contigs > 0 && !store_words_off();
+    P.bnd = b->d_bnd;
+    if (!P.store_words) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.err = b->d_err;
@@ -1018,7 +1034,10 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     P.n_work = b->d_work + b->rd.n_reads + kPrepChunk;
     // pass 1: the common reads in lock step; pass 2: the rest, one thread each
     const int64_t blocks = (b->rd.n_reads + kPrepChunk - 1) / kPrepChunk;
-    hipLaunchKernelGGL(bqsr_prep_kernel, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
+    if (P.store_words)
+      hipLaunchKernelGGL(bqsr_prep_kernel<true>, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
+    else
+      hipLaunchKernelGGL(bqsr_prep_kernel<false>, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
     hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)blocks), dim3(kComplexThreads), 0, s, P);
     HIP_TRY(hipGetLastError());
     if (b->bucketed) {  // counting sort of the reads by read group

@@ -155,7 +155,9 @@ struct PrepParams {
   ReadsDev rd;
   SitesDev sites;
   ReadInfo* info;      // [n_reads]
-  uint64_t* sbits;     // [n_slots / 32 + 2], zeroed before the launch
+  uint64_t* sbits;     // [n_slots / 32 + 2]: zeroed before the launch, or (store_words) written whole by pass 1
+  int32_t store_words; // pass 1 stores every sbits word (reads of <= 128 bases), no zeroing, no atomics
+  uint64_t* bnd;       // store_words: per wavefront of pass 1 [bits, word] its first read's share of the word the previous wavefront stored
   unsigned long long* err;  // error words
   uint32_t* work;      // [n_reads] reads bqsr_prep_kernel left to bqsr_prep_complex, per workgroup segment
   uint32_t* n_work;    // [workgroups] their count per segment

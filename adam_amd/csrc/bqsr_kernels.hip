@@ -496,6 +496,14 @@ __device__ __forceinline__ bool mask_sites_bitmap(const PrepParams& P, int32_t c
   return true;
 }
 
+struct PrepRec {
+  ReadMeta m;
+  ReadAlign a;
+  uint64_t nslot;  // store_words, last lane of a wavefront: the next read's slot (n_slots past the batch)
+};
+struct PrepCols {
+  uint4 c4, md4;
+};
 // A read's sbits words in registers (prep_fast, reads whose bits fit in
 // kAccWords words): bit b of the accumulator = slot (rs & ~31) + b; static
 // indices only (a dynamic one would put the array in scratch).
@@ -563,9 +571,36 @@ __device__ __forceinline__ bool sites_bitmap_acc(const PrepParams& P, int32_t co
 // itself is left to the first pass over the quals (kInfoTrim, resolve_info).
 // Returns false for anything else: the read goes to bqsr_prep_complex, which
 // runs prep_one with the full exception order.
-__device__ bool prep_fast(const PrepParams& P, int64_t r) {
-  const ReadMeta m = P.rd.meta[r];
-  const ReadAlign a = P.rd.align[r];
+// A read's columns as prep_fast reads them, loaded an iteration or two
+// ahead by bqsr_prep_kernel (the three dependent loads of a read -- record,
+// then its CIGAR / MD, then the site bitmap -- were a chain of memory round
+// trips per iteration): PrepRec first, PrepCols once the record is in.
+__device__ __forceinline__ PrepRec prep_rec(const PrepParams& P, int64_t r) {
+  PrepRec x{};
+  if (r < P.rd.n_reads) {
+    x.m = P.rd.meta[r];
+    x.a = P.rd.align[r];
+  }
+  if (P.store_words && (threadIdx.x & 63) == 63)
+    x.nslot = r + 1 < P.rd.n_reads ? P.rd.meta[r + 1].slot : (uint64_t)P.rd.n_slots;
+  return x;
+}
+// (the columns have 32 B of padding; only reads prep_fast may take load)
+__device__ __forceinline__ PrepCols prep_cols(const PrepParams& P, const PrepRec& x) {
+  PrepCols c{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  const uint16_t f = x.m.flags;
+  if (eligible_read(f) && x.a.n_cigar > 0 && x.a.n_cigar <= 3) {
+    c.c4 = *(const uint4*)(P.rd.cigar + x.a.cigar_off);
+    if (usable_read(f) && x.a.md_len > 0 && x.a.md_len <= 16) c.md4 = *(const uint4*)(P.rd.md + x.a.md_off);
+  }
+  return c;
+}
+
+template <bool kStore>
+__device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, const PrepCols& cols,
+                          uint64_t acc_out[kAccWords]) {
+  const ReadMeta m = x.m;
+  const ReadAlign a = x.a;
   const uint16_t f = m.flags;
   if (!eligible_read(f)) {
     P.info[r] = ReadInfo{0, 0, kInfoPass, 0};
@@ -578,8 +613,7 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
     return false;
   const bool usable = usable_read(f);
   if (usable && (a.md_len == 0 || a.md_len > 16)) return false;
-  const uint4 c4 = *(const uint4*)(P.rd.cigar + a.cigar_off);  // the column has 32 B of padding
-  const uint4 md4 = usable ? *(const uint4*)(P.rd.md + a.md_off) : make_uint4(0, 0, 0, 0);
+  const uint4 c4 = cols.c4, md4 = cols.md4;
   const int st = 0, en = m.lq;  // bits over the whole read (see above)
   const uint32_t cw[3] = {c4.x, c4.y, c4.z};
   const int nc = a.n_cigar;
@@ -618,8 +652,14 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
     const int n = a.md_len;
     int64_t num = 0, pos = 0;
     bool ok = true;
+    // one pass: validity, the tag's span and (reads of < 256 bases) the
+    // mismatch offsets inside [st, en) as a list of bytes o + 1 (at most 7
+    // letters fit 16 bytes), set below -- per letter, not per tag byte
+    bool listed = en < 256;
+    uint64_t lst = 0;
+    uint32_t lsh = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {  // validity and the tag's span
+    for (int i = 0; i < 16; ++i) {
       const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
       if (i < n) {
         if (c >= '0' && c <= '9') {
@@ -627,7 +667,14 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
           ok &= num <= 2147483647LL;  // Integer.parseInt
         } else {
           ok &= md_base((uint8_t)c) && i > 0 && i + 1 < n;
-          pos += num + 1;
+          pos += num;
+          const int64_t o = lead + pos;  // reference position start + pos
+          if (pos < mlen && o >= st && o < en) {
+            listed &= lsh < 64;  // (more than 8 letters: adjacent ones, e.g. "5AC5")
+            lst |= lsh < 64 ? (uint64_t)(o + 1) << lsh : 0ull;
+            lsh += 8;
+          }
+          pos += 1;
           num = 0;
         }
       }
@@ -637,7 +684,8 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
     // with known sites (several bits per read, from three sources) the bits
     // are gathered per word first; without, the few bits go straight out
     // (measured: the gathering costs more than it saves on cfg2's reads)
-    if (P.sites.n_contigs > 0 && (int64_t)(rs & 31) + en <= 32 * kAccWords) {
+    if (kStore && (int64_t)(rs & 31) + en > 32 * kAccWords) return false;  // (not with <= 128 bases)
+    if ((kStore || P.sites.n_contigs > 0) && (int64_t)(rs & 31) + en <= 32 * kAccWords) {
       // the read's sbits words in registers, one atomic OR per word with bits
       // (measured: plain stores of the words a read owns alone, mixed with
       // the neighbours' atomics on the same lines, were 2x slower)
@@ -645,23 +693,8 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
       const uint32_t r0 = (uint32_t)(rs & 31);  // bit of offset 0 in acc
       if (lead > st) acc_range(acc, r0 + st, r0 + (uint32_t)min(lead, (int64_t)en), 0);
       if (lead + mlen < en) acc_range(acc, r0 + (uint32_t)max((int64_t)st, lead + mlen), r0 + en, 0);
-      num = 0;
-      pos = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        if (i < n) {
-          if (c >= '0' && c <= '9') {
-            num = num * 10 + (int64_t)(c - '0');
-          } else {
-            pos += num;
-            num = 0;
-            const int64_t o = lead + pos;
-            if (pos < mlen && o >= st && o < en) acc_bit(acc, r0 + (uint32_t)o, 32);
-            pos += 1;
-          }
-        }
-      }
+      if (!listed) return false;  // (en <= 160: only a list overflow)
+      for (uint64_t l = lst; l; l >>= 8) acc_bit(acc, r0 + (uint32_t)(l & 0xFFu) - 1u, 32);
       if (md_total < mlen) {
         const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
         if (lo < hi) acc_range(acc, r0 + (uint32_t)lo, r0 + (uint32_t)hi, 32);
@@ -670,33 +703,48 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
       if (a.contig >= 0 && a.contig < P.sites.n_contigs) {
         if (!sites_bitmap_acc(P, a.contig, unclipped, en, r0, acc)) linear = true;
       }
-      const uint64_t wb = rs >> 5;
+      if (kStore) {
+        // the words go out with the wavefront's stores (prep_store_words); a
+        // contig without a bitmap goes to pass 2, whose atomics land on them
+        if (linear) return false;
 #pragma unroll
-      for (int j = 0; j < kAccWords; ++j) {
-        if (!acc[j]) continue;
-        const uint64_t wi = wb + (uint64_t)j;
-        atomicOr((unsigned long long*)&P.sbits[wi], (unsigned long long)acc[j]);
+        for (int j = 0; j < kAccWords; ++j) acc_out[j] = acc[j];
+      } else {
+        const uint64_t wb = rs >> 5;
+#pragma unroll
+        for (int j = 0; j < kAccWords; ++j) {
+          if (!acc[j]) continue;
+          const uint64_t wi = wb + (uint64_t)j;
+          atomicOr((unsigned long long*)&P.sbits[wi], (unsigned long long)acc[j]);
+        }
+        if (linear) mask_sites_linear(P, a.contig, unclipped, st, en, rs);
       }
-      if (linear) mask_sites_linear(P, a.contig, unclipped, st, en, rs);
     } else {
       // masked: the clips (reference positions outside [start, start + mlen))
       if (lead > st) set_sbits(P.sbits, rs + st, rs + min(lead, (int64_t)en), 0);
       if (lead + mlen < en) set_sbits(P.sbits, rs + max((int64_t)st, lead + mlen), rs + en, 0);
       // mismatches: each letter's position, then every position past the tag's span
-      num = 0;
-      pos = 0;
+      if (listed) {
+        for (uint64_t l = lst; l; l >>= 8) {
+          const uint64_t o = (l & 0xFFu) - 1u;
+          set_sbits(P.sbits, rs + o, rs + o + 1, 32);
+        }
+      } else {
+        num = 0;
+        pos = 0;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        if (i < n) {
-          if (c >= '0' && c <= '9') {
-            num = num * 10 + (int64_t)(c - '0');
-          } else {
-            pos += num;
-            num = 0;
-            const int64_t o = lead + pos;  // reference position start + pos
-            if (pos < mlen && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
-            pos += 1;
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+          if (i < n) {
+            if (c >= '0' && c <= '9') {
+              num = num * 10 + (int64_t)(c - '0');
+            } else {
+              pos += num;
+              num = 0;
+              const int64_t o = lead + pos;  // reference position start + pos
+              if (pos < mlen && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
+              pos += 1;
+            }
           }
         }
       }
@@ -716,12 +764,62 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r) {
   return true;
 }
 
+// store_words: the wavefront's sbits words as plain stores (no zeroing
+// pass, no read-modify-write atomics at the memory side: measured 1 ms of
+// cfg3's 3 ms prep).  Lane l (read r, first slot s_l) owns the words whose
+// first slot lies in [s_l, s_l+1) -- every word once, gaps included -- and
+// stores its read's bits there.  A read starting inside a word owns neither
+// that word nor its bits in it: those go down the wavefront to the owner by a
+// segmented OR scan keyed by the word (keys are nondecreasing along the
+// lanes); lane 0's go to bnd for pass 2 (the owner is in an earlier
+// wavefront).  Read 0 owns its first word outright.
+__device__ __forceinline__ uint64_t shfl_down_u64(uint64_t v, int d) {
+  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, d), hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ void prep_store_words(const PrepParams& P, int64_t r, const PrepRec& x,
+                                                 const uint64_t acc[kAccWords]) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = P.rd.n_reads;
+  const uint64_t slot = r < n ? x.m.slot : (uint64_t)P.rd.n_slots;
+  uint64_t nslot = shfl_down_u64(slot, 1);
+  if (lane == 63) nslot = r < n ? x.nslot : (uint64_t)P.rd.n_slots;
+  const uint64_t fw = slot >> 5;
+  const bool mid = (slot & 31) != 0 && r != 0;  // starts inside a word it does not own
+  const uint64_t own_lo = mid ? fw + 1 : fw, own_hi = (nslot + 31) >> 5;
+  uint64_t S = mid ? acc[0] : 0ull;
+  const uint32_t key = (uint32_t)fw;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t So = shfl_down_u64(S, d);
+    const uint32_t ko = (uint32_t)__shfl_down((int)key, d);
+    if (lane + d < 64 && ko == key) S |= So;
+  }
+  const uint64_t Sn = shfl_down_u64(S, 1);
+  const uint32_t kn = (uint32_t)__shfl_down((int)key, 1);
+  const uint64_t extra = (lane < 63 && own_hi > own_lo && kn == (uint32_t)(own_hi - 1)) ? Sn : 0ull;
+  for (uint64_t w = own_lo; w < own_hi; ++w) {
+    const uint64_t j = w - fw;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kAccWords; ++k) v = j == (uint64_t)k ? acc[k] : v;
+    P.sbits[w] = v | (w + 1 == own_hi ? extra : 0ull);
+  }
+  if (lane == 0) {
+    const int64_t g = r >> 6;
+    P.bnd[2 * g] = mid ? S : 0ull;
+    P.bnd[2 * g + 1] = fw;
+  }
+}
+
 // Pass 1: workgroup w takes reads [w * kPrepChunk, (w + 1) * kPrepChunk); the
 // common ones are finished in lock step, the others listed (in read order)
 // in the workgroup's own segment of the worklist -- LDS-compacted, no global
 // atomics (one counter shared by every wavefront serialised at the memory
 // side: measured 1.8 ms for 10M reads).
-extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
+// (kStore = PrepParams::store_words, a template so each form gets its own registers)
+template <bool kStore>
+__global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
   __shared__ uint32_t list[kPrepChunk];
   __shared__ uint32_t cnt;
   if (threadIdx.x == 0) cnt = 0;
@@ -729,9 +827,27 @@ extern "C" __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(Prep
   const int64_t n = P.rd.n_reads;
   const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
   const int lane = threadIdx.x & 63;
+  // software pipeline: the record of the read two iterations ahead and the
+  // CIGAR / MD of the next one load while this one is worked
+  const int64_t rt = c0 + threadIdx.x;
+  PrepRec x0 = prep_rec(P, rt), x1 = prep_rec(P, rt + kPrepThreads);
+  PrepCols k0 = prep_cols(P, x0);
   for (int i = 0; i < kPrepChunk; i += kPrepThreads) {
-    const int64_t r = c0 + i + threadIdx.x;
-    const bool todo = r < n && !prep_fast(P, r);
+    const int64_t r = rt + i;
+    const PrepRec x2 = i + 2 * kPrepThreads < kPrepChunk ? prep_rec(P, r + 2 * kPrepThreads) : PrepRec{};
+    const PrepCols k1 = i + kPrepThreads < kPrepChunk ? prep_cols(P, x1) : PrepCols{};
+    uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
+    const bool todo = r < n && !prep_fast<kStore>(P, r, x0, k0, acc);
+    if (kStore) {
+      if (todo) {
+#pragma unroll
+        for (int k = 0; k < kAccWords; ++k) acc[k] = 0;
+      }
+      prep_store_words(P, r, x0, acc);
+    }
+    x0 = x1;
+    x1 = x2;
+    k0 = k1;
     const uint64_t mask = __builtin_amdgcn_ballot_w64(todo);
     if (mask) {
       uint32_t base = 0;
@@ -753,6 +869,11 @@ extern "C" __global__ void __launch_bounds__(kComplexThreads) bqsr_prep_complex(
   __shared__ uint32_t s_md[kComplexThreads * kPrepMdStride];
   const uint32_t k = P.n_work[blockIdx.x];
   const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
+  if (P.store_words && threadIdx.x < kPrepChunk / 64) {  // pass 1's wavefront-boundary shares
+    const int64_t g = (c0 >> 6) + threadIdx.x;
+    if (g * 64 < P.rd.n_reads && P.bnd[2 * g])
+      atomicOr((unsigned long long*)&P.sbits[P.bnd[2 * g + 1]], (unsigned long long)P.bnd[2 * g]);
+  }
   for (uint32_t i = threadIdx.x; i < k; i += kComplexThreads)
     prep_one(P, (int64_t)P.work[c0 + i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
 }
@@ -1211,8 +1332,8 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           // (monotone in k: both ends)
           const uint32_t nv = (uint32_t)min(kChunk, n - j);
           const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
-          const bool cok = full_rg && (unsigned)(wc0 + klo * x.dir) < (unsigned)cw &&
-                           (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)cw;
+          const bool cok = full_rg && (unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)cw &&
+                           (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)cw;
           const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
           // fast path: window rows of the piece's read group; offsets it skips
           // are redone below
@@ -1233,7 +1354,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
             const int row = q - q_lo;
             const bool f = cok && (unsigned)row < (unsigned)qw && ((vr >> k) & 1u);
             const bool m = (bmr >> k) & 1u;
-            const int base = row * wcells;
+            const int base = __mul24(row, wcells);  // 24-bit: full rate (v_mul_lo_u32 is quarter rate)
             if (f) {
               atomicAdd(m ? &w_masked[row] : &w_obs[base + wc0 + x.dir * kk], 1u);
               if (!m) atomicAdd(&w_obs[base + cw + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu)], 1u);
@@ -1244,12 +1365,15 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           uint32_t mmk = fastm & ~bm & bx;
           if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
             const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+            const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
             while (mmk) {
               const int k = __builtin_ctz(mmk);
               mmk &= mmk - 1;
-              const int q = (int)(int8_t)qp[o0 + k];
-              const int base = (q - q_lo) * wcells;
-              atomicAdd(&w_mm[base + wc0 + x.dir * k], 1u);
+              // the qual from the chunk's registers (a byte load here is a
+              // memory round trip in nearly every chunk: 1 base in 100 of 1024)
+              const int q = (int)(int8_t)(((k < 8 ? q01 : q23) >> (8 * (k & 7))) & 0xFFu);
+              const int base = __mul24(q - q_lo, wcells);
+              atomicAdd(&w_mm[base + wc0 + __mul24(x.dir, k)], 1u);
               atomicAdd(&w_mm[base + cw + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
             }
           }
@@ -1264,7 +1388,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
                 report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
               } else if (full) {  // outside the LDS window: straight to the int64 table
                 const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
-                const int ccell = cc0 + x.dir * k;
+                const int ccell = cc0 + __mul24(x.dir, k);
                 const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
                 if (ident) atomicAdd(&blk_hist[q], 1u);
                 const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
@@ -1354,8 +1478,8 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
   const int wc0 = cc0 - pc.c_lo;                 // ... and window cycle cell
   const uint32_t nv = (uint32_t)min(kChunk, n - j);
   const int klo = j < 0 ? -j : 0;
-  const bool cok = full && x.rg == pc.rg_w && (unsigned)(wc0 + klo * x.dir) < (unsigned)pc.cw &&
-                   (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)pc.cw;
+  const bool cok = full && x.rg == pc.rg_w && (unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)pc.cw &&
+                   (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)pc.cw;
   const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
   uint32_t fastm = 0;
   if (cok) {
@@ -1365,7 +1489,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
       const int row = q - pc.q_lo;
       const bool f = (unsigned)row < (unsigned)pc.qw && ((vmask >> k) & 1u);
       const bool m = (bm >> k) & 1u;
-      const int base = row * pc.wcells;
+      const int base = __mul24(row, pc.wcells);
       if (f) {
         atomicAdd(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k], 1u);
         if (!m) atomicAdd(&pc.w_obs[base + pc.cw + (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)], 1u);
@@ -1381,8 +1505,8 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
       const int k = __builtin_ctz(mmk);
       mmk &= mmk - 1;
       const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
-      const int base = (q - pc.q_lo) * pc.wcells;
-      atomicAdd(&pc.w_mm[base + wc0 + x.dir * k], 1u);
+      const int base = __mul24(q - pc.q_lo, pc.wcells);
+      atomicAdd(&pc.w_mm[base + wc0 + __mul24(x.dir, k)], 1u);
       atomicAdd(&pc.w_mm[base + pc.cw + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
     }
   }
@@ -1397,7 +1521,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
         report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
       } else if (full) {  // outside the LDS window: straight to the int64 table
         const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
-        const int ccell = cc0 + x.dir * k;
+        const int ccell = cc0 + __mul24(x.dir, k);
         const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
         if (pc.ident) atomicAdd(&pc.blk_hist[q], 1u);
         const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
@@ -1920,7 +2044,7 @@ __device__ __forceinline__ uint4 apply_slow(const ApplyParams* Pp, LaneRead x, i
     }
     if (!app) continue;
     const int64_t rq = (int64_t)x.rg * kQBins + q;
-    const int ccell = x.cell0 + x.dir * o;
+    const int ccell = x.cell0 + __mul24(x.dir, o);
     const double p = P.s1[rq * P.g.C + ccell] + P.d2[rq * kCtxSlots + xs];
     const int32_t Q = phred_q(p, P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
     const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
@@ -1967,8 +2091,8 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     // (monotone in k: both ends)
     const uint32_t nv = (uint32_t)min(kChunk, n - j);
     const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
-    const bool cok = app && x.rg == pc.rg_lo && (unsigned)(wc0 + klo * x.dir) < (unsigned)pc.cw &&
-                     (unsigned)(wc0 + (int)(nv - 1) * x.dir) < (unsigned)pc.cw;
+    const bool cok = app && x.rg == pc.rg_lo && (unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)pc.cw &&
+                     (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)pc.cw;
     const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
     const int dx = x.dir * kCtxSlots;
     // LDS address of offset k: lut + (q - q_lo) * cw21 + wc0 * 21 + dx * k +

@@ -175,6 +175,21 @@ def test_sites_bitmap_dense(lens):
     assert not np.array_equal(g_sites.words, g_none.words)
 
 
+@pytest.mark.parametrize("lens,seed", [((1, 3, 7, 15, 16, 17, 31), 81), ((5, 33, 64, 100, 128), 82),
+                                       ((101,), 83)])
+def test_sites_word_stores(lens, seed):
+    """Known sites with reads of <= 128 bases: prep's pass 1 stores every
+    bitmap word (PrepParams::store_words) -- several short reads per word,
+    reads starting mid-word, words shared across wavefronts (the boundary
+    shares pass 2 ORs in), complex reads (indels) whose bits pass 2 adds on
+    the stored words -- against the oracle, with dense and sparse sites."""
+    rng = np.random.default_rng(seed)
+    dense = np.unique(np.concatenate([np.arange(2_000, 6_000), rng.integers(1, 60_000, size=8_000)]))
+    b = synth.generate(30000, lens, 1, seed, contig_len=60_000, contig="chr20", p_indel=0.1, p_softclip=0.2)
+    check([b], {"chr20": dense.tolist()})
+    check([b.slice(0, 12345), b.slice(12345, 30000)], {"chr20": dense.tolist(), "chr7": [5, 90_000_000]})
+
+
 # ---- the fold at scale --------------------------------------------------------
 
 def test_fold_one_million_reads():
