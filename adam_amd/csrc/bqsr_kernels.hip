@@ -1754,12 +1754,14 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
 // part into hq_block (zeroed first); lanes as in the lane-per-super-chunk
 // passes (2^ls lanes per read, 64 offsets each, 16-B loads), every folded
 // base one LDS atomic into its wavefront's histogram: kFhCopies copies by
-// lane & 7 against same-bin conflicts, rows kQBins + 1 words apart so one
-// bin's copies sit in different LDS banks.  66 KB of LDS: two workgroups per
+// lane & 15 against same-bin conflicts (8 copies: 1.70 ms on cfg4, 16: 1.43,
+// 32: 1.46; a copy per lane needs 32 KB per wavefront: 2.57), rows kQBins + 1
+// words apart so one bin's copies sit in different LDS banks; a byte past the
+// read's end adds 0 (no branch per byte).  66 KB of LDS: two workgroups per
 // CU.
-constexpr int kFhWaves = 16;
-constexpr int kFhSplit = 2;
-constexpr int kFhCopies = 8;
+constexpr int kFhWaves = 8;
+constexpr int kFhSplit = 4;
+constexpr int kFhCopies = 16;
 constexpr int kFhStride = kQBins + 1;
 constexpr size_t fold_hist_lds() { return (size_t)kFhWaves * kFhCopies * kFhStride * 4; }
 extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(ReadsDev rd, const ReadInfo* info,
@@ -1795,10 +1797,11 @@ extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(Reads
 #pragma unroll
       for (int i = 0; i < kSub; ++i) {
         const int m = n - j0 - kChunk * i;  // valid bytes of chunk i (all when >= 16)
+        const uint32_t vm = m >= kChunk ? 0xFFFFu : (m > 0 ? (1u << m) - 1u : 0u);
         const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k)
-          if (k < m) atomicAdd(&hw[(w[k >> 2] >> (8 * (k & 3))) & 0x7Fu], 1u);
+        for (int k = 0; k < kChunk; ++k)  // (a byte past the end adds 0: no branch per byte)
+          atomicAdd(&hw[__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 7)], __builtin_amdgcn_ubfe(vm, k, 1));
       }
     }
   }
