@@ -221,11 +221,11 @@ bool store_words_off() {
   }();
   return v;
 }
-// observe's rotated fast path (bqsr_observe_kernel<true, false>); ADAM_BQSR_OBSERVE_ROTATE=0/1 overrides
-bool observe_rotate() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_OBSERVE_ROTATE");
-    return e ? atoi(e) != 0 : false;
+// observe's window row length mod 32 (ADAM_BQSR_WMOD=r pads it to r; unset: unpadded)
+int window_mod() {
+  static const int v = [] {
+    const char* e = getenv("ADAM_BQSR_WMOD");
+    return e ? (atoi(e) & 31) : -1;
   }();
   return v;
 }
@@ -385,8 +385,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  for (const void* f : {(const void*)bqsr_observe_kernel<false, false>, (const void*)bqsr_observe_kernel<true, false>,
-                        (const void*)bqsr_observe_kernel<false, true>, (const void*)bqsr_apply_kernel,
+  for (const void* f : {(const void*)bqsr_observe_kernel<false>, (const void*)bqsr_observe_kernel<true>,
+                        (const void*)bqsr_apply_kernel,
                         (const void*)bqsr_observe_chunks})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
@@ -1084,7 +1084,11 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
+    // window row length, optionally padded to a residue mod 32 LDS banks
+    // (ADAM_BQSR_WMOD, A/B); pad words stay 0
     P.wcells = window_cw(b, P.g) + kCtxSlots;
+    if (window_mod() >= 0)
+      while ((P.wcells & 31) != window_mod()) ++P.wcells;
     P.w = window_rows(b, observe_rows(P.wcells));
     P.touched = t->touched();
     P.obs = t->obs();
@@ -1113,11 +1117,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     if (form == 0)
       hipLaunchKernelGGL(bqsr_observe_chunks, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else if (form == 2 || chunk_lanes(b->bucketed))
-      hipLaunchKernelGGL((bqsr_observe_kernel<false, true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
-    else if (observe_rotate())
-      hipLaunchKernelGGL((bqsr_observe_kernel<true, false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+      hipLaunchKernelGGL((bqsr_observe_kernel<true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else
-      hipLaunchKernelGGL((bqsr_observe_kernel<false, false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+      hipLaunchKernelGGL((bqsr_observe_kernel<false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_keys : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);

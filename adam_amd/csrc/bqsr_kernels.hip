@@ -1104,18 +1104,6 @@ __device__ __forceinline__ void ctx_first(uint32_t xo[4], int k) {
   xo[3] = (uint32_t)(hi >> 32);
 }
 
-// 16 bytes rotated right by r (0..15) bytes: byte k of the result = byte (k + r) & 15
-__device__ __forceinline__ void rotr16(uint32_t w[4], uint32_t r) {
-  const uint32_t d = r >> 2, b = r & 3;
-  const uint32_t t0 = (d & 1) ? w[1] : w[0], t1 = (d & 1) ? w[2] : w[1];
-  const uint32_t t2 = (d & 1) ? w[3] : w[2], t3 = (d & 1) ? w[0] : w[3];
-  const uint32_t u0 = (d & 2) ? t2 : t0, u1 = (d & 2) ? t3 : t1, u2 = (d & 2) ? t0 : t2, u3 = (d & 2) ? t1 : t3;
-  w[0] = __builtin_amdgcn_alignbyte(u1, u0, b);
-  w[1] = __builtin_amdgcn_alignbyte(u2, u1, b);
-  w[2] = __builtin_amdgcn_alignbyte(u3, u2, b);
-  w[3] = __builtin_amdgcn_alignbyte(u0, u3, b);
-}
-
 // ------------------------------------------------------- lane per chunk ----
 //
 // The per-base passes' wavefront walk: every lane takes one 16-offset chunk
@@ -1227,16 +1215,81 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
 
 // ------------------------------------------------------------ observe ------
 
+typedef __attribute__((address_space(3))) uint32_t* LdsWords;
+__device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
+  __hip_atomic_fetch_add((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_sub(uint32_t addr, uint32_t v) {
+  __hip_atomic_fetch_sub((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// SWAR: every byte of a chunk's 16 quals is a window row, q_lo <= q < hi
+// (hi = q_lo + qw <= 128; a byte >= 128 is a negative Java byte, never a row)
+__device__ __forceinline__ bool quals_in_rows(const uint32_t qd[4], int q_lo, int hi) {
+  const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)hi * 0x01010101u;
+  uint32_t bad = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t v = qd[w] | 0x80808080u;  // per byte no borrow: v >= 128 >= lo, hi
+    bad |= qd[w] | ~(v - lo4) | (v - hi4);   // high bit: q >= 128, q < lo, q >= hi
+  }
+  return (bad & 0x80808080u) == 0u;
+}
+
+// A clean chunk (a read of the window's read group, all 16 offsets visited,
+// every qual a window row): both increments of every offset without a
+// predicate -- per offset a row address, the cycle cell (cb stepping by the
+// cycle direction) and the context cell -- then the masked offsets, counted
+// on the key only (RecalTable.+=), are moved back out: their two increments
+// undone, the row's masked count raised.  The unconditional form issues
+// about a third of the predicated loop's VALU and none of its exec-mask
+// juggling.
+__device__ __forceinline__ void observe_clean(uint32_t lb, const uint32_t qd[4], const uint32_t xo[4], uint32_t bm,
+                                              int wc0, int dir, int q_lo, int wcells, int cw, uint32_t lmasked) {
+  const uint32_t w4 = 4u * (uint32_t)wcells;
+  const uint32_t qoff = 4u * (uint32_t)(q_lo * wcells);
+  const uint32_t cb0 = lb + 4u * (uint32_t)wc0 - qoff;
+  const uint32_t xb = lb + 4u * (uint32_t)cw - qoff;
+  const uint32_t d4 = 4u * (uint32_t)dir;
+  uint32_t cb = cb0;
+#pragma unroll
+  for (int k = 0; k < kChunk; ++k) {
+    const uint32_t q = __builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
+    const uint32_t xs = __builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8);
+    const uint32_t rq = __mul24(q, w4);
+    lds_add(rq + cb, 1u);
+    lds_add(rq + xb + 4u * xs, 1u);
+    cb += d4;
+  }
+  uint32_t mk = bm & 0xFFFFu;
+  if (__builtin_amdgcn_ballot_w64(mk != 0)) {  // masked offsets (clips, insertions, known sites)
+    const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+    const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
+    while (mk) {
+      const int k = __builtin_ctz(mk);
+      mk &= mk - 1;
+      const uint32_t q = (uint32_t)((k < 8 ? q01 : q23) >> (8 * (k & 7))) & 0xFFu;
+      const uint32_t xs = (uint32_t)((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu;
+      const uint32_t rq = __mul24(q, w4);
+      lds_sub(rq + cb0 + d4 * (uint32_t)k, 1u);
+      lds_sub(rq + xb + 4u * xs, 1u);
+      lds_add(lmasked + 4u * (q - (uint32_t)q_lo), 1u);
+    }
+  }
+}
+
 // LDS: [obs window qw*wcells u32][mm window qw*wcells u32][masked qw u32][block hist 128 u32]
 // The window holds a piece's counts for rows (rg, q_lo..q_lo+qw-1) where rg is
 // the piece's read group; other keys go straight to the int64 table.  Each
 // piece's window is written to its slab of `part` and summed into the table by
 // bqsr_window_reduce.
-// kRot: lane l visits a chunk's offsets rotated by l & 15, so the lanes of a
-// wavefront (reads of equal length at equal offsets) hit different cycle
-// cells in each step instead of piling onto one LDS address.
-// kCL: lane per chunk (see kCL below).
-template <bool kRot, bool kCL>
+// kCL: lanes per super-chunk (see kCL below), else a lane per read.
+// (Tried: visiting a clean chunk's offsets in eight lane-dependent orders so
+// that lanes of one qual stop piling onto one cycle cell halved
+// SQ_LDS_ADDR_CONFLICT but the byte shuffles and their registers cost more:
+// cfg2 0.92 -> 1.58 ms; an odd or 32-aligned row length: 0.94 -> 1.00 /
+// 1.25 ms.)
+template <bool kCL>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -1245,6 +1298,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   uint32_t* w_mm = w_obs + qw * wcells;
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
+  const uint32_t lds_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, lds_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1337,29 +1391,28 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
           // fast path: window rows of the piece's read group; offsets it skips
           // are redone below
-          const uint32_t rot = kRot ? (uint32_t)lane & 15u : 0u;
-          uint32_t qr[4] = {qd[0], qd[1], qd[2], qd[3]}, xr[4] = {xo[0], xo[1], xo[2], xo[3]};
-          uint32_t bmr = bm & 0xFFFFu, vr = vmask;
-          if (kRot) {
-            rotr16(qr, rot);
-            rotr16(xr, rot);
-            bmr = ((bmr | (bmr << 16)) >> rot) & 0xFFFFu;
-            vr = ((vr | (vr << 16)) >> rot) & 0xFFFFu;
-          }
           uint32_t fastm = 0;
+          if (cok && vmask == 0xFFFFu && quals_in_rows(qd, q_lo, q_lo + qw)) {
+            observe_clean(lds_obs, qd, xo, bm, wc0, x.dir, q_lo, wcells, cw, lds_masked);
+            fastm = 0xFFFFu;
+          } else {
+            const uint32_t* qr = qd;
+            const uint32_t* xr = xo;
+            const uint32_t bmr = bm & 0xFFFFu, vr = vmask;
 #pragma unroll
-          for (int k = 0; k < kChunk; ++k) {
-            const int kk = kRot ? (k + (int)rot) & 15 : k;  // the chunk offset visited
-            const int q = (int)((qr[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-            const int row = q - q_lo;
-            const bool f = cok && (unsigned)row < (unsigned)qw && ((vr >> k) & 1u);
-            const bool m = (bmr >> k) & 1u;
-            const int base = __mul24(row, wcells);  // 24-bit: full rate (v_mul_lo_u32 is quarter rate)
-            if (f) {
-              atomicAdd(m ? &w_masked[row] : &w_obs[base + wc0 + x.dir * kk], 1u);
-              if (!m) atomicAdd(&w_obs[base + cw + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu)], 1u);
+            for (int k = 0; k < kChunk; ++k) {
+              const int kk = k;
+              const int q = (int)((qr[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+              const int row = q - q_lo;
+              const bool f = cok && (unsigned)row < (unsigned)qw && ((vr >> k) & 1u);
+              const bool m = (bmr >> k) & 1u;
+              const int base = __mul24(row, wcells);  // 24-bit: full rate (v_mul_lo_u32 is quarter rate)
+              if (f) {
+                atomicAdd(m ? &w_masked[row] : &w_obs[base + wc0 + x.dir * kk], 1u);
+                if (!m) atomicAdd(&w_obs[base + cw + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu)], 1u);
+              }
+              fastm |= (uint32_t)f << kk;
             }
-            fastm |= (uint32_t)f << kk;
           }
           uint32_t slow = vmask & ~fastm;
           uint32_t mmk = fastm & ~bm & bx;
@@ -1633,7 +1686,7 @@ extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd,
       const int j = i < nc ? i : i - nc;
       const int slot = j / wcells, wc = j - slot * wcells;
       const int cell = wc < gm.cw ? gm.c_lo + wc : g.C + (wc - gm.cw);
-      if (key0 + slot >= g.K) continue;
+      if (key0 + slot >= g.K || wc >= gm.cw + kCtxSlots) continue;  // past the contexts: the row's pad word
       // atomics: two read groups' rows can alias one key (q >= 60, quirk Q3)
       int64_t* dst = i < nc ? obs : mm;
       atomicAdd((unsigned long long*)&dst[(key0 + slot) * g.cells + cell], (unsigned long long)s);
@@ -2229,9 +2282,8 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   }  // pieces
 }
 
-template __global__ void bqsr_observe_kernel<false, false>(ObserveParams);
-template __global__ void bqsr_observe_kernel<true, false>(ObserveParams);
-template __global__ void bqsr_observe_kernel<false, true>(ObserveParams);
+template __global__ void bqsr_observe_kernel<false>(ObserveParams);
+template __global__ void bqsr_observe_kernel<true>(ObserveParams);
 
 // RecalTable.++ over partitions in a declared order (RecalTable.scala:90-108):
 // expectedMismatch = ((0.0 + e_0) + e_1) + ... -- one lane, each `+` one IEEE
