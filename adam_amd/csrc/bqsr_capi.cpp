@@ -221,11 +221,11 @@ bool store_words_off() {
   }();
   return v;
 }
-// observe's window row length mod 32 (ADAM_BQSR_WMOD=r pads it to r; unset: unpadded)
+// observe's window row length mod 32: ADAM_BQSR_WMOD=r pads it to r, -1 leaves it; unset: 2 mod 4 (-2)
 int window_mod() {
   static const int v = [] {
     const char* e = getenv("ADAM_BQSR_WMOD");
-    return e ? (atoi(e) & 31) : -1;
+    return !e ? -2 : atoi(e) < 0 ? -1 : (atoi(e) & 31);
   }();
   return v;
 }
@@ -1084,10 +1084,16 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
-    // window row length, optionally padded to a residue mod 32 LDS banks
-    // (ADAM_BQSR_WMOD, A/B); pad words stay 0
+    // window row length padded to 2 mod 4 words: the lanes of a wavefront add
+    // to one cycle cell of many rows at once, which a row length sharing a
+    // factor 4 or more with the 32 banks folds onto few banks (cfg3, 224
+    // words: 7.6 ms observe; 225: 5.8; cfg2 222 against 223 / 224: 0.94 /
+    // 1.00 / 1.25 ms).  ADAM_BQSR_WMOD=r pads to r mod 32 instead (A/B), -1
+    // not at all.  Pad words stay 0.
     P.wcells = window_cw(b, P.g) + kCtxSlots;
-    if (window_mod() >= 0)
+    if (window_mod() == -2)
+      while ((P.wcells & 3) != 2) ++P.wcells;
+    else if (window_mod() >= 0)
       while ((P.wcells & 31) != window_mod()) ++P.wcells;
     P.w = window_rows(b, observe_rows(P.wcells));
     P.touched = t->touched();

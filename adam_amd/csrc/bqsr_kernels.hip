@@ -1067,6 +1067,18 @@ __device__ __forceinline__ void sub_bits(const uint64_t* w, uint32_t b0, int i, 
   mism = __builtin_amdgcn_alignbit((uint32_t)(hi >> 32), (uint32_t)(lo >> 32), sh);
 }
 
+// The same bits when the step's first slot sits at bit 16 h of w[0] (h = 0
+// or 1: 16-aligned slots, ReadsDev::slots_aligned): chunk i's bits are one
+// half of word (h + i) >> 1 -- a select for odd i instead of a scan.
+template <int NW>
+__device__ __forceinline__ void sub_bits16(const uint64_t* w, uint32_t h, int i, uint32_t& masked, uint32_t& mism) {
+  const int a = i >> 1, b = (i + 1) >> 1 < NW ? (i + 1) >> 1 : NW - 1;
+  const uint64_t v = (i & 1) ? (h ? w[b] : w[a]) : w[a];
+  const uint32_t sh = 16u * ((h + (uint32_t)i) & 1u);
+  masked = (uint32_t)v >> sh;
+  mism = (uint32_t)(v >> 32) >> sh;
+}
+
 // Context slots (ctx + 4) of the 16 offsets of a chunk, one per byte
 // (xo[k >> 2] byte k & 3), from its 17-code window: with A = idx(a) + 1 and
 // B = idx(b) + 1 (0 for 'other'), ctx + 4 = 4A + B, and 4 when either base is
@@ -1092,16 +1104,11 @@ __device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[
   }
 }
 
-// context slot of chunk offset k := 4 (context 0); shifts on two u64 halves,
-// not a dynamically indexed array (which the compiler would put in scratch)
-__device__ __forceinline__ void ctx_first(uint32_t xo[4], int k) {
-  const uint64_t m = 0xFFull << (8 * (k & 7)), v = 0x0404040404040404ull & m;
-  uint64_t lo = ((uint64_t)xo[1] << 32) | xo[0], hi = ((uint64_t)xo[3] << 32) | xo[2];
-  if (k < 8) lo = (lo & ~m) | v; else hi = (hi & ~m) | v;
-  xo[0] = (uint32_t)lo;
-  xo[1] = (uint32_t)(lo >> 32);
-  xo[2] = (uint32_t)hi;
-  xo[3] = (uint32_t)(hi >> 32);
+// the read's first visited offset k has context 0 (slot 4): its predecessor
+// in the 17-code window (nibble k, after any reverse complement) read as N
+__device__ __forceinline__ uint64_t window_first(uint64_t lo, int k) {
+  const uint32_t sh = 4u * (uint32_t)k;
+  return (lo & ~(0xFull << sh)) | ((uint64_t)kCodeN << sh);
 }
 
 // ------------------------------------------------------- lane per chunk ----
@@ -1373,12 +1380,19 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           uint32_t bm = 0, bx = 0;
           uint32_t xo[4] = {4u, 4u, 4u, 4u};
           if (full) {
-            sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
+            if (P.rd.slots_aligned)
+              sub_bits16<NW>(bw, (uint32_t)(s0 >> 4) & 1u, i, bm, bx);
+            else
+              sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
             uint64_t clo;
             uint32_t chi;
+#ifndef BQSR_PROBE_NOCTX
             chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
+            if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
             ctx_slots(clo, chi, xo);
-            if (j <= 0) ctx_first(xo, -j);  // the read's first visited offset: context 0
+#else
+            xo[0] ^= cr[i].x & 0x03030303u; xo[1] ^= cr[i].y & 0x03030303u;
+#endif
           }
           const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
           const int wc0 = cc0 - c_lo;                     // ... and window cycle cell
@@ -1524,8 +1538,8 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
     uint64_t clo;
     uint32_t chi;
     chunk_finish(P.rd, x, chunk_n0(x, o0), ld.cr, clo, chi);
+    if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
     ctx_slots(clo, chi, xo);
-    if (j <= 0) ctx_first(xo, -j);  // the read's first visited offset: context 0
   }
   const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
   const int wc0 = cc0 - pc.c_lo;                 // ... and window cycle cell
@@ -2131,17 +2145,11 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
   } else {
     uint64_t clo = 0;
     uint32_t chi = 0;
+#ifndef BQSR_PROBE_NOCTX
     chunk_finish(P.rd, x, chunk_n0(x, o0), ld.cr, clo, chi);
+    if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
     ctx_slots(clo, chi, xo);
-    {  // the read's first visited offset (chunk offset -j when j <= 0): context 0
-      const uint32_t kf = (uint32_t)(-j) & 15u;
-      const uint32_t bm = j <= 0 ? 0xFFu << (8 * (kf & 3)) : 0u;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const uint32_t m = (kf >> 2) == (uint32_t)w ? bm : 0u;
-        xo[w] = (xo[w] & ~m) | (0x04040404u & m);
-      }
-    }
+#endif
     const int wc0 = x.cell0 + __mul24(x.dir, o0) - pc.c_lo;  // window cycle cell of offset k: wc0 + dir * k
     // the cycle cells of the chunk's valid offsets inside the table
     // (monotone in k: both ends)
@@ -2161,6 +2169,7 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     const uint32_t amax = lbase + (uint32_t)(pc.qw * pc.cw21 - 1);
     uint32_t ei[kChunk];
     uint32_t ek = lbase + (uint32_t)(wc0 * kCtxSlots - pc.q_lo * pc.cw21);
+#ifndef BQSR_PROBE_NOLUT
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) {
       const uint32_t q = __builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
@@ -2177,6 +2186,9 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
       b.y = *(LdsBytes)(uintptr_t)ei[4 * w + 3];
       out[w] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
     }
+#else
+    for (int w = 0; w < 4; ++w) out[w] = qd[w] ^ xo[w] ^ ek;
+#endif
     // per word: bytes whose qual is outside the window rows (SWAR; q >= 128
     // never is in them) or whose entry is 0 (the checked path decides),
     // gathered to one bit per offset
@@ -2193,6 +2205,9 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
       badm |= (bad | (bad >> 7) | (bad >> 14) | (bad >> 21)) << (4 * w);  // bits 0..3 (higher bits: masked below)
     }
     slow = vmask & (cok ? badm : 0xFFFFu);
+#ifdef BQSR_PROBE_NOBAD
+    slow = 0;
+#endif
   }
   // ---- the checked path ----
   if (__builtin_amdgcn_ballot_w64(slow != 0)) {
