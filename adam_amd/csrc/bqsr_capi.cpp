@@ -170,12 +170,13 @@ TableGeom geom(const bqsr_dims& d) {
 }
 
 constexpr size_t kLdsMax = 163840;
-// LDS of the per-base passes: observe's u32 window [qw][wcells] x {obs, mm}
-// + masked counts + block histogram; apply's char table [qw][cw][21]
+// LDS of the per-base passes: the context table (both), observe's u32 window
+// [qw][wcells] x {obs, mm} + masked counts + block histogram, apply's char
+// table [qw][cw][21]
 size_t observe_lds(int qw, int wcells) {
-  return (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 + (size_t)kMkWords * 4;
+  return (size_t)kCtxTabBytes + (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 + (size_t)kMkWords * 4;
 }
-size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + (size_t)qw * cw * kCtxSlots; }
+size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)qw * cw * kCtxSlots; }
 int observe_rows(int wcells) {
   int qw = kQBins;
   while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;

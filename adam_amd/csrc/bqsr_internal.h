@@ -61,6 +61,8 @@ constexpr uint8_t kCodeA = 0, kCodeC = 1, kCodeG = 2, kCodeT = 3, kCodeN = 4, kC
 
 constexpr int kMaxQ = 60;      // RecalUtil.Constants.MAX_REASONABLE_QSCORE
 constexpr int kCtxSlots = 21;  // contexts -4..16
+constexpr uint32_t kCtxTab = 4096;            // context table entries per strand (3 codes of 4 bits)
+constexpr int kCtxTabBytes = 2 * kCtxTab * 2;  // both strands, u16 entries (LDS of the per-base passes)
 constexpr int kQBins = 128;    // qual values 0..127 (Java byte >= 0)
 
 // Read tiles: `reads_per_tile` consecutive reads (<= 64) whose base slots fit

@@ -1019,9 +1019,9 @@ __device__ __forceinline__ WinGeom win_geom(const OrderDev& o, const TableGeom& 
 
 
 // The 17-code window of chunk o0 of a read (forward: codes o0-1 .. o0+15;
-// reverse: the mirrored codes, complemented -- quirk Q9).  Split in two so a
-// super-chunk's loads all issue before any is used: chunk_n0 / chunk_raw
-// issue the 16-B load, chunk_finish shifts (and reverse-complements).
+// reverse: the mirrored codes, o0's mirror + 1 down to o0+15's -- quirk Q9).
+// Split so a super-chunk's loads all issue before any is used: chunk_n0 /
+// chunk_raw issue the 16-B load, chunk_ctx turns it into context slots.
 __device__ __forceinline__ int64_t chunk_n0(const LaneRead& x, int o0) {
   const bool neg = x.fl & kInfoNeg;
   return (int64_t)x.slot + (neg ? (int64_t)(x.en + x.st - o0 - 16) : (int64_t)(o0 - 1));
@@ -1029,6 +1029,8 @@ __device__ __forceinline__ int64_t chunk_n0(const LaneRead& x, int o0) {
 __device__ __forceinline__ uint4 chunk_raw(const ReadsDev& rd, int64_t n0) {
   return n0 >= 0 ? *(const uint4*)(rd.bases + (n0 >> 1)) : make_uint4(0, 0, 0, 0);
 }
+// (bqsr_observe_kernel's lane per read: the arithmetic form below, whose
+// registers it has; the other passes take the table lookup, chunk_ctx)
 __device__ __forceinline__ void chunk_finish(const ReadsDev& rd, const LaneRead& x, int64_t n0, uint4 v, uint64_t& lo,
                                              uint32_t& hi) {
   if (__builtin_expect(n0 >= 0, 1)) {
@@ -1109,6 +1111,74 @@ __device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[
 __device__ __forceinline__ uint64_t window_first(uint64_t lo, int k) {
   const uint32_t sh = 4u * (uint32_t)k;
   return (lo & ~(0xFull << sh)) | ((uint64_t)kCodeN << sh);
+}
+
+// ---- context table (LDS, kCtxTabBytes) ----
+// The context slots of two neighbouring offsets from three codes of the raw
+// (forward) window: entry c0 | c1 << 4 | c2 << 8 of the forward half holds
+// slot(c0, c1) | slot(c1, c2) << 8, so a chunk's 16 slots are 8 u16 reads
+// instead of spreading the codes to bytes and two lookups per offset.  The
+// reverse half holds what the reverse-complemented window gives (quirk Q9,
+// BaseContext.simpleReverseComplement): lookup m of the raw window yields the
+// slots of offsets 15 - m and 14 - m, so the 16 bytes come out mirrored and
+// one byte permute per dword restores them -- no reverse complement of the
+// window.  Slot (ctx + 4) of the pair (a, b) = (previous, current) code:
+// 4 (context 0) when either is N, else 4 (idx(a) + 1) + (idx(b) + 1) with
+// idx 0..3 for ACGT and -1 for any other byte (BaseContext.scala).
+__device__ __forceinline__ uint32_t ctx_slot(uint32_t a, uint32_t b) {
+  if (a == kCodeN || b == kCodeN) return 4u;
+  return 4u * (a < 4u ? a + 1u : 0u) + (b < 4u ? b + 1u : 0u);
+}
+__device__ __forceinline__ uint32_t comp_code(uint32_t c) { return c < 4u ? c ^ 3u : c; }
+__device__ __forceinline__ void ctx_table_fill(uint16_t* t, int tid, int nthreads) {
+  for (int i = tid; i < 2 * kCtxTab; i += nthreads) {
+    const uint32_t e = (uint32_t)i & (kCtxTab - 1u);
+    const uint32_t c0 = e & 15u, c1 = (e >> 4) & 15u, c2 = e >> 8;
+    t[i] = (uint16_t)(i < kCtxTab ? ctx_slot(c0, c1) | ctx_slot(c1, c2) << 8
+                                  : ctx_slot(comp_code(c1), comp_code(c0)) |
+                                        ctx_slot(comp_code(c2), comp_code(c1)) << 8);
+  }
+}
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const uint16_t* LdsHalves;
+// raw window (lo: codes 0..15, hi: code 16) of a chunk -> its 16 slots;
+// tb = LDS address of the table half (forward, or reverse for neg reads)
+__device__ __forceinline__ void ctx_lookup(uint64_t lo, uint32_t hi, uint32_t tb, bool neg, uint32_t xo[4]) {
+  const uint32_t d0 = (uint32_t)lo, d1 = (uint32_t)(lo >> 32);
+  const uint32_t ix[8] = {__builtin_amdgcn_ubfe(d0, 0, 12),  __builtin_amdgcn_ubfe(d0, 8, 12),
+                          __builtin_amdgcn_ubfe(d0, 16, 12), __builtin_amdgcn_alignbit(d1, d0, 24) & 0xFFFu,
+                          __builtin_amdgcn_ubfe(d1, 0, 12),  __builtin_amdgcn_ubfe(d1, 8, 12),
+                          __builtin_amdgcn_ubfe(d1, 16, 12), __builtin_amdgcn_alignbit(hi, d1, 24) & 0xFFFu};
+  uint32_t X[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    u16x2v v;
+    v.x = *(LdsHalves)(uintptr_t)(tb + 2u * ix[2 * w]);
+    v.y = *(LdsHalves)(uintptr_t)(tb + 2u * ix[2 * w + 1]);
+    X[w] = __builtin_bit_cast(uint32_t, v);
+  }
+  const uint32_t sel = neg ? 0x04050607u : 0x03020100u;  // bytes of X[3 - w] reversed, or X[w]
+#pragma unroll
+  for (int w = 0; w < 4; ++w) xo[w] = __builtin_amdgcn_perm(X[3 - w], X[w], sel);
+}
+// a chunk's 16 context slots from its raw 16-B bases load: the 17-code window
+// (forward), the read's first offset given context 0, the table lookups
+__device__ __forceinline__ void chunk_ctx(const ReadsDev& rd, bool neg, int64_t n0, uint4 v, int j, uint32_t tb,
+                                          uint32_t xo[4]) {
+  uint64_t lo;
+  uint32_t hi;
+  if (__builtin_expect(n0 >= 0, 1)) {
+    const uint32_t sh = (uint32_t)(n0 & 1) * 4u;
+    lo = ((uint64_t)__builtin_amdgcn_alignbit(v.z, v.y, sh) << 32) | __builtin_amdgcn_alignbit(v.y, v.x, sh);
+    hi = __builtin_amdgcn_alignbit(v.w, v.z, sh) & 0xFu;
+  } else {
+    load_window_head(rd.bases, n0, rd.n_slots, lo, hi);
+  }
+  if (j <= 0) {  // the first visited offset -j: its predecessor (raw nibble -j, or 16 + j mirrored) read as N
+    const int t = neg ? 16 + j : -j;
+    if (t < 16) lo = window_first(lo, t); else hi = kCodeN;
+  }
+  ctx_lookup(lo, hi, neg ? tb + 2u * kCtxTab : tb, neg, xo);
 }
 
 // ------------------------------------------------------- lane per chunk ----
@@ -1301,7 +1371,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
   const int wcells = P.wcells;  // window row: [cycle cells cw][contexts 21]
-  uint32_t* w_obs = (uint32_t*)smem;
+  uint32_t* w_obs = (uint32_t*)(smem + kCtxTabBytes);  // (the context table's LDS unused here)
   uint32_t* w_mm = w_obs + qw * wcells;
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
@@ -1386,13 +1456,9 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
               sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
             uint64_t clo;
             uint32_t chi;
-#ifndef BQSR_PROBE_NOCTX
             chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
             if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
             ctx_slots(clo, chi, xo);
-#else
-            xo[0] ^= cr[i].x & 0x03030303u; xo[1] ^= cr[i].y & 0x03030303u;
-#endif
           }
           const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
           const int wc0 = cc0 - c_lo;                     // ... and window cycle cell
@@ -1520,6 +1586,7 @@ struct ObsPiece {
   uint32_t *w_obs, *w_mm, *w_masked, *blk_hist;
   int rg_w, c_lo, cw, q_lo, qw, wcells;
   bool ident;
+  uint32_t tb;  // LDS address of the context table
 };
 
 __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsPiece& pc, const LaneRead& x, int j,
@@ -1535,11 +1602,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
     const uint32_t sb = (uint32_t)((x.slot + (uint64_t)o0) & 31);
     bm = __builtin_amdgcn_alignbit((uint32_t)ld.bw1, (uint32_t)ld.bw0, sb);
     bx = __builtin_amdgcn_alignbit((uint32_t)(ld.bw1 >> 32), (uint32_t)(ld.bw0 >> 32), sb);
-    uint64_t clo;
-    uint32_t chi;
-    chunk_finish(P.rd, x, chunk_n0(x, o0), ld.cr, clo, chi);
-    if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
-    ctx_slots(clo, chi, xo);
+    chunk_ctx(P.rd, x.fl & kInfoNeg, chunk_n0(x, o0), ld.cr, j, pc.tb, xo);
   }
   const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
   const int wc0 = cc0 - pc.c_lo;                 // ... and window cycle cell
@@ -1612,7 +1675,8 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, L = P.g.L;
   const int wcells = P.wcells;
-  uint32_t* w_obs = (uint32_t*)smem;
+  uint16_t* ctab = (uint16_t*)smem;
+  uint32_t* w_obs = (uint32_t*)(smem + kCtxTabBytes);
   uint32_t* w_mm = w_obs + qw * wcells;
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
@@ -1623,6 +1687,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
   const int G = P.n_blocks;
   const bool ident = P.ord.perm == nullptr;
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
+  ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
@@ -1632,7 +1697,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
     if (p0 >= p1) continue;
     const WinGeom gm = win_geom(P.ord, P.g, key);
     const ObsPiece pc{w_obs, w_mm, w_masked, blk_hist, key_rg(P.ord, key, P.w.rg_lo), gm.c_lo, gm.cw, P.w.q_lo, qw,
-                      wcells, ident};
+                      wcells, ident, (uint32_t)(uintptr_t)(LdsHalves)ctab};
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
     chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads>(
@@ -2066,6 +2131,7 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
 struct ApplyPiece {
   const uint8_t* lut;
   int rg_lo, c_lo, cw, cw21, q_lo, qw;
+  uint32_t tb;  // LDS address of the context table
 };
 
 struct ChunkLoads {
@@ -2143,13 +2209,7 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
 #pragma unroll
     for (int i2 = 0; i2 < 4; ++i2) out[i2] = ((qd[i2] & 0x7F7F7F7Fu) + 0x21212121u) ^ (qd[i2] & 0x80808080u);
   } else {
-    uint64_t clo = 0;
-    uint32_t chi = 0;
-#ifndef BQSR_PROBE_NOCTX
-    chunk_finish(P.rd, x, chunk_n0(x, o0), ld.cr, clo, chi);
-    if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
-    ctx_slots(clo, chi, xo);
-#endif
+    chunk_ctx(P.rd, x.fl & kInfoNeg, chunk_n0(x, o0), ld.cr, j, pc.tb, xo);
     const int wc0 = x.cell0 + __mul24(x.dir, o0) - pc.c_lo;  // window cycle cell of offset k: wc0 + dir * k
     // the cycle cells of the chunk's valid offsets inside the table
     // (monotone in k: both ends)
@@ -2169,7 +2229,6 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     const uint32_t amax = lbase + (uint32_t)(pc.qw * pc.cw21 - 1);
     uint32_t ei[kChunk];
     uint32_t ek = lbase + (uint32_t)(wc0 * kCtxSlots - pc.q_lo * pc.cw21);
-#ifndef BQSR_PROBE_NOLUT
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) {
       const uint32_t q = __builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
@@ -2186,9 +2245,6 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
       b.y = *(LdsBytes)(uintptr_t)ei[4 * w + 3];
       out[w] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
     }
-#else
-    for (int w = 0; w < 4; ++w) out[w] = qd[w] ^ xo[w] ^ ek;
-#endif
     // per word: bytes whose qual is outside the window rows (SWAR; q >= 128
     // never is in them) or whose entry is 0 (the checked path decides),
     // gathered to one bit per offset
@@ -2205,9 +2261,6 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
       badm |= (bad | (bad >> 7) | (bad >> 14) | (bad >> 21)) << (4 * w);  // bits 0..3 (higher bits: masked below)
     }
     slow = vmask & (cok ? badm : 0xFFFFu);
-#ifdef BQSR_PROBE_NOBAD
-    slow = 0;
-#endif
   }
   // ---- the checked path ----
   if (__builtin_amdgcn_ballot_w64(slow != 0)) {
@@ -2238,7 +2291,9 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
   uint32_t* mk_all = (uint32_t*)smem;
-  uint8_t* lut = smem + kMkWords * 4;
+  uint16_t* ctab = (uint16_t*)(smem + kMkWords * 4);
+  uint8_t* lut = smem + kMkWords * 4 + kCtxTabBytes;
+  const uint32_t tb = (uint32_t)(uintptr_t)(LdsHalves)ctab;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2248,6 +2303,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   const int G = gridDim.x;
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
+  ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -2256,7 +2312,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     if (p0 >= p1) continue;
     const int rg_lo = key_rg(P.ord, key, P.w.rg_lo);
     const WinGeom gm = win_geom(P.ord, P.g, key);
-    const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw};
+    const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb};
     const bool win_ok = rg_lo < P.n_rg;
     const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
     __syncthreads();  // the previous piece is done with the table
