@@ -176,7 +176,9 @@ constexpr size_t kLdsMax = 163840;
 size_t observe_lds(int qw, int wcells) {
   return (size_t)kCtxTabBytes + (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 + (size_t)kMkWords * 4;
 }
-size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)qw * cw * kCtxSlots; }
+// a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
+int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
+size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)piece_bytes(qw, cw); }
 int observe_rows(int wcells) {
   int qw = kQBins;
   while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;
@@ -290,6 +292,8 @@ struct bqsr_batch {
   FoldParams fold{};               // the fold's device buffers (FoldParams)
   uint32_t* d_part = nullptr;      // per-block window counts
   size_t part_words = 0;
+  uint8_t* d_chars = nullptr;      // apply: the pieces' char tables (ApplyParams::chars)
+  size_t chars_bytes = 0;
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
   int32_t n_blocks = 0;
@@ -307,6 +311,7 @@ struct bqsr_batch {
   uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
   ~bqsr_batch() {
     if (d_part) (void)hipFree(d_part);
+    if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
     for (void* p : allocs) (void)hipFree(p);
   }
@@ -1474,6 +1479,21 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
+  P.piece_stride = piece_bytes(P.w.qw, cw);
+  const size_t need = (size_t)P.piece_stride * (size_t)b->n_keys;
+  if (b->chars_bytes < need) {  // grows with the window; kept across calls
+    if (b->d_chars) {
+      HIP_TRY(hipStreamSynchronize(s));
+      (void)hipFree(b->d_chars);
+      b->d_chars = nullptr;
+      b->chars_bytes = 0;
+    }
+    HIP_TRY(hipMalloc((void**)&b->d_chars, need));
+    b->chars_bytes = need;
+  }
+  P.chars = b->d_chars;
+  const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
+  hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
   const size_t lds = apply_lds(P.w.qw, cw);
   hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());

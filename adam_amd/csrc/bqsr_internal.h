@@ -290,6 +290,8 @@ struct ApplyParams {
   unsigned long long* n_exc;
   unsigned long long* err;
   int32_t lane_shift;  // lane-per-chunk kernel: log2(lanes per read)
+  const uint8_t* chars;   // [n_keys][piece_stride] the pieces' char tables (bqsr_apply_chars)
+  int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
 };
 
 // finalize results read back by the host

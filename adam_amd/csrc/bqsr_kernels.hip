@@ -2287,6 +2287,37 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
 
 constexpr int kApplyU = 4;  // chunks in flight per lane
 
+// Every piece's char table, once per apply launch: entry (row, cycle cell,
+// context) of piece `key` = errorProbabilityToPhred(s1 + d2) + 33, 0 where
+// the checked path must decide (key not in the table, a char above 0xFF).
+// A thread per entry; each workgroup of bqsr_apply_kernel then copies its
+// piece's table into LDS (it used to compute it itself: 65 us of a 0.87 ms
+// cfg2 launch with every workgroup repeating the same 156K entries).
+extern "C" __global__ void bqsr_apply_chars(ApplyParams P, uint8_t* chars) {
+  const int nk = order_keys(P.ord), qw = P.w.qw, q_lo = P.w.q_lo;
+  const int64_t total = (int64_t)nk * P.piece_stride;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int key = (int)(t / P.piece_stride);
+    const int64_t e = t - (int64_t)key * P.piece_stride;
+    const WinGeom gm = win_geom(P.ord, P.g, key);
+    const int64_t cw21 = (int64_t)gm.cw * kCtxSlots;
+    if (e >= (int64_t)qw * cw21) continue;  // the piece's padding
+    const int row = (int)(e / cw21);
+    const int rem = (int)(e - row * cw21), c = rem / kCtxSlots, x = rem - c * kCtxSlots;
+    const int rg = key_rg(P.ord, key, P.w.rg_lo);
+    const int64_t rq = (int64_t)rg * kQBins + q_lo + row;
+    uint8_t v = 0;
+    if (rg < P.n_rg && q_lo + row < kQBins && P.rq_ok[rq]) {
+      // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+      const int32_t Q = phred_q(P.s1[rq * P.g.C + gm.c_lo + c] + P.d2[rq * kCtxSlots + x], P.qb_thr, P.qb_q, P.thr,
+                                P.thr_qmin, P.thr_n);
+      const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+      v = code <= 0xFFu ? (uint8_t)code : 0;
+    }
+    chars[t] = v;
+  }
+}
+
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
@@ -2313,27 +2344,13 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     const int rg_lo = key_rg(P.ord, key, P.w.rg_lo);
     const WinGeom gm = win_geom(P.ord, P.g, key);
     const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb};
-    const bool win_ok = rg_lo < P.n_rg;
-    const int64_t rq0 = (int64_t)rg_lo * kQBins + q_lo;
     __syncthreads();  // the previous piece is done with the table
-    // ---- the piece's char table: one thread per (row, cycle cell), 21 contexts each ----
-    for (int i = tid; i < qw * pc.cw; i += blockDim.x) {
-      const int row = i / pc.cw, c = i - row * pc.cw;
-      const int64_t rq = rq0 + row;
-      const bool ok = win_ok && q_lo + row < kQBins && P.rq_ok[rq];
-      uint8_t* dst = lut + (int64_t)i * kCtxSlots;
-      if (!ok) {
-        for (int x = 0; x < kCtxSlots; ++x) dst[x] = 0;
-        continue;
-      }
-      const double s1 = P.s1[rq * C + pc.c_lo + c];
-      const double* d2 = P.d2 + rq * kCtxSlots;
-      for (int x = 0; x < kCtxSlots; ++x) {
-        // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-        const int32_t Q = phred_q(s1 + d2[x], P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
-        const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-        dst[x] = code <= 0xFFu ? (uint8_t)code : 0;
-      }
+    // ---- the piece's char table (bqsr_apply_chars) into LDS, 16 B a thread ----
+    {
+      const uint4* src = (const uint4*)(P.chars + (int64_t)key * P.piece_stride);
+      uint4* dst = (uint4*)lut;
+      const int n16 = (int)(P.piece_stride >> 4);
+      for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
     }
     __syncthreads();
     chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads>(
