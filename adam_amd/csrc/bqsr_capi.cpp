@@ -1038,13 +1038,15 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     P.err = b->d_err;
     P.work = b->d_work;
     P.n_work = b->d_work + b->rd.n_reads + kPrepChunk;
-    // pass 1: the common reads in lock step; pass 2: the rest, one thread each
+    // pass 1: the common reads in lock step; the rest, one thread each (in
+    // pass 1's workgroups, or pass 2 after word stores)
     const int64_t blocks = (b->rd.n_reads + kPrepChunk - 1) / kPrepChunk;
-    if (P.store_words)
+    if (P.store_words) {
       hipLaunchKernelGGL(bqsr_prep_kernel<true>, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
-    else
+      hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)blocks), dim3(kComplexThreads), 0, s, P);
+    } else {  // the listed reads finished by the same workgroups
       hipLaunchKernelGGL(bqsr_prep_kernel<false>, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
-    hipLaunchKernelGGL(bqsr_prep_complex, dim3((unsigned)blocks), dim3(kComplexThreads), 0, s, P);
+    }
     HIP_TRY(hipGetLastError());
     if (b->bucketed) {  // counting sort of the reads by read group
       const int64_t n = b->rd.n_reads;

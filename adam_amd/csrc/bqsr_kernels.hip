@@ -818,10 +818,18 @@ __device__ __forceinline__ void prep_store_words(const PrepParams& P, int64_t r,
 // atomics (one counter shared by every wavefront serialised at the memory
 // side: measured 1.8 ms for 10M reads).
 // (kStore = PrepParams::store_words, a template so each form gets its own registers)
+// Without word stores (kStore false: a zeroed bitmap, bits OR-ed atomically)
+// the workgroup then finishes its listed reads itself (prep_one, a thread a
+// read): no second launch waiting for every workgroup of this one, and the
+// listed reads' latency chains overlap other workgroups' lock-step work.
+// With word stores they wait for bqsr_prep_complex, whose atomics must land
+// on words every workgroup has stored.
 template <bool kStore>
 __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
   __shared__ uint32_t list[kPrepChunk];
   __shared__ uint32_t cnt;
+  __shared__ uint32_t s_cig[kStore ? 1 : kPrepThreads * kPrepCigStride];
+  __shared__ uint32_t s_md[kStore ? 1 : kPrepThreads * kPrepMdStride];
   if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
   const int64_t n = P.rd.n_reads;
@@ -858,12 +866,17 @@ __global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
   }
   __syncthreads();
   const uint32_t k = cnt;
+  if (!kStore) {
+    for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads)
+      prep_one(P, (int64_t)list[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
+    return;
+  }
   for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads) P.work[c0 + i] = list[i];
   if (threadIdx.x == 0) P.n_work[blockIdx.x] = k;
 }
 
-// Pass 2: workgroup w takes the reads pass 1's workgroup w listed, one thread
-// per read, the full per-read path (prep_one).
+// Pass 2 (word stores only): workgroup w takes the reads pass 1's workgroup w
+// listed, one thread per read, the full per-read path (prep_one).
 extern "C" __global__ void __launch_bounds__(kComplexThreads) bqsr_prep_complex(PrepParams P) {
   __shared__ uint32_t s_cig[kComplexThreads * kPrepCigStride];
   __shared__ uint32_t s_md[kComplexThreads * kPrepMdStride];
