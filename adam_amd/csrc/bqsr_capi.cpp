@@ -178,7 +178,7 @@ size_t observe_lds(int qw, int wcells) {
 }
 // a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
 int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
-size_t apply_lds(int qw, int cw) { return (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)piece_bytes(qw, cw); }
+size_t apply_lds(int qw, int cw) { return 16 + (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)piece_bytes(qw, cw); }
 int observe_rows(int wcells) {
   int qw = kQBins;
   while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;
@@ -1482,7 +1482,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
   P.piece_stride = piece_bytes(P.w.qw, cw);
-  const size_t need = (size_t)P.piece_stride * (size_t)b->n_keys;
+  const size_t need = (size_t)P.piece_stride * (size_t)b->n_keys + (size_t)b->n_keys * 16;  // + rowbad
   if (b->chars_bytes < need) {  // grows with the window; kept across calls
     if (b->d_chars) {
       HIP_TRY(hipStreamSynchronize(s));
@@ -1494,6 +1494,8 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     b->chars_bytes = need;
   }
   P.chars = b->d_chars;
+  P.rowbad = (uint32_t*)(b->d_chars + (size_t)P.piece_stride * (size_t)b->n_keys);
+  HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_keys * 16, s));
   const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
   hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
   const size_t lds = apply_lds(P.w.qw, cw);

@@ -292,6 +292,7 @@ struct ApplyParams {
   int32_t lane_shift;  // lane-per-chunk kernel: log2(lanes per read)
   const uint8_t* chars;   // [n_keys][piece_stride] the pieces' char tables (bqsr_apply_chars)
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
+  uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
 };
 
 // finalize results read back by the host

@@ -2144,7 +2144,9 @@ __device__ __forceinline__ int32_t phred_q(double p, const double* qb_thr, const
 struct ApplyPiece {
   const uint8_t* lut;
   int rg_lo, c_lo, cw, cw21, q_lo, qw;
-  uint32_t tb;  // LDS address of the context table
+  uint32_t tb;         // LDS address of the context table
+  int clean_lo, clean_hi;  // quals whose rows hold no 0 entry
+  bool all_cycles;     // the window holds every cycle cell (read order)
 };
 
 struct ChunkLoads {
@@ -2228,8 +2230,9 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     // (monotone in k: both ends)
     const uint32_t nv = (uint32_t)min(kChunk, n - j);
     const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
-    const bool cok = app && x.rg == pc.rg_lo && (unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)pc.cw &&
-                     (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)pc.cw;
+    const bool cok = app && x.rg == pc.rg_lo &&
+                     (pc.all_cycles || ((unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)pc.cw &&
+                                        (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)pc.cw));
     const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
     const int dx = x.dir * kCtxSlots;
     // LDS address of offset k: lut + (q - q_lo) * cw21 + wc0 * 21 + dx * k +
@@ -2258,19 +2261,16 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
       b.y = *(LdsBytes)(uintptr_t)ei[4 * w + 3];
       out[w] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, a), 0x06020400u);
     }
-    // per word: bytes whose qual is outside the window rows (SWAR; q >= 128
-    // never is in them) or whose entry is 0 (the checked path decides),
-    // gathered to one bit per offset
-    const int hi_lim = min(pc.q_lo + pc.qw, kQBins);
-    const uint32_t lo4 = (uint32_t)pc.q_lo * 0x01010101u, hi4 = (uint32_t)hi_lim * 0x01010101u;
+    // per word: bytes whose qual is outside the clean rows (SWAR, per byte
+    // no borrow; q >= 128 never is in them) -- entries 0 (key not in the
+    // table, a char above 0xFF: the checked path decides) lie only in other
+    // rows -- gathered to one bit per offset
+    const uint32_t lo4 = (uint32_t)pc.clean_lo * 0x01010101u, hi4 = (uint32_t)pc.clean_hi * 0x01010101u;
     uint32_t badm = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const uint32_t v = qd[w] & 0x7F7F7F7Fu;
-      const uint32_t ge_lo = (v | 0x80808080u) - lo4;  // byte high bit: v >= q_lo
-      const uint32_t ge_hi = hi_lim < kQBins ? (v | 0x80808080u) - hi4 : 0u;
-      const uint32_t z = ~(((out[w] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | out[w] | 0x7F7F7F7Fu);  // zero bytes
-      const uint32_t bad = (((qd[w] | ~ge_lo | ge_hi) & 0x80808080u) | z) >> 7;  // bit 8i: byte i
+      const uint32_t v = qd[w] | 0x80808080u;
+      const uint32_t bad = ((qd[w] | ~(v - lo4) | (v - hi4)) & 0x80808080u) >> 7;  // bit 8i: byte i
       badm |= (bad | (bad >> 7) | (bad >> 14) | (bad >> 21)) << (4 * w);  // bits 0..3 (higher bits: masked below)
     }
     slow = vmask & (cok ? badm : 0xFFFFu);
@@ -2314,29 +2314,37 @@ extern "C" __global__ void bqsr_apply_chars(ApplyParams P, uint8_t* chars) {
     const int64_t e = t - (int64_t)key * P.piece_stride;
     const WinGeom gm = win_geom(P.ord, P.g, key);
     const int64_t cw21 = (int64_t)gm.cw * kCtxSlots;
-    if (e >= (int64_t)qw * cw21) continue;  // the piece's padding
-    const int row = (int)(e / cw21);
+    const bool pad = e >= (int64_t)qw * cw21;  // the piece's padding
+    const int row = pad ? 0 : (int)(e / cw21);
     const int rem = (int)(e - row * cw21), c = rem / kCtxSlots, x = rem - c * kCtxSlots;
     const int rg = key_rg(P.ord, key, P.w.rg_lo);
     const int64_t rq = (int64_t)rg * kQBins + q_lo + row;
     uint8_t v = 0;
-    if (rg < P.n_rg && q_lo + row < kQBins && P.rq_ok[rq]) {
+    if (!pad && rg < P.n_rg && q_lo + row < kQBins && P.rq_ok[rq]) {
       // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
       const int32_t Q = phred_q(P.s1[rq * P.g.C + gm.c_lo + c] + P.d2[rq * kCtxSlots + x], P.qb_thr, P.qb_q, P.thr,
                                 P.thr_qmin, P.thr_n);
       const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
       v = code <= 0xFFu ? (uint8_t)code : 0;
     }
-    chars[t] = v;
+    if (!pad) chars[t] = v;
+    // rows holding a 0 entry: one atomic per run of such entries in the
+    // wavefront (a run is one row's; its first lane reports it)
+    const int zr = (!pad && v == 0) ? key * kQBins + row : -1;
+    const int prev = __shfl_up(zr, 1);
+    if (zr >= 0 && ((threadIdx.x & 63) == 0 || prev != zr))
+      atomicOr(&P.rowbad[(zr >> 7) * 4 + ((zr & 127) >> 5)], 1u << (zr & 31));
   }
 }
 
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
-  uint32_t* mk_all = (uint32_t*)smem;
-  uint16_t* ctab = (uint16_t*)(smem + kMkWords * 4);
-  uint8_t* lut = smem + kMkWords * 4 + kCtxTabBytes;
+  // LDS: [clean rows 16 B][walk markers][context table][char table]
+  uint32_t* clean_rows = (uint32_t*)smem;  // [lo, hi): quals whose char-table rows hold no 0 entry
+  uint32_t* mk_all = (uint32_t*)(smem + 16);
+  uint16_t* ctab = (uint16_t*)(smem + 16 + kMkWords * 4);
+  uint8_t* lut = smem + 16 + kMkWords * 4 + kCtxTabBytes;
   const uint32_t tb = (uint32_t)(uintptr_t)(LdsHalves)ctab;
 
   const int tid = threadIdx.x;
@@ -2356,7 +2364,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     if (p0 >= p1) continue;
     const int rg_lo = key_rg(P.ord, key, P.w.rg_lo);
     const WinGeom gm = win_geom(P.ord, P.g, key);
-    const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb};
     __syncthreads();  // the previous piece is done with the table
     // ---- the piece's char table (bqsr_apply_chars) into LDS, 16 B a thread ----
     {
@@ -2365,7 +2372,22 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
       const int n16 = (int)(P.piece_stride >> 4);
       for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
     }
+    if (tid == 0) {  // the longest run of rows without a 0 entry: quals there need no per-entry check
+      int best_lo = 0, best_n = 0, run = 0;
+      for (int r = 0; r < qw; ++r) {
+        const bool bad = (P.rowbad[key * 4 + (r >> 5)] >> (r & 31)) & 1u;
+        run = bad ? 0 : run + 1;
+        if (run > best_n) {
+          best_n = run;
+          best_lo = r - run + 1;
+        }
+      }
+      clean_rows[0] = (uint32_t)(q_lo + best_lo);
+      clean_rows[1] = (uint32_t)(q_lo + best_lo + best_n);
+    }
     __syncthreads();
+    const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb, (int)clean_rows[0],
+                        (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C};
     chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads>(
         P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk,
         [&](const LaneRead& x, bool live) {
