@@ -1334,8 +1334,12 @@ __device__ __forceinline__ bool quals_in_rows(const uint32_t qd[4], int q_lo, in
 // undone, the row's masked count raised.  The unconditional form issues
 // about a third of the predicated loop's VALU and none of its exec-mask
 // juggling.
+// The fix-ups of masked offsets and the mismatch increments (unmasked
+// mismatches: both cells of the mm window, qw * wcells words on) share one
+// loop, so a wavefront pays for the larger of the two counts, not their sum.
 __device__ __forceinline__ void observe_clean(uint32_t lb, const uint32_t qd[4], const uint32_t xo[4], uint32_t bm,
-                                              int wc0, int dir, int q_lo, int wcells, int cw, uint32_t lmasked) {
+                                              uint32_t bx, int wc0, int dir, int q_lo, int qw, int wcells, int cw,
+                                              uint32_t lmasked) {
   const uint32_t w4 = 4u * (uint32_t)wcells;
   const uint32_t qoff = 4u * (uint32_t)(q_lo * wcells);
   const uint32_t cb0 = lb + 4u * (uint32_t)wc0 - qoff;
@@ -1351,19 +1355,23 @@ __device__ __forceinline__ void observe_clean(uint32_t lb, const uint32_t qd[4],
     lds_add(rq + xb + 4u * xs, 1u);
     cb += d4;
   }
-  uint32_t mk = bm & 0xFFFFu;
-  if (__builtin_amdgcn_ballot_w64(mk != 0)) {  // masked offsets (clips, insertions, known sites)
+  uint32_t mk = (bm | bx) & 0xFFFFu;
+  if (__builtin_amdgcn_ballot_w64(mk != 0)) {  // masked (clips, insertions, known sites) or mismatch
     const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
     const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
+    const uint32_t mm_off = 4u * (uint32_t)(qw * wcells);
     while (mk) {
       const int k = __builtin_ctz(mk);
       mk &= mk - 1;
       const uint32_t q = (uint32_t)((k < 8 ? q01 : q23) >> (8 * (k & 7))) & 0xFFu;
       const uint32_t xs = (uint32_t)((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu;
       const uint32_t rq = __mul24(q, w4);
-      lds_sub(rq + cb0 + d4 * (uint32_t)k, 1u);
-      lds_sub(rq + xb + 4u * xs, 1u);
-      lds_add(lmasked + 4u * (q - (uint32_t)q_lo), 1u);
+      const bool masked = (bm >> k) & 1u;
+      // masked: undo both increments (-1 in the obs window); mismatch: +1 in the mm window
+      const uint32_t off = masked ? 0u : mm_off, val = masked ? ~0u : 1u;
+      lds_add(rq + cb0 + d4 * (uint32_t)k + off, val);
+      lds_add(rq + xb + 4u * xs + off, val);
+      if (masked) lds_add(lmasked + 4u * (q - (uint32_t)q_lo), 1u);
     }
   }
 }
@@ -1423,6 +1431,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
     const int rg_w = key_rg(P.ord, key, P.w.rg_lo);  // the read group of the window rows
     const WinGeom gm = win_geom(P.ord, P.g, key);
     const int c_lo = gm.c_lo, cw = gm.cw;
+    const bool all_cycles = c_lo == 0 && cw == C;  // read order: the window holds every cycle cell
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
 
@@ -1479,14 +1488,15 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
           // (monotone in k: both ends)
           const uint32_t nv = (uint32_t)min(kChunk, n - j);
           const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
-          const bool cok = full_rg && (unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)cw &&
-                           (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)cw;
+          const bool cok = full_rg && (all_cycles || ((unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)cw &&
+                                                     (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)cw));
           const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
           // fast path: window rows of the piece's read group; offsets it skips
           // are redone below
           uint32_t fastm = 0;
           if (cok && vmask == 0xFFFFu && quals_in_rows(qd, q_lo, q_lo + qw)) {
-            observe_clean(lds_obs, qd, xo, bm, wc0, x.dir, q_lo, wcells, cw, lds_masked);
+            observe_clean(lds_obs, qd, xo, bm, bx, wc0, x.dir, q_lo, qw, wcells, cw, lds_masked);
+            bx = 0;  // its mismatches are counted
             fastm = 0xFFFFu;
           } else {
             const uint32_t* qr = qd;
