@@ -248,3 +248,20 @@ def test_prep_fast_path_borders(read_order):
 def test_prep_fast_path_errors(bad, err):
     ok = [rec32(), rec32(qual="H" * 32)]
     check([RecordBatch.from_records(ok + [bad] + ok)], expect_error=err)
+
+
+@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
+def test_char_table_row_gap(read_order):
+    """Quals drawn from 5..14 and 30..41 only: the char-table rows 15..29 of
+    the window hold no key (0 entries), so apply's clean rows are one side of
+    the gap and the other side's offsets take the checked path -- every char
+    must still match the oracle."""
+    b = synth.generate(12000, (100,), 2, 77)
+    rng = np.random.default_rng(77)
+    q = b.qual.copy()
+    lo = rng.integers(5, 15, q.size)
+    hi = rng.integers(30, 42, q.size)
+    pick = np.where(rng.random(q.size) < 0.35, lo, hi) + 33
+    keep = q <= 33 + 2  # leave the Q2 tails (trimming) as they are
+    b.qual = np.where(keep, q, pick).astype(q.dtype)
+    check([b.slice(0, 5000), b.slice(5000, 12000)])
