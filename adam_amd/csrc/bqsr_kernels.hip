@@ -2383,9 +2383,11 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
       for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
     }
     if (tid == 0) {  // the longest run of rows without a 0 entry: quals there need no per-entry check
+      const uint4 rb = *(const uint4*)(P.rowbad + key * 4);  // one load, not one per row
+      const uint32_t rw[4] = {rb.x, rb.y, rb.z, rb.w};
       int best_lo = 0, best_n = 0, run = 0;
       for (int r = 0; r < qw; ++r) {
-        const bool bad = (P.rowbad[key * 4 + (r >> 5)] >> (r & 31)) & 1u;
+        const bool bad = (rw[r >> 5] >> (r & 31)) & 1u;
         run = bad ? 0 : run + 1;
         if (run > best_n) {
           best_n = run;
