@@ -825,7 +825,7 @@ __device__ __forceinline__ void prep_store_words(const PrepParams& P, int64_t r,
 // With word stores they wait for bqsr_prep_complex, whose atomics must land
 // on words every workgroup has stored.
 template <bool kStore>
-__global__ void __launch_bounds__(kPrepThreads) bqsr_prep_kernel(PrepParams P) {
+__global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel(PrepParams P) {
   __shared__ uint32_t list[kPrepChunk];
   __shared__ uint32_t cnt;
   __shared__ uint32_t s_cig[kStore ? 1 : kPrepThreads * kPrepCigStride];
