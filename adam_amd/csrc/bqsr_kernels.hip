@@ -823,7 +823,10 @@ __device__ __forceinline__ void prep_store_words(const PrepParams& P, int64_t r,
 // read): no second launch waiting for every workgroup of this one, and the
 // listed reads' latency chains overlap other workgroups' lock-step work.
 // With word stores they wait for bqsr_prep_complex, whose atomics must land
-// on words every workgroup has stored.
+// on words every workgroup has stored.  The atomic form asks for 6 waves per
+// SIMD (80 VGPRs, a few spills, against 90 and 5: cfg2 prep 0.316 -> 0.308
+// ms, cfg4 0.616 -> 0.593); the store form keeps its 104 (at 6 waves it ran
+// 2.08 -> 3.08 ms on cfg3).
 template <bool kStore>
 __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel(PrepParams P) {
   __shared__ uint32_t list[kPrepChunk];
