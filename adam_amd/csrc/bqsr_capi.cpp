@@ -173,15 +173,17 @@ constexpr size_t kLdsMax = 163840;
 // LDS of the per-base passes: the context table (both), observe's u32 window
 // [qw][wcells] x {obs, mm} + masked counts + block histogram, apply's char
 // table [qw][cw][21]
-size_t observe_lds(int qw, int wcells) {
-  return (size_t)kCtxTabBytes + (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 + (size_t)kMkWords * 4;
+// (the context table only for the chunk walk, bqsr_observe_chunks)
+size_t observe_lds(int qw, int wcells, bool table) {
+  return (table ? (size_t)kCtxTabBytes : 0) + (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 +
+         (size_t)kMkWords * 4;
 }
 // a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
 int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
 size_t apply_lds(int qw, int cw) { return 16 + (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)piece_bytes(qw, cw); }
-int observe_rows(int wcells) {
+int observe_rows(int wcells, bool table) {
   int qw = kQBins;
-  while (qw > 1 && observe_lds(qw, wcells) > kLdsMax) --qw;
+  while (qw > 1 && observe_lds(qw, wcells, table) > kLdsMax) --qw;
   return qw;
 }
 // 16-aligned packed layout (ReadsDev::slots_aligned); ADAM_BQSR_ALIGN=0 packs reads back to back
@@ -1103,7 +1105,10 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       while ((P.wcells & 3) != 2) ++P.wcells;
     else if (window_mod() >= 0)
       while ((P.wcells & 31) != window_mod()) ++P.wcells;
-    P.w = window_rows(b, observe_rows(P.wcells));
+    // measured (cfg2 / cfg4 / cfg3): the chunk walk wins on bucketed batches (4.63 vs 5.03 ms),
+    // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
+    const int form = observe_form() >= 0 ? observe_form() : (b->bucketed ? 0 : 1);
+    P.w = window_rows(b, observe_rows(P.wcells, form == 0));
     P.touched = t->touched();
     P.obs = t->obs();
     P.mm = t->mm();
@@ -1123,11 +1128,8 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = observe_lds(P.w.qw, P.wcells);
+    const size_t lds = observe_lds(P.w.qw, P.wcells, form == 0);
     P.lane_shift = lane_shift(b);
-    // measured (cfg2 / cfg4 / cfg3): the chunk walk wins on bucketed batches (4.63 vs 5.03 ms),
-    // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
-    const int form = observe_form() >= 0 ? observe_form() : (b->bucketed ? 0 : 1);
     if (form == 0)
       hipLaunchKernelGGL(bqsr_observe_chunks, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else if (form == 2 || chunk_lanes(b->bucketed))

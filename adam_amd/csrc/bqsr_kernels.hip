@@ -1395,7 +1395,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObservePara
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
   const int wcells = P.wcells;  // window row: [cycle cells cw][contexts 21]
-  uint32_t* w_obs = (uint32_t*)(smem + kCtxTabBytes);  // (the context table's LDS unused here)
+  uint32_t* w_obs = (uint32_t*)smem;  // (no context table: observe_lds without it)
   uint32_t* w_mm = w_obs + qw * wcells;
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
