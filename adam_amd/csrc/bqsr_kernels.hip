@@ -1312,9 +1312,6 @@ typedef __attribute__((address_space(3))) uint32_t* LdsWords;
 __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
   __hip_atomic_fetch_add((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_sub(uint32_t addr, uint32_t v) {
-  __hip_atomic_fetch_sub((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // SWAR: every byte of a chunk's 16 quals is a window row, q_lo <= q < hi
 // (hi = q_lo + qw <= 128; a byte >= 128 is a negative Java byte, never a row)
@@ -1370,7 +1367,7 @@ __device__ __forceinline__ void observe_clean(uint32_t lb, const uint32_t qd[4],
       const uint32_t xs = (uint32_t)((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu;
       const uint32_t rq = __mul24(q, w4);
       const bool masked = (bm >> k) & 1u;
-      // masked: undo both increments (-1 in the obs window); mismatch: +1 in the mm window
+      // masked: undo both increments (add ~0u = -1 in the obs window); mismatch: +1 in the mm window
       const uint32_t off = masked ? 0u : mm_off, val = masked ? ~0u : 1u;
       lds_add(rq + cb0 + d4 * (uint32_t)k + off, val);
       lds_add(rq + xb + 4u * xs + off, val);
