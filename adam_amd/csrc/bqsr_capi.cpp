@@ -1613,6 +1613,23 @@ bqsr_status bqsr_job_reset_async(bqsr_batch* b, bqsr_table* t, void* stream) {
   return ok();
 }
 
+bqsr_status bqsr_job_errors_export_async(bqsr_batch* b, int64_t read_base, int64_t* dst_device, void* stream) {
+  if (!b || !dst_device || read_base < 0) return fail(BQSR_ERR_INVALID_ARG, "null / negative read base");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipLaunchKernelGGL(bqsr_job_err_export, dim3(1), dim3(64), 0, S(stream), (const unsigned long long*)b->d_err,
+                     read_base, dst_device);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+bqsr_status bqsr_job_errors_import_async(bqsr_batch* b, const int64_t* src_device, void* stream) {
+  if (!b || !src_device) return fail(BQSR_ERR_INVALID_ARG, "null");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  hipLaunchKernelGGL(bqsr_job_err_import, dim3(1), dim3(64), 0, S(stream), (unsigned long long*)b->d_err, src_device);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
 bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_exceptions, void* stream) {
   if (!b || !L) return fail(BQSR_ERR_INVALID_ARG, "null");
   HIP_TRY(hipSetDevice(b->ctx->device));
@@ -1623,9 +1640,9 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(s));
   const uint64_t* h = b->h_status;
-  std::memcpy(&L->out, h + 5, sizeof(FinalOut));
+  std::memcpy(&L->out, h + kErrWords + 1, sizeof(FinalOut));
   L->out_pending = false;
-  if (em) std::memcpy(em, h + 4, 8);
+  if (em) std::memcpy(em, h + kErrWords, 8);
   if (n_exceptions) *n_exceptions = (int64_t)h[kNExc];
   bqsr_status st = from_err_key(h[kErrObs], 0);
   if (st != BQSR_OK) return st;

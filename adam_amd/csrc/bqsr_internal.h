@@ -302,6 +302,9 @@ struct FinalOut {
   int32_t any_key;
   int32_t pad;
 };
+// bqsr_job_status_kernel's host words: error words, expectedMismatch, FinalOut
+static_assert(kErrWords + 1 + sizeof(FinalOut) / 8 <= (size_t)kJobStatusWords, "job status words overflow");
+static_assert(sizeof(FinalOut) % 8 == 0, "FinalOut is whole words");
 
 // errorProbabilityToPhred step function: thr[i] = the largest p > 0 whose
 // javaD2I(-10*log10(p)) >= thr_qmin + i.  Q(p) = max{n : p <= thr[n - qmin]}.

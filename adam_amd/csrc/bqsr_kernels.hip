@@ -2436,13 +2436,31 @@ extern "C" __global__ void bqsr_job_reset_kernel(int64_t* words, int64_t n, unsi
     words[i] = 0;
   if (blockIdx.x == 0 && threadIdx.x < kErrWords) err[threadIdx.x] = threadIdx.x == kNExc ? 0ull : ~0ull;
 }
-// [0, kErrWords) error words, [4] expectedMismatch bits, [5, 10) FinalOut
+// [0, kErrWords) error words, [kErrWords] expectedMismatch bits, then FinalOut
 extern "C" __global__ void bqsr_job_status_kernel(const unsigned long long* err, const double* em, const FinalOut* fo,
                                                   uint64_t* host) {
   const int t = threadIdx.x;
   if (t < kErrWords) host[t] = err[t];
   else if (t == kErrWords) host[t] = (uint64_t)__double_as_longlong(*em);
   else if (t < kErrWords + 1 + (int)(sizeof(FinalOut) / 8)) host[t] = ((const uint64_t*)fo)[t - kErrWords - 1];
+}
+
+// Multi-rank error exchange (every rank raises the job's first error in global
+// read order, as the reference's one job fails on its first failing
+// partition): the batch's observe and apply error keys rebased to global read
+// indices (read_base << 28 added) as signed int64, no error = INT64_MAX, for
+// an all-reduce MIN; then the reduced keys written back as the batch's own.
+extern "C" __global__ void bqsr_job_err_export(const unsigned long long* err, int64_t read_base, int64_t* out) {
+  const int t = threadIdx.x;
+  if (t >= 2) return;
+  const unsigned long long k = t == 0 ? err[kErrObs] : min(err[kErrAppPrep], err[kErrAppKern]);
+  out[t] = k == kNoError ? INT64_MAX : (int64_t)(k + ((unsigned long long)read_base << 28));
+}
+extern "C" __global__ void bqsr_job_err_import(unsigned long long* err, const int64_t* in) {
+  const int t = threadIdx.x;
+  if (t == 0) err[kErrObs] = in[0] == INT64_MAX ? kNoError : (unsigned long long)in[0];
+  if (t == 1) err[kErrAppPrep] = in[1] == INT64_MAX ? kNoError : (unsigned long long)in[1];
+  if (t == 2) err[kErrAppKern] = kNoError;
 }
 
 // --------------------------------------------------------- table merge -----

@@ -62,6 +62,8 @@ struct SynthSpec {
   int32_t n_rg;           // read groups, chosen uniformly
   int64_t contig_len;
   double p_unmapped, p_duplicate, p_secondary, p_n, p_q2tail, p_indel, p_softclip;
+  int64_t first_read;     // index of read 0 in the whole dataset: reads [first, first + n) of one
+                          // (seed, ...) dataset, so a rank's shard is a slice of the job's reads
 };
 
 // flag bits as include/adam_bqsr.h
@@ -103,6 +105,7 @@ void append_int(std::string& s, int v) {
 }
 
 void gen_read(const SynthSpec& sp, int64_t r, Read& R) {
+  r += sp.first_read;
   Rng g(sp.seed * 0x9E3779B97F4A7C15ull ^ (uint64_t)r * 0xD1B54A32D192ED03ull ^ 0x5851F42D4C957F2Dull);
   g.next();
   const int L = sp.lens[sp.n_len > 1 ? g.below((uint32_t)sp.n_len) : 0];

@@ -61,6 +61,21 @@ def allreduce_table(words: torch.Tensor) -> torch.Tensor:
     return words
 
 
+def allreduce_error_keys(keys: torch.Tensor) -> torch.Tensor:
+    """MIN over the ranks of the int64 error keys (global read order; no error
+    = INT64_MAX), in place: the job's first error, which every rank raises."""
+    if keys.dtype != torch.int64:
+        raise TypeError("error keys are int64")
+    if _multi():
+        if _host_coll(keys):
+            h = keys.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MIN)
+            keys.copy_(h)
+        else:
+            dist.all_reduce(keys, op=dist.ReduceOp.MIN)
+    return keys
+
+
 def _all_gather(t: torch.Tensor) -> torch.Tensor:
     """[world * n] = every rank's 1-D `t` (same n on every rank), rank-major."""
     world = dist.get_world_size()

@@ -13,7 +13,10 @@ ranks' shards, in rank order).  One ``step``:
 4. finalize on the device (expectedMismatch read from HBM: no host round trip);
 5. apply into device outputs (u8 chars per packed slot, per-read start and
    length, exception list for chars above 0xFF);
-6. the job's errors, in the order the reference raises them (one transfer, one sync).
+6. N > 1: the ranks' error keys (global read order) MIN-reduced, so every
+   rank raises the job's first error, as the reference's one Spark job fails
+   on its first failing partition;
+7. the job's errors, in the order the reference raises them (one transfer, one sync).
 
 Only the HIP library computes; this module orders launches.
 """
@@ -34,7 +37,9 @@ class ResidentJob:
     STAGES = ("prep", "observe", "fold", "apply")
 
     def __init__(self, batch: RecordBatch, dims, snp: Optional["bqsr.SnpTable"] = None, device: int = 0,
-                 max_exc: int = 1 << 16):
+                 max_exc: int = 1 << 16, read_base: int = 0):
+        """read_base: global index of the shard's first read (reads of the
+        ranks before this one): errors are reported in global read order."""
         import torch
         self.torch = torch
         self.L = L = _capi.lib()
@@ -65,6 +70,8 @@ class ResidentJob:
         self.em_part = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self.lut = ctypes.c_void_p()
         self.world = D.dist.get_world_size() if D._multi() else 1
+        self.read_base = int(read_base)
+        self.err_keys = torch.empty(2, dtype=torch.int64, device=self.dev)
         self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         self.kt: Dict[str, List[float]] = {k: [] for k in self.STAGES}
         self.n_exc = 0
@@ -104,6 +111,10 @@ class ResidentJob:
         mark(3)
         check(L.bqsr_apply_stage(*args, _capi.STAGE_KERNEL, sp))
         mark(4)
+        if self.world > 1:
+            check(L.bqsr_job_errors_export_async(bh, self.read_base, self._ptr(self.err_keys), sp))
+            D.allreduce_error_keys(self.err_keys)
+            check(L.bqsr_job_errors_import_async(bh, self._ptr(self.err_keys), sp))
         # the job's results and errors, in the order the reference raises them
         # (one transfer and one sync)
         em = ctypes.c_double()

@@ -94,6 +94,10 @@ class ADAMRecord:
     primary_alignment: bool = False
     duplicate_read: bool = False
     read_name: Optional[str] = None
+    # optional fields other than MD, "TAG:TYPE:VALUE" joined by tabs in the
+    # converter's order (SAMRecordConverter.scala:110-121 prepends each: the
+    # reverse of the SAM line's order); not read by BQSR
+    attributes: Optional[str] = None
 
     @property
     def flag_bits(self) -> int:
@@ -298,6 +302,24 @@ class RecordBatch:
 def read_sam(path: str) -> RecordBatch:
     """Load a SAM text file the way ``sc.adamLoad`` + ``SAMRecordConverter.convert``
     would (core/rdd/AdamContext.scala:122-137, converters/SAMRecordConverter.scala:26-144)."""
+    return RecordBatch.from_records(read_sam_records(path))
+
+
+def characterize_tags(recs: Iterable[ADAMRecord]) -> dict:
+    """Records carrying each optional-field tag, MD excluded
+    (AdamRDDFunctions.scala:200-202 adamCharacterizeTags over the converter's
+    attributes)."""
+    counts: dict = {}
+    for r in recs:
+        for t in (r.attributes or "").split("\t"):
+            if t:
+                k = t.split(":", 1)[0]
+                counts[k] = counts.get(k, 0) + 1
+    return counts
+
+
+def read_sam_records(path: str) -> List[ADAMRecord]:
+    """The ADAMRecords of a SAM text file (SAMRecordConverter semantics)."""
     rg_names: List[str] = []
     sq_names: List[str] = []
     body: List[List[str]] = []
@@ -322,9 +344,12 @@ def read_sam(path: str) -> RecordBatch:
         qname, flag, rname, pos, _mapq, cigar, _rnext, _pnext, _tlen, seq, qual = f[:11]
         flag = int(flag)
         tags = {}
+        attrs = []
         for t in f[11:]:
             k, typ, v = t.split(":", 2)
             tags[k] = v
+            if k != "MD":
+                attrs.insert(0, t)
         # getReadString / getBaseQualityString / getCigarString return "*" when
         # absent, and the converter stores those strings as they are
         r = ADAMRecord(read_name=qname, sequence=seq, qual=qual, cigar=cigar)
@@ -350,5 +375,7 @@ def read_sam(path: str) -> RecordBatch:
             r.mismatching_positions = tags["MD"]
         if "RG" in tags and tags["RG"] in rg_index:
             r.record_group_id = rg_index[tags["RG"]]
+        if len(f) > 11:  # samRecord.getAttributes is null without optional fields
+            r.attributes = "\t".join(attrs)
         recs.append(r)
-    return RecordBatch.from_records(recs)
+    return recs

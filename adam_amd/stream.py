@@ -38,7 +38,9 @@ class StreamedShard:
     """Partitions of one rank's shard: pinned host copies + device batches."""
 
     def __init__(self, ctx, parts: Sequence, dims, sites_handle=None, device: int = 0, max_exc: int = 1 << 16,
-                 site_contigs: Optional[Sequence[str]] = None):
+                 site_contigs: Optional[Sequence[str]] = None, read_base: int = 0):
+        """read_base: global index of the shard's first read (reads of the
+        ranks before this one): multi-rank errors are raised in global order."""
         import torch
         self.torch = torch
         self.L = L = _capi.lib()
@@ -53,6 +55,7 @@ class StreamedShard:
         self.n_bases = 0
         self.staged_bytes = 0
         self.site_contigs = site_contigs
+        self.read_base = int(read_base)
         for p in parts:
             self.add_partition(p)
         if parts:
@@ -169,6 +172,8 @@ class StreamedShard:
         L = self.L
         comp = self.torch.cuda.current_stream(self.dev)
         sp = ctypes.c_void_p(comp.cuda_stream)
+        if D._multi():
+            self._exchange_errors(sp)
         em = ctypes.c_double()
         for bh in self.batches:
             check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
@@ -186,6 +191,28 @@ class StreamedShard:
         if total:  # rare: only then are the exception lists copied back
             self.host_exc.copy_(self.exc.cpu())
         return total
+
+    def _exchange_errors(self, sp):
+        """Several ranks: the first observe error and the first apply error of
+        the whole job (global read order) on every rank -- the partitions'
+        error keys rebased to global reads, MIN over partitions and ranks, and
+        written back into every partition (the first partition carries them,
+        the others none), so every rank raises the same error in `finish`."""
+        torch, L = self.torch, self.L
+        n = len(self.batches)
+        keys = torch.empty(max(1, n), 2, dtype=torch.int64, device=self.dev)
+        base = self.read_base
+        for i, bh in enumerate(self.batches):
+            check(L.bqsr_job_errors_export_async(bh, base, ctypes.c_void_p(keys[i].data_ptr()), sp))
+            base += self.n_reads[i]
+        red = keys[:max(1, n)].min(dim=0).values.contiguous() if n else torch.full((2,), 2 ** 63 - 1,
+                                                                                     dtype=torch.int64,
+                                                                                     device=self.dev)
+        D.allreduce_error_keys(red)
+        none = torch.full((2,), 2 ** 63 - 1, dtype=torch.int64, device=self.dev)
+        for i, bh in enumerate(self.batches):
+            check(L.bqsr_job_errors_import_async(bh, ctypes.c_void_p((red if i == 0 else none).data_ptr()), sp))
+        self._err_keep = (keys, red, none)
 
     def exceptions(self, i: int):
         """Partition i's chars above 0xFF of the last job: (slot, Java char) pairs."""

@@ -7,9 +7,13 @@ One step = one whole BQSR job over the GPU's read shard, inputs resident in
 HBM: zero the covariate table, observe (+ the exact expectedMismatch fold),
 [N > 1: RCCL int64 all-reduce of the table, all-gather of the per-shard
 expectedMismatch folded in rank order], finalize, apply.  `bases` = sum of the
-sequence lengths of ALL reads (filtered ones included).  Reads shard across
-ranks (each rank its own synthetic shard: weak scaling); rank 0 prints one
-JSON line.  See DESIGN.md "Measurement".
+sequence lengths of ALL reads (filtered ones included).  The ranks' shards
+are consecutive read ranges of one synthetic dataset (cfg2 / cfg4: the
+config's reads per GPU, weak scaling; cfg3: the 60M-read set split over the
+ranks), the job's partitions in rank order.  After the timed jobs every rank
+checks the last job's table, expectedMismatch and recalibrated chars against
+the oracle (oracle/, outside the timed region); rank 0 prints one JSON line.
+See DESIGN.md "Measurement".
 """
 from __future__ import annotations
 
@@ -45,8 +49,10 @@ def parse():
     ap.add_argument("--cpu-reads", type=int, default=10_000_000, help="oracle baseline sample (reads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed job's results")
-    ap.add_argument("--event-every", type=int, default=10, help="time the stages with HIP events on every n-th timed step")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--event-steps", type=int, default=3,
+                    help="untimed jobs after the timed region whose stages are timed with HIP events")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic json (default profiles/pmc_traffic_<config>.json)")
     ap.add_argument("--part-reads", type=int, default=4_000_000, help="cfg5: reads per streamed partition")
     return ap.parse_args()
 
@@ -75,18 +81,26 @@ def main():
     cfg = dict(synth.CONFIGS[args.config])
     if args.config == "cfg5":
         return main_stream(args, cfg, world, rank, dev, ctx)
-    n_reads = args.reads or cfg["n_reads"]
+    # one dataset per job (seed, config): cfg3 is the 60M-read set sharded by
+    # read index over the ranks; cfg2 / cfg4 give every rank the config's read
+    # count (weak scaling) as reads [rank*n, (rank+1)*n) of one bigger set --
+    # the ranks' shards are the job's partitions in rank order either way
     if args.config == "cfg3":
-        n_reads = args.reads or (cfg["n_reads"] // max(1, world))  # cfg3 is one dataset sharded over the GPUs
+        total = args.reads or cfg["n_reads"]
+        r0, r1 = D.shard_bounds(total, rank, world)
+    else:
+        n = args.reads or cfg["n_reads"]
+        r0, r1 = rank * n, (rank + 1) * n
+    n_reads = r1 - r0
     t_gen = time.time()
-    batch = synth.generate(n_reads, cfg["lens"], cfg["n_rg"], cfg["seed"] + 1_000_003 * rank)
+    batch = synth.generate(n_reads, cfg["lens"], cfg["n_rg"], cfg["seed"], first_read=r0)
     sites = synth.known_sites(cfg["sites"]) if cfg["sites"] else None
     snp = bqsr.SnpTable(sites) if sites else None
     t_gen = time.time() - t_gen
     n_bases = batch.n_bases
 
     from adam_amd.job import ResidentJob
-    job = ResidentJob(batch, Dims(cfg["n_rg"], max(cfg["lens"])), snp, local)
+    job = ResidentJob(batch, Dims(cfg["n_rg"], max(cfg["lens"])), snp, local, read_base=r0)
 
     for _ in range(args.warmup):
         job.step(False)
@@ -94,14 +108,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        # stage events on every event_every-th step: an event record stalls
-        # the stream ~30 us (6 per step), the sampled steps give the same means
-        job.step(i % args.event_every == 0)
+    for _ in range(args.steps):
+        job.step(False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # per-stage times: HIP events on the launch stream over extra jobs after
+    # the timed region (an event record costs the stream ~30 us, so the timed
+    # jobs carry none; the stage times include their launch gaps)
+    for _ in range(max(0, args.event_steps)):
+        job.step(True)
+    torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -113,17 +131,34 @@ def main():
         total_bases = n_bases
     kt = job.kt
 
+    # parity of the last job's results against the oracle (every rank checks
+    # its own shard; N > 1 with the all-reduced oracle table), outside the
+    # timed region; the CPU baseline on rank 0 at N = 1
+    cpu_line, parity = None, None
+    if world == 1:
+        ref = None
+        if not args.no_cpu_baseline:
+            cpu_line, ref = cpu_baseline(args, cfg, batch, sites, whole=not args.no_parity)
+        if not args.no_parity:
+            if ref is None:
+                ref = oracle_shard(cfg, batch, sites)
+            parity = parity_check(job, batch, ref)
+            del ref
+    elif not args.no_parity:
+        parity = parity_multi(job, cfg, batch, sites, world, rank, dev)
+
     if rank == 0:
-        ms = {k: float(np.mean(v)) for k, v in kt.items()}
+        ms = {k: float(np.mean(v)) for k, v in kt.items() if v}
         R = batch.n_reads
         # algorithmic bytes: observe 1.75 B/base + 16 B/read, apply 2.5 B/base + 16 B/read
         alg = {"observe": 1.75 * n_bases + 16 * R, "apply": 2.5 * n_bases + 16 * R}
-        dom = "observe" if ms["observe"] >= ms["apply"] else "apply"
-        achieved = alg[dom] / (ms[dom] * 1e-3) / 1e9
+        dom = "observe" if ms.get("observe", 0) >= ms.get("apply", 0) else "apply"
+        achieved = alg[dom] / (ms[dom] * 1e-3) / 1e9 if dom in ms else None
         traffic = None
         kname = "bqsr_%s_kernel" % dom
-        try:  # PMC bytes of the same kernel on the same workload (tools/fetch_profile.sh)
-            with open(args.traffic) as fh:
+        tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.config)
+        try:  # PMC bytes of the same kernel on the same workload (tools/make_traffic.py)
+            with open(tpath) as fh:
                 tr = json.load(fh)
             if tr.get("config") == args.config and tr.get("reads_per_gpu") == R:
                 traffic = tr["kernels"].get(dom, {}).get("hbm_bytes_per_launch")
@@ -140,7 +175,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.config != "cfg3" else "strong",
             "vs_baseline": None,
             "dtype": "u8 in, int64 counts, f64 recalibration",
             "data": "synthetic (deterministic generator, SURVEY.md 8d spec), resident in HBM",
@@ -148,6 +183,7 @@ def main():
                 "workload": WORKLOADS[args.config],
                 "reads_per_gpu": R,
                 "bases_per_gpu": n_bases,
+                "reads_total": R * world if args.config != "cfg3" else (args.reads or cfg["n_reads"]),
                 "read_len": list(cfg["lens"]),
                 "read_groups": cfg["n_rg"],
                 "known_sites": int(sum(len(v) for v in sites.values())) if sites else 0,
@@ -159,26 +195,40 @@ def main():
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic,
+                "traffic_source": tpath if traffic is not None else None,
                 "alg_bytes_per_launch": alg[dom],
                 "kernel_ms": ms,
+                "kernel_ms_method": "HIP events on the launch stream over %d untimed jobs after the timed region "
+                                    "(stage brackets include launch gaps; rocprofv3 kernel averages in profiles/ "
+                                    "are the kernel-only times)" % args.event_steps,
             },
             "hbm_roofline_frac_step": (total_bases / world) * (4.25 + 32.0 / max(cfg["lens"])) /
                                       (elapsed / args.steps) / (HBM_PEAK_GBS * 1e9),
             "gen_s": t_gen,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"], ref = cpu_baseline(args, cfg, batch, sites, whole=not args.no_parity)
-            if ref is not None:
-                line["parity"] = parity_check(job, batch, ref)
-        elif world > 1:
-            line["parity"] = {"checked": False, "reason": "N > 1: the table is the all-reduce over every rank's shard; "
-                                                           "multi-rank parity is tests/test_gpu_multirank.py"}
+        if cpu_line is not None:
+            line["cpu_baseline"] = cpu_line
+        if parity is not None:
+            line["parity"] = parity
         print(json.dumps(line), flush=True)
     job.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def oracle_shard(cfg, batch, sites):
+    """The oracle over the whole shard as ONE partition (table by partitions in
+    parallel, expectedMismatch folded sequentially), for the parity check."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    cores, _ = host_cores()
+    osites = O.Sites(sites) if sites else None
+    d = O.Dims(cfg["n_rg"], max(cfg["lens"]))
+    words, em = O.observe_mt(batch, osites, d, n_parts=cores, nthreads=cores, fold1=True)
+    out, out_len = O.apply_mt(batch, d, words, em, n_parts=cores, nthreads=cores)
+    return words, em, out, out_len
 
 
 def parity_check(job, batch, ref):
@@ -201,6 +251,52 @@ def parity_check(job, batch, ref):
             "chars_above_0xff": int(len(exc)),
             "against": "oracle/ (C++ restatement of ADAM BQSR) on the same shard as one partition, "
                        "table built by partitions in parallel, expectedMismatch folded sequentially",
+            "check_s": time.perf_counter() - t}
+
+
+def parity_multi(job, cfg, batch, sites, world, rank, dev):
+    """N > 1 (called on every rank): each rank runs the oracle's observe over
+    its own shard as one partition; the oracle tables are all-reduced and the
+    shards' expectedMismatch values folded in rank order (the job's partitions
+    merged in partition order, RecalibrateBaseQualities.scala:63); each rank
+    then checks the GPU's all-reduced table, the job's expectedMismatch and
+    its own recalibrated chars against the oracle's apply with that table.
+    Mismatch counts and equalities are reduced to every rank."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from adam_amd import distributed as D
+    t = time.perf_counter()
+    cores, _ = host_cores()
+    osites = O.Sites(sites) if sites else None
+    d = O.Dims(cfg["n_rg"], max(cfg["lens"]))
+    words, em_shard = O.observe_mt(batch, osites, d, n_parts=cores, nthreads=cores, fold1=True)
+    wt = torch.from_numpy(words).to(dev)
+    D.allreduce_table(wt)
+    rwords = wt.cpu().numpy()
+    rem = D.fold_expected_mismatch(em_shard, dev)
+    rout, rlen = O.apply_mt(batch, d, rwords, rem, n_parts=cores, nthreads=cores)
+    gw, gem, q, st, ln, exc = job.results()
+    table_ok = bool(np.array_equal(gw, rwords))
+    em_ok = gem == rem
+    bad, first = O.compare_device_output(batch, rout, rlen, q, st, ln, exc if len(exc) else None,
+                                         nthreads=max(1, cores))
+    first_g = (job.read_base + first) if bad else np.iinfo(np.int64).max
+    red = torch.tensor([bad, int(not table_ok), int(not em_ok), len(exc), batch.n_reads], dtype=torch.int64,
+                       device=dev)
+    dist.all_reduce(red)
+    fr = torch.tensor([first_g], dtype=torch.int64, device=dev)
+    dist.all_reduce(fr, op=dist.ReduceOp.MIN)
+    red = red.cpu().tolist()
+    fr = int(fr.item())
+    return {"checked": True, "ok": red[0] == 0 and red[1] == 0 and red[2] == 0,
+            "table_words_equal": red[1] == 0, "expected_mismatch_equal": red[2] == 0,
+            "expected_mismatch": float(gem).hex(), "reads_checked": red[4], "reads_differing": red[0],
+            "first_differing_read": fr if red[0] else -1, "chars_above_0xff": red[3], "ranks": world,
+            "against": "oracle/ (C++ restatement of ADAM BQSR): every rank's shard as one partition, oracle tables "
+                       "all-reduced, shard expectedMismatch folded in rank order; every rank checks its own chars",
             "check_s": time.perf_counter() - t}
 
 

@@ -338,6 +338,16 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin);
 bqsr_status bqsr_job_reset_async(bqsr_batch* b, bqsr_table* t, void* stream);
 bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* l, double* expected_mismatch, int64_t* n_exceptions,
                             void* stream);
+/* Multi-rank jobs (one partition per rank, in rank order): the reference's
+ * job fails with the first error of the first failing partition
+ * (RecalibrateBaseQualities.scala:63,75 -- a Spark job aborts on its first
+ * failed task).  export writes the batch's observe and apply error keys,
+ * rebased to global read indices (reads before this rank's = read_base), as
+ * two int64 at dst_device (no error = INT64_MAX); the caller all-reduces them
+ * with MIN over the ranks and imports the result, so bqsr_job_result raises
+ * the same error (global read index) on every rank. */
+bqsr_status bqsr_job_errors_export_async(bqsr_batch* b, int64_t read_base, int64_t* dst_device, void* stream);
+bqsr_status bqsr_job_errors_import_async(bqsr_batch* b, const int64_t* src_device, void* stream);
 
 #ifdef __cplusplus
 }

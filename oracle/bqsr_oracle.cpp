@@ -718,9 +718,12 @@ int64_t oracle_compare_device_output(const bqsr_records* R, const uint16_t* ref,
   return bad.load();
 }
 
-static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
-                     bool fold1, uint16_t* out_qual, uint32_t* out_len, int64_t* words_out, double* em_out,
-                     int64_t* err_read) {
+// computeTable over the batch split into n_parts partitions (observe per
+// partition on nthreads threads, RecalTable.++ in partition order,
+// RecalibrateBaseQualities.scala:52-64).  fold1: expectedMismatch folded as if
+// the batch were ONE partition (one more thread, sequential over all reads).
+int oracle_observe_mt(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
+                      int32_t fold1, int64_t* words_out, double* em_out, int64_t* err_read) {
   if (n_parts < 1 || nthreads < 1) return BQSR_ERR_INVALID_ARG;
   Dims d(dims);
   const int64_t n = R->n_reads;
@@ -743,7 +746,6 @@ static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, 
   if (fold1) th.emplace_back([&]() { oracle_em_fold(R, 0, n, &em1); });
   for (int32_t i = 0; i < nthreads; ++i) th.emplace_back(work_obs);
   for (auto& t : th) t.join();
-  th.clear();
   for (int32_t p = 0; p < n_parts; ++p)
     if (st[(size_t)p] != BQSR_OK) {
       *err_read = er[(size_t)p];
@@ -758,14 +760,29 @@ static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, 
   if (fold1) em = em1;
   if (words_out) std::memcpy(words_out, acc.data(), acc.size() * sizeof(int64_t));
   if (em_out) *em_out = em;
+  return BQSR_OK;
+}
+
+// finalizeTable of (words, em) then applyTable over the batch, n_parts
+// partitions on nthreads threads (RecalibrateBaseQualities.scala:66-76).
+// Outputs like oracle_apply.
+int oracle_apply_mt(const bqsr_records* R, int32_t n_parts, bqsr_dims dims, int32_t nthreads, const int64_t* words,
+                    double em, uint16_t* out_qual, uint32_t* out_len, int64_t* err_read) {
+  if (n_parts < 1 || nthreads < 1) return BQSR_ERR_INVALID_ARG;
+  const int64_t n = R->n_reads;
+  std::vector<int64_t> bounds((size_t)n_parts + 1);
+  for (int32_t i = 0; i <= n_parts; ++i) bounds[(size_t)i] = n * i / n_parts;
+  std::vector<int> st((size_t)n_parts, BQSR_OK);
+  std::vector<int64_t> er((size_t)n_parts, -1);
   int fst;
-  void* F = oracle_finalize(dims, acc.data(), em, &fst);
+  void* F = oracle_finalize(dims, words, em, &fst);
   if (!F) return fst;
-  next = 0;
+  std::atomic<int32_t> next{0};
   auto work_apply = [&]() {
     for (int32_t p; (p = next.fetch_add(1)) < n_parts;)
       st[(size_t)p] = oracle_apply(R, bounds[(size_t)p], bounds[(size_t)p + 1], F, out_qual, out_len, &er[(size_t)p]);
   };
+  std::vector<std::thread> th;
   for (int32_t i = 0; i < nthreads; ++i) th.emplace_back(work_apply);
   for (auto& t : th) t.join();
   oracle_final_destroy(F);
@@ -775,6 +792,19 @@ static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, 
       return st[(size_t)p];
     }
   return BQSR_OK;
+}
+
+static int bqsr_impl(const bqsr_records* R, int32_t n_parts, const void* sites, bqsr_dims dims, int32_t nthreads,
+                     bool fold1, uint16_t* out_qual, uint32_t* out_len, int64_t* words_out, double* em_out,
+                     int64_t* err_read) {
+  if (n_parts < 1 || nthreads < 1) return BQSR_ERR_INVALID_ARG;
+  std::vector<int64_t> acc((size_t)Dims(dims).words(), 0);
+  double em = 0.0;
+  int st = oracle_observe_mt(R, n_parts, sites, dims, nthreads, fold1 ? 1 : 0, acc.data(), &em, err_read);
+  if (st != BQSR_OK) return st;
+  if (words_out) std::memcpy(words_out, acc.data(), acc.size() * sizeof(int64_t));
+  if (em_out) *em_out = em;
+  return oracle_apply_mt(R, n_parts, dims, nthreads, acc.data(), em, out_qual, out_len, err_read);
 }
 
 // Exposed for the reference-suite ports (RichADAMRecordSuite / MdTagSuite).

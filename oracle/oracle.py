@@ -57,6 +57,10 @@ def lib():
         L.oracle_bqsr.argtypes = [vp, i32, vp, Dims, i32, vp, vp, vp, vp, vp]
         L.oracle_bqsr_fold1.restype = ctypes.c_int
         L.oracle_bqsr_fold1.argtypes = [vp, i32, vp, Dims, i32, vp, vp, vp, vp, vp]
+        L.oracle_observe_mt.restype = ctypes.c_int
+        L.oracle_observe_mt.argtypes = [vp, i32, vp, Dims, i32, i32, vp, vp, vp]
+        L.oracle_apply_mt.restype = ctypes.c_int
+        L.oracle_apply_mt.argtypes = [vp, i32, Dims, i32, vp, dbl, vp, vp, vp]
         L.oracle_em_fold.restype = None
         L.oracle_em_fold.argtypes = [vp, i64, i64, vp]
         L.oracle_compare_device_output.restype = i64
@@ -213,6 +217,37 @@ def bqsr(batch, sites: Optional[Sites], d: Dims, n_parts: int = 1, nthreads: int
     if st != 0:
         raise OracleError(st, err.value)
     return words, em.value, out, out_len
+
+
+def observe_mt(batch, sites: Optional[Sites], d: Dims, n_parts: int = 1, nthreads: int = 1,
+               fold1: bool = False) -> Tuple[np.ndarray, float]:
+    """computeTable over the batch as n_parts partitions on nthreads threads
+    (merged in partition order); fold1: expectedMismatch as ONE partition."""
+    cid = batch.contig_ids_for(sites.contigs if sites else None)
+    s, keep = batch.c_struct(cid)
+    words = np.zeros(table_words(d), dtype=np.int64)
+    em = ctypes.c_double(0.0)
+    err = ctypes.c_int64(-1)
+    st = lib().oracle_observe_mt(ctypes.byref(s), n_parts, sites.handle if sites else None, d, nthreads, int(fold1),
+                                 _p(words), ctypes.byref(em), ctypes.byref(err))
+    if st != 0:
+        raise OracleError(st, err.value)
+    return words, em.value
+
+
+def apply_mt(batch, d: Dims, words: np.ndarray, em: float, n_parts: int = 1, nthreads: int = 1):
+    """finalizeTable(words, em) then applyTable over the batch on nthreads
+    threads: (uint16 chars in qual_offset layout, out_len)."""
+    s, keep = batch.c_struct()
+    words = np.ascontiguousarray(words, dtype=np.int64)
+    out = np.zeros(max(1, int(batch.qual_offset[-1])), dtype=np.uint16)
+    out_len = np.zeros(max(1, batch.n_reads), dtype=np.uint32)
+    err = ctypes.c_int64(-1)
+    st = lib().oracle_apply_mt(ctypes.byref(s), n_parts, d, nthreads, _p(words), em, _p(out), _p(out_len),
+                               ctypes.byref(err))
+    if st != 0:
+        raise OracleError(st, err.value)
+    return out, out_len
 
 
 def em_fold(batch, r0: int = 0, r1: Optional[int] = None, em: float = 0.0) -> float:

@@ -156,3 +156,90 @@ def test_shard_bounds_cover_in_order(n, world):
     assert all(bounds[i][1] == bounds[i + 1][0] for i in range(world - 1))
     sizes = [b - a for a, b in bounds]
     assert max(sizes) - min(sizes) <= 1
+
+
+class _StubJob:
+    """Stands in for adam_amd.job.ResidentJob on a CPU rank: `results()` in the
+    device layout (u8 chars per 16-aligned packed slot, per-read start and
+    length, exception list) built from a single-process oracle run over every
+    rank's shard -- what a correct multi-rank GPU job returns."""
+
+    def __init__(self, shard, words, em, out, out_len, read_base, corrupt=None):
+        lq = np.diff(shard.qual_offset.astype(np.int64))
+        ls = np.diff(shard.seq_offset.astype(np.int64))
+        span = (np.maximum(lq, ls) + 15) // 16 * 16
+        slot = np.concatenate([[0], np.cumsum(span)])
+        q = np.zeros(int(slot[-1]) + 16, dtype=np.uint8)
+        for r in range(shard.n_reads):
+            a = int(shard.qual_offset[r])
+            q[slot[r]:slot[r] + out_len[r]] = out[a:a + out_len[r]]
+        if corrupt is not None:
+            q[slot[corrupt]] ^= 1
+        self._res = (words, em, q, np.zeros(shard.n_reads, np.int32), out_len[:shard.n_reads].astype(np.int32),
+                     np.zeros(0, np.int64))
+        self.read_base = read_base
+
+    def results(self):
+        return self._res
+
+
+def _parity_rank_main(rank, port, out_dir, corrupt):
+    """bench.py's N > 1 parity leg (bench.parity_multi), on gloo CPU ranks."""
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch.distributed as dist
+
+    import bench
+    import oracle as O
+    from adam_amd import distributed as D
+    from adam_amd import synth
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        cfg = dict(lens=(100, 150), n_rg=2)
+        n = 2000
+        r0, r1 = D.shard_bounds(n, rank, WORLD)
+        shard = synth.generate(r1 - r0, cfg["lens"], cfg["n_rg"], 4242, first_read=r0)
+        sites = synth.known_sites(20_000, contig_len=2_000_000)
+        # the job's expected results: the ranks' shards as partitions in order
+        d = O.Dims(2, 150)
+        osites = O.Sites(sites)
+        words = np.zeros(O.table_words(d), dtype=np.int64)
+        em = 0.0
+        for rr in range(WORLD):
+            a, b = D.shard_bounds(n, rr, WORLD)
+            part = synth.generate(b - a, cfg["lens"], cfg["n_rg"], 4242, first_read=a)
+            w, e = O.observe(part, osites, d)
+            words += w
+            em = em + e
+        out, out_len = O.apply(shard, O.Final(d, words, em))
+        job = _StubJob(shard, words, em, out, out_len, r0, corrupt if rank == 1 else None)
+        res = bench.parity_multi(job, cfg, shard, sites, WORLD, rank, "cpu")
+        with open(os.path.join(out_dir, "parity%d.json" % rank), "w") as fh:
+            json.dump({"res": res, "r0": r0}, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [None, 7])
+def test_bench_multi_rank_parity_leg(tmp_path, corrupt):
+    """Every rank checks its own shard against the oracle with the all-reduced
+    table and rank-order expectedMismatch; counts reach every rank."""
+    import json
+    mp.start_processes(_parity_rank_main, args=(_free_port(), str(tmp_path), corrupt), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    res = [json.load(open(tmp_path / ("parity%d.json" % r))) for r in range(WORLD)]
+    for z in res:
+        p = z["res"]
+        assert p["checked"] and p["table_words_equal"] and p["expected_mismatch_equal"]
+        assert p["reads_checked"] == 2000 and p["ranks"] == WORLD
+        if corrupt is None:
+            assert p["ok"] and p["reads_differing"] == 0 and p["first_differing_read"] == -1
+        else:
+            assert not p["ok"] and p["reads_differing"] == 1
+            assert p["first_differing_read"] == res[1]["r0"] + corrupt

@@ -146,3 +146,88 @@ def test_two_ranks_one_gpu(tmp_path):
             bad, first = O.compare_device_output(p, ref_out, ref_len, z["s_q%d" % i], z["s_st%d" % i],
                                                  z["s_ln%d" % i])
             assert bad == 0, (rank, i, first)
+
+
+def _bad_md(shard, k):
+    """Read k's MD tag made unparseable (MdTag.scala:52: must start with a digit)."""
+    a = int(shard.md_offset[k])
+    f = int(shard.flags[k])
+    usable = (f & 2) and (f & 16) and not (f & 32)  # mapped, primary, not a duplicate (include/adam_bqsr.h)
+    if usable and int(shard.md_offset[k + 1]) > a:
+        shard.md[a] = ord("Z")
+        return True
+    return False
+
+
+def _rank_err_main(rank, port, out_dir, bad_rank):
+    """bench.py's multi-rank step with one bad MD tag on `bad_rank` (and, on
+    the other rank, a later bad one), then bench.parity_multi on clean data."""
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from adam_amd import _capi, bqsr, synth
+    from adam_amd.distributed import shard_bounds
+    from adam_amd.job import ResidentJob
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    torch.zeros(1, device=dev)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    out = {}
+    try:
+        cfg = dict(lens=(100,), n_rg=1)
+        n = 6000
+        r0, r1 = shard_bounds(n, rank, WORLD)
+        dims = _capi.Dims(1, 100)
+        # clean: the parity leg of bench.py on the real job
+        shard = synth.generate(r1 - r0, cfg["lens"], 1, 31337, first_read=r0)
+        job = ResidentJob(shard, dims, None, 0, read_base=r0)
+        job.step(False)
+        out["parity"] = bench.parity_multi(job, cfg, shard, None, WORLD, rank, dev)
+        job.close()
+        # errors: the first bad read of the job in global read order
+        shard = synth.generate(r1 - r0, cfg["lens"], 1, 31337, first_read=r0)
+        k = 100 if rank == bad_rank else 2000
+        while not _bad_md(shard, k):
+            k += 1
+        out["bad_local"] = k
+        job = ResidentJob(shard, dims, None, 0, read_base=r0)
+        try:
+            job.step(False)
+            out["raised"] = None
+        except _capi.BQSRError as e:
+            out["raised"] = [e.name, e.read]
+        job.close()
+        with open(os.path.join(out_dir, "err%d.json" % rank), "w") as fh:
+            json.dump(out, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("bad_rank", [0, 1])
+def test_two_ranks_raise_the_jobs_first_error_and_parity_leg(tmp_path, bad_rank):
+    import json
+    ctx = mp.start_processes(_rank_err_main, args=(_free_port(), str(tmp_path), bad_rank), nprocs=WORLD,
+                             join=False, start_method="spawn")
+    for _ in range(600):
+        if ctx.join(timeout=1):
+            break
+    else:
+        for p in ctx.processes:
+            p.kill()
+        pytest.fail("ranks did not finish")
+    res = [json.load(open(tmp_path / ("err%d.json" % r))) for r in range(WORLD)]
+    from adam_amd.distributed import shard_bounds
+    first = min(shard_bounds(6000, r, WORLD)[0] + res[r]["bad_local"] for r in range(WORLD))
+    for z in res:
+        p = z["parity"]
+        assert p["ok"] and p["reads_checked"] == 6000, p
+        assert z["raised"] == ["MD_PARSE", first], (z["raised"], first)

@@ -275,3 +275,10 @@ def test_compare_baseqs_transform_output(tmp_path):
     r = compare_baseqs(src, str(out), "latin-1", "utf-8")
     assert r["unique1"] == r["unique2"] == 0
     assert r["count"] > 0 and r["identity"] < r["count"]
+
+
+@pytest.mark.parametrize("name,count", [("unmapped.sam", 200), ("small.sam", 20), ("reads12.sam", 200)])
+def test_device_parse_reference_fixture_counts(name, count):
+    """AdamContextSuite.scala:32-43 / AdamRDDFunctionsSuite.scala:539-547:
+    the reference loads 200, 20 and 200 records from these files."""
+    assert SamText.read(os.path.join(GOLD, name)).batch().n_reads == count

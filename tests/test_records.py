@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from adam_amd import records as R
-from adam_amd.records import ADAMRecord, RecordBatch, cigar_to_text, parse_cigar, read_sam
+from adam_amd.records import (ADAMRecord, RecordBatch, characterize_tags, cigar_to_text, parse_cigar, read_sam,
+                              read_sam_records)
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_resources")
 
@@ -63,3 +64,33 @@ def test_batch_round_trip_and_offsets():
     assert np.array_equal(b2.qual_offset, b.qual_offset)
     assert b.n_bases == int(sum(len(r.sequence) for r in rs))
     assert [r.flag_bits & R.F_HAS_MD != 0 for r in rs] == [r.mismatching_positions is not None for r in rs]
+
+
+# The reference's own facts about its fixtures (AdamContextSuite.scala:32-43,
+# AdamRDDFunctionsSuite.scala:539-547).
+REF_COUNTS = {"unmapped.sam": 200, "small.sam": 20, "reads12.sam": 200}
+
+
+@pytest.mark.parametrize("name,count", sorted(REF_COUNTS.items()))
+def test_reference_fixture_read_counts(name, count):
+    path = os.path.join(GOLD, name)
+    assert read_sam(path).n_reads == count
+    assert len(read_sam_records(path)) == count
+
+
+def test_reference_reads12_tag_counts():
+    # adamCharacterizeTags over reads12.sam: NM, AS and XS on all 200 reads
+    counts = characterize_tags(read_sam_records(os.path.join(GOLD, "reads12.sam")))
+    assert counts["NM"] == 200 and counts["AS"] == 200 and counts["XS"] == 200
+    assert "MD" not in counts  # MD becomes mismatchingPositions, not an attribute
+
+
+def test_synth_slice_is_the_same_reads_of_the_bigger_set():
+    """A rank's shard (first_read = r0) equals reads [r0, r1) of one generation."""
+    from adam_amd import synth
+    whole = synth.generate(3000, (100, 150), 3, 99)
+    part = synth.generate(1200, (100, 150), 3, 99, first_read=1100)
+    ref = whole.slice(1100, 2300)
+    for c in ("flags", "rg_id", "start", "seq", "qual", "cigar", "md", "seq_offset", "qual_offset", "cigar_offset",
+              "md_offset"):
+        assert np.array_equal(getattr(part, c), getattr(ref, c)), c
