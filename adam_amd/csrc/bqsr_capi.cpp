@@ -214,10 +214,15 @@ int lane_shift(const bqsr_batch* b);
 int observe_form() {
   static const int v = [] {
     const char* e = getenv("ADAM_BQSR_OBSERVE");
-    return !e ? -1 : strcmp(e, "read") == 0 ? 1 : strcmp(e, "superchunk") == 0 ? 2 : 0;
+    return !e ? -1 : strcmp(e, "read") == 0 ? 1 : strcmp(e, "superchunk") == 0 ? 2 : strcmp(e, "rows") == 0 ? 3 : 0;
   }();
   return v;
 }
+// bqsr_observe_rows' LDS: obs rows [qw][orow], mm rows [qw][wcells], masked, block histogram, context tables
+size_t rows_lds(int qw, int orow, int wcells) {
+  return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes;
+}
+int rows_orow(int nc, int cw) { return (kCtxSlots * nc + cw + 31) & ~31; }
 // prep's word stores (PrepParams::store_words); ADAM_BQSR_PREP_ATOMIC=1 turns them off (A/B)
 bool store_words_off() {
   static const bool v = [] {
@@ -395,7 +400,9 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   for (const void* f : {(const void*)bqsr_observe_kernel<false>, (const void*)bqsr_observe_kernel<true>,
                         (const void*)bqsr_apply_kernel,
-                        (const void*)bqsr_observe_chunks})
+                        (const void*)bqsr_observe_chunks, (const void*)bqsr_observe_rows<2, true>,
+                        (const void*)bqsr_observe_rows<4, true>, (const void*)bqsr_observe_rows<2, false>,
+                        (const void*)bqsr_observe_rows<4, false>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -1001,6 +1008,14 @@ Window window_rows(const bqsr_batch* b, int max_rows) {
 // cycle cells of the windows: all of them in read order, one mate class's
 // half when bucketed (OrderDev, WinGeom)
 int window_cw(const bqsr_batch* b, const TableGeom& g) { return b->bucketed ? g.L : g.C; }
+// rows the batch's quals span (all 128 without a histogram)
+int qual_span(const bqsr_batch* b) {
+  if (!b->have_qhist) return kQBins;
+  int lo = 0, hi = kQBins - 1;
+  while (lo < kQBins - 1 && b->qhist[lo] == 0) ++lo;
+  while (hi > lo && b->qhist[hi] == 0) --hi;
+  return hi - lo + 1;
+}
 int lane_shift(const bqsr_batch* b) {
   const int c = (b->dims.max_len + kSuper - 1) / kSuper;
   int s = 0;
@@ -1107,8 +1122,33 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       while ((P.wcells & 31) != window_mod()) ++P.wcells;
     // measured (cfg2 / cfg4 / cfg3): the chunk walk wins on bucketed batches (4.63 vs 5.03 ms),
     // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
-    const int form = observe_form() >= 0 ? observe_form() : (b->bucketed ? 0 : 1);
-    P.w = window_rows(b, observe_rows(P.wcells, form == 0));
+    const int form = observe_form() >= 0 ? observe_form() : 3;
+    if (form == 3) {
+      // bqsr_observe_rows: the most context copies whose rows still hold the
+      // batch's qual span (fewer rows than the span: the rest take the
+      // global atomics)
+      const int cw = window_cw(b, P.g), span = qual_span(b);
+      int best_rows = 0;
+      for (int nc = 16; nc >= 1; nc >>= 1) {
+        const int orow = rows_orow(nc, cw);
+        int qw = kQBins;
+        while (qw > 1 && rows_lds(qw, orow, P.wcells) > kLdsMax) --qw;
+        if (qw > best_rows) {
+          best_rows = qw;
+          P.nc = nc;
+          P.orow = orow;
+        }
+        if (qw >= span) {
+          P.nc = nc;
+          P.orow = orow;
+          best_rows = qw;
+          break;
+        }
+      }
+      P.w = window_rows(b, best_rows);
+    } else {
+      P.w = window_rows(b, observe_rows(P.wcells, form == 0));
+    }
     P.touched = t->touched();
     P.obs = t->obs();
     P.mm = t->mm();
@@ -1128,9 +1168,17 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = observe_lds(P.w.qw, P.wcells, form == 0);
+    const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, form == 0);
     P.lane_shift = lane_shift(b);
-    if (form == 0)
+    if (form == 3) {
+      const bool wide = b->dims.max_len > 128;
+      if (b->bucketed)
+        hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, false> : bqsr_observe_rows<2, false>), dim3(b->n_blocks),
+                           dim3(kBlockThreads), lds, s, P);
+      else
+        hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, true> : bqsr_observe_rows<2, true>), dim3(b->n_blocks),
+                           dim3(kBlockThreads), lds, s, P);
+    } else if (form == 0)
       hipLaunchKernelGGL(bqsr_observe_chunks, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else if (form == 2 || chunk_lanes(b->bucketed))
       hipLaunchKernelGGL((bqsr_observe_kernel<true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);

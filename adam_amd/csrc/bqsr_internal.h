@@ -201,6 +201,8 @@ struct ObserveParams {
   int32_t n_blocks;
   int32_t wcells;      // window row length: WinGeom::cw + 21
   int32_t lane_shift;  // lane-per-chunk kernels: log2(lanes per read)
+  int32_t orow;        // bqsr_observe_rows: LDS obs row words ([ctx copies 21 * nc][cycle cells cw][pad]), 0 mod 32
+  int32_t nc;          // bqsr_observe_rows: copies of a row's context counters (power of 2, <= 16)
 };
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----

@@ -1750,6 +1750,332 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
     for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
 }
 
+// ------------------------------------------------- observe: lane per offset --
+//
+// bqsr_observe_rows: a wavefront takes its reads one at a time and lane l the
+// read's offset o0 + l (rows of 64 offsets), so everything per read is
+// wavefront-uniform (SGPRs: read_lane fields), the read's trimmed range and
+// its masked / mismatch bits are 64-bit lane masks (the mismatch and masked
+// bits straight from the slot bitmap) used as exec masks, and per base a lane
+// has: its qual byte (one byte load per row), the two base codes of its
+// context (one u16 load: Q9's mirrored pair for reverse reads), the context
+// slot from a 512-B LDS table, and two LDS adds (RecalTable.+=,
+// RecalTable.scala:55-62 / ErrorCount.+= :195-201).  About 5 VALU per base
+// against 27 of the lane-per-read walk, and the adds no longer pile up:
+//  * the 64 cycle-cell adds of a row go to 64 consecutive cells of the
+//    lanes' qual rows; the LDS row length is 0 mod 32 words, so their banks
+//    are the cells' and differ whatever the quals (the walk's wavefront added
+//    to ONE cell per mate class in many rows: same-address and bank conflicts);
+//  * a row's context counters have `nc` copies (copy = lane & (nc - 1), the
+//    copies of one context adjacent), so lanes of one qual and context add
+//    to different words and nearly always different banks; the slab write
+//    sums the copies.
+// The obs window row is [context copies 21 * nc][cycle cells cw][pad]; the mm
+// window (mismatches, about 1 base in 100) and the slab keep the
+// [cycle cells cw][contexts 21][pad] rows of bqsr_window_reduce.  R rows of
+// G = 16 / R reads have their loads issued before the first is used.
+constexpr int kLutBytes = 512;
+
+__device__ __forceinline__ uint64_t lane_range(int lo, int hi) {  // lanes [lo, hi) of 64, clamped
+  lo = max(lo, 0);
+  hi = min(hi, 64);
+  if (lo >= hi) return 0ull;
+  const uint64_t h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  return h & ~((1ull << lo) - 1ull);
+}
+
+struct URead {  // one read, wavefront-uniform
+  int64_t r;
+  uint64_t slot;
+  int st, en, fl, cell0, dir, rg;
+};
+
+struct RowsLane {  // per-lane constants of bqsr_observe_rows
+  uint32_t kl;     // LDS address of (qual row q, context copy of the lane) = q * row4 + kl
+  uint32_t bound;  // kl + q * row4 < bound <=> q is a window row
+  uint32_t row4, nc4;
+  int32_t cyc_a, cyc_b;  // cycle cell term of the lane for dir +1 / -1, minus its copy offset
+  uint32_t sh_f, sh_e;   // bit offset of a lane's code pair in its u16 (forward / reverse, E even)
+  uint32_t vo_f, vo_re, vo_ro;  // byte offset of a lane's u16 (forward / reverse, E even / odd)
+};
+
+__device__ __forceinline__ URead uread(int j, uint32_t p_r, uint32_t p_slo, uint32_t p_shi, uint32_t p_se,
+                                       uint32_t p_fl, uint32_t p_rg) {
+  URead u;
+  u.r = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)p_r, j);
+  u.slot = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)p_shi, j) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)p_slo, j);
+  const uint32_t se = (uint32_t)__builtin_amdgcn_readlane((int)p_se, j);
+  const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)p_fl, j);
+  u.st = (int)(se & 0xFFFFu);
+  u.en = (int)(se >> 16);
+  u.fl = (int)(fl & 0x7FFFu);
+  u.dir = (fl & kPkRev) ? -1 : 1;
+  u.cell0 = (int)(fl >> 16);
+  u.rg = __builtin_amdgcn_readlane((int)p_rg, j);
+  return u;
+}
+
+// issue a row's loads: quals, context code pairs, the bitmap words of its slots
+__device__ __forceinline__ void row_load(const ObserveParams& P, const URead& u, int o0, int lane, const RowsLane& c,
+                                         uint32_t& q, uint32_t& pr, uint64_t& bw) {
+  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
+  const bool full = u.fl & kInfoObs;
+  if (__builtin_amdgcn_inverse_ballot_w64(valid)) q = P.rd.qual[u.slot + (uint64_t)(o0 + lane)];
+  if (!full) return;
+  const int kf = u.st - o0;  // the read's first visited offset: context 0, no pair needed
+  const uint64_t pm = valid & ~((kf >= 0 && kf < 64) ? (1ull << kf) : 0ull);
+  if (!(u.fl & kInfoNeg)) {
+    // offset o: codes o-1 (low nibble of the pair) and o
+    const uint8_t* b = P.rd.bases + (((u.slot + (uint64_t)o0) >> 1) - 1);
+    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + c.vo_f);
+  } else {
+    // offset o = st + k: codes at E - o and E - o + 1 (E = st + en - 1), complemented by the table (Q9)
+    const int e = u.st + u.en - 1;
+    const int64_t x = (int64_t)u.slot + e - o0;
+    const uint8_t* b = P.rd.bases + ((x - 63) >> 1);
+    const uint32_t vo = (e & 1) ? c.vo_ro : c.vo_re;
+    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + vo);
+  }
+  const uint64_t s0 = u.slot + (uint64_t)o0;
+  const int hi = min(u.en - o0, 64);
+  const int nw = (int)(((s0 & 31) + (uint64_t)hi + 31) >> 5);
+  if (lane < nw) bw = P.sbits[(s0 >> 5) + (uint64_t)lane];
+}
+
+template <bool kIdent>
+__device__ __forceinline__ void row_slow(const ObserveParams& P, const URead& u, int o, uint32_t q, uint32_t slot,
+                                         bool masked, bool mism, uint32_t* blk_hist) {
+  const int qs = (int)(int8_t)(uint8_t)q;
+  if (qs < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+    report(P.err, err_key((uint64_t)u.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+    return;
+  }
+  if (kIdent) atomicAdd(&blk_hist[qs], 1u);
+  const int cells = P.g.cells;
+  const int64_t key = (int64_t)qs + (int64_t)kMaxQ * u.rg;
+  atomicAdd((unsigned long long*)&P.touched[key], 1ull);
+  if (masked) return;
+  const int ccell = u.cell0 + u.dir * o, xcell = P.g.C + (int)slot;
+  atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
+  atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
+  if (mism) {
+    atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
+    atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+  }
+}
+
+typedef __attribute__((address_space(3))) const uint8_t* LdsBytes;
+
+template <bool kIdent>
+__device__ __forceinline__ void row_proc(const ObserveParams& P, const URead& u, int o0, int lane, const RowsLane& c,
+                                         uint32_t q, uint32_t pr, uint64_t bw, int rg_w, int c_lo, int cw, int q_lo,
+                                         int nc, uint32_t a_mm, uint32_t a_masked, uint32_t a_lut,
+                                         uint32_t* blk_hist) {
+  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
+  if (!(u.fl & kInfoObs)) {  // usable but failing at `en` (prep reported it): quals before it only checked
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_inverse_ballot_w64(valid) && q >= 128u);
+    if (bad && lane == 0) report(P.err, err_key((uint64_t)u.r, (uint32_t)(o0 + __builtin_ctzll(bad)), kRankTable,
+                                                BQSR_ERR_QUAL_RANGE));
+    return;
+  }
+  // masked (refPos None / outside the read / known site) and mismatch bits of the row's 64 slots
+  const uint32_t sh = (uint32_t)((u.slot + (uint64_t)o0) & 31);
+  const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bw, 0);
+  const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bw, 1);
+  const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bw, 2);
+  const uint32_t x0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bw >> 32), 0);
+  const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bw >> 32), 1);
+  const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bw >> 32), 2);
+  uint64_t masked, mism;
+  if (sh == 0) {
+    masked = (uint64_t)m0 | ((uint64_t)m1 << 32);
+    mism = (uint64_t)x0 | ((uint64_t)x1 << 32);
+  } else {  // 16-aligned slots: the row starts at bit 16
+    masked = (uint64_t)(m0 >> 16) | ((uint64_t)m1 << 16) | ((uint64_t)m2 << 48);
+    mism = (uint64_t)(x0 >> 16) | ((uint64_t)x1 << 16) | ((uint64_t)x2 << 48);
+  }
+  const bool neg = u.fl & kInfoNeg;
+  const uint32_t sh_p = (neg && !((u.st + u.en - 1) & 1)) ? c.sh_e : c.sh_f;
+  uint32_t pair = __builtin_amdgcn_ubfe(pr, sh_p, 8);
+  if (lane == u.st - o0) pair = 0xFFu;  // the read's first visited offset: context 0 (BaseContext k == 0)
+  const uint32_t slot = *(LdsBytes)(uintptr_t)(a_lut + (neg ? 256u : 0u) + pair);
+  const uint32_t trl = __mul24(q, c.row4) + c.kl;
+  const bool inrow = trl < c.bound && u.rg == rg_w;
+  const int cellrow = u.cell0 + u.dir * o0 - c_lo;  // window cycle cell of lane 0
+  const uint32_t cyc = trl + (uint32_t)(4 * (kCtxSlots * nc + cellrow) + (u.dir > 0 ? c.cyc_a : c.cyc_b));
+  const uint32_t ctx = __mul24(slot, c.nc4) + trl;
+  const uint64_t em = valid & ~masked;
+  if (inrow && __builtin_amdgcn_inverse_ballot_w64(em)) {
+    lds_add(cyc, 1u);
+    lds_add(ctx, 1u);
+  }
+  const uint64_t mx = em & mism;
+  if (mx) {
+    if (inrow && __builtin_amdgcn_inverse_ballot_w64(mx)) {
+      const uint32_t mrow = a_mm + 4u * __mul24(q - (uint32_t)q_lo, (uint32_t)P.wcells);
+      lds_add(mrow + 4u * (uint32_t)(cellrow + u.dir * lane), 1u);
+      lds_add(mrow + 4u * ((uint32_t)cw + slot), 1u);
+    }
+  }
+  const uint64_t mk = valid & masked;
+  if (mk) {
+    if (inrow && __builtin_amdgcn_inverse_ballot_w64(mk)) lds_add(a_masked + 4u * (q - (uint32_t)q_lo), 1u);
+  }
+  if (__builtin_amdgcn_ballot_w64(!inrow && __builtin_amdgcn_inverse_ballot_w64(valid))) {
+    if (!inrow && __builtin_amdgcn_inverse_ballot_w64(valid))
+      row_slow<kIdent>(P, u, o0 + lane, q, slot, (masked >> lane) & 1u, (mism >> lane) & 1u, blk_hist);
+  }
+}
+
+// LDS: [obs qw * orow][mm qw * wcells][masked qw][block hist 128][context tables 512 B]
+template <int R, bool kIdent>
+__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_rows(ObserveParams P) {
+  constexpr int G = 8 / R;  // reads per group: G * R rows' loads in flight per wavefront
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int qw = P.w.qw, wcells = P.wcells, orow = P.orow, nc = P.nc, L = P.g.L;
+  uint32_t* w_obs = (uint32_t*)smem;
+  uint32_t* w_mm = w_obs + qw * orow;
+  uint32_t* w_masked = w_mm + qw * wcells;
+  uint32_t* blk_hist = w_masked + qw;
+  uint8_t* lut = (uint8_t*)(blk_hist + kQBins);
+  const uint32_t a_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, a_mm = (uint32_t)(uintptr_t)(LdsWords)w_mm;
+  const uint32_t a_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
+  const uint32_t a_lut = (uint32_t)(uintptr_t)(LdsWords)(uint32_t*)lut;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
+  // context slot (ctx + 4) of a code pair: forward (previous | current << 4),
+  // reverse (the mirrored pair, complemented: BaseContext.simpleReverseComplement);
+  // 0xFF: a read's first visited offset (context 0)
+  for (int i = tid; i < kLutBytes; i += blockDim.x) {
+    const uint32_t e = (uint32_t)i & 255u, lo = e & 15u, hi = e >> 4;
+    lut[i] = (uint8_t)(e == 0xFFu ? 4u : i < 256 ? ctx_slot(lo, hi) : ctx_slot(comp_code(hi), comp_code(lo)));
+  }
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, P.n_blocks), wb = wg_begin(P.rd, blockIdx.x + 1, P.n_blocks);
+  const int q_lo = P.w.q_lo;
+  const int nk = order_keys(P.ord);
+  RowsLane c;
+  c.row4 = 4u * (uint32_t)orow;
+  c.nc4 = 4u * (uint32_t)nc;
+  const uint32_t lanepart = 4u * ((uint32_t)lane & (uint32_t)(nc - 1));
+  c.kl = a_obs + lanepart - (uint32_t)q_lo * c.row4;
+  c.bound = a_obs + (uint32_t)qw * c.row4;
+  c.cyc_a = 4 * lane - (int)lanepart;
+  c.cyc_b = -4 * lane - (int)lanepart;
+  c.sh_f = 4u * (uint32_t)((lane + 1) & 1);
+  c.sh_e = 4u * (uint32_t)(lane & 1);
+  c.vo_f = (uint32_t)((lane + 1) >> 1);
+  c.vo_re = 32u - (uint32_t)((lane + 1) >> 1);
+  c.vo_ro = 31u - (uint32_t)(lane >> 1);
+
+  for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
+    const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
+    const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
+    if (p0 >= wb) break;
+    if (p0 >= p1) continue;
+    const int rg_w = key_rg(P.ord, key, P.w.rg_lo);
+    const WinGeom gm = win_geom(P.ord, P.g, key);
+    for (int i = tid; i < qw * orow + qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
+    __syncthreads();
+    for (int64_t pb = p0 + 64 * wave; pb < p1; pb += 64 * kWaves) {
+      const bool live = pb + lane < p1;
+      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, pb + lane) : 0, live, L);
+      if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+      const bool act = live && (x.fl & (kInfoObs | kInfoObsCheck)) && x.en > x.st;
+      const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
+      const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
+      const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
+      const uint32_t p_rg = (uint32_t)x.rg;
+      uint64_t todo = __builtin_amdgcn_ballot_w64(act), tail = 0;
+      while (todo) {
+        URead u[G];
+        bool has[G];
+        int jj[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          has[g] = todo != 0;
+          jj[g] = has[g] ? (int)__builtin_ctzll(todo) : 0;
+          todo &= todo - 1;
+          u[g] = uread(jj[g], p_r, p_slo, p_shi, p_se, p_fl, p_rg);
+        }
+        uint32_t q[G][R], pr[G][R];
+        uint64_t bw[G][R];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            q[g][i] = 0;
+            pr[g][i] = 0;
+            bw[g][i] = 0;
+            const int o0 = (u[g].st & ~63) + 64 * i;
+            if (has[g] && o0 < u[g].en) row_load(P, u[g], o0, lane, c, q[g][i], pr[g][i], bw[g][i]);
+          }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            const int o0 = (u[g].st & ~63) + 64 * i;
+            if (has[g] && o0 < u[g].en)
+              row_proc<kIdent>(P, u[g], o0, lane, c, q[g][i], pr[g][i], bw[g][i], rg_w, gm.c_lo, gm.cw, q_lo, nc,
+                               a_mm, a_masked, a_lut, blk_hist);
+          }
+        // reads longer than the R rows held: their remaining rows below
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (has[g] && (u[g].st & ~63) + 64 * R < u[g].en) tail |= 1ull << jj[g];
+      }
+      // rows past the R held ones, one at a time
+      while (tail) {
+        const int j = (int)__builtin_ctzll(tail);
+        tail &= tail - 1;
+        const URead v = uread(j, p_r, p_slo, p_shi, p_se, p_fl, p_rg);
+        for (int o0 = (v.st & ~63) + 64 * R; o0 < v.en; o0 += 64) {
+          uint32_t q1 = 0, pr1 = 0;
+          uint64_t bw1 = 0;
+          row_load(P, v, o0, lane, c, q1, pr1, bw1);
+          row_proc<kIdent>(P, v, o0, lane, c, q1, pr1, bw1, rg_w, gm.c_lo, gm.cw, q_lo, nc, a_mm, a_masked, a_lut,
+                           blk_hist);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- the piece's window -> its slab ([cycle cells][contexts 21][pad] rows; the copies summed) ----
+    uint32_t* pb = P.part + (int64_t)(blockIdx.x + (kIdent ? 0 : key)) * P.part_stride;
+    const int cw = gm.cw, cx = kCtxSlots * nc;
+    for (int i = tid; i < qw * wcells; i += blockDim.x) {
+      const int t = i / wcells, cc = i - t * wcells;
+      const uint32_t* row = w_obs + t * orow;
+      uint32_t v = 0;
+      if (cc < cw) {
+        v = row[cx + cc];
+      } else if (cc < cw + kCtxSlots) {
+        const uint32_t* cp = row + (cc - cw) * nc;
+        for (int k = 0; k < nc; ++k) v += cp[k];
+      }
+      pb[i] = v;
+      pb[qw * wcells + i] = w_mm[i];
+    }
+    for (int slot = wave; slot < qw; slot += kWaves) {
+      uint32_t v = 0;
+      for (int cc = lane; cc < cw; cc += 64) v += w_obs[slot * orow + cx + cc];  // every unmasked base: one cycle cell
+      v = wave_sum(v);
+      if (lane == 0) {
+        const uint32_t tot = v + w_masked[slot];
+        pb[2 * qw * wcells + slot] = tot;
+        if (kIdent && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+      }
+    }
+    __syncthreads();
+  }
+  if (kIdent)
+    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
+}
+template __global__ void bqsr_observe_rows<2, true>(ObserveParams);
+template __global__ void bqsr_observe_rows<4, true>(ObserveParams);
+template __global__ void bqsr_observe_rows<2, false>(ObserveParams);
+template __global__ void bqsr_observe_rows<4, false>(ObserveParams);
+
 // Sum the pieces' window counts into the int64 table: one thread per (key,
 // window cell, slab group), over the slabs (w + key) of the workgroups whose
 // range meets the key's positions (the observe kernel's direct atomics have
