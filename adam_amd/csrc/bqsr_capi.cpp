@@ -219,8 +219,9 @@ int observe_form() {
   return v;
 }
 // bqsr_observe_rows' LDS: obs rows [qw][orow], mm rows [qw][wcells], masked, block histogram, context tables
-size_t rows_lds(int qw, int orow, int wcells) {
-  return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes;
+size_t rows_lds(int qw, int orow, int wcells, int hc) {
+  return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes +
+         (size_t)kWaves * qw * hc * 4;
 }
 int rows_orow(int nc, int cw) { return (kCtxSlots * nc + cw + 31) & ~31; }
 // prep's word stores (PrepParams::store_words); ADAM_BQSR_PREP_ATOMIC=1 turns them off (A/B)
@@ -304,6 +305,7 @@ struct bqsr_batch {
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
   int32_t n_blocks = 0;
+  bool hq_by_observe = false;  // bucketed: the observe kernel wrote the fold's read-order block histograms
   // read-group buckets (OrderDev): several read groups -> the per-base passes
   // walk the reads grouped by read group
   bool bucketed = false;
@@ -1124,27 +1126,24 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
     const int form = observe_form() >= 0 ? observe_form() : 3;
     if (form == 3) {
-      // bqsr_observe_rows: the most context copies whose rows still hold the
-      // batch's qual span (fewer rows than the span: the rest take the
-      // global atomics)
+      // bqsr_observe_rows: the most context copies (and, bucketed, fold
+      // histogram copies) whose rows still hold the batch's qual span (fewer
+      // rows than the span: the rest take the global atomics)
       const int cw = window_cw(b, P.g), span = qual_span(b);
       int best_rows = 0;
-      for (int nc = 16; nc >= 1; nc >>= 1) {
-        const int orow = rows_orow(nc, cw);
-        int qw = kQBins;
-        while (qw > 1 && rows_lds(qw, orow, P.wcells) > kLdsMax) --qw;
-        if (qw > best_rows) {
-          best_rows = qw;
-          P.nc = nc;
-          P.orow = orow;
+      for (int nc = 16; nc >= 1 && best_rows < span; nc >>= 1)
+        for (int hc = b->bucketed ? 16 : 0; hc >= (b->bucketed ? 1 : 0) && best_rows < span; hc = hc > 1 ? hc >> 1 : -1) {
+          const int orow = rows_orow(nc, cw);
+          int qw = kQBins;
+          while (qw > 1 && rows_lds(qw, orow, P.wcells, hc) > kLdsMax) --qw;
+          if (qw > best_rows) {
+            best_rows = qw;
+            P.nc = nc;
+            P.orow = orow;
+            P.hc = hc;
+          }
+          if (hc == 0) break;
         }
-        if (qw >= span) {
-          P.nc = nc;
-          P.orow = orow;
-          best_rows = qw;
-          break;
-        }
-      }
       P.w = window_rows(b, best_rows);
     } else {
       P.w = window_rows(b, observe_rows(P.wcells, form == 0));
@@ -1168,8 +1167,10 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, form == 0);
+    const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc) : observe_lds(P.w.qw, P.wcells, form == 0);
     P.lane_shift = lane_shift(b);
+    b->hq_by_observe = form == 3 && b->bucketed;
+    if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
     if (form == 3) {
       const bool wide = b->dims.max_len > 128;
       if (b->bucketed)
@@ -1192,7 +1193,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-    if (b->bucketed) {  // the observe kernel did not walk the fold's blocks: their histograms
+    if (b->bucketed && !b->hq_by_observe) {  // the observe kernel did not walk the fold's blocks: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
                          b->n_blocks, lane_shift(b), b->d_hq);

@@ -1865,13 +1865,46 @@ __device__ __forceinline__ void row_slow(const ObserveParams& P, const URead& u,
   }
 }
 
+
 typedef __attribute__((address_space(3))) const uint8_t* LdsBytes;
+
+// Bucketed batches: the fold needs per-block qual histograms of the folded
+// bases in READ order (fold blocks = read-order ranges, wg_begin), which the
+// bucketed walk does not follow.  Each wavefront keeps the histogram of the
+// block of the read it is on in LDS (`hc` copies, copy lane & (hc - 1)) and
+// adds it to hq_block with global atomics when a read of another block comes
+// (a key's reads come in runs of one sort chunk, nearly always one block).
+struct FoldHist {
+  uint32_t* wh;         // the wavefront's [qw][hc] counters
+  int64_t blk, lo, hi;  // its block and that block's reads [lo, hi)
+};
+__device__ __forceinline__ void hist_flush(const ObserveParams& P, FoldHist& h, int qw, int hc, int q_lo, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (h.blk >= 0)
+    for (int t = lane; t < qw; t += 64) {
+      uint32_t s = 0;
+      for (int k = 0; k < hc; ++k) {
+        s += h.wh[t * hc + k];
+        h.wh[t * hc + k] = 0;
+      }
+      if (s) atomicAdd(&P.hq_block[h.blk * kQBins + q_lo + t], s);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+__device__ __forceinline__ void hist_block(const ObserveParams& P, FoldHist& h, int64_t r, int qw, int hc, int q_lo,
+                                           int lane) {
+  if (r >= h.lo && r < h.hi) return;
+  hist_flush(P, h, qw, hc, q_lo, lane);
+  h.blk = wg_of(P.rd, r, P.n_blocks);
+  h.lo = wg_begin(P.rd, h.blk, P.n_blocks);
+  h.hi = wg_begin(P.rd, h.blk + 1, P.n_blocks);
+}
 
 template <bool kIdent>
 __device__ __forceinline__ void row_proc(const ObserveParams& P, const URead& u, int o0, int lane, const RowsLane& c,
                                          uint32_t q, uint32_t pr, uint64_t bw, int rg_w, int c_lo, int cw, int q_lo,
                                          int nc, uint32_t a_mm, uint32_t a_masked, uint32_t a_lut,
-                                         uint32_t* blk_hist) {
+                                         uint32_t* blk_hist, FoldHist& fh, int hc) {
   const uint64_t valid = lane_range(u.st - o0, u.en - o0);
   if (!(u.fl & kInfoObs)) {  // usable but failing at `en` (prep reported it): quals before it only checked
     const uint64_t bad = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_inverse_ballot_w64(valid) && q >= 128u);
@@ -1922,13 +1955,22 @@ __device__ __forceinline__ void row_proc(const ObserveParams& P, const URead& u,
   if (mk) {
     if (inrow && __builtin_amdgcn_inverse_ballot_w64(mk)) lds_add(a_masked + 4u * (q - (uint32_t)q_lo), 1u);
   }
+  if (!kIdent) {  // the folded bases' quals into the read's read-order block histogram
+    hist_block(P, fh, u.r, P.w.qw, hc, q_lo, lane);
+    if (inrow && __builtin_amdgcn_inverse_ballot_w64(valid))
+      lds_add((uint32_t)(uintptr_t)(LdsWords)fh.wh + 4u * (__mul24(q - (uint32_t)q_lo, (uint32_t)hc) +
+                                                        ((uint32_t)lane & (uint32_t)(hc - 1))), 1u);
+  }
   if (__builtin_amdgcn_ballot_w64(!inrow && __builtin_amdgcn_inverse_ballot_w64(valid))) {
-    if (!inrow && __builtin_amdgcn_inverse_ballot_w64(valid))
+    if (!inrow && __builtin_amdgcn_inverse_ballot_w64(valid)) {
       row_slow<kIdent>(P, u, o0 + lane, q, slot, (masked >> lane) & 1u, (mism >> lane) & 1u, blk_hist);
+      if (!kIdent && q < (uint32_t)kQBins) atomicAdd(&P.hq_block[fh.blk * kQBins + q], 1u);
+    }
   }
 }
 
 // LDS: [obs qw * orow][mm qw * wcells][masked qw][block hist 128][context tables 512 B]
+//      (bucketed: [per wavefront fold-block histograms kWaves * qw * hc])
 template <int R, bool kIdent>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_rows(ObserveParams P) {
   constexpr int G = 8 / R;  // reads per group: G * R rows' loads in flight per wavefront
@@ -1944,7 +1986,11 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_rows(ObserveParams
   const uint32_t a_lut = (uint32_t)(uintptr_t)(LdsWords)(uint32_t*)lut;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hc = kIdent ? 1 : P.hc;
+  FoldHist fh{(uint32_t*)(lut + kLutBytes) + wave * qw * hc, -1, 0, 0};
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
+  if (!kIdent)
+    for (int i = tid; i < kWaves * qw * hc; i += blockDim.x) ((uint32_t*)(lut + kLutBytes))[i] = 0;
   // context slot (ctx + 4) of a code pair: forward (previous | current << 4),
   // reverse (the mirrored pair, complemented: BaseContext.simpleReverseComplement);
   // 0xFF: a read's first visited offset (context 0)
@@ -2018,7 +2064,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_rows(ObserveParams
             const int o0 = (u[g].st & ~63) + 64 * i;
             if (has[g] && o0 < u[g].en)
               row_proc<kIdent>(P, u[g], o0, lane, c, q[g][i], pr[g][i], bw[g][i], rg_w, gm.c_lo, gm.cw, q_lo, nc,
-                               a_mm, a_masked, a_lut, blk_hist);
+                               a_mm, a_masked, a_lut, blk_hist, fh, hc);
           }
         // reads longer than the R rows held: their remaining rows below
 #pragma unroll
@@ -2035,9 +2081,14 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_rows(ObserveParams
           uint64_t bw1 = 0;
           row_load(P, v, o0, lane, c, q1, pr1, bw1);
           row_proc<kIdent>(P, v, o0, lane, c, q1, pr1, bw1, rg_w, gm.c_lo, gm.cw, q_lo, nc, a_mm, a_masked, a_lut,
-                           blk_hist);
+                           blk_hist, fh, hc);
         }
       }
+    }
+    if (!kIdent) {
+      hist_flush(P, fh, qw, hc, q_lo, lane);
+      fh.blk = -1;
+      fh.lo = fh.hi = 0;
     }
     __syncthreads();
     // ---- the piece's window -> its slab ([cycle cells][contexts 21][pad] rows; the copies summed) ----
@@ -2499,7 +2550,7 @@ __device__ __forceinline__ ChunkLoads apply_load(const ApplyParams& P, const Lan
 }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) const uint8_t* LdsBytes;
+
 
 // The checked path of a chunk's flagged offsets (RecalUtil.recalibrate with
 // the table's key checks), out of line: its table pointers stay out of the
