@@ -218,6 +218,15 @@ int observe_form() {
   }();
   return v;
 }
+// apply's form: ADAM_BQSR_APPLY=chunk (bqsr_apply_kernel, the lane-per-chunk walk); unset: rows
+// (bqsr_apply_rows, lane per offset) (1)
+int apply_form() {
+  static const int v = [] {
+    const char* e = getenv("ADAM_BQSR_APPLY");
+    return e && strcmp(e, "chunk") == 0 ? 0 : 1;
+  }();
+  return v;
+}
 // bqsr_observe_rows' LDS: obs rows [qw][orow], mm rows [qw][wcells], masked, block histogram, context tables
 size_t rows_lds(int qw, int orow, int wcells, int hc) {
   return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes +
@@ -404,7 +413,9 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
                         (const void*)bqsr_apply_kernel,
                         (const void*)bqsr_observe_chunks, (const void*)bqsr_observe_rows<2, true>,
                         (const void*)bqsr_observe_rows<4, true>, (const void*)bqsr_observe_rows<2, false>,
-                        (const void*)bqsr_observe_rows<4, false>})
+                        (const void*)bqsr_observe_rows<4, false>, (const void*)bqsr_apply_rows<2, true>,
+                        (const void*)bqsr_apply_rows<4, true>, (const void*)bqsr_apply_rows<2, false>,
+                        (const void*)bqsr_apply_rows<4, false>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -1532,6 +1543,39 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
+  if (apply_form() == 1) {
+    // bqsr_apply_rows: a packed char table per (read group, mate class) piece,
+    // rows of cwp = roundup(L, 32) cycle cells x 6 context groups (dwords)
+    P.cwp = (P.g.L + 31) & ~31;
+    const int n_pieces = b->bucketed ? b->n_keys : 2;
+    int qw = kQBins;
+    while (qw > 1 && (size_t)qw * 24 * P.cwp + 2 * kLutBytes > kLdsMax) --qw;
+    P.w = window_rows(b, qw);
+    const size_t need = (size_t)n_pieces * P.w.qw * 24 * P.cwp;
+    if (b->chars_bytes < need) {
+      if (b->d_chars) {
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(b->d_chars);
+        b->d_chars = nullptr;
+        b->chars_bytes = 0;
+      }
+      HIP_TRY(hipMalloc((void**)&b->d_chars, need));
+      b->chars_bytes = need;
+    }
+    P.chars = b->d_chars;
+    const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need / 4 + 255) / 256, (int64_t)ctx->n_cu * 16);
+    hipLaunchKernelGGL(bqsr_apply_chars_rows, dim3(cb), dim3(256), 0, s, P, n_pieces, (uint32_t*)b->d_chars);
+    const size_t lds = (size_t)P.w.qw * 24 * P.cwp + 2 * kLutBytes;
+    const bool wide = b->dims.max_len > 128;
+    if (b->bucketed)
+      hipLaunchKernelGGL((wide ? bqsr_apply_rows<4, false> : bqsr_apply_rows<2, false>), dim3(b->n_blocks),
+                         dim3(kBlockThreads), lds, s, P);
+    else
+      hipLaunchKernelGGL((wide ? bqsr_apply_rows<4, true> : bqsr_apply_rows<2, true>), dim3(b->n_blocks),
+                         dim3(kBlockThreads), lds, s, P);
+    HIP_TRY(hipGetLastError());
+    return ok();
+  }
   P.piece_stride = piece_bytes(P.w.qw, cw);
   const size_t need = (size_t)P.piece_stride * (size_t)b->n_keys + (size_t)b->n_keys * 16;  // + rowbad
   if (b->chars_bytes < need) {  // grows with the window; kept across calls

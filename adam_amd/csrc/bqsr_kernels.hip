@@ -2794,6 +2794,271 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   }  // pieces
 }
 
+// ------------------------------------------------- apply: lane per offset --
+//
+// bqsr_apply_rows: RecalUtil.recalibrate (RecalUtil.scala:31-42) with the
+// read-per-wavefront, lane-per-offset walk of bqsr_observe_rows.  A piece is
+// one read group and mate class (readPaired && secondOfPair decides the sign
+// of DiscreteCycle, so a piece's reads use one half of the cycle cells, L
+// cells): in read order a workgroup walks its reads twice, class 0 then
+// class 1, with that class's char table in LDS; bucketed batches have a
+// piece per key.  The char table is packed for the walk: dword (row q,
+// context group x >> 2, cycle cell c) holds the chars of contexts 4 (x >> 2)
+// .. +3, rows of cwp = roundup(L, 32) dwords, so the 64 lanes of a row --
+// consecutive cycle cells, any quals and contexts -- read 64 different banks'
+// worth of dwords in consecutive banks: no bank conflicts whatever the quals
+// (the lane-per-chunk walk's byte reads conflicted 60 % of their cycles).
+// A char 0 (key not in the table, a char above 0xFF) and quals outside the
+// rows take the exact checked path.
+
+// context slot (ctx + 4) of a code pair: forward (previous | current << 4),
+// reverse (the mirrored pair, complemented: BaseContext.simpleReverseComplement);
+// 0xFF: a read's first visited offset (context 0)
+__device__ __forceinline__ uint32_t pair_slot(uint32_t e, bool rev) {
+  const uint32_t lo = e & 15u, hi = e >> 4;
+  return e == 0xFFu ? 4u : !rev ? ctx_slot(lo, hi) : ctx_slot(comp_code(hi), comp_code(lo));
+}
+
+// a piece's packed char table: (class, read group, cycle cells c_lo .. c_lo + L - 1)
+struct ApplyRowsPiece {
+  int rg, c_lo, cls;
+};
+__device__ __forceinline__ ApplyRowsPiece apply_rows_piece(const ApplyParams& P, int pi) {
+  const bool ident = P.ord.perm == nullptr;
+  const int cls = ident ? pi : (pi & 1);
+  return ApplyRowsPiece{ident ? P.w.rg_lo : (pi >> 1), cls ? 0 : P.g.L + 1, cls};
+}
+
+// Every piece's packed char table, once per apply launch: a thread per dword.
+extern "C" __global__ void bqsr_apply_chars_rows(ApplyParams P, int32_t n_pieces, uint32_t* chars) {
+  const int qw = P.w.qw, q_lo = P.w.q_lo, cwp = P.cwp, L = P.g.L;
+  const int64_t per = (int64_t)qw * 6 * cwp;
+  const int64_t total = (int64_t)n_pieces * per;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int pi = (int)(t / per);
+    const int64_t e = t - (int64_t)pi * per;
+    const int row = (int)(e / (6 * cwp));
+    const int rem = (int)(e - (int64_t)row * 6 * cwp), xg = rem / cwp, c = rem - xg * cwp;
+    const ApplyRowsPiece pc = apply_rows_piece(P, pi);
+    const int64_t rq = (int64_t)pc.rg * kQBins + q_lo + row;
+    uint32_t v = 0;
+    if (c < L && pc.rg < P.n_rg && q_lo + row < kQBins && P.rq_ok[rq]) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int x = 4 * xg + k;
+        if (x >= kCtxSlots) break;
+        // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
+        const int32_t Q = phred_q(P.s1[rq * P.g.C + pc.c_lo + c] + P.d2[rq * kCtxSlots + x], P.qb_thr, P.qb_q, P.thr,
+                                  P.thr_qmin, P.thr_n);
+        const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+        v |= (code <= 0xFFu ? code : 0u) << (8 * k);
+      }
+    }
+    chars[t] = v;
+  }
+}
+
+// the checked path of one offset (apply_slow's body): key checks, QUAL_RANGE,
+// the exact char, exceptions above 0xFF; returns the output byte
+__device__ __forceinline__ uint32_t apply_one(const ApplyParams& P, const URead& u, int o, uint32_t qb, uint32_t xs) {
+  const int q = (int)(int8_t)(uint8_t)qb;
+  const int64_t key = (int64_t)q + (int64_t)kMaxQ * u.rg;
+  const int64_t gr = (key - 1) / kMaxQ;
+  const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
+  const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
+  if (!grp || !kok) {
+    report(P.err, err_key((uint64_t)u.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
+    return 0;
+  }
+  if (q < 0) {
+    report(P.err, err_key((uint64_t)u.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+    return 0;
+  }
+  if (!(u.fl & kInfoApp)) return 0;
+  const int64_t rq = (int64_t)u.rg * kQBins + q;
+  const int ccell = u.cell0 + u.dir * o;
+  const double p = P.s1[rq * P.g.C + ccell] + P.d2[rq * kCtxSlots + xs];
+  const int32_t Q = phred_q(p, P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
+  const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
+  if (code > 0xFFu) {
+    const unsigned long long e = atomicAdd(P.n_exc, 1ull);
+    if ((int64_t)e < P.max_exc) P.exc[e] = ((u.slot + (uint64_t)o) << 16) | code;
+  }
+  return code & 0xFFu;
+}
+
+struct ApplyLane {
+  uint32_t kt, bound, rowb;  // row address of qual q: q * rowb + kt (< bound: a table row)
+  uint32_t sh_f, sh_e, vo_f, vo_re, vo_ro;
+};
+
+__device__ __forceinline__ void apply_row_load(const ApplyParams& P, const URead& u, int o0, int lane,
+                                               const ApplyLane& c, uint32_t& q, uint32_t& pr) {
+  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
+  if (__builtin_amdgcn_inverse_ballot_w64(valid)) q = P.rd.qual[u.slot + (uint64_t)(o0 + lane)];
+  if (u.fl & kInfoPass) return;
+  const int kf = u.st - o0;
+  const uint64_t pm = valid & ~((kf >= 0 && kf < 64) ? (1ull << kf) : 0ull);
+  if (!(u.fl & kInfoNeg)) {
+    const uint8_t* b = P.rd.bases + (((u.slot + (uint64_t)o0) >> 1) - 1);
+    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + c.vo_f);
+  } else {
+    const int e = u.st + u.en - 1;
+    const int64_t x = (int64_t)u.slot + e - o0;
+    const uint8_t* b = P.rd.bases + ((x - 63) >> 1);
+    const uint32_t vo = (e & 1) ? c.vo_ro : c.vo_re;
+    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + vo);
+  }
+}
+
+typedef __attribute__((address_space(3))) const uint16_t* LdsHalfs;
+
+__device__ __forceinline__ void apply_row_proc(const ApplyParams& P, const URead& u, int o0, int lane,
+                                               const ApplyLane& c, uint32_t q, uint32_t pr, int rg_p, int c_lo,
+                                               uint32_t a_lut) {
+  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
+  uint8_t* op = P.out_qual + u.slot + (uint64_t)o0;
+  if (u.fl & kInfoPass) {  // the original chars: qual + 33 (Java byte -> char)
+    if (__builtin_amdgcn_inverse_ballot_w64(valid)) op[lane] = (uint8_t)(((q & 0x7Fu) + 0x21u) ^ (q & 0x80u));
+    return;
+  }
+  const bool neg = u.fl & kInfoNeg;
+  const uint32_t sh_p = (neg && !((u.st + u.en - 1) & 1)) ? c.sh_e : c.sh_f;
+  uint32_t pair = __builtin_amdgcn_ubfe(pr, sh_p, 8);
+  if (lane == u.st - o0) pair = 0xFFu;  // the read's first visited offset: context 0
+  // context slot and its packed-table offset ((x >> 2) * 4 cwp + (x & 3)): one u16 entry
+  const uint32_t xe = *(LdsHalfs)(uintptr_t)(a_lut + 2u * ((neg ? 256u : 0u) + pair));  // (no conflicts:
+  // pairs other than 0xFF and those of an N or other base lie in the first 64 entries)
+  const uint32_t at = __mul24(q, c.rowb) + c.kt;
+  const bool inrow = at < c.bound && u.rg == rg_p && (u.fl & kInfoApp);
+  const int cellrow = u.cell0 + u.dir * o0 - c_lo;
+  const uint32_t addr = at + (uint32_t)(4 * (cellrow + u.dir * lane)) + xe;
+  uint32_t ch = 0;
+  if (inrow && __builtin_amdgcn_inverse_ballot_w64(valid)) ch = *(LdsBytes)(uintptr_t)addr;
+  const bool fast = inrow && ch != 0u;
+  if (__builtin_amdgcn_ballot_w64(!fast && __builtin_amdgcn_inverse_ballot_w64(valid))) {
+    if (!fast && __builtin_amdgcn_inverse_ballot_w64(valid)) ch = apply_one(P, u, o0 + lane, q, pair_slot(pair, neg));
+  }
+  if ((u.fl & kInfoApp) && __builtin_amdgcn_inverse_ballot_w64(valid)) op[lane] = (uint8_t)ch;
+}
+
+// LDS: [the piece's packed char table qw * 6 * cwp dwords][context tables 2 * 256 u16]
+template <int R, bool kIdent>
+__global__ void __launch_bounds__(kBlockThreads) bqsr_apply_rows(ApplyParams P) {
+  constexpr int G = 8 / R;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int qw = P.w.qw, cwp = P.cwp, L = P.g.L;
+  uint32_t* tab = (uint32_t*)smem;
+  uint16_t* lut = (uint16_t*)(tab + (int64_t)qw * 6 * cwp);
+  const uint32_t a_tab = (uint32_t)(uintptr_t)(LdsWords)tab;
+  const uint32_t a_lut = (uint32_t)(uintptr_t)(LdsWords)(uint32_t*)lut;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // packed-table offset (x >> 2) * 4 cwp + (x & 3) of the context slot x of
+  // a code pair (forward / reverse; 0xFF: a read's first offset, context 0)
+  for (int i = tid; i < kLutBytes; i += blockDim.x) {
+    const uint32_t x = pair_slot((uint32_t)i & 255u, i >= 256);
+    lut[i] = (uint16_t)((x >> 2) * 4u * (uint32_t)cwp + (x & 3u));
+  }
+  ApplyLane c;
+  c.rowb = 4u * 6u * (uint32_t)cwp;
+  c.kt = a_tab - (uint32_t)P.w.q_lo * c.rowb;
+  c.bound = a_tab + (uint32_t)qw * c.rowb;
+  c.sh_f = 4u * (uint32_t)((lane + 1) & 1);
+  c.sh_e = 4u * (uint32_t)(lane & 1);
+  c.vo_f = (uint32_t)((lane + 1) >> 1);
+  c.vo_re = 32u - (uint32_t)((lane + 1) >> 1);
+  c.vo_ro = 31u - (uint32_t)(lane >> 1);
+  const int G_blocks = gridDim.x;
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, G_blocks), wb = wg_begin(P.rd, blockIdx.x + 1, G_blocks);
+  const int nk = order_keys(P.ord);
+  const int64_t tab_words = (int64_t)qw * 6 * cwp;
+  // pieces: read order -> class 0, class 1 over the workgroup's range; bucketed -> its keys
+  const int pi0 = kIdent ? 0 : (wa < wb ? key_at(P.ord, wa) : nk), pi1 = kIdent ? (wa < wb ? 2 : 0) : nk;
+  for (int pi = pi0; pi < pi1; ++pi) {
+    const int64_t p0 = kIdent ? wa : max(wa, key_begin(P.ord, P.rd.n_reads, pi));
+    const int64_t p1 = kIdent ? wb : min(wb, key_begin(P.ord, P.rd.n_reads, pi + 1));
+    if (p0 >= wb) break;
+    if (p0 >= p1) continue;
+    const ApplyRowsPiece pc = apply_rows_piece(P, pi);
+    __syncthreads();  // the previous piece is done with the table
+    {
+      const uint4* src = (const uint4*)(P.chars + (int64_t)pi * tab_words * 4);
+      uint4* dst = (uint4*)tab;
+      for (int64_t i = tid; i < tab_words / 4; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    for (int64_t pb = p0 + 64 * wave; pb < p1; pb += 64 * kWaves) {
+      const bool live = pb + lane < p1;
+      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, pb + lane) : 0, live, L);
+      const bool pass = x.fl & kInfoPass;
+      // read order: class pass 0 takes class-0 reads and every pass-through read
+      const bool mine = !kIdent || (pass ? pi == 0 : ((x.fl & kInfoSecond) ? 1 : 0) == pi);
+      if (live && mine) {
+        if (pass) {  // quality string passed through
+          P.out_start[x.r] = 0;
+          P.out_len[x.r] = (uint32_t)x.en;
+        } else {
+          P.out_start[x.r] = (uint32_t)x.st;
+          P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
+        }
+      }
+      const bool act = live && mine && (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) && x.en > x.st;
+      const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
+      const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
+      const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
+      const uint32_t p_rg = (uint32_t)x.rg;
+      uint64_t todo = __builtin_amdgcn_ballot_w64(act), tail = 0;
+      while (todo) {
+        URead u[G];
+        bool has[G];
+        int jj[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          has[g] = todo != 0;
+          jj[g] = has[g] ? (int)__builtin_ctzll(todo) : 0;
+          todo &= todo - 1;
+          u[g] = uread(jj[g], p_r, p_slo, p_shi, p_se, p_fl, p_rg);
+        }
+        uint32_t q[G][R], pr[G][R];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            q[g][i] = 0;
+            pr[g][i] = 0;
+            const int o0 = (u[g].st & ~63) + 64 * i;
+            if (has[g] && o0 < u[g].en) apply_row_load(P, u[g], o0, lane, c, q[g][i], pr[g][i]);
+          }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            const int o0 = (u[g].st & ~63) + 64 * i;
+            if (has[g] && o0 < u[g].en) apply_row_proc(P, u[g], o0, lane, c, q[g][i], pr[g][i], pc.rg, pc.c_lo, a_lut);
+          }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          if (has[g] && (u[g].st & ~63) + 64 * R < u[g].en) tail |= 1ull << jj[g];
+      }
+      while (tail) {
+        const int j = (int)__builtin_ctzll(tail);
+        tail &= tail - 1;
+        const URead v = uread(j, p_r, p_slo, p_shi, p_se, p_fl, p_rg);
+        for (int o0 = (v.st & ~63) + 64 * R; o0 < v.en; o0 += 64) {
+          uint32_t q1 = 0, pr1 = 0;
+          apply_row_load(P, v, o0, lane, c, q1, pr1);
+          apply_row_proc(P, v, o0, lane, c, q1, pr1, pc.rg, pc.c_lo, a_lut);
+        }
+      }
+    }
+  }
+}
+template __global__ void bqsr_apply_rows<2, true>(ApplyParams);
+template __global__ void bqsr_apply_rows<4, true>(ApplyParams);
+template __global__ void bqsr_apply_rows<2, false>(ApplyParams);
+template __global__ void bqsr_apply_rows<4, false>(ApplyParams);
+
 template __global__ void bqsr_observe_kernel<false>(ObserveParams);
 template __global__ void bqsr_observe_kernel<true>(ObserveParams);
 
