@@ -1723,11 +1723,42 @@ bqsr_status bqsr_job_errors_import_async(bqsr_batch* b, const int64_t* src_devic
   return ok();
 }
 
+// Snapshots for pipelined jobs (adam_amd/stream.py): the batch's status words
+// of a job copied on `stream` into pinned slot `slot`, read after the caller
+// has waited for the stream past that point; the next job may already reset
+// the live words.
+bqsr_status bqsr_job_status_async(bqsr_batch* b, bqsr_lut* L, int32_t slot, void* stream) {
+  if (!b || !L || slot < 0 || slot >= kStatusSlots) return fail(BQSR_ERR_INVALID_ARG, "null / bad slot");
+  HIP_TRY(hipSetDevice(b->ctx->device));
+  if (!b->h_status)
+    HIP_TRY(hipHostMalloc((void**)&b->h_status, kJobStatusWords * 8 * (1 + kStatusSlots), hipHostMallocDefault));
+  hipLaunchKernelGGL(bqsr_job_status_kernel, dim3(1), dim3(64), 0, S(stream), (const unsigned long long*)b->d_err,
+                     (const double*)b->d_em, (const FinalOut*)L->d_out, b->h_status + kJobStatusWords * (1 + slot));
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+bqsr_status bqsr_job_status_get(const bqsr_batch* b, int32_t slot, int32_t part, double* em, int64_t* n_exceptions) {
+  if (!b || !b->h_status || slot < 0 || slot >= kStatusSlots || part < 0 || part > 2)
+    return fail(BQSR_ERR_INVALID_ARG, "no snapshot / bad slot or part");
+  const uint64_t* h = b->h_status + kJobStatusWords * (1 + slot);
+  if (em) std::memcpy(em, h + kErrWords, 8);
+  if (n_exceptions) *n_exceptions = (int64_t)h[kNExc];
+  if (part == 0) return from_err_key(h[kErrObs], 0);
+  if (part == 1) {
+    FinalOut fo;
+    std::memcpy(&fo, h + kErrWords + 1, sizeof(FinalOut));
+    return fo.any_key ? ok() : fail(BQSR_ERR_EMPTY_TABLE, "empty.reduceLeft: no usable base was observed");
+  }
+  return from_err_key(std::min(h[kErrAppPrep], h[kErrAppKern]), 0);
+}
+
 bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_exceptions, void* stream) {
   if (!b || !L) return fail(BQSR_ERR_INVALID_ARG, "null");
   HIP_TRY(hipSetDevice(b->ctx->device));
   hipStream_t s = S(stream);
-  if (!b->h_status) HIP_TRY(hipHostMalloc((void**)&b->h_status, kJobStatusWords * 8, hipHostMallocDefault));
+  if (!b->h_status)
+    HIP_TRY(hipHostMalloc((void**)&b->h_status, kJobStatusWords * 8 * (1 + kStatusSlots), hipHostMallocDefault));
   hipLaunchKernelGGL(bqsr_job_status_kernel, dim3(1), dim3(64), 0, s, (const unsigned long long*)b->d_err,
                      (const double*)b->d_em, (const FinalOut*)L->d_out, b->h_status);
   HIP_TRY(hipGetLastError());

@@ -99,6 +99,7 @@ enum : uint32_t {
 // error words of a batch
 enum { kErrObs = 0, kErrAppPrep = 1, kErrAppKern = 2, kNExc = 3, kErrWords = 4 };
 constexpr int kJobStatusWords = 16;  // bqsr_job_result: error words, em, FinalOut
+constexpr int kStatusSlots = 4;      // bqsr_job_status_async: snapshots of pipelined jobs
 
 // ---- known sites -------------------------------------------------------------
 struct SitesDev {

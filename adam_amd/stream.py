@@ -17,8 +17,16 @@ hands over per Spark partition).  One job (``StreamedShard.run``):
    the device (adam_amd/distributed.py, ``bqsr_em_fold_async``).
 3. finalize on the device, then apply partition by partition from the
    partitions still resident in HBM, each partition's recalibrated qualities
-   (and per-read start / length) copied back to pinned host memory on the copy
-   stream while the next partition is applied (double-buffered device output).
+   (and per-read start / length) copied back to pinned host memory on the
+   download stream while the next partition is applied (double-buffered
+   device output).
+4. the job's status words snapshot into pinned memory (``bqsr_job_status_async``).
+
+Jobs pipeline over both link directions: uploads run on a stream of their
+own, and job k+1's upload of partition i starts as soon as job k's apply is
+done with it, while job k's results still move back on the download stream.
+``finish`` checks a job's snapshot (errors in the reference's order) after
+the next job has been enqueued.
 
 Reference: RecalibrateBaseQualities.scala:34-76 (computeTable / applyTable over
 an RDD's partitions).  Only the HIP library computes; this module orders
@@ -102,30 +110,47 @@ class StreamedShard:
         self.max_exc = max_exc
         self.counts = None  # every rank's partition count (exchanged on the first multi-rank job)
         self.em = torch.zeros(max(1, len(self.batches)), dtype=torch.float64, device=dev)
-        self.copy_stream = torch.cuda.Stream(dev)
-        n = len(self.batches)
+        # H2D and D2H on copy streams of their own: a job's uploads overlap
+        # the previous job's downloads (both link directions)
+        self.up_stream = torch.cuda.Stream(dev)
+        self.dn_stream = torch.cuda.Stream(dev)
+        self.copy_stream = self.dn_stream
         self.ev_up = [torch.cuda.Event() for _ in range(n)]
         self.ev_ap = [torch.cuda.Event() for _ in range(n)]
         self.ev_dl = [torch.cuda.Event() for _ in range(2)]
+        self.dl_used = [False, False]
+        self.ev_status = [torch.cuda.Event() for _ in range(2)]
+        self.ev_done = [torch.cuda.Event() for _ in range(2)]
         self.ev_apply_t = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                            for _ in range(n)]
         self.lut = ctypes.c_void_p()
+        self.jobs = 0
+        self.pending: List[int] = []  # status slots of jobs run but not finished, oldest first
 
     def run(self, table_handle, table_words=None, record_apply: bool = False):
-        """One whole job over the shard; returns the job's expectedMismatch
-        tensor (device).  Results land in host_qual / host_start / host_len
-        once the compute and copy streams are synchronised (``finish``)."""
+        """Enqueue one whole job over the shard (no host sync); returns the
+        job's expectedMismatch tensor (device).  Jobs pipeline: this job's
+        uploads start as soon as the previous job's apply is done with each
+        partition, while its results still move back on the other copy
+        stream.  At most two jobs may be pending; ``finish`` raises a job's
+        errors and makes its results (host_qual / host_start / host_len)
+        valid until the next ``run``."""
         torch, L = self.torch, self.L
+        if len(self.pending) >= 2:
+            raise RuntimeError("two jobs pending: finish() one first")
         comp = torch.cuda.current_stream(self.dev)
-        copy = self.copy_stream
+        up, dn = self.up_stream, self.dn_stream
         sp = ctypes.c_void_p(comp.cuda_stream)
-        cp = ctypes.c_void_p(copy.cuda_stream)
+        upp = ctypes.c_void_p(up.cuda_stream)
         ctx = self.ctx.handle
+        slot = self.jobs & 1
         check(L.bqsr_table_zero_async(table_handle, sp))
         # (1) stream the partitions in, observing each as it lands
         for i, bh in enumerate(self.batches):
-            check(L.bqsr_batch_upload_async(bh, self.staged[i], cp))
-            self.ev_up[i].record(copy)
+            if self.jobs:
+                up.wait_event(self.ev_ap[i])  # the previous job's apply is done with partition i's columns
+            check(L.bqsr_batch_upload_async(bh, self.staged[i], upp))
+            self.ev_up[i].record(up)
             comp.wait_event(self.ev_up[i])
             check(L.bqsr_observe_async(ctx, bh, self.sites, table_handle, sp))
             check(L.bqsr_batch_em_copy_async(bh, ctypes.c_void_p(self.em.data_ptr() + 8 * i), sp))
@@ -143,7 +168,7 @@ class StreamedShard:
         # (3) apply from the resident partitions, results streamed back
         for i, bh in enumerate(self.batches):
             k = i & 1
-            if i >= 2:
+            if self.dl_used[k]:
                 comp.wait_event(self.ev_dl[k])  # output buffer k drained to the host
             if record_apply:
                 self.ev_apply_t[i][0].record(comp)
@@ -155,41 +180,53 @@ class StreamedShard:
             if record_apply:
                 self.ev_apply_t[i][1].record(comp)
             self.ev_ap[i].record(comp)
-            copy.wait_event(self.ev_ap[i])
-            with torch.cuda.stream(copy):
+            dn.wait_event(self.ev_ap[i])
+            with torch.cuda.stream(dn):
                 ns, nr = self.n_slots[i], max(1, self.n_reads[i])
                 self.host_qual[i][:ns].copy_(self.out_qual[k][:ns], non_blocking=True)
                 self.host_start[i][:nr].copy_(self.out_start[k][:nr], non_blocking=True)
                 self.host_len[i][:nr].copy_(self.out_len[k][:nr], non_blocking=True)
-            self.ev_dl[k].record(copy)
+                e0 = i * self.max_exc
+                self.host_exc[e0:e0 + self.max_exc].copy_(self.exc[e0:e0 + self.max_exc], non_blocking=True)
+            self.ev_dl[k].record(dn)
+            self.dl_used[k] = True
+        # (4) several ranks: the job's first error in global read order on every rank
+        if D._multi():
+            self._exchange_errors(sp)
+        # (5) the job's status, snapshot for `finish` (the next job resets the live words)
+        for bh in self.batches:
+            check(L.bqsr_job_status_async(bh, self.lut, slot, sp))
+        self.ev_status[slot].record(comp)
+        self.ev_done[slot].record(dn)
+        self.pending.append(slot)
+        self.jobs += 1
         return acc
 
     def finish(self):
-        """Synchronise, then raise the first error in the reference's order
-        (observe errors partition by partition, finalize, apply).  Returns the
-        number of recalibrated chars above 0xFF (Q14); their codes are in
-        ``exceptions(i)`` and ``qual_chars`` applies them."""
+        """Wait for the oldest pending job, then raise its first error in the
+        reference's order (observe errors partition by partition, finalize,
+        apply).  Returns the number of recalibrated chars above 0xFF (Q14);
+        their codes are in ``exceptions(i)`` and ``qual_chars`` applies them."""
         L = self.L
-        comp = self.torch.cuda.current_stream(self.dev)
-        sp = ctypes.c_void_p(comp.cuda_stream)
-        if D._multi():
-            self._exchange_errors(sp)
+        if not self.pending:
+            raise RuntimeError("no job pending")
+        slot = self.pending.pop(0)
+        self.ev_status[slot].synchronize()
+        self.ev_done[slot].synchronize()
         em = ctypes.c_double()
-        for bh in self.batches:
-            check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
-        check(L.bqsr_finalize_result(self.lut, sp))
         nexc = ctypes.c_int64()
+        for bh in self.batches:
+            check(L.bqsr_job_status_get(bh, slot, 0, ctypes.byref(em), ctypes.byref(nexc)))
+        if self.batches:
+            check(L.bqsr_job_status_get(self.batches[0], slot, 1, ctypes.byref(em), ctypes.byref(nexc)))
         total = 0
         for i, bh in enumerate(self.batches):
-            check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
+            check(L.bqsr_job_status_get(bh, slot, 2, ctypes.byref(em), ctypes.byref(nexc)))
             self.n_exc[i] = int(nexc.value)
             if self.n_exc[i] > self.max_exc:
                 raise _capi.BQSRError(_capi.UNSUPPORTED, "partition %d: %d chars above 0xFF exceed the exception "
                                       "list (%d)" % (i, self.n_exc[i], self.max_exc))
             total += self.n_exc[i]
-        self.copy_stream.synchronize()
-        if total:  # rare: only then are the exception lists copied back
-            self.host_exc.copy_(self.exc.cpu())
         return total
 
     def _exchange_errors(self, sp):

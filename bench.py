@@ -340,23 +340,29 @@ def main_stream(args, cfg, world, rank, dev, ctx):
     torch.cuda.synchronize()
 
     def step(record):
+        # jobs pipeline (stream.py): this job's uploads overlap the previous
+        # job's downloads; its status is checked one job later
         sh.run(th, table_t if world > 1 else None, record_apply=record)
-        sh.finish()
+        if len(sh.pending) > 1:
+            sh.finish()
 
     for _ in range(args.warmup):
         step(False)
+    while sh.pending:
+        sh.finish()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    apply_ms = []
-    for _ in range(args.steps):
-        step(True)
-        apply_ms.append(sh.apply_ms())
+    for i in range(args.steps):
+        step(i == args.steps - 1)
+    while sh.pending:  # every job's results on the host, every status checked
+        sh.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    apply_ms = [sh.apply_ms()]
     n_bases = sh.n_bases
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -375,7 +381,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         alg_part = 2.5 * n_bases / parts_n + 16 * R_part
         achieved = alg_part / (am * 1e-3) / 1e9 if am else None
         h2d = sh.staged_bytes
-        d2h = sum(sh.n_slots) + 8 * n_reads
+        d2h = sum(sh.n_slots) + 8 * n_reads + 8 * sh.max_exc * parts_n
         line = {
             "metric": METRIC,
             "value": args.steps * total_bases / elapsed,
@@ -418,10 +424,63 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         if world == 1 and not args.no_cpu_baseline:
             args.cpu_reads = min(args.cpu_reads, 2_000_000)
             line["cpu_baseline"] = cpu_baseline(args, cfg, first, None)[0]
+        if world == 1 and not args.no_parity:
+            line["parity"] = parity_stream(cfg, sh, table_t, n_reads, pr, rank, dims)
         print(json.dumps(line), flush=True)
     sh.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def parity_stream(cfg, sh, table_t, n_reads, pr, rank, dims):
+    """cfg5: the last job's table words and expectedMismatch against the oracle
+    over every partition (each observed as one partition, the tables summed
+    and the expectedMismatch values folded in partition order), and the
+    recalibrated chars of the first and last partitions (outside the timed
+    region; partitions regenerated from their seeds)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from adam_amd import synth
+    t = time.perf_counter()
+    cores, _ = host_cores()
+    d = O.Dims(dims.n_rg, dims.max_len)
+    words = np.zeros(O.table_words(d), dtype=np.int64)
+    em = 0.0
+    starts = list(range(0, n_reads, pr))
+    sampled = {0, len(starts) - 1}
+    keep = {}
+    for i, r0 in enumerate(starts):
+        part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"], cfg["seed"] + 1_000_003 * rank + 7919 * i)
+        w, e = O.observe_mt(part, None, d, n_parts=cores, nthreads=cores, fold1=True)
+        words += w
+        em = em + e
+        if i in sampled:
+            keep[i] = part
+        del part
+    gw = table_t.cpu().numpy()
+    gem = float(sh._em_keep.cpu()[0])
+    table_ok = bool(np.array_equal(gw, words))
+    em_ok = gem == em
+    bad_total, checked, first_bad = 0, 0, -1
+    for i, part in sorted(keep.items()):
+        out, out_len = O.apply_mt(part, d, words, em, n_parts=cores, nthreads=cores)
+        ns, nr = sh.n_slots[i], sh.n_reads[i]
+        exc = sh.host_exc[i * sh.max_exc: i * sh.max_exc + sh.n_exc[i]].numpy()
+        bad, first = O.compare_device_output(part, out, out_len, sh.host_qual[i].numpy()[:ns],
+                                             sh.host_start[i].numpy()[:nr], sh.host_len[i].numpy()[:nr],
+                                             exc if len(exc) else None, nthreads=cores)
+        bad_total += bad
+        checked += part.n_reads
+        if bad and first_bad < 0:
+            first_bad = sum(sh.n_reads[:i]) + first
+    return {"checked": True, "ok": bool(table_ok and em_ok and bad_total == 0), "table_words_equal": table_ok,
+            "expected_mismatch_equal": bool(em_ok), "expected_mismatch": float(gem).hex(),
+            "reads_checked": checked, "partitions_checked": sorted(keep), "reads_differing": bad_total,
+            "first_differing_read": first_bad,
+            "against": "oracle/ (C++ restatement of ADAM BQSR): table and expectedMismatch over every partition "
+                       "(merged in partition order), chars of the first and last partitions",
+            "check_s": time.perf_counter() - t}
 
 
 def host_cores():

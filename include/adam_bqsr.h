@@ -346,6 +346,16 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* l, double* expected_mismatc
  * two int64 at dst_device (no error = INT64_MAX); the caller all-reduces them
  * with MIN over the ranks and imports the result, so bqsr_job_result raises
  * the same error (global read index) on every rank. */
+/* Pipelined jobs (streamed partitions, adam_amd/stream.py): the batch's
+ * status of one job -- observe error, expectedMismatch, finalize's
+ * EMPTY_TABLE, apply error, exception count -- snapshot on `stream` into
+ * pinned slot `slot` (< 4) without a sync; after the caller has waited for
+ * the stream past that point, bqsr_job_status_get returns the part's status
+ * (0 observe, 1 finalize, 2 apply), so the job's errors are raised in the
+ * reference's order while the next job already runs. */
+bqsr_status bqsr_job_status_async(bqsr_batch* b, bqsr_lut* l, int32_t slot, void* stream);
+bqsr_status bqsr_job_status_get(const bqsr_batch* b, int32_t slot, int32_t part, double* expected_mismatch,
+                                int64_t* n_exceptions);
 bqsr_status bqsr_job_errors_export_async(bqsr_batch* b, int64_t read_base, int64_t* dst_device, void* stream);
 bqsr_status bqsr_job_errors_import_async(bqsr_batch* b, const int64_t* src_device, void* stream);
 
