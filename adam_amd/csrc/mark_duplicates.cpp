@@ -1,4 +1,6 @@
-// MarkDuplicates (include/adam_sam.h) on the host.
+// MarkDuplicates (include/adam_sam.h) on the host: the
+// drop-in for host columns (bqsr_mark_duplicates, the JNI records case) and
+// the fallback of the device path (mark_duplicates.hip).
 //
 // adam-core/.../rdd/MarkDuplicates.scala:24-111 restated over columns:
 //   SingleReadBucket (models/SingleReadBucket.scala:27-37): reads grouped by
@@ -227,8 +229,10 @@ bqsr_status bqsr_mark_duplicates(const bqsr_dup_reads* R, uint8_t* dup_out) {
   return ok();
 }
 
-bqsr_status bqsr_sam_mark_duplicates(bqsr_sam* s, int64_t* n_duplicates) {
-  if (!s) return fail(BQSR_ERR_INVALID_ARG, "null");
+namespace {
+// the host path of bqsr_sam_mark_duplicates (mark_duplicates.hip's fallback):
+// the columns copied back, bqsr_mark_duplicates, FLAG copied up
+bqsr_status mark_duplicates_host(bqsr_sam* s, int64_t* n_duplicates) {
   HIP_TRY(hipSetDevice(s->ctx->device));
   const size_t n = (size_t)s->n_reads;
   std::vector<uint32_t> flags(n), raw(n);
@@ -281,3 +285,6 @@ bqsr_status bqsr_sam_mark_duplicates(bqsr_sam* s, int64_t* n_duplicates) {
   if (n_duplicates) *n_duplicates = nd;
   return ok();
 }
+}  // namespace
+
+#include "mark_duplicates.hip"

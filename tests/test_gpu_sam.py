@@ -282,3 +282,53 @@ def test_device_parse_reference_fixture_counts(name, count):
     """AdamContextSuite.scala:32-43 / AdamRDDFunctionsSuite.scala:539-547:
     the reference loads 200, 20 and 200 records from these files."""
     assert SamText.read(os.path.join(GOLD, name)).batch().n_reads == count
+
+
+def _dup_sam(n_reads, seed, contig_len, n_rg=2):
+    """Synthetic SAM with pairs (mates share a QNAME) and fragments stacked on
+    few positions, secondary and unmapped reads included."""
+    b = synth.generate(n_reads, (60, 80), n_rg, seed, contig_len=contig_len, p_duplicate=0.0, p_secondary=0.05,
+                       p_unmapped=0.05)
+    text = sam_text(b, n_rg=n_rg, qname="q")
+    lines = text.split(b"\n")
+    head = [l for l in lines if l.startswith(b"@")]
+    body = [l for l in lines if l and not l.startswith(b"@")]
+    for k in range(1, len(body), 3):  # two reads of every three share a QNAME
+        f = body[k].split(b"\t")
+        f[0] = body[k - 1].split(b"\t")[0]
+        body[k] = b"\t".join(f)
+    return b"\n".join(head + body) + b"\n"
+
+
+def _host_markdup(text, n_rg):
+    """bqsr_mark_duplicates (the host path) over the same records' columns."""
+    from adam_amd import sam as S
+    s = SamText(text)
+    try:
+        batch = s.batch()
+    finally:
+        s.close()
+    recs = _records(text)
+    n = batch.n_reads
+    names = [f[0].decode("latin-1") for f in recs]
+    libs = [("lib%d" % (int(batch.rg_id[r]) % 2)) if int(batch.flags[r]) & R.F_HAS_RG else None for r in range(n)]
+    mate = [int(f[1]) != 0 and bool(int(f[1]) & 1) and not int(f[1]) & 8 for f in recs]
+    return S.mark_duplicates(names, libs, batch.flags, mate, batch.rg_id, batch.ref_index, batch.start,
+                             batch.qual_offset, batch.qual, batch.cigar_offset, batch.cigar)
+
+
+@pytest.mark.parametrize("n_reads,contig_len", [(3000, 2000), (60000, 20000), (200000, 1_000_000)])
+def test_mark_duplicates_device_equals_host(n_reads, contig_len):
+    """The device MarkDuplicates (sorts + segmented passes) flags exactly the
+    reads the host path flags (MarkDuplicates.scala:24-111, ties by first
+    appearance in both)."""
+    text = _dup_sam(n_reads, 700 + n_reads, contig_len)
+    want = _host_markdup(text, 2)
+    s = SamText(text)
+    try:
+        nd = s.mark_duplicates()
+        got = (s.batch().flags & R.F_DUPLICATE) != 0
+    finally:
+        s.close()
+    assert nd == int(want.sum()) > 0
+    assert np.array_equal(got, want), int(np.nonzero(got != want)[0][0])
