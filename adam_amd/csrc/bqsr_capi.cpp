@@ -218,12 +218,12 @@ int observe_form() {
   }();
   return v;
 }
-// apply's form: ADAM_BQSR_APPLY=chunk (bqsr_apply_kernel, the lane-per-chunk walk); unset: rows
-// (bqsr_apply_rows, lane per offset) (1)
+// apply's form: ADAM_BQSR_APPLY=rows (bqsr_apply_rows, lane per offset: SALU-bound, 5.9 ms cfg2 in
+// round 3) (1); unset: the lane-per-chunk walk (bqsr_apply_kernel) (0)
 int apply_form() {
   static const int v = [] {
     const char* e = getenv("ADAM_BQSR_APPLY");
-    return e && strcmp(e, "chunk") == 0 ? 0 : 1;
+    return e && strcmp(e, "rows") == 0 ? 1 : 0;
   }();
   return v;
 }
@@ -1135,7 +1135,10 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       while ((P.wcells & 31) != window_mod()) ++P.wcells;
     // measured (cfg2 / cfg4 / cfg3): the chunk walk wins on bucketed batches (4.63 vs 5.03 ms),
     // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
-    const int form = observe_form() >= 0 ? observe_form() : 3;
+    // measured (round 3, cfg2 / cfg4): the lane-per-offset rows kernel is SALU-bound (2.7e9 scalar
+    // instructions per cfg2 launch, 6.0 ms) -- opt-in only; the chunk walk wins on bucketed batches
+    // (4.63 vs 5.03 ms cfg4), the lane per read on read order (1.00 vs 1.16 ms cfg2)
+    const int form = observe_form() >= 0 ? observe_form() : (b->bucketed ? 0 : 1);
     if (form == 3) {
       // bqsr_observe_rows: the most context copies (and, bucketed, fold
       // histogram copies) whose rows still hold the batch's qual span (fewer
