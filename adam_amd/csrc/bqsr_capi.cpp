@@ -1781,4 +1781,5 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
 
 // ---- SAM ingest / output (include/adam_sam.h) ----
 #include "sam_ingest.hip"
+#include "bam_ingest.hip"
 #include "mark_duplicates.cpp"

@@ -717,6 +717,7 @@ struct bqsr_sam {
   uint64_t* line_span = nullptr;
   uint64_t* qual_span = nullptr;
   bool dup_marked = false;  // bqsr_sam_mark_duplicates ran: FLAG 0x400 rewritten on output
+  bool from_bam = false;    // bqsr_bam_parse: d_text holds the BAM records (no SAM text to rewrite)
   std::vector<void*> allocs;
   ~bqsr_sam() {
     for (void* p : allocs) (void)hipFree(p);
@@ -793,15 +794,19 @@ const char* kSamErrors[] = {"ok", "fewer than 11 fields", "optional field withou
                             "POS is not an integer", "malformed CIGAR", "header line after the first record",
                             "'\\r' inside a line"};
 
-}  // namespace
-
-bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void* stream, bqsr_sam** out) {
-  if (!ctx || !out || n < 0 || (n > 0 && !text)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_parse: bad arguments");
-  HIP_TRY(hipSetDevice(ctx->device));
-  hipStream_t s = S(stream);
-  // ---- header (host): @RG IDs sorted (RecordGroupDictionary), @SQ names ----
+// the SAM header text (SAM input, or a BAM's l_text): @RG IDs sorted into
+// the RecordGroupDictionary (RecordGroupDictionary.scala:36-43) with their LB,
+// @SQ names -> header index; body = where the records start
+struct SamHeader {
+  int64_t body = 0;
   std::vector<std::string> rg_names, sq_names;
-  std::map<std::string, std::pair<bool, std::string>> rg_lb;  // the last @RG line of an ID
+  std::map<std::string, std::pair<bool, std::string>> rg_lb;
+  HostNames rgh, sqh;
+};
+bqsr_status parse_sam_header(const char* text, int64_t n, SamHeader* H) {
+  std::vector<std::string>& rg_names = H->rg_names;
+  std::vector<std::string>& sq_names = H->sq_names;
+  std::map<std::string, std::pair<bool, std::string>>& rg_lb = H->rg_lb;  // the last @RG line of an ID
   int64_t p = 0;
   while (p < n) {
     const char* nlp = (const char*)memchr(text + p, '\n', (size_t)(n - p));
@@ -849,9 +854,10 @@ bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void*
     }
     p = e0 + 1;
   }
-  const int64_t body = std::min(p, n);
+  H->body = std::min(p, n);
   std::sort(rg_names.begin(), rg_names.end());  // readGroupNames.sorted.zipWithIndex (the last duplicate wins)
-  HostNames rgh, sqh;
+  HostNames& rgh = H->rgh;
+  HostNames& sqh = H->sqh;
   for (size_t i = 0; i < rg_names.size(); ++i) {
     if (i + 1 < rg_names.size() && rg_names[i + 1] == rg_names[i]) continue;
     rgh.add(rg_names[i], (int32_t)i);
@@ -863,6 +869,26 @@ bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void*
   }
   rgh.build();
   sqh.build();
+
+  return BQSR_OK;
+}
+
+}  // namespace
+
+bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void* stream, bqsr_sam** out) {
+  if (!ctx || !out || n < 0 || (n > 0 && !text)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_parse: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = S(stream);
+  // ---- header (host): @RG IDs sorted (RecordGroupDictionary), @SQ names ----
+  SamHeader H;
+  bqsr_status hst = parse_sam_header(text, n, &H);
+  if (hst != BQSR_OK) return hst;
+  const int64_t body = H.body;
+  std::vector<std::string>& rg_names = H.rg_names;
+  std::vector<std::string>& sq_names = H.sq_names;
+  std::map<std::string, std::pair<bool, std::string>>& rg_lb = H.rg_lb;
+  HostNames& rgh = H.rgh;
+  HostNames& sqh = H.sqh;
 
   std::unique_ptr<bqsr_sam> S_(new bqsr_sam);
   bqsr_sam* o = S_.get();
@@ -1074,6 +1100,7 @@ bqsr_status bqsr_sam_rewrite_quals(bqsr_context* ctx, bqsr_sam* sm, const bqsr_b
                                    int64_t n_exc, void* stream) {
   if (!ctx || !sm || (b && (!out_qual || !out_start || !out_len)) || n_exc < 0 || (n_exc > 0 && !exceptions))
     return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_rewrite_quals: bad arguments");
+  if (sm->from_bam) return fail(BQSR_ERR_UNSUPPORTED, "bqsr_sam_rewrite_quals: BAM input has no SAM text to rewrite");
   if (b && b->rd.n_reads != sm->n_reads) return fail(BQSR_ERR_INVALID_ARG, "batch and SAM read counts differ");
   if (b && !b->prepped) return fail(BQSR_ERR_INVALID_ARG, "the batch has not been through apply");
   if (!b) {  // QUAL fields kept (only FLAG rewritten, after MarkDuplicates)
@@ -1157,6 +1184,7 @@ bqsr_status bqsr_sam_rewrite_quals(bqsr_context* ctx, bqsr_sam* sm, const bqsr_b
 
 bqsr_status bqsr_sam_text_download(const bqsr_sam* s, char* dst) {
   if (!s || (!dst && s->n_text > 0)) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (s->from_bam) return fail(BQSR_ERR_UNSUPPORTED, "bqsr_sam_text_download: BAM input has no SAM text");
   HIP_TRY(hipSetDevice(s->ctx->device));
   if (s->n_text > 0) HIP_TRY(hipMemcpy(dst, s->d_text, (size_t)s->n_text, hipMemcpyDeviceToHost));
   return ok();

@@ -51,6 +51,7 @@ def _lib():
         pp = ctypes.POINTER(ctypes.c_void_p)
         sig = {
             "bqsr_sam_parse": (ctypes.c_int, [vp, ctypes.c_char_p, i64, vp, pp]),
+            "bqsr_bam_parse": (ctypes.c_int, [vp, ctypes.c_char_p, i64, vp, pp]),
             "bqsr_sam_destroy": (None, [vp]),
             "bqsr_sam_get_counts": (ctypes.c_int, [vp, ctypes.POINTER(SamCounts)]),
             "bqsr_sam_ref_name": (ctypes.c_char_p, [vp, i32]),
@@ -72,16 +73,22 @@ def _lib():
 class SamText:
     """A SAM file parsed into device columns (bqsr_sam)."""
 
-    def __init__(self, data: bytes, ctx: Optional[bqsr.Context] = None, stream=None):
+    def __init__(self, data: bytes, ctx: Optional[bqsr.Context] = None, stream=None, bam: bool = False):
+        """data: SAM text, or BAM bytes (BGZF) with bam=True -- the same
+        columns either way (bqsr_bam_parse; a BAM has no text to rewrite)."""
         self.L = _lib()
         self.ctx = ctx or bqsr.Context.get(0)
         self.h = ctypes.c_void_p()
-        check(self.L.bqsr_sam_parse(self.ctx.handle, data, len(data), stream, ctypes.byref(self.h)))
+        self.bam = bam
+        parse = self.L.bqsr_bam_parse if bam else self.L.bqsr_sam_parse
+        check(parse(self.ctx.handle, data, len(data), stream, ctypes.byref(self.h)))
 
     @classmethod
     def read(cls, path: str, ctx: Optional[bqsr.Context] = None) -> "SamText":
+        """A .sam or .bam file (BAM by its BGZF magic)."""
         with open(path, "rb") as fh:
-            return cls(fh.read(), ctx)
+            data = fh.read()
+        return cls(data, ctx, bam=data[:4] == b"\x1f\x8b\x08\x04")
 
     def counts(self) -> SamCounts:
         c = SamCounts()

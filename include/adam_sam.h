@@ -43,6 +43,14 @@ typedef struct bqsr_sam bqsr_sam;
  * the first record and lone '\r' bytes. */
 bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n_bytes, void* stream, bqsr_sam** out);
 void bqsr_sam_destroy(bqsr_sam* s);
+/* BAM bytes (BGZF) -> the same device columns bqsr_sam_parse builds from the
+ * SAM text of the same records (AdamContext.scala:122-137 adamBamLoad,
+ * SAMRecordConverter.scala:26-144): BGZF blocks inflated by host threads,
+ * records decoded on the device.  The result serves bqsr_sam_get_counts,
+ * bqsr_sam_download / device_columns and bqsr_sam_mark_duplicates; there is
+ * no SAM text to rewrite (bqsr_sam_rewrite_quals / text_download:
+ * BQSR_ERR_UNSUPPORTED).  MD / RG values of type f, H or B: UNSUPPORTED. */
+bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* bam, int64_t n_bytes, void* stream, bqsr_sam** out);
 
 typedef struct bqsr_sam_counts {
   int64_t n_reads;     /* records (empty lines skipped)   */

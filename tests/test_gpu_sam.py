@@ -332,3 +332,43 @@ def test_mark_duplicates_device_equals_host(n_reads, contig_len):
         s.close()
     assert nd == int(want.sum()) > 0
     assert np.array_equal(got, want), int(np.nonzero(got != want)[0][0])
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_bam_ingest_reference_fixtures(name):
+    """The reference's SAM fixtures converted to BAM (adam_amd/bam_writer.py)
+    ingest to the same columns as their SAM text (AdamContext.scala:122-137
+    adamBamLoad, SAMRecordConverter semantics)."""
+    from adam_amd.bam_writer import sam_to_bam
+    path = os.path.join(GOLD, name)
+    with open(path, "rb") as fh:
+        text = fh.read()
+    s = SamText(sam_to_bam(text), bam=True)
+    try:
+        got = s.batch()
+    finally:
+        s.close()
+    assert_same_columns(got, read_sam(path))
+
+
+def test_bam_ingest_synthetic_and_mark_duplicates(tmp_path):
+    """60k synthetic reads (pairs, fragments, 2 read groups): BAM columns equal
+    the SAM text's, and MarkDuplicates flags the same reads from either."""
+    from adam_amd.bam_writer import sam_to_bam
+    text = _dup_sam(60000, 4242, 30000)
+    bam = sam_to_bam(text)
+    p = tmp_path / "x.bam"
+    p.write_bytes(bam)
+    a, b = SamText(text), SamText.read(str(p))
+    try:
+        assert b.bam
+        assert_same_columns(b.batch(), a.batch())
+        na, nb = a.mark_duplicates(), b.mark_duplicates()
+        assert na == nb > 0
+        assert np.array_equal(a.batch().flags, b.batch().flags)
+        with pytest.raises(_capi.BQSRError) as e:
+            b.rewrite()
+        assert e.value.status == _capi.UNSUPPORTED
+    finally:
+        a.close()
+        b.close()

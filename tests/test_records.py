@@ -94,3 +94,31 @@ def test_synth_slice_is_the_same_reads_of_the_bigger_set():
     for c in ("flags", "rg_id", "start", "seq", "qual", "cigar", "md", "seq_offset", "qual_offset", "cigar_offset",
               "md_offset"):
         assert np.array_equal(getattr(part, c), getattr(ref, c)), c
+
+
+def test_bam_writer_bgzf_structure():
+    """The in-tree BAM writer's output is BGZF (gzip members with a BC
+    subfield) holding BAM\\1, the header text and one record per SAM line."""
+    import gzip
+    import struct
+    from adam_amd.bam_writer import sam_to_bam
+    path = os.path.join(GOLD, "small_realignment_targets.sam")
+    text = open(path, "rb").read()
+    bam = sam_to_bam(text)
+    assert bam[:4] == b"\x1f\x8b\x08\x04" and bam[12:14] == b"BC"
+    raw = gzip.decompress(bam)
+    assert raw[:4] == b"BAM\x01"
+    l_text = struct.unpack("<i", raw[4:8])[0]
+    assert raw[8:8 + l_text].startswith(b"@")
+    p = 8 + l_text
+    n_ref = struct.unpack("<i", raw[p:p + 4])[0]
+    p += 4
+    for _ in range(n_ref):
+        ln = struct.unpack("<i", raw[p:p + 4])[0]
+        p += 4 + ln + 4
+    n = 0
+    while p < len(raw):
+        p += 4 + struct.unpack("<i", raw[p:p + 4])[0]
+        n += 1
+    assert p == len(raw)
+    assert n == sum(1 for l in text.split(b"\n") if l and not l.startswith(b"@"))
