@@ -46,7 +46,7 @@ class StreamedShard:
     """Partitions of one rank's shard: pinned host copies + device batches."""
 
     def __init__(self, ctx, parts: Sequence, dims, sites_handle=None, device: int = 0, max_exc: int = 1 << 16,
-                 site_contigs: Optional[Sequence[str]] = None, read_base: int = 0):
+                 site_contigs: Optional[Sequence[str]] = None, read_base: int = 0, zero_copy: bool = False):
         """read_base: global index of the shard's first read (reads of the
         ranks before this one): multi-rank errors are raised in global order."""
         import torch
@@ -64,6 +64,9 @@ class StreamedShard:
         self.staged_bytes = 0
         self.site_contigs = site_contigs
         self.read_base = int(read_base)
+        # zero_copy: apply writes its outputs straight into the pinned host
+        # buffers (device stores over PCIe, no download copies)
+        self.zero_copy = bool(zero_copy)
         for p in parts:
             self.add_partition(p)
         if parts:
@@ -168,14 +171,19 @@ class StreamedShard:
         # (3) apply from the resident partitions, results streamed back
         for i, bh in enumerate(self.batches):
             k = i & 1
-            if self.dl_used[k]:
-                comp.wait_event(self.ev_dl[k])  # output buffer k drained to the host
+            if self.zero_copy:
+                if self.jobs:
+                    comp.wait_event(self.ev_done[slot])  # the job two back is done with these host buffers
+                oq, os_, ol = self.host_qual[i], self.host_start[i], self.host_len[i]
+            else:
+                if self.dl_used[k]:
+                    comp.wait_event(self.ev_dl[k])  # output buffer k drained to the host
+                oq, os_, ol = self.out_qual[k], self.out_start[k], self.out_len[k]
             if record_apply:
                 self.ev_apply_t[i][0].record(comp)
             exc_i = ctypes.c_void_p(self.exc.data_ptr() + 8 * i * self.max_exc)
-            check(L.bqsr_apply_stage(ctx, bh, self.lut, ctypes.c_void_p(self.out_qual[k].data_ptr()),
-                                     ctypes.c_void_p(self.out_start[k].data_ptr()),
-                                     ctypes.c_void_p(self.out_len[k].data_ptr()), exc_i,
+            check(L.bqsr_apply_stage(ctx, bh, self.lut, ctypes.c_void_p(oq.data_ptr()),
+                                     ctypes.c_void_p(os_.data_ptr()), ctypes.c_void_p(ol.data_ptr()), exc_i,
                                      self.max_exc, _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
             if record_apply:
                 self.ev_apply_t[i][1].record(comp)
@@ -183,9 +191,10 @@ class StreamedShard:
             dn.wait_event(self.ev_ap[i])
             with torch.cuda.stream(dn):
                 ns, nr = self.n_slots[i], max(1, self.n_reads[i])
-                self.host_qual[i][:ns].copy_(self.out_qual[k][:ns], non_blocking=True)
-                self.host_start[i][:nr].copy_(self.out_start[k][:nr], non_blocking=True)
-                self.host_len[i][:nr].copy_(self.out_len[k][:nr], non_blocking=True)
+                if not self.zero_copy:
+                    self.host_qual[i][:ns].copy_(self.out_qual[k][:ns], non_blocking=True)
+                    self.host_start[i][:nr].copy_(self.out_start[k][:nr], non_blocking=True)
+                    self.host_len[i][:nr].copy_(self.out_len[k][:nr], non_blocking=True)
                 e0 = i * self.max_exc
                 self.host_exc[e0:e0 + self.max_exc].copy_(self.exc[e0:e0 + self.max_exc], non_blocking=True)
             self.ev_dl[k].record(dn)

@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic json (default profiles/pmc_traffic_<config>.json)")
     ap.add_argument("--part-reads", type=int, default=4_000_000, help="cfg5: reads per streamed partition")
+    ap.add_argument("--stream-mode", default="pipe", choices=("pipe", "serial", "zerocopy"),
+                    help="cfg5: jobs pipelined over both link directions, one at a time, or pipelined with "
+                         "apply writing into pinned host memory")
     return ap.parse_args()
 
 
@@ -320,7 +323,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
     pr = max(1, args.part_reads)
     dims = Dims(cfg["n_rg"], max(cfg["lens"]))
     t_gen = time.time()
-    sh = StreamedShard(ctx, [], dims, None, dev.index)
+    sh = StreamedShard(ctx, [], dims, None, dev.index, zero_copy=args.stream_mode == "zerocopy")
     first = None
     for i, r0 in enumerate(range(0, n_reads, pr)):
         part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"],
@@ -343,7 +346,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         # jobs pipeline (stream.py): this job's uploads overlap the previous
         # job's downloads; its status is checked one job later
         sh.run(th, table_t if world > 1 else None, record_apply=record)
-        if len(sh.pending) > 1:
+        if len(sh.pending) > (0 if args.stream_mode == "serial" else 1):
             sh.finish()
 
     for _ in range(args.warmup):
@@ -404,6 +407,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
                 "read_groups": cfg["n_rg"],
                 "known_sites": 0,
                 "partitions_per_gpu": parts_n,
+                "stream_mode": args.stream_mode,
                 "parallelism": "dp%d: read shards per GPU, RCCL int64 table all-reduce" % world,
             },
             "roofline": {
