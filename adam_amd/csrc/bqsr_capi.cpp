@@ -296,6 +296,8 @@ struct bqsr_batch {
   int64_t qhist[kQBins] = {0};
   std::vector<void*> allocs;
   std::vector<size_t> staged_cnt;  // column element counts (bqsr_batch_create_staged)
+  uint8_t* d_bases2 = nullptr;     // staged: the uploaded 2-bit base codes
+  uint64_t* d_bexc = nullptr;      //         and their exceptions
   // per-read prep results (valid once `prepped`)
   ReadInfo* d_info = nullptr;
   uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
@@ -779,10 +781,16 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
 // block; bqsr_batch_create_staged allocates matching device columns;
 // bqsr_batch_upload_async enqueues the six H2D copies on a copy stream, so
 // the next partition's transfer overlaps the current one's kernels.
+// A partition staged for streaming: pinned host columns in the device layout,
+// except the base codes, which travel as 2 bits per slot (A C G T) plus an
+// exception list (slot << 8 | code) for N / other bytes and are expanded to
+// the 4-bit column on the device after the upload (a third of the bytes the
+// link would carry for them).
+constexpr int kStagedCols = 8;  // meta | align | qual | bases (device only) | md | cigar | bases2 | exceptions
 struct bqsr_staged {
-  unsigned char* host = nullptr;  // pinned: meta | align | qual | bases | md | cigar
+  unsigned char* host = nullptr;  // pinned: the columns, bases excepted
   size_t bytes = 0;
-  size_t off[6] = {0, 0, 0, 0, 0, 0}, cnt[6] = {0, 0, 0, 0, 0, 0};  // byte offset, element count per column
+  size_t off[kStagedCols] = {0}, cnt[kStagedCols] = {0};  // byte offset, element count per column
   int64_t n_reads = 0, n_slots = 0, n_bases = 0, max_slot = 0;
   bqsr_dims dims{1, 1};
   int32_t rg_lo = 0, q_lo = 0;
@@ -801,19 +809,34 @@ bqsr_status bqsr_stage_records(bqsr_context* ctx, const bqsr_records* R, bqsr_st
   if (P.max_slot > kMaxReadLen)
     return fail(BQSR_ERR_UNSUPPORTED, "reads longer than " + std::to_string(kMaxReadLen) + " bases are not supported");
   std::unique_ptr<bqsr_staged> s(new bqsr_staged);
-  const size_t esz[6] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t)};
-  const size_t cnt[6] = {P.meta.size(), P.align.size(), P.qual.size(), P.bases.size(), P.md.size(), P.cigar.size()};
-  const void* src[6] = {P.meta.data(), P.align.data(), P.qual.data(), P.bases.data(), P.md.data(), P.cigar.data()};
+  // base codes: 2 bits a slot (4 slots a byte; N / other as A plus an exception)
+  const size_t nb = P.bases.size();
+  std::vector<uint8_t> b2((nb + 1) / 2 + 8, 0);
+  std::vector<uint64_t> exc;
+  for (size_t j = 0; j < nb; ++j) {
+    const uint8_t v = P.bases[j];
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t c = (v >> (4 * h)) & 0xFu;
+      const uint64_t slot = 2 * (uint64_t)j + (uint64_t)h;
+      if (c >= 4) exc.push_back((slot << 8) | c);
+      else b2[slot >> 2] |= (uint8_t)(c << (2 * (slot & 3)));
+    }
+  }
+  const size_t esz[kStagedCols] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t), 1, 8};
+  const size_t cnt[kStagedCols] = {P.meta.size(), P.align.size(), P.qual.size(), nb, P.md.size(), P.cigar.size(),
+                                   b2.size(), exc.size()};
+  const void* src[kStagedCols] = {P.meta.data(), P.align.data(), P.qual.data(), nullptr, P.md.data(), P.cigar.data(),
+                                  b2.data(), exc.data()};
   size_t tot = 0;
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < kStagedCols; ++i) {
     s->off[i] = tot;
     s->cnt[i] = cnt[i];
-    tot = (tot + cnt[i] * esz[i] + 255) & ~(size_t)255;
+    if (src[i]) tot = (tot + cnt[i] * esz[i] + 255) & ~(size_t)255;
   }
   HIP_TRY(hipHostMalloc((void**)&s->host, std::max<size_t>(tot, 1), hipHostMallocDefault));
   s->bytes = tot;
-  for (int i = 0; i < 6; ++i)
-    if (cnt[i]) memcpy(s->host + s->off[i], src[i], cnt[i] * esz[i]);
+  for (int i = 0; i < kStagedCols; ++i)
+    if (cnt[i] && src[i]) memcpy(s->host + s->off[i], src[i], cnt[i] * esz[i]);
   s->n_reads = R->n_reads;
   s->n_slots = P.n_slots;
   s->n_bases = P.n_bases;
@@ -863,24 +886,39 @@ bqsr_status bqsr_batch_create_staged(bqsr_context* ctx, const bqsr_staged* S_, b
   b->rd.md = md;
   b->rd.cigar = cigar;
   b->rd.slots_aligned = align_slots();
+  if ((st = dalloc(b->allocs, &b->d_bases2, S_->cnt[6] + 16)) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->d_bexc, std::max<size_t>(S_->cnt[7], 1))) != BQSR_OK)
+    return st;
   if ((st = finish_batch(b.get(), S_->max_slot)) != BQSR_OK) return st;
-  b->staged_cnt.assign(S_->cnt, S_->cnt + 6);
+  b->staged_cnt.assign(S_->cnt, S_->cnt + kStagedCols);
   *out = b.release();
   return ok();
 }
 
 bqsr_status bqsr_batch_upload_async(bqsr_batch* b, const bqsr_staged* S_, void* stream) {
   if (!b || !S_) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: bad arguments");
-  if (b->staged_cnt.size() != 6 || !std::equal(b->staged_cnt.begin(), b->staged_cnt.end(), S_->cnt) ||
+  if (b->staged_cnt.size() != kStagedCols || !std::equal(b->staged_cnt.begin(), b->staged_cnt.end(), S_->cnt) ||
       b->rd.n_reads != S_->n_reads)
     return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: batch was not created from a partition of this shape");
   HIP_TRY(hipSetDevice(b->ctx->device));
-  void* dst[6] = {(void*)b->rd.meta, (void*)b->rd.align, (void*)b->rd.qual,
-                  (void*)b->rd.bases, (void*)b->rd.md, (void*)b->rd.cigar};
-  const size_t esz[6] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t)};
+  void* dst[kStagedCols] = {(void*)b->rd.meta, (void*)b->rd.align, (void*)b->rd.qual, nullptr,
+                            (void*)b->rd.md,   (void*)b->rd.cigar, (void*)b->d_bases2, (void*)b->d_bexc};
+  const size_t esz[kStagedCols] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t), 1, 8};
   hipStream_t s = S(stream);
-  for (int i = 0; i < 6; ++i)
-    if (S_->cnt[i]) HIP_TRY(hipMemcpyAsync(dst[i], S_->host + S_->off[i], S_->cnt[i] * esz[i], hipMemcpyHostToDevice, s));
+  for (int i = 0; i < kStagedCols; ++i)
+    if (S_->cnt[i] && dst[i])
+      HIP_TRY(hipMemcpyAsync(dst[i], S_->host + S_->off[i], S_->cnt[i] * esz[i], hipMemcpyHostToDevice, s));
+  // the 4-bit base codes back from 2 bits a slot, then the exceptions (on the upload's stream)
+  const int64_t nw = (int64_t)(S_->cnt[3] + 7) / 8;  // u64 words of the 4-bit column
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (nw + 255) / 256), (int64_t)b->ctx->n_cu * 16);
+  hipLaunchKernelGGL(bqsr_bases_expand, dim3(g), dim3(256), 0, s, (const uint32_t*)b->d_bases2, (int64_t)S_->cnt[3],
+                     (uint8_t*)b->rd.bases);
+  if (S_->cnt[7]) {
+    const unsigned ge = (unsigned)std::min<int64_t>(((int64_t)S_->cnt[7] + 255) / 256, (int64_t)b->ctx->n_cu * 16);
+    hipLaunchKernelGGL(bqsr_bases_exceptions, dim3(ge), dim3(256), 0, s, (const uint64_t*)b->d_bexc,
+                       (int64_t)S_->cnt[7], (uint8_t*)b->rd.bases);
+  }
+  HIP_TRY(hipGetLastError());
   b->prepped = false;  // new contents: the next observe / apply re-runs prep
   return ok();
 }

@@ -3105,6 +3105,38 @@ extern "C" __global__ void bqsr_job_err_import(unsigned long long* err, const in
   if (t == 2) err[kErrAppKern] = kNoError;
 }
 
+// ------------------------------------------------ staged base codes -----
+// 2 bits a slot -> the 4-bit column (bqsr_batch_upload_async): a thread per
+// 16 slots, the 2-bit groups spread to nibbles; n = bytes of the 4-bit column
+extern "C" __global__ void bqsr_bases_expand(const uint32_t* b2, int64_t n, uint8_t* bases) {
+  const int64_t nw = (n + 7) / 8;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nw; t += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t x = b2[t];
+    uint64_t y = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t v = (x >> (16 * h)) & 0xFFFFu;
+      v = (v | (v << 8)) & 0x00FF00FFu;
+      v = (v | (v << 4)) & 0x0F0F0F0Fu;
+      v = (v | (v << 2)) & 0x33333333u;
+      y |= (uint64_t)v << (32 * h);
+    }
+    if (8 * t + 8 <= n) {
+      *(uint64_t*)(bases + 8 * t) = y;
+    } else {
+      for (int64_t k = 0; 8 * t + k < n; ++k) bases[8 * t + k] = (uint8_t)(y >> (8 * k));
+    }
+  }
+}
+// the N / other codes over their slots' zero nibbles
+extern "C" __global__ void bqsr_bases_exceptions(const uint64_t* exc, int64_t n, uint8_t* bases) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = exc[i], slot = e >> 8;
+    const uint32_t code = (uint32_t)(e & 0xFu);
+    atomicOr((unsigned int*)(bases + ((slot >> 1) & ~(uint64_t)3)), code << (4 * (uint32_t)(slot & 7)));
+  }
+}
+
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

@@ -23,14 +23,32 @@ def _slots(batch):
     return np.concatenate([[0], np.cumsum(span)])[:-1]
 
 
-@pytest.mark.parametrize("sizes,lens,n_rg,with_sites", [((7000, 5000, 9000), (150,), 1, True),
-                                                        ((3000, 1, 4000), (100, 250), 4, False)])
-def test_streamed_partitions(sizes, lens, n_rg, with_sites):
+def _odd_bases(b):
+    """Forward reads with lowercase / non-ACGTN bytes (context index -1, Q10):
+    the staged 2-bit codes' exception list carries them."""
+    from adam_amd.records import F_NEG_STRAND
+    for r in range(0, b.n_reads, 37):
+        if not b.flags[r] & F_NEG_STRAND and b.seq_offset[r + 1] - b.seq_offset[r] > 10:
+            a = int(b.seq_offset[r])
+            b.seq[a + 3] = ord("x")
+            b.seq[a + 7] = ord("a")
+            b.seq[a + 8] = ord("N")
+    return b
+
+
+@pytest.mark.parametrize("sizes,lens,n_rg,with_sites,odd,zero_copy", [
+    ((7000, 5000, 9000), (150,), 1, True, False, False),
+    ((3000, 1, 4000), (100, 250), 4, False, False, False),
+    ((4000, 6000), (101,), 2, False, True, False),
+    ((5000, 3000), (150,), 1, True, True, True)])
+def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy):
     import torch
     from adam_amd.stream import StreamedShard
     dev = torch.device("cuda", 0)
     torch.zeros(1, device=dev)  # torch's HIP runtime first, as bench.py does
     parts = [synth.generate(n, lens, n_rg, 900 + i) for i, n in enumerate(sizes)]
+    if odd:
+        parts = [_odd_bases(p) for p in parts]
     sites = synth.known_sites(200_000) if with_sites else None
     snp = bqsr.SnpTable(sites) if sites else None
     d = bqsr.dims_of(parts)
@@ -40,7 +58,7 @@ def test_streamed_partitions(sizes, lens, n_rg, with_sites):
     th = ctypes.c_void_p()
     _capi.check(L.bqsr_table_create(ctx.handle, d, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
     sh = StreamedShard(ctx, parts, d, snp.handle(ctx) if snp else None, 0,
-                       site_contigs=snp.contigs if snp else None)
+                       site_contigs=snp.contigs if snp else None, zero_copy=zero_copy)
     try:
         for _ in range(2):  # the second job re-uploads over the resident partitions
             em_t = sh.run(th)
