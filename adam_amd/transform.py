@@ -10,25 +10,175 @@ BQSR (`adamBQSR(loadSnpTable)`: an empty SnpTable without -dbsnp_sites,
 :96-105), save.  The output is SAM text -- the input records with their QUAL
 fields replaced by the recalibrated strings (and FLAG 0x400 by MarkDuplicates'
 result) -- where the reference writes ADAM/Parquet (adamSave,
-core/rdd/AdamRDDFunctions.scala:37-56).  The input is one partition (one
-Hadoop split of a small file).  -sort_reads, -coalesce and -realignIndels are
-outside this build and are refused.
+core/rdd/AdamRDDFunctions.scala:37-56).  -sort_reads, -coalesce and
+-realignIndels are outside this build and are refused.
+
+Partitions: an input whose records exceed ``partition_bytes`` is cut at line
+boundaries into partitions (the Hadoop splits the reference's RDD is read
+as, each parsed with the header as a SAM file of its own) that stream through
+the device: every partition is parsed and packed into a resident batch and
+observed into the one count table (computeTable's per-partition aggregate
+merged by ``RecalTable.++``, RecalibrateBaseQualities.scala:52-64), the
+per-partition expectedMismatch values folded in partition order, then per
+partition: apply, its text re-read (the reference re-reads its input per
+stage, cli/Transform.scala:62-97), QUAL rewritten on the device and the
+records appended to the output.  Errors are raised in the reference's order:
+observe errors partition by partition, finalize, then apply errors partition
+by partition; the output file appears only when the job succeeds.
+MarkDuplicates groups reads across the whole input (its groupBy), so it runs
+on one partition: with -mark_duplicate_reads the input is not cut.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
+import mmap
+import os
 import sys
 import time
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Tuple
 
-from . import bqsr
+from . import _capi, bqsr
+from . import distributed as D
+from ._capi import check
 from .sam import SamText
+
+DEFAULT_PARTITION_BYTES = 1 << 30
+
+
+def sam_partitions(data, partition_bytes: int) -> Tuple[bytes, List[Tuple[int, int]]]:
+    """(header, ranges): the SAM header lines and the byte ranges [a, b) of
+    the records, each range cut after the first newline at or beyond
+    partition_bytes from its start (so every record lies in one range)."""
+    n = len(data)
+    pos = 0
+    while pos < n and data[pos:pos + 1] == b"@":
+        nl = data.find(b"\n", pos)
+        pos = n if nl < 0 else nl + 1
+    ranges = []
+    a = pos
+    step = max(1, int(partition_bytes))
+    while a < n:
+        b = min(n, a + step)
+        if b < n:
+            nl = data.find(b"\n", b - 1)
+            b = n if nl < 0 else nl + 1
+        ranges.append((a, b))
+        a = b
+    return bytes(data[:pos]), ranges
+
+
+def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ctx, device: int, out_fh,
+                     max_exc: int = 1 << 16) -> Dict[str, float]:
+    """BQSR over several partitions of one SAM input (see the module doc);
+    writes the recalibrated text to out_fh in partition order."""
+    import torch
+    L = _capi.lib()
+    dev = torch.device("cuda", device)
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    h = ctx.handle
+    contigs = snp.contigs if snp else None
+    sites_h = snp.handle(ctx) if snp else None
+    batches: List[ctypes.c_void_p] = []
+    th, lut = ctypes.c_void_p(), ctypes.c_void_p()
+    n_reads = 0
+    try:
+        # (1) every partition parsed on the device and packed into a resident batch
+        n_rg = max_len = 1
+        slots, reads = [], []
+        for a, b in ranges:
+            sam = SamText(header + bytes(data[a:b]), ctx)
+            try:
+                rb = sam.batch()
+            finally:
+                sam.close()
+            s, keep = rb.c_struct(rb.contig_ids_for(contigs))
+            bh = ctypes.c_void_p()
+            check(L.bqsr_batch_create(h, ctypes.byref(s), sp, ctypes.byref(bh)))
+            del keep
+            batches.append(bh)
+            n_rg, max_len = max(n_rg, rb.n_rg()), max(max_len, rb.max_len())
+            slots.append(int(L.bqsr_batch_slots(bh)))
+            reads.append(rb.n_reads)
+        n_reads = sum(reads)
+        # (2) computeTable: every partition observed into the one table, its
+        # errors raised partition by partition, expectedMismatch folded in
+        # partition order
+        dims = _capi.Dims(n_rg, max_len)
+        table = torch.zeros(int(L.bqsr_table_words(dims)), dtype=torch.int64, device=dev)
+        check(L.bqsr_table_create(h, dims, ctypes.c_void_p(table.data_ptr()), ctypes.byref(th)))
+        em = torch.zeros(max(1, len(batches)), dtype=torch.float64, device=dev)
+        for i, bh in enumerate(batches):
+            check(L.bqsr_observe_async(h, bh, sites_h, th, sp))
+            check(L.bqsr_batch_em_copy_async(bh, ctypes.c_void_p(em.data_ptr() + 8 * i), sp))
+        for bh in batches:
+            v = ctypes.c_double()
+            check(L.bqsr_observe_result(bh, ctypes.byref(v), sp))
+        acc = D.fold_partition_ems_device(em[:len(batches)], [len(batches)], ctx, stream)
+        check(L.bqsr_finalize_device(h, th, ctypes.c_void_p(acc.data_ptr()), ctypes.byref(lut), sp))
+        # (3) applyTable partition by partition, each partition's records
+        # re-read, rewritten on the device and appended
+        out_qual = torch.empty(max(slots or [0]) + 64, dtype=torch.uint8, device=dev)
+        out_start = torch.empty(max(1, max(reads or [1])), dtype=torch.int32, device=dev)
+        out_len = torch.empty_like(out_start)
+        exc = torch.empty(max_exc, dtype=torch.int64, device=dev)
+        ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        for i, (a, b) in enumerate(ranges):
+            bh = batches[i]
+            check(L.bqsr_apply_stage(h, bh, lut, ptr(out_qual), ptr(out_start), ptr(out_len), ptr(exc), max_exc,
+                                     _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
+            v, nexc = ctypes.c_double(), ctypes.c_int64()
+            check(L.bqsr_job_result(bh, lut, ctypes.byref(v), ctypes.byref(nexc), sp))
+            if nexc.value > max_exc:
+                raise _capi.BQSRError(_capi.UNSUPPORTED, "partition %d: %d chars above 0xFF exceed the exception "
+                                      "list" % (i, nexc.value))
+            sam = SamText(header + bytes(data[a:b]), ctx)
+            try:
+                check(L.bqsr_sam_rewrite_quals(h, sam.h, bh, ptr(out_qual), ptr(out_start), ptr(out_len), ptr(exc),
+                                               nexc.value, sp))
+                text = sam.text()
+            finally:
+                sam.close()
+            out_fh.write(text if i == 0 else text[len(header):])
+            L.bqsr_batch_destroy(bh)
+            batches[i] = None
+    finally:
+        if lut:
+            L.bqsr_lut_destroy(lut)
+        if th:
+            L.bqsr_table_destroy(th)
+        for bh in batches:
+            if bh:
+                L.bqsr_batch_destroy(bh)
+    return {"reads": n_reads, "partitions": len(ranges)}
 
 
 def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
-              dbsnp: Optional[str] = None, device: int = 0) -> Dict[str, float]:
+              dbsnp: Optional[str] = None, device: int = 0,
+              partition_bytes: int = DEFAULT_PARTITION_BYTES) -> Dict[str, float]:
     t0 = time.perf_counter()
     ctx = bqsr.Context.get(device)
+    if recalibrate and not mark_duplicates and os.path.getsize(inp) > 0:
+        with open(inp, "rb") as fh:
+            data = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+            try:
+                header, ranges = sam_partitions(data, partition_bytes)
+                if len(ranges) > 1 and data[:4] != b"\x1f\x8b\x08\x04":
+                    snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
+                    tmp = out + ".partial"
+                    try:
+                        with open(tmp, "wb") as ofh:
+                            stats = _bqsr_partitions(data, header, ranges, snp if snp.table else None, ctx, device,
+                                                     ofh)
+                        os.replace(tmp, out)
+                    finally:
+                        if os.path.exists(tmp):
+                            os.remove(tmp)
+                    stats["seconds"] = time.perf_counter() - t0
+                    return stats
+            finally:
+                data.close()
     with open(inp, "rb") as fh:
         data = fh.read()
     sam = SamText(data, ctx)
@@ -68,10 +218,13 @@ def main(argv=None) -> int:
     for flag in ("-sort_reads", "-realignIndels"):
         ap.add_argument(flag, action="store_true")
     ap.add_argument("-coalesce", type=int, default=-1)
+    ap.add_argument("-partition_bytes", type=int, default=DEFAULT_PARTITION_BYTES,
+                    help="records per streamed partition, in bytes of SAM text (BQSR without MarkDuplicates)")
     a = ap.parse_args(argv)
     if a.sort_reads or a.realignIndels or a.coalesce != -1:
         ap.error("-sort_reads / -coalesce / -realignIndels are outside this build")
-    st = transform(a.input, a.output, a.mark_duplicate_reads, a.recalibrate_base_qualities, a.dbsnp_sites)
+    st = transform(a.input, a.output, a.mark_duplicate_reads, a.recalibrate_base_qualities, a.dbsnp_sites,
+                   partition_bytes=a.partition_bytes)
     print(" ".join("%s=%s" % kv for kv in st.items()), file=sys.stderr)
     return 0
 

@@ -15,7 +15,7 @@ from adam_amd import records as R
 from adam_amd.records import read_sam
 from adam_amd.sam import SamText
 from adam_amd.samgen import sam_text
-from adam_amd.transform import transform
+from adam_amd.transform import sam_partitions, transform
 
 pytestmark = pytest.mark.gpu
 
@@ -168,6 +168,74 @@ def test_transform_synthetic_reads(tmp_path):
             assert c[10] == "".join(map(chr, quals[r])).encode("utf-8"), r
         else:
             assert c[10] == a[10]
+
+
+def _partition_batches(tmp_path, text: bytes, partition_bytes: int):
+    header, ranges = sam_partitions(text, partition_bytes)
+    parts = []
+    for i, (a, b) in enumerate(ranges):
+        f = tmp_path / ("part%d.sam" % i)
+        f.write_bytes(header + text[a:b])
+        parts.append(read_sam(str(f)))
+    return parts
+
+
+@pytest.mark.parametrize("n_parts", [2, 7])
+def test_transform_partitions(tmp_path, n_parts):
+    # an input larger than one partition: cut at line boundaries, every
+    # partition observed into one table, expectedMismatch folded in partition
+    # order, applied and rewritten partition by partition -- against the
+    # oracle over the same partitions (the reference's RDD of those splits)
+    b = synth.generate(30000, (100, 151), 3, 11, contig_len=500_000)
+    text = sam_text(b, n_rg=3)
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    sites = synth.known_sites(5000, contig_len=500_000)
+    vcf = tmp_path / "s.vcf"
+    vcf.write_text("".join("chr20\t%d\t.\tA\tC\n" % p for p in sites["chr20"]))
+    pb = len(text) // n_parts + 1
+    st = transform(str(src), str(out), recalibrate=True, dbsnp=str(vcf), partition_bytes=pb)
+    parts = _partition_batches(tmp_path, text, pb)
+    assert st["partitions"] == len(parts) >= n_parts
+    o = run_oracle(parts, {"chr20": sites["chr20"].tolist()})
+    assert o.error is None, o.error
+    quals = []
+    for p, (chars, out_len) in zip(parts, o.outs):
+        quals += [chars[int(p.qual_offset[r]):int(p.qual_offset[r]) + int(out_len[r])] for r in range(p.n_reads)]
+    flags = np.concatenate([p.flags for p in parts])
+    res = out.read_bytes()
+    assert res.startswith(sam_partitions(text, pb)[0])
+    before, after = _records(text), _records(res)
+    assert len(before) == len(after) == len(quals) == b.n_reads
+    for r, (a, c) in enumerate(zip(before, after)):
+        f = int(flags[r])
+        assert a[:10] == c[:10] and a[11:] == c[11:]
+        if (f & R.F_MAPPED) and (f & R.F_PRIMARY) and not (f & R.F_DUPLICATE):
+            assert c[10] == "".join(map(chr, quals[r])).encode("utf-8"), r
+        else:
+            assert c[10] == a[10]
+
+
+def test_transform_partitions_error_order(tmp_path):
+    # a read without a read group in the third partition: the job raises
+    # NULL_RG (computeTable's error, before any apply) and writes no output
+    b = synth.generate(6000, (100,), 1, 12, contig_len=500_000)
+    text = sam_text(b, n_rg=1)
+    lines = text.split(b"\n")
+    body = [i for i, l in enumerate(lines) if l and not l.startswith(b"@")]
+    k = body[len(body) // 2]
+    lines[k] = b"\t".join(f for f in lines[k].split(b"\t") if not f.startswith(b"RG:Z:"))
+    text = b"\n".join(lines)
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    pb = len(text) // 4 + 1
+    parts = _partition_batches(tmp_path, text, pb)
+    o = run_oracle(parts)
+    assert o.error == "NULL_RG"
+    with pytest.raises(_capi.BQSRError) as e:
+        transform(str(src), str(out), recalibrate=True, partition_bytes=pb)
+    assert e.value.name == o.error
+    assert not out.exists() and not (tmp_path / "out.sam.partial").exists()
 
 
 def test_rewrite_java_chars_as_utf8():

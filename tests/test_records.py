@@ -122,3 +122,21 @@ def test_bam_writer_bgzf_structure():
         n += 1
     assert p == len(raw)
     assert n == sum(1 for l in text.split(b"\n") if l and not l.startswith(b"@"))
+
+
+def test_sam_partitions_cut_at_records():
+    # transform's streamed partitions: the header once, the records cut after
+    # a newline, every record in exactly one range, ranges in file order
+    from adam_amd.transform import sam_partitions
+    text = open(os.path.join(GOLD, "artificial.realigned.sam"), "rb").read()
+    body = text[len(sam_partitions(text, 1 << 30)[0]):]
+    for pb in (1, 57, 500, 4096, 1 << 30):
+        header, ranges = sam_partitions(text, pb)
+        assert not header or header.endswith(b"\n")
+        assert all(l.startswith(b"@") for l in header.split(b"\n") if l)
+        assert b"".join(text[a:b] for a, b in ranges) == body
+        assert all(text[b - 1:b] == b"\n" for a, b in ranges[:-1])
+        assert all(b - a >= min(pb, len(body)) or i == len(ranges) - 1 for i, (a, b) in enumerate(ranges))
+    assert sam_partitions(b"", 10) == (b"", [])
+    assert sam_partitions(b"@HD\tVN:1.4\n", 10) == (b"@HD\tVN:1.4\n", [])
+    assert sam_partitions(b"r\t0\n", 10) == (b"", [(0, 4)])
