@@ -298,6 +298,9 @@ struct bqsr_batch {
   std::vector<size_t> staged_cnt;  // column element counts (bqsr_batch_create_staged)
   uint8_t* d_bases2 = nullptr;     // staged: the uploaded 2-bit base codes
   uint64_t* d_bexc = nullptr;      //         and their exceptions
+  uint64_t* d_qcodes = nullptr;    // staged: the uploaded qual chunks (codes, base bytes)
+  uint8_t* d_qbase = nullptr;
+  uint64_t* d_qexc = nullptr;      //         and their exceptions
   // per-read prep results (valid once `prepped`)
   ReadInfo* d_info = nullptr;
   uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
@@ -785,8 +788,55 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
 // except the base codes, which travel as 2 bits per slot (A C G T) plus an
 // exception list (slot << 8 | code) for N / other bytes and are expanded to
 // the 4-bit column on the device after the upload (a third of the bytes the
-// link would carry for them).
-constexpr int kStagedCols = 8;  // meta | align | qual | bases (device only) | md | cigar | bases2 | exceptions
+// link would carry for them), and the quals, which travel as 16-slot chunks:
+// a base byte and sixteen 4-bit codes (qual - base + 7 for -7 .. +6, 15 for a
+// 0 byte -- the slots' padding --, 14 for an exception), plus an exception
+// list (slot << 8 | byte) -- 9 bytes a chunk instead of 16 when a chunk's
+// quals span at most 14 values, which neighbouring quals of a read mostly do
+// (quals_expand on the device).
+constexpr int kStagedCols = 11;  // meta | align | qual (device only) | bases (device only) | md | cigar | bases2 |
+                                 // base exceptions | qual codes | qual bases | qual exceptions
+constexpr uint32_t kQCodeZero = 15u, kQCodeExc = 14u;
+// One 16-slot chunk of quals (n <= 16 bytes) -> base byte and codes; exceptions appended.
+static void encode_qual_chunk(const uint8_t* q, int n, uint64_t slot0, uint8_t& base, uint64_t& codes,
+                              std::vector<uint64_t>& exc) {
+  int mn = 256, mx = -1;
+  for (int k = 0; k < n; ++k)
+    if (q[k]) {
+      mn = std::min(mn, (int)q[k]);
+      mx = std::max(mx, (int)q[k]);
+    }
+  int b = mn + 7;  // covers mn .. mn + 13
+  if (mx >= 0 && mx - mn > 13) {  // wider: of three windows, the one covering the most quals
+    const int cand[3] = {mn, mx - 13, (mn + mx) / 2 - 7};
+    int best = -1;
+    for (int c : cand) {
+      int cnt = 0;
+      for (int k = 0; k < n; ++k) cnt += q[k] && q[k] >= c && q[k] <= c + 13;
+      if (cnt > best) {
+        best = cnt;
+        b = c + 7;
+      }
+    }
+  }
+  b = std::min(std::max(b, 0), 255);
+  uint64_t w = 0;
+  for (int k = 0; k < 16; ++k) {
+    uint32_t c = kQCodeZero;
+    if (k < n && q[k]) {
+      const int d = (int)q[k] - b;
+      if (d >= -7 && d <= 6) {
+        c = (uint32_t)(d + 7);
+      } else {
+        c = kQCodeExc;
+        exc.push_back(((slot0 + (uint64_t)k) << 8) | q[k]);
+      }
+    }
+    w |= (uint64_t)c << (4 * k);
+  }
+  base = (uint8_t)b;
+  codes = w;
+}
 struct bqsr_staged {
   unsigned char* host = nullptr;  // pinned: the columns, bases excepted
   size_t bytes = 0;
@@ -822,11 +872,30 @@ bqsr_status bqsr_stage_records(bqsr_context* ctx, const bqsr_records* R, bqsr_st
       else b2[slot >> 2] |= (uint8_t)(c << (2 * (slot & 3)));
     }
   }
-  const size_t esz[kStagedCols] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t), 1, 8};
-  const size_t cnt[kStagedCols] = {P.meta.size(), P.align.size(), P.qual.size(), nb, P.md.size(), P.cigar.size(),
-                                   b2.size(), exc.size()};
-  const void* src[kStagedCols] = {P.meta.data(), P.align.data(), P.qual.data(), nullptr, P.md.data(), P.cigar.data(),
-                                  b2.data(), exc.data()};
+  // quals: 16-slot chunks (threads over chunk ranges, exception lists joined in slot order)
+  const size_t nq = P.qual.size(), n16 = (nq + 15) / 16;
+  std::vector<uint64_t> qcodes(std::max<size_t>(n16, 1), 0);
+  std::vector<uint8_t> qbase(std::max<size_t>(n16, 1), 0);
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>(16, n16 / 65536));
+  std::vector<std::vector<uint64_t>> qexc_t((size_t)nt);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        const size_t c0 = n16 * (size_t)t / (size_t)nt, c1 = n16 * (size_t)(t + 1) / (size_t)nt;
+        for (size_t c = c0; c < c1; ++c)
+          encode_qual_chunk(P.qual.data() + 16 * c, (int)std::min<size_t>(16, nq - 16 * c), 16 * (uint64_t)c,
+                            qbase[c], qcodes[c], qexc_t[(size_t)t]);
+      });
+    for (auto& x : th) x.join();
+  }
+  std::vector<uint64_t> qexc;
+  for (auto& v : qexc_t) qexc.insert(qexc.end(), v.begin(), v.end());
+  const size_t esz[kStagedCols] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t), 1, 8, 8, 1, 8};
+  const size_t cnt[kStagedCols] = {P.meta.size(), P.align.size(), nq,          nb,          P.md.size(), P.cigar.size(),
+                                   b2.size(),     exc.size(),     n16,         n16,         qexc.size()};
+  const void* src[kStagedCols] = {P.meta.data(), P.align.data(), nullptr,       nullptr,      P.md.data(), P.cigar.data(),
+                                  b2.data(),     exc.data(),     qcodes.data(), qbase.data(), qexc.data()};
   size_t tot = 0;
   for (int i = 0; i < kStagedCols; ++i) {
     s->off[i] = tot;
@@ -887,7 +956,10 @@ bqsr_status bqsr_batch_create_staged(bqsr_context* ctx, const bqsr_staged* S_, b
   b->rd.cigar = cigar;
   b->rd.slots_aligned = align_slots();
   if ((st = dalloc(b->allocs, &b->d_bases2, S_->cnt[6] + 16)) != BQSR_OK ||
-      (st = dalloc(b->allocs, &b->d_bexc, std::max<size_t>(S_->cnt[7], 1))) != BQSR_OK)
+      (st = dalloc(b->allocs, &b->d_bexc, std::max<size_t>(S_->cnt[7], 1))) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->d_qcodes, std::max<size_t>(S_->cnt[8], 1))) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->d_qbase, std::max<size_t>(S_->cnt[9], 1))) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->d_qexc, std::max<size_t>(S_->cnt[10], 1))) != BQSR_OK)
     return st;
   if ((st = finish_batch(b.get(), S_->max_slot)) != BQSR_OK) return st;
   b->staged_cnt.assign(S_->cnt, S_->cnt + kStagedCols);
@@ -901,9 +973,10 @@ bqsr_status bqsr_batch_upload_async(bqsr_batch* b, const bqsr_staged* S_, void* 
       b->rd.n_reads != S_->n_reads)
     return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: batch was not created from a partition of this shape");
   HIP_TRY(hipSetDevice(b->ctx->device));
-  void* dst[kStagedCols] = {(void*)b->rd.meta, (void*)b->rd.align, (void*)b->rd.qual, nullptr,
-                            (void*)b->rd.md,   (void*)b->rd.cigar, (void*)b->d_bases2, (void*)b->d_bexc};
-  const size_t esz[kStagedCols] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t), 1, 8};
+  void* dst[kStagedCols] = {(void*)b->rd.meta,  (void*)b->rd.align,  nullptr,           nullptr,
+                            (void*)b->rd.md,    (void*)b->rd.cigar,  (void*)b->d_bases2, (void*)b->d_bexc,
+                            (void*)b->d_qcodes, (void*)b->d_qbase,   (void*)b->d_qexc};
+  const size_t esz[kStagedCols] = {sizeof(ReadMeta), sizeof(ReadAlign), 1, 1, 1, sizeof(uint32_t), 1, 8, 8, 1, 8};
   hipStream_t s = S(stream);
   for (int i = 0; i < kStagedCols; ++i)
     if (S_->cnt[i] && dst[i])
@@ -917,6 +990,18 @@ bqsr_status bqsr_batch_upload_async(bqsr_batch* b, const bqsr_staged* S_, void* 
     const unsigned ge = (unsigned)std::min<int64_t>(((int64_t)S_->cnt[7] + 255) / 256, (int64_t)b->ctx->n_cu * 16);
     hipLaunchKernelGGL(bqsr_bases_exceptions, dim3(ge), dim3(256), 0, s, (const uint64_t*)b->d_bexc,
                        (int64_t)S_->cnt[7], (uint8_t*)b->rd.bases);
+  }
+  // the quals from their 16-slot chunks, then their exceptions
+  const int64_t n16 = (int64_t)S_->cnt[8];
+  if (n16) {
+    const unsigned gq = (unsigned)std::min<int64_t>((n16 + 255) / 256, (int64_t)b->ctx->n_cu * 16);
+    hipLaunchKernelGGL(bqsr_quals_expand, dim3(gq), dim3(256), 0, s, (const uint64_t*)b->d_qcodes,
+                       (const uint8_t*)b->d_qbase, n16, (int64_t)S_->cnt[2], (uint8_t*)b->rd.qual);
+  }
+  if (S_->cnt[10]) {
+    const unsigned ge = (unsigned)std::min<int64_t>(((int64_t)S_->cnt[10] + 255) / 256, (int64_t)b->ctx->n_cu * 16);
+    hipLaunchKernelGGL(bqsr_quals_exceptions, dim3(ge), dim3(256), 0, s, (const uint64_t*)b->d_qexc,
+                       (int64_t)S_->cnt[10], (uint8_t*)b->rd.qual);
   }
   HIP_TRY(hipGetLastError());
   b->prepped = false;  // new contents: the next observe / apply re-runs prep

@@ -3137,6 +3137,39 @@ extern "C" __global__ void bqsr_bases_exceptions(const uint64_t* exc, int64_t n,
   }
 }
 
+// staged quals (bqsr_batch_upload_async): a thread per 16-slot chunk, code c
+// -> base + c - 7, 0 for the zero code and (overwritten next) exceptions;
+// nq = bytes of the qual column
+extern "C" __global__ void bqsr_quals_expand(const uint64_t* codes, const uint8_t* base, int64_t n16, int64_t nq,
+                                             uint8_t* qual) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n16; t += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = codes[t];
+    const uint32_t b = (uint32_t)base[t] - 7u;
+    uint32_t out[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t c = (uint32_t)(w >> (16 * i + 4 * k)) & 15u;
+        v |= (c >= 14u ? 0u : ((b + c) & 0xFFu)) << (8 * k);
+      }
+      out[i] = v;
+    }
+    if (16 * t + 16 <= nq) {
+      *(uint4*)(qual + 16 * t) = make_uint4(out[0], out[1], out[2], out[3]);
+    } else {
+      for (int64_t k = 0; 16 * t + k < nq; ++k) qual[16 * t + k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+extern "C" __global__ void bqsr_quals_exceptions(const uint64_t* exc, int64_t n, uint8_t* qual) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = exc[i];
+    qual[e >> 8] = (uint8_t)(e & 0xFFu);
+  }
+}
+
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

@@ -25,7 +25,9 @@ def _slots(batch):
 
 def _odd_bases(b):
     """Forward reads with lowercase / non-ACGTN bytes (context index -1, Q10):
-    the staged 2-bit codes' exception list carries them."""
+    the staged 2-bit codes' exception list carries them.  And quals the
+    staged 16-slot qual chunks cannot code (a chunk spanning more than 14
+    values, qual 0): their exception list and zero code carry them."""
     from adam_amd.records import F_NEG_STRAND
     for r in range(0, b.n_reads, 37):
         if not b.flags[r] & F_NEG_STRAND and b.seq_offset[r + 1] - b.seq_offset[r] > 10:
@@ -33,6 +35,14 @@ def _odd_bases(b):
             b.seq[a + 3] = ord("x")
             b.seq[a + 7] = ord("a")
             b.seq[a + 8] = ord("N")
+    for r in range(5, b.n_reads, 29):
+        a, e = int(b.qual_offset[r]), int(b.qual_offset[r + 1])
+        if e - a > 40:
+            # (SAM chars: phred + 33)
+            b.qual[a + 17: a + 33: 2] = 33 + 4   # alternating with ~38: a chunk spanning 35 values
+            b.qual[a + 20] = 33                  # '!' (phred 0): the zero code
+            b.qual[a + 35] = 33 + 59
+            b.qual[a + 36: a + 40] = np.array([33 + 45, 33 + 58, 33 + 3, 33 + 50], np.uint8)
     return b
 
 
