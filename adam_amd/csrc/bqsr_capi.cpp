@@ -4,6 +4,7 @@
 // (bqsr_internal.h), launches the kernels of bqsr_kernels.hip and maps device
 // error words back to the reference's exception classes.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <array>
@@ -227,6 +228,15 @@ int apply_form() {
   }();
   return v;
 }
+// bucket-major copies of bucketed batches (bqsr_bucket_gather): on unless
+// ADAM_BQSR_GATHER=0 (A/B), with the chunk-walk passes (not the rows forms)
+bool gather_on() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_GATHER");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return v;
+}
 // bqsr_observe_rows' LDS: obs rows [qw][orow], mm rows [qw][wcells], masked, block histogram, context tables
 size_t rows_lds(int qw, int orow, int wcells, int hc) {
   return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes +
@@ -329,10 +339,27 @@ struct bqsr_batch {
   uint32_t* d_key_cnt = nullptr;
   uint32_t* d_cursor = nullptr;
   OrderDev order() const {
-    return bucketed ? OrderDev{d_perm, d_key_off, n_keys} : OrderDev{nullptr, nullptr, 1};
+    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, gathered ? d_oslot : nullptr} : OrderDev{nullptr, nullptr, 1};
   }
+  // bucket-major copies (bqsr_bucket_gather; valid once prepped with `gathered`):
+  // the per-base passes' ReadsDev / ReadInfo in sorted order
+  bool gathered = false;
+  ReadsDev grd{};
+  uint32_t* d_inv = nullptr;     // read -> sorted position
+  uint64_t* d_gspan = nullptr;   // sorted position -> slot span, then
+  uint64_t* d_gslot = nullptr;   //   its slot in the copies (exclusive scan)
+  ReadMeta* d_gmeta = nullptr;
+  ReadInfo* d_ginfo = nullptr;
+  uint64_t* d_oslot = nullptr;
+  uint8_t* d_gqual = nullptr;
+  uint8_t* d_gbases = nullptr;
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  const ReadsDev& pass_rd() const { return gathered ? grd : rd; }
+  ReadInfo* pass_info() const { return gathered ? d_ginfo : d_info; }
   uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
   ~bqsr_batch() {
+    if (d_scan_tmp) (void)hipFree(d_scan_tmp);
     if (d_part) (void)hipFree(d_part);
     if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
@@ -415,8 +442,9 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   for (const void* f : {(const void*)bqsr_observe_kernel<false>, (const void*)bqsr_observe_kernel<true>,
-                        (const void*)bqsr_apply_kernel,
-                        (const void*)bqsr_observe_chunks, (const void*)bqsr_observe_rows<2, true>,
+                        (const void*)bqsr_apply_kernel<false>, (const void*)bqsr_apply_kernel<true>,
+                        (const void*)bqsr_observe_chunks<false>, (const void*)bqsr_observe_chunks<true>,
+                        (const void*)bqsr_observe_rows<2, true>,
                         (const void*)bqsr_observe_rows<4, true>, (const void*)bqsr_observe_rows<2, false>,
                         (const void*)bqsr_observe_rows<4, false>, (const void*)bqsr_apply_rows<2, true>,
                         (const void*)bqsr_apply_rows<4, true>, (const void*)bqsr_apply_rows<2, false>,
@@ -424,6 +452,9 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)bqsr_bucket_gather, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)fold_hist_lds());
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)chain_lds(kMaxFoldBlocks));
@@ -1173,6 +1204,40 @@ bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
 //   BQSR_STAGE_FOLD    the expectedMismatch fold kernel
 // Exposed separately so a caller can bracket one kernel with HIP events.
 namespace {
+// bucket-major copies of a bucketed batch (bqsr_bucket_gather), after the key sort
+bqsr_status launch_gather(bqsr_context* ctx, bqsr_batch* b, hipStream_t s) {
+  const int64_t n = b->rd.n_reads;
+  bqsr_status st;
+  if (!b->d_inv) {  // once per batch
+    const size_t nr = (size_t)std::max<int64_t>(1, n);
+    if ((st = dalloc(b->allocs, &b->d_inv, nr)) != BQSR_OK || (st = dalloc(b->allocs, &b->d_gspan, nr)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &b->d_gslot, nr)) != BQSR_OK || (st = dalloc(b->allocs, &b->d_gmeta, nr)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &b->d_ginfo, nr)) != BQSR_OK || (st = dalloc(b->allocs, &b->d_oslot, nr)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &b->d_gqual, (size_t)b->rd.n_slots + 64)) != BQSR_OK ||
+        (st = dalloc(b->allocs, &b->d_gbases, (size_t)(b->rd.n_slots + 1) / 2 + 64)) != BQSR_OK)
+      return st;
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, b->d_gspan, b->d_gslot, (int)n, s));
+    HIP_TRY(hipMalloc(&b->d_scan_tmp, std::max<size_t>(tb, 16)));
+    b->scan_tmp_bytes = std::max<size_t>(tb, 16);
+    b->grd = b->rd;
+    b->grd.meta = b->d_gmeta;
+    b->grd.qual = b->d_gqual;
+    b->grd.bases = b->d_gbases;
+  }
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8);
+  hipLaunchKernelGGL(bqsr_key_inverse, dim3(g), dim3(256), 0, s, (const uint32_t*)b->d_perm,
+                     (const ReadMeta*)b->rd.meta, n, b->d_inv, b->d_gspan);
+  size_t tb = b->scan_tmp_bytes;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(b->d_scan_tmp, tb, b->d_gspan, b->d_gslot, (int)n, s));
+  HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
+  hipLaunchKernelGGL(bqsr_bucket_gather, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd,
+                     b->d_info, (const uint32_t*)b->d_inv, (const uint64_t*)b->d_gslot, b->n_blocks, lane_shift(b),
+                     b->d_hq, b->d_gmeta, b->d_ginfo, b->d_oslot, b->d_gqual, b->d_gbases);
+  HIP_TRY(hipGetLastError());
+  return BQSR_OK;
+}
+
 bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
   HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
   if (b->rd.n_reads > 0) {
@@ -1213,6 +1278,11 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
       hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
                          b->d_cursor, b->d_perm);
       HIP_TRY(hipGetLastError());
+      b->gathered = gather_on() && b->rd.slots_aligned && observe_form() <= 0 && apply_form() == 0;
+      if (b->gathered) {
+        const bqsr_status gst = launch_gather(ctx, b, s);
+        if (gst != BQSR_OK) return gst;
+      }
     }
   }
   b->prepped = true;
@@ -1240,9 +1310,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     return fail(BQSR_ERR_INVALID_ARG, "observe kernel before the prep stage (or with other known sites)");
   if (stages & BQSR_STAGE_KERNEL) {
     ObserveParams P{};
-    P.rd = b->rd;
+    P.rd = b->pass_rd();
     P.ord = b->order();
-    P.info = b->d_info;
+    P.info = b->pass_info();
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
     // window row length padded to 2 mod 4 words: the lanes of a wavefront add
@@ -1317,7 +1387,8 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
         hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, true> : bqsr_observe_rows<2, true>), dim3(b->n_blocks),
                            dim3(kBlockThreads), lds, s, P);
     } else if (form == 0)
-      hipLaunchKernelGGL(bqsr_observe_chunks, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+      hipLaunchKernelGGL((b->gathered ? bqsr_observe_chunks<true> : bqsr_observe_chunks<false>), dim3(b->n_blocks),
+                         dim3(kBlockThreads), lds, s, P);
     else if (form == 2 || chunk_lanes(b->bucketed))
       hipLaunchKernelGGL((bqsr_observe_kernel<true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else
@@ -1330,7 +1401,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-    if (b->bucketed && !b->hq_by_observe) {  // the observe kernel did not walk the fold's blocks: their histograms
+    if (b->bucketed && !b->hq_by_observe && !b->gathered) {  // the observe kernel did not walk the fold's blocks: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
                          b->n_blocks, lane_shift(b), b->d_hq);
@@ -1644,9 +1715,9 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   if (b->rd.n_reads == 0 || !(stages & BQSR_STAGE_KERNEL)) return ok();
   ApplyParams P{};
-  P.rd = b->rd;
+  P.rd = b->pass_rd();
   P.ord = b->order();
-  P.info = b->d_info;
+  P.info = b->pass_info();
   P.g = geom(L->dims);
   const int cw = window_cw(b, P.g);
   P.w = window_rows(b, apply_rows(cw));
@@ -1720,7 +1791,8 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
   hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
   const size_t lds = apply_lds(P.w.qw, cw);
-  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+  hipLaunchKernelGGL((b->gathered ? bqsr_apply_kernel<true> : bqsr_apply_kernel<false>), dim3(b->n_blocks),
+                     dim3(kBlockThreads), lds, s, P);
   HIP_TRY(hipGetLastError());
   return ok();
 }

@@ -182,6 +182,11 @@ struct OrderDev {
   const uint32_t* perm;    // [n_reads] or nullptr (identity, one piece per workgroup, group = Window::rg_lo)
   const int64_t* key_off;  // [n_keys + 1]
   int32_t n_keys;          // 2 * n_rg when bucketed
+  // gathered (bqsr_bucket_gather): the passes' ReadsDev / ReadInfo hold the
+  // reads in sorted order (record i = sorted position i, its quals and base
+  // codes copied bucket-major); oslot[i] = the read's slot in the batch (slot
+  // bitmap, outputs), perm[i] its index.  nullptr: records are read indices.
+  const uint64_t* oslot = nullptr;
 };
 
 struct ObserveParams {

@@ -951,8 +951,10 @@ __device__ __forceinline__ void revcomp_window(uint64_t& lo, uint32_t& hi) {
 
 // Per-lane read decode shared by observe and apply.
 struct LaneRead {
-  int64_t r;      // read index
-  uint64_t slot;  // first base slot
+  int64_t r;      // record index (into rd.meta / info)
+  int64_t ro;     // the read's index in the batch (errors, per-read outputs): r, or perm[r] when gathered
+  uint64_t slot;  // first base slot of rd's qual / base columns
+  uint64_t oslot; // its slot in the batch (slot bitmap, output): slot, or OrderDev::oslot[r] when gathered
   int st, en;     // visited offsets [st, en)
   int fl;         // kInfo* bits
   bool trimmed;   // st / en computed here (kInfoTrim): observe writes the ReadInfo back
@@ -965,6 +967,7 @@ struct LaneRead {
 __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L) {
   LaneRead x;
   x.r = live ? r : rd.n_reads;
+  x.ro = x.r;
   ReadMeta m{0, 0, 0, 0, 0};
   ReadInfo inf{0, 0, 0, 0};
   if (live) {
@@ -975,6 +978,7 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
   inf = resolve_info(rd, inf, m.slot, m.lq);
   x.inf = inf;
   x.slot = m.slot;
+  x.oslot = m.slot;
   x.fl = inf.fl;
   x.rg = m.rg;
   x.lq = m.lq;
@@ -1021,6 +1025,9 @@ __device__ __forceinline__ int key_at(const OrderDev& o, int64_t p) {
   return lo;
 }
 __device__ __forceinline__ int64_t order_read(const OrderDev& o, int64_t i) { return o.perm ? (int64_t)o.perm[i] : i; }
+// the record of sorted position i in the passes' columns: i itself when the
+// batch's columns were gathered into sorted order (bqsr_bucket_gather)
+__device__ __forceinline__ int64_t order_rec(const OrderDev& o, int64_t i) { return o.oslot ? i : order_read(o, i); }
 // the read group of a key's window rows
 __device__ __forceinline__ int key_rg(const OrderDev& o, int key, int rg_lo) { return o.perm ? key >> 1 : rg_lo; }
 // the cycle cells a piece's windows hold: all of them in read order, the
@@ -1250,13 +1257,17 @@ constexpr uint32_t kPkRev = 0x8000u;  // packed flags: cycle direction -1
 // (fchunk(x, j, n, on, ld)), so a lane has kU chunks' loads in flight; x
 // holds r, slot, st, en, fl, rg, cell0 and dir of the chunk's read, j = jb +
 // 16k, n = en - st.
-template <uint32_t kAct, int kU, class LD, class FRead, class FLoad, class FChunk>
+template <uint32_t kAct, int kU, class LD, bool kG, class FRead, class FLoad, class FChunk>
 __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* info, const OrderDev& ord, int64_t q0,
                                            int64_t q1, int64_t qstep, int L, int lane, uint32_t* mk, FRead&& fread,
                                            FLoad&& fload, FChunk&& fchunk) {
   for (int64_t wb = q0; wb < q1; wb += qstep) {
     const bool live = wb + lane < q1;
-    const LaneRead x = lane_read(rd, info, live ? order_read(ord, wb + lane) : 0, live, L);
+    LaneRead x = lane_read(rd, info, live ? (kG ? wb + lane : order_read(ord, wb + lane)) : 0, live, L);
+    if (kG) {  // gathered columns (OrderDev::oslot): the read's own index and slot
+      x.ro = live ? order_read(ord, wb + lane) : rd.n_reads;
+      x.oslot = live ? ord.oslot[wb + lane] : 0;
+    }
     fread(x, live);
     const int n = (live && (x.fl & kAct)) ? x.en - x.st : 0;
     const int jb = rd.slots_aligned ? -(x.st & 15) : 0;
@@ -1264,6 +1275,8 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
     const uint32_t pe = wave_incl_add(nch), ps = pe - nch;
     const uint32_t total = __builtin_amdgcn_readlane(pe, 63);
     const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
+    const uint32_t p_ro = kG ? (uint32_t)x.ro : 0u, p_oslo = kG ? (uint32_t)x.oslot : 0u,
+                   p_oshi = kG ? (uint32_t)(x.oslot >> 32) : 0u;
     const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
     const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
     const uint32_t p_rg = (uint32_t)x.rg;
@@ -1287,6 +1300,13 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
         const int ri = (int)wave_incl_max(v);
         c[u].r = bperm(ri, p_r);
         c[u].slot = ((uint64_t)bperm(ri, p_shi) << 32) | bperm(ri, p_slo);
+        if (kG) {
+          c[u].ro = bperm(ri, p_ro);
+          c[u].oslot = ((uint64_t)bperm(ri, p_oshi) << 32) | bperm(ri, p_oslo);
+        } else {
+          c[u].ro = c[u].r;
+          c[u].oslot = c[u].slot;
+        }
         const uint32_t se = bperm(ri, p_se), fl = bperm(ri, p_fl);
         c[u].st = (int)(se & 0xFFFFu);
         c[u].en = (int)(se >> 16);
@@ -1598,7 +1618,7 @@ __device__ __forceinline__ ObsChunkLoads observe_load(const ObserveParams& P, co
   v.qs = *(const uint4*)(P.rd.qual + x.slot + o0);
   if (x.fl & kInfoObs) {
     v.cr = chunk_raw(P.rd, chunk_n0(x, o0));
-    const uint64_t s0 = x.slot + (uint64_t)o0;
+    const uint64_t s0 = x.oslot + (uint64_t)o0;
     v.bw0 = P.sbits[s0 >> 5];
     if ((s0 & 31) > 16) v.bw1 = P.sbits[(s0 >> 5) + 1];  // an unaligned layout's chunk across two words
   }
@@ -1622,7 +1642,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
   uint32_t bm = 0, bx = 0;
   uint32_t xo[4] = {4u, 4u, 4u, 4u};
   if (full) {
-    const uint32_t sb = (uint32_t)((x.slot + (uint64_t)o0) & 31);
+    const uint32_t sb = (uint32_t)((x.oslot + (uint64_t)o0) & 31);
     bm = __builtin_amdgcn_alignbit((uint32_t)ld.bw1, (uint32_t)ld.bw0, sb);
     bx = __builtin_amdgcn_alignbit((uint32_t)(ld.bw1 >> 32), (uint32_t)(ld.bw0 >> 32), sb);
     chunk_ctx(P.rd, x.fl & kInfoNeg, chunk_n0(x, o0), ld.cr, j, pc.tb, xo);
@@ -1671,7 +1691,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
       const int o = o0 + k;
       const int q = (int)(int8_t)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
       if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-        report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+        report(P.err, err_key((uint64_t)x.ro, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
       } else if (full) {  // outside the LDS window: straight to the int64 table
         const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
         const int ccell = cc0 + __mul24(x.dir, k);
@@ -1694,6 +1714,9 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
 
 constexpr int kObserveU = 2;  // chunks in flight per lane
 
+// kG: the batch's columns gathered into sorted order (OrderDev::oslot; a
+// kernel of its own: the gathered walk's extra fields cost registers)
+template <bool kG>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, L = P.g.L;
@@ -1723,13 +1746,15 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
                       wcells, ident, (uint32_t)(uintptr_t)(LdsHalves)ctab};
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
-    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads>(
-        P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk,
-        [&](const LaneRead& x, bool live) {
-          if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
-        },
-        [&](const LaneRead& x, int j, bool on) { return observe_load(P, x, j, on); },
-        [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) { observe_chunk(P, pc, x, j, n, on, ld); });
+    const auto fread = [&](const LaneRead& x, bool live) {
+      if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+    };
+    const auto fload = [&](const LaneRead& x, int j, bool on) { return observe_load(P, x, j, on); };
+    const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) {
+      observe_chunk(P, pc, x, j, n, on, ld);
+    };
+    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, kG>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+                                                                      64 * kWaves, L, lane, mk, fread, fload, fchunk);
     __syncthreads();
     // ---- the piece's window -> its slab; window rows into the block histogram ----
     uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
@@ -2383,6 +2408,107 @@ __device__ __forceinline__ bool err_prob(int64_t obs, int64_t mm, double mre, do
 }
 
 // one workgroup: groups, globals, average, then a2 per (rg, q)
+// ---- bucket-major copies of a bucketed batch (cfg4: several read groups) ----
+// The bucketed passes visit reads in key order, where a read's neighbours in
+// memory belong to other keys and are visited at other times: most of every
+// cache line a pass touches was fetched for one read (PMC fetch 2.2x apply,
+// 3.1x observe the algorithmic bytes on cfg4, against 1.3x in read order).
+// So once per job the reads' quals, base codes, records and ReadInfo are
+// copied into sorted order (record p = sorted position p), and both passes
+// stream through them; the slot bitmap and the outputs stay in the batch's
+// layout (OrderDev::oslot).
+// Sorted position p -> the read's index (perm) and slot span; read r -> p.
+extern "C" __global__ void bqsr_key_inverse(const uint32_t* perm, const ReadMeta* meta, int64_t n, uint32_t* inv,
+                                            uint64_t* span) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = perm[p];
+    const ReadMeta m = meta[r];
+    inv[r] = (uint32_t)p;
+    span[p] = slot_span(m.lq, m.ls);
+  }
+}
+
+// In read order (coalesced reads; each read's spans written whole at its
+// sorted slot gslot[inv[r]]): a read's quals and base codes, its record with
+// the new slot, its ReadInfo with the trimming resolved (also written back in
+// place for the fold), and -- bqsr_fold_hist's work, which this replaces --
+// the fold's per-block quality histograms of the folded bases.  Lanes as in
+// bqsr_fold_hist: 2^ls lanes per read, 64 slots each.  Aligned layout only
+// (every read's span a multiple of 16 slots).
+extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_bucket_gather(
+    ReadsDev rd, ReadInfo* info, const uint32_t* inv, const uint64_t* gslot, int32_t n_blocks, int32_t ls,
+    uint32_t* hq_block, ReadMeta* gmeta, ReadInfo* ginfo, uint64_t* oslot, uint8_t* gqual, uint8_t* gbases) {
+  extern __shared__ uint32_t fh_smem[];
+  uint32_t* hist = fh_smem;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < kFhWaves * kFhCopies * kFhStride; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const int blk = blockIdx.x / kFhSplit, part = blockIdx.x - blk * kFhSplit;
+  const int64_t b0 = wg_begin(rd, blk, n_blocks), b1 = wg_begin(rd, blk + 1, n_blocks);
+  const int64_t r0 = b0 + (b1 - b0) * part / kFhSplit, r1 = b0 + (b1 - b0) * (part + 1) / kFhSplit;
+  uint32_t* hw = hist + (wv * kFhCopies + (lane & (kFhCopies - 1))) * kFhStride;
+  const int sub = lane & ((1 << ls) - 1), rl = lane >> ls, rpw = 64 >> ls;
+  for (int64_t g0 = r0 + (int64_t)rpw * wv; g0 < r1; g0 += (int64_t)rpw * kFhWaves) {
+    const int64_t r = g0 + rl;
+    int span = 0, st = 0, en = 0;
+    uint64_t src = 0, dst = 0;
+    if (r < r1) {
+      const ReadMeta m = rd.meta[r];
+      const ReadInfo raw = info[r];
+      const ReadInfo inf = resolve_info(rd, raw, m.slot, m.lq);
+      const uint32_t p = inv[r];
+      src = m.slot;
+      dst = gslot[p];
+      span = (int)slot_span(m.lq, m.ls);
+      if ((inf.fl & kInfoObs) && inf.en > inf.st) {
+        st = inf.st;
+        en = inf.en;
+      }
+      if (sub == 0) {
+        ReadMeta gm = m;
+        gm.slot = dst;
+        gmeta[p] = gm;
+        ginfo[p] = inf;
+        oslot[p] = m.slot;
+        if (raw.fl & kInfoTrim) info[r] = inf;  // the fold reads the trimmed range
+      }
+    }
+    for (int j0 = kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < span); j0 += kSuper << ls) {
+      if (j0 >= span) continue;
+      uint4 v[kSub];
+      uint2 b[kSub];
+#pragma unroll
+      for (int i = 0; i < kSub; ++i) {
+        const int o = j0 + kChunk * i;
+        v[i] = o < span ? *(const uint4*)(rd.qual + src + o) : make_uint4(0, 0, 0, 0);
+        b[i] = o < span ? *(const uint2*)(rd.bases + ((src + o) >> 1)) : make_uint2(0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < kSub; ++i) {
+        const int o = j0 + kChunk * i;
+        if (o >= span) continue;
+        *(uint4*)(gqual + dst + o) = v[i];
+        *(uint2*)(gbases + ((dst + o) >> 1)) = b[i];
+        // folded bases: offsets [st, en) of usable reads
+        const int lo = max(st - o, 0), hi = min(en - o, kChunk);
+        const uint32_t vm = hi > lo ? ((hi >= 16 ? 0xFFFFu : (1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+        if (__builtin_amdgcn_ballot_w64(vm != 0)) {
+          const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+          for (int k = 0; k < kChunk; ++k)  // (an offset outside adds 0: no branch per byte)
+            atomicAdd(&hw[__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 7)], __builtin_amdgcn_ubfe(vm, k, 1));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < kQBins; q += blockDim.x) {
+    uint32_t s = 0;
+    for (int i = 0; i < kFhWaves * kFhCopies; ++i) s += hist[i * kFhStride + q];
+    if (s) atomicAdd(&hq_block[(int64_t)blk * kQBins + q], s);
+  }
+}
+
 extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_t* touched, const int64_t* qk_obs,
                                                                       const int64_t* qk_mm, TableGeom g, int32_t n_rg,
                                                                       double em_host, const double* em_dev,
@@ -2573,11 +2699,11 @@ __device__ __forceinline__ uint4 apply_slow(const ApplyParams* Pp, LaneRead x, i
     const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
     const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
     if (!grp || !kok) {
-      report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
+      report(P.err, err_key((uint64_t)x.ro, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
       continue;
     }
     if (q < 0) {
-      report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+      report(P.err, err_key((uint64_t)x.ro, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
       continue;
     }
     if (!app) continue;
@@ -2588,7 +2714,7 @@ __device__ __forceinline__ uint4 apply_slow(const ApplyParams* Pp, LaneRead x, i
     const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
     if (code > 0xFFu) {
       const unsigned long long e = atomicAdd(P.n_exc, 1ull);
-      if ((int64_t)e < P.max_exc) P.exc[e] = ((x.slot + (uint64_t)o) << 16) | code;
+      if ((int64_t)e < P.max_exc) P.exc[e] = ((x.oslot + (uint64_t)o) << 16) | code;
     }
     // byte k := code
     const uint64_t m = 0xFFull << (8 * (k & 7)), v = (uint64_t)(code & 0xFFu) << (8 * (k & 7));
@@ -2674,7 +2800,7 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     }
   }
   if (app || pass) {
-    uint8_t* op = P.out_qual + x.slot;
+    uint8_t* op = P.out_qual + x.oslot;
     if (j + kChunk <= n || P.rd.slots_aligned) {  // aligned: the chunk's other bytes are this read's scratch
       *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
     } else {
@@ -2724,6 +2850,7 @@ extern "C" __global__ void bqsr_apply_chars(ApplyParams P, uint8_t* chars) {
   }
 }
 
+template <bool kG>  // (as bqsr_observe_chunks)
 __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
@@ -2777,20 +2904,23 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     __syncthreads();
     const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb, (int)clean_rows[0],
                         (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C};
-    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads>(
-        P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk,
-        [&](const LaneRead& x, bool live) {
-          if (!live) return;
-          if (x.fl & kInfoPass) {  // quality string passed through
-            P.out_start[x.r] = 0;
-            P.out_len[x.r] = (uint32_t)x.en;
-          } else {
-            P.out_start[x.r] = (uint32_t)x.st;
-            P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
-          }
-        },
-        [&](const LaneRead& x, int j, bool on) { return apply_load(P, x, j, on); },
-        [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) { apply_chunk(P, &P, pc, x, j, n, on, ld); });
+    const auto fread = [&](const LaneRead& x, bool live) {
+      if (!live) return;
+      if (x.fl & kInfoPass) {  // quality string passed through
+        P.out_start[x.ro] = 0;
+        P.out_len[x.ro] = (uint32_t)x.en;
+      } else {
+        P.out_start[x.ro] = (uint32_t)x.st;
+        P.out_len[x.ro] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
+      }
+    };
+    const auto fload = [&](const LaneRead& x, int j, bool on) { return apply_load(P, x, j, on); };
+    const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
+      apply_chunk(P, &P, pc, x, j, n, on, ld);
+    };
+    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, kG>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+                                                                             64 * kWaves, L, lane, mk, fread, fload,
+                                                                             fchunk);
   }  // pieces
 }
 
@@ -3061,6 +3191,10 @@ template __global__ void bqsr_apply_rows<4, false>(ApplyParams);
 
 template __global__ void bqsr_observe_kernel<false>(ObserveParams);
 template __global__ void bqsr_observe_kernel<true>(ObserveParams);
+template __global__ void bqsr_observe_chunks<false>(ObserveParams);
+template __global__ void bqsr_observe_chunks<true>(ObserveParams);
+template __global__ void bqsr_apply_kernel<false>(ApplyParams);
+template __global__ void bqsr_apply_kernel<true>(ApplyParams);
 
 // RecalTable.++ over partitions in a declared order (RecalTable.scala:90-108):
 // expectedMismatch = ((0.0 + e_0) + e_1) + ... -- one lane, each `+` one IEEE

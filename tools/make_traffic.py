@@ -6,7 +6,7 @@ import json
 import sys
 
 STAGES = (("prep_complex", "bqsr_prep_complex"), ("prep", "bqsr_prep_kernel"), ("observe", "bqsr_observe"),
-          ("apply", "bqsr_apply_kernel"), ("fold_hist", "bqsr_fold_hist"))
+          ("apply", "bqsr_apply_kernel"), ("fold_hist", "bqsr_fold_hist"), ("gather", "bqsr_bucket_gather"))
 
 summ = json.load(open(sys.argv[1]))
 kernels = {}
