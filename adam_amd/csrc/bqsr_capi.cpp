@@ -228,12 +228,24 @@ int apply_form() {
   }();
   return v;
 }
-// bucket-major copies of bucketed batches (bqsr_bucket_gather): on unless
-// ADAM_BQSR_GATHER=0 (A/B), with the chunk-walk passes (not the rows forms)
+// known sites as sorted lists only (no position bitmaps): ADAM_BQSR_SITES_BITMAP=0 (A/B)
+bool sites_bitmap_off() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_SITES_BITMAP");
+    return e && strcmp(e, "0") == 0;
+  }();
+  return v;
+}
+// bucket-major copies of bucketed batches (bqsr_bucket_gather), opt-in with
+// ADAM_BQSR_GATHER=1 (chunk-walk passes only).  Measured (round 3, cfg4, one
+// box): the passes over the copies ran faster (apply 5.37 -> 3.91 ms, observe
+// 4.47 -> 3.77 ms, no bqsr_fold_hist: -3.6 ms), but the copy itself -- each
+// read's spans written at its sorted slot, random 128-256 B writes -- took
+// 6.54 ms (+0.59 ms for the inverse permutation): 12.97 -> 16.91 ms a job.
 bool gather_on() {
   static const bool v = [] {
     const char* e = getenv("ADAM_BQSR_GATHER");
-    return !(e && strcmp(e, "0") == 0);
+    return e && strcmp(e, "1") == 0;
   }();
   return v;
 }
@@ -511,7 +523,7 @@ bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, con
     // common path), unless it would hold over 64 words per site
     const int64_t b0 = v.empty() ? 0 : (int64_t)((uint64_t)base & ~(uint64_t)63);  // floor to 64
     const int64_t nw = v.empty() ? 0 : ((v.back() - b0) >> 6) + 1;
-    const bool dense = nw > 0 && nw <= 64 * (int64_t)v.size() + 64 && nw <= (int64_t(1) << 28);
+    const bool dense = !sites_bitmap_off() && nw > 0 && nw <= 64 * (int64_t)v.size() + 64 && nw <= (int64_t(1) << 28);
     if (dense) {
       const size_t w0 = bm.size();
       bm.resize(w0 + (size_t)nw, 0ull);
