@@ -32,7 +32,7 @@ EXPORTS = [
     "bqsr_lut_destroy", "bqsr_lut_stats", "bqsr_lut_shifts", "bqsr_apply", "bqsr_apply_records",
     "bqsr_stage_records", "bqsr_staged_destroy", "bqsr_staged_bytes", "bqsr_staged_reads", "bqsr_staged_bases",
     "bqsr_batch_create_staged", "bqsr_batch_upload_async", "bqsr_em_fold_async", "bqsr_batch_em_copy_async",
-    "bqsr_finalize_device", "bqsr_observe_stage", "bqsr_apply_stage", "bqsr_job_reset_async", "bqsr_job_result",
+    "bqsr_finalize_device", "bqsr_observe_stage", "bqsr_apply_stage", "bqsr_job_reset_async", "bqsr_job_result", "bqsr_copy_async",
     "bqsr_job_errors_export_async", "bqsr_job_errors_import_async", "bqsr_job_status_async", "bqsr_job_status_get",
 ]
 
@@ -151,6 +151,7 @@ def lib():
             "bqsr_apply_records": (ctypes.c_int, [vp, vp, vp, vp, vp]),
             "bqsr_job_reset_async": (ctypes.c_int, [vp, vp, vp]),
             "bqsr_job_result": (ctypes.c_int, [vp, vp, ctypes.POINTER(dbl), ctypes.POINTER(i64), vp]),
+            "bqsr_copy_async": (ctypes.c_int, [vp, vp, vp, i64, vp]),
             "bqsr_job_errors_export_async": (ctypes.c_int, [vp, i64, vp, vp]),
             "bqsr_job_errors_import_async": (ctypes.c_int, [vp, vp, vp]),
             "bqsr_job_status_async": (ctypes.c_int, [vp, vp, i32, vp]),

@@ -1963,6 +1963,22 @@ bqsr_status bqsr_job_status_get(const bqsr_batch* b, int32_t slot, int32_t part,
   return from_err_key(std::min(h[kErrAppPrep], h[kErrAppKern]), 0);
 }
 
+bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64_t bytes, void* stream) {
+  if (!ctx || bytes < 0 || (bytes && (!dst || !src))) return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_async: bad arguments");
+  if (!bytes) return ok();
+  HIP_TRY(hipSetDevice(ctx->device));
+  const bool vec = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+  const int64_t n16 = vec ? bytes / 16 : 0;
+  const int64_t head = 16 * n16, tail = bytes - head;
+  if (tail > 1 << 20) return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_async: unaligned buffers above 1 MiB");
+  const int64_t need = std::max<int64_t>((n16 + 255) / 256, (tail + 255) / 256);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)ctx->n_cu * 8));
+  hipLaunchKernelGGL(bqsr_copy16, dim3(g), dim3(256), 0, S(stream), (const uint4*)src, (uint4*)dst, n16,
+                     (const uint8_t*)src + head, (uint8_t*)dst + head, (int32_t)tail);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
 bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_exceptions, void* stream) {
   if (!b || !L) return fail(BQSR_ERR_INVALID_ARG, "null");
   HIP_TRY(hipSetDevice(b->ctx->device));

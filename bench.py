@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--stream-mode", default="pipe", choices=("pipe", "serial", "zerocopy"),
                     help="cfg5: jobs pipelined over both link directions, one at a time, or pipelined with "
                          "apply writing into pinned host memory")
+    ap.add_argument("--d2h", default="kernel", choices=("kernel", "dma"),
+                    help="cfg5: results copied back by a kernel (beside the DMA uploads) or by DMA copies")
     return ap.parse_args()
 
 
@@ -323,7 +325,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
     pr = max(1, args.part_reads)
     dims = Dims(cfg["n_rg"], max(cfg["lens"]))
     t_gen = time.time()
-    sh = StreamedShard(ctx, [], dims, None, dev.index, zero_copy=args.stream_mode == "zerocopy")
+    sh = StreamedShard(ctx, [], dims, None, dev.index, zero_copy=args.stream_mode == "zerocopy", d2h=args.d2h)
     first = None
     for i, r0 in enumerate(range(0, n_reads, pr)):
         part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"],
@@ -408,6 +410,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
                 "known_sites": 0,
                 "partitions_per_gpu": parts_n,
                 "stream_mode": args.stream_mode,
+                "d2h": args.d2h,
                 "parallelism": "dp%d: read shards per GPU, RCCL int64 table all-reduce" % world,
             },
             "roofline": {

@@ -329,6 +329,14 @@ int bqsr_lut_group(const bqsr_lut* l, int32_t r, int64_t* obs, int64_t* mm);
  * out[i] = largest p with phred(p) >= qmin + i; returns the entry count */
 int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin);
 
+/* A copy by a kernel on `stream` (either side may be pinned host memory the
+ * device can address): the streamed path's D2H of results, which then runs
+ * beside the DMA engines' H2D of the next partitions instead of sharing them
+ * (tools/link_probe.hip).  16-B aligned buffers of any size, or unaligned
+ * ones up to 1 MiB.  Replaces, for the JNI side, the memcpy of a partition's
+ * output buffers back into the executor's direct buffers. */
+bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64_t bytes, void* stream);
+
 /* One job's launches with the fewest host round trips (what bench.py's step
  * runs): the table zeroed and the batch's error words reset in one kernel
  * (replaces bqsr_table_zero_async and the BQSR_STAGE_RESET stages), and, after

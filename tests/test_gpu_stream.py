@@ -46,12 +46,13 @@ def _odd_bases(b):
     return b
 
 
-@pytest.mark.parametrize("sizes,lens,n_rg,with_sites,odd,zero_copy", [
-    ((7000, 5000, 9000), (150,), 1, True, False, False),
-    ((3000, 1, 4000), (100, 250), 4, False, False, False),
-    ((4000, 6000), (101,), 2, False, True, False),
-    ((5000, 3000), (150,), 1, True, True, True)])
-def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy):
+@pytest.mark.parametrize("sizes,lens,n_rg,with_sites,odd,zero_copy,d2h", [
+    ((7000, 5000, 9000), (150,), 1, True, False, False, "kernel"),
+    ((3000, 1, 4000), (100, 250), 4, False, False, False, "kernel"),
+    ((4000, 6000), (101,), 2, False, True, False, "dma"),
+    ((4000, 6001), (101,), 2, False, True, False, "kernel"),
+    ((5000, 3000), (150,), 1, True, True, True, "kernel")])
+def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy, d2h):
     import torch
     from adam_amd.stream import StreamedShard
     dev = torch.device("cuda", 0)
@@ -68,7 +69,7 @@ def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy):
     th = ctypes.c_void_p()
     _capi.check(L.bqsr_table_create(ctx.handle, d, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
     sh = StreamedShard(ctx, parts, d, snp.handle(ctx) if snp else None, 0,
-                       site_contigs=snp.contigs if snp else None, zero_copy=zero_copy)
+                       site_contigs=snp.contigs if snp else None, zero_copy=zero_copy, d2h=d2h)
     try:
         for _ in range(2):  # the second job re-uploads over the resident partitions
             em_t = sh.run(th)
