@@ -1963,6 +1963,16 @@ bqsr_status bqsr_job_status_get(const bqsr_batch* b, int32_t slot, int32_t part,
   return from_err_key(std::min(h[kErrAppPrep], h[kErrAppKern]), 0);
 }
 
+// workgroups of a kernel copy: enough stores in flight for the link, few
+// enough CUs that the compute streams' kernels keep running beside it
+// (ADAM_BQSR_COPY_BLOCKS, default 128)
+static int64_t copy_blocks(const bqsr_context* ctx) {
+  static const int64_t v = [] {
+    const char* e = getenv("ADAM_BQSR_COPY_BLOCKS");
+    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)128;
+  }();
+  return std::min<int64_t>(v, (int64_t)ctx->n_cu * 8);
+}
 bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64_t bytes, void* stream) {
   if (!ctx || bytes < 0 || (bytes && (!dst || !src))) return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_async: bad arguments");
   if (!bytes) return ok();
@@ -1972,7 +1982,7 @@ bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64
   const int64_t head = 16 * n16, tail = bytes - head;
   if (tail > 1 << 20) return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_async: unaligned buffers above 1 MiB");
   const int64_t need = std::max<int64_t>((n16 + 255) / 256, (tail + 255) / 256);
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)ctx->n_cu * 8));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, copy_blocks(ctx)));
   hipLaunchKernelGGL(bqsr_copy16, dim3(g), dim3(256), 0, S(stream), (const uint4*)src, (uint4*)dst, n16,
                      (const uint8_t*)src + head, (uint8_t*)dst + head, (int32_t)tail);
   HIP_TRY(hipGetLastError());
