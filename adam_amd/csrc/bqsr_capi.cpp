@@ -24,6 +24,7 @@ using namespace bqsr;
 
 // the kernels are compiled in this translation unit (one HIP module)
 #include "bqsr_kernels.hip"
+#include "bqsr_observe_lean.hip"
 #include "bqsr_fold.hip"
 
 // ------------------------------------------------------------- errors -----
@@ -182,6 +183,13 @@ size_t observe_lds(int qw, int wcells, bool table) {
 // a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
 int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
 size_t apply_lds(int qw, int cw) { return 16 + (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)piece_bytes(qw, cw); }
+// bqsr_observe_lean: obs rows qw + 2 (pad, dump), mm rows qw, masked qw, block histogram
+size_t lean_lds(int qw, int wcells) { return ((size_t)(2 * qw + 2) * wcells + qw + kQBins) * 4; }
+int lean_rows(int wcells) {
+  int qw = kQBins;
+  while (qw > 1 && lean_lds(qw, wcells) > kLdsMax) --qw;
+  return qw;
+}
 int observe_rows(int wcells, bool table) {
   int qw = kQBins;
   while (qw > 1 && observe_lds(qw, wcells, table) > kLdsMax) --qw;
@@ -215,7 +223,12 @@ int lane_shift(const bqsr_batch* b);
 int observe_form() {
   static const int v = [] {
     const char* e = getenv("ADAM_BQSR_OBSERVE");
-    return !e ? -1 : strcmp(e, "read") == 0 ? 1 : strcmp(e, "superchunk") == 0 ? 2 : strcmp(e, "rows") == 0 ? 3 : 0;
+    return !e                            ? -1
+           : strcmp(e, "read") == 0       ? 1
+           : strcmp(e, "superchunk") == 0 ? 2
+           : strcmp(e, "rows") == 0       ? 3
+           : strcmp(e, "lean") == 0       ? 4
+                                          : 0;
   }();
   return v;
 }
@@ -1333,7 +1346,13 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     // words: 7.6 ms observe; 225: 5.8; cfg2 222 against 223 / 224: 0.94 /
     // 1.00 / 1.25 ms).  ADAM_BQSR_WMOD=r pads to r mod 32 instead (A/B), -1
     // not at all.  Pad words stay 0.
-    P.wcells = window_cw(b, P.g) + kCtxSlots;
+    // the lean lane per read (read order) is the default; ADAM_BQSR_OBSERVE=read / superchunk / rows /
+    // chunks select the others
+    const int form = observe_form() >= 0 && !(observe_form() == 4 && b->bucketed) ? observe_form()
+                     : b->bucketed                                               ? 0
+                                                                                 : 4;
+    const bool lean = form == 4;
+    P.wcells = window_cw(b, P.g) + (lean ? kCtxCells : kCtxSlots);
     if (window_mod() == -2)
       while ((P.wcells & 3) != 2) ++P.wcells;
     else if (window_mod() >= 0)
@@ -1343,7 +1362,6 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     // measured (round 3, cfg2 / cfg4): the lane-per-offset rows kernel is SALU-bound (2.7e9 scalar
     // instructions per cfg2 launch, 6.0 ms) -- opt-in only; the chunk walk wins on bucketed batches
     // (4.63 vs 5.03 ms cfg4), the lane per read on read order (1.00 vs 1.16 ms cfg2)
-    const int form = observe_form() >= 0 ? observe_form() : (b->bucketed ? 0 : 1);
     if (form == 3) {
       // bqsr_observe_rows: the most context copies (and, bucketed, fold
       // histogram copies) whose rows still hold the batch's qual span (fewer
@@ -1365,7 +1383,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
         }
       P.w = window_rows(b, best_rows);
     } else {
-      P.w = window_rows(b, observe_rows(P.wcells, form == 0));
+      P.w = window_rows(b, lean ? lean_rows(P.wcells) : observe_rows(P.wcells, form == 0));
     }
     P.touched = t->touched();
     P.obs = t->obs();
@@ -1386,11 +1404,15 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
-    const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc) : observe_lds(P.w.qw, P.wcells, form == 0);
+    const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc)
+                       : lean    ? lean_lds(P.w.qw, P.wcells)
+                                 : observe_lds(P.w.qw, P.wcells, form == 0);
     P.lane_shift = lane_shift(b);
     b->hq_by_observe = form == 3 && b->bucketed;
     if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
-    if (form == 3) {
+    if (lean) {
+      hipLaunchKernelGGL(bqsr_observe_lean, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    } else if (form == 3) {
       const bool wide = b->dims.max_len > 128;
       if (b->bucketed)
         hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, false> : bqsr_observe_rows<2, false>), dim3(b->n_blocks),
@@ -1409,7 +1431,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_keys : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb, ry), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
-                       b->n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm);
+                       b->n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
@@ -1965,11 +1987,12 @@ bqsr_status bqsr_job_status_get(const bqsr_batch* b, int32_t slot, int32_t part,
 
 // workgroups of a kernel copy: enough stores in flight for the link, few
 // enough CUs that the compute streams' kernels keep running beside it
-// (ADAM_BQSR_COPY_BLOCKS, default 128)
+// (ADAM_BQSR_COPY_BLOCKS, default 32: cfg5 374.8 / 402.9 / 407.0 ms per job
+// at 32 / 128 / 512 workgroups on one box, profiles/r03n_cfg3_sites_bitmap_ab.txt)
 static int64_t copy_blocks(const bqsr_context* ctx) {
   static const int64_t v = [] {
     const char* e = getenv("ADAM_BQSR_COPY_BLOCKS");
-    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)128;
+    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)32;
   }();
   return std::min<int64_t>(v, (int64_t)ctx->n_cu * 8);
 }

@@ -2158,7 +2158,7 @@ template __global__ void bqsr_observe_rows<4, false>(ObserveParams);
 // all landed).
 extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd, OrderDev ord, int32_t n_blocks,
                                               int32_t stride, int32_t wcells, Window w, TableGeom g, int64_t* touched,
-                                              int64_t* obs, int64_t* mm) {
+                                              int64_t* obs, int64_t* mm, int32_t junk) {
   const int nk = order_keys(ord);
   const int nc = w.qw * wcells;
   const int64_t total = (int64_t)nk * stride;
@@ -2189,8 +2189,11 @@ extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd,
     if (i < 2 * nc) {
       const int j = i < nc ? i : i - nc;
       const int slot = j / wcells, wc = j - slot * wcells;
-      const int cell = wc < gm.cw ? gm.c_lo + wc : g.C + (wc - gm.cw);
-      if (key0 + slot >= g.K || wc >= gm.cw + kCtxSlots) continue;  // past the contexts: the row's pad word
+      // context cells past the 21 slots: bqsr_observe_lean's `junk` cells of
+      // windows with an N, context 0 (slot 4); then the row's pad words
+      const int xw = wc - gm.cw;
+      const int cell = wc < gm.cw ? gm.c_lo + wc : g.C + (xw < kCtxSlots ? xw : 4);
+      if (key0 + slot >= g.K || xw >= kCtxSlots + junk) continue;
       // atomics: two read groups' rows can alias one key (q >= 60, quirk Q3)
       int64_t* dst = i < nc ? obs : mm;
       atomicAdd((unsigned long long*)&dst[(key0 + slot) * g.cells + cell], (unsigned long long)s);

@@ -1,0 +1,344 @@
+// bqsr_observe_lean.hip -- observe in read order, a lane per read, with the
+// per-base VALU cut to the table updates (RecalTable.+=, RecalTable.scala:42-62;
+// ErrorCount.+=, :195-201; covariates ReadCovariates.scala:30-60,
+// StandardCovariate.scala:39-70).
+//
+// Same counts as bqsr_observe_kernel<false> (read order, one read group), laid
+// out so that a clean 16-offset chunk costs about 4 VALU per offset beside its
+// two ds_add_u32 (bqsr_observe_kernel: ~27 per offset, VALU-issue-bound at
+// 0.95 ms cfg2):
+//  * contexts from two v_perm byte-table lookups per 4 offsets.  Slot(a, b) =
+//    T1[a] + T2[b] with T1 = 4 (idx + 1), T2 = idx + 1 (other: 0), and an N
+//    in either position lands on 21..42: 22 "junk" context cells per window
+//    row that bqsr_window_reduce folds into slot 4 (context 0, BaseContext's
+//    N rule).  The reverse strand (quirk Q9) swaps in the complemented tables
+//    and mirrors the 16 slots: no reverse complement of the window.
+//  * processing order: a lane whose cycle cell decreases with the offset
+//    (DiscreteCycle, StandardCovariate.scala:39-48) walks its chunk's quals,
+//    slots and bits mirrored, so the cycle address of position p is one
+//    per-chunk base + 4p, an immediate offset of the ds_add.
+//  * partial chunks (a read's first and last): offsets outside [st, en) get a
+//    dump row (two rows past the window, cycle cells -15 .. C+15 stay inside
+//    them), so every chunk whose quals are window rows takes the clean form.
+//  * the three loads a chunk needs issue for a read's 8 chunks at once (its
+//    cache lines fetched once), bases as 12-B dword-aligned pieces.
+// Masked offsets (clips, insertions, known sites: counted on the key only)
+// and mismatches are fixed up in one loop over their bits, as in
+// observe_clean.  Chunks with quals outside the window, check-only reads
+// (kInfoObsCheck) and the batch's first bases keep the exact per-offset path.
+
+namespace bqsr {
+
+constexpr int kCtxJunk = 22;                     // context cells 21..42 of a lean window row
+constexpr int kCtxCells = kCtxSlots + kCtxJunk;  // 43
+constexpr int kLeanSub = 8;                      // chunks per step
+
+// 4 x T[code] for codes 0..7 (A C G T N other, 6 and 7 unused), as v_perm
+// byte tables {lo: codes 0..3, hi: codes 4..7}
+constexpr uint32_t kT1lo = 0x40302010u, kT1hi = 0x00000054u;   // 4 (idx(a) + 1) x 4; N 84 = 4 x 21
+constexpr uint32_t kT2lo = 0x100C0804u, kT2hi = 0x00000054u;   // (idx(b) + 1) x 4
+constexpr uint32_t kT1clo = 0x10203040u, kT2clo = 0x04080C10u;  // complemented (A<->T, C<->G)
+constexpr uint32_t kPermId = 0x03020100u, kPermRev = 0x04050607u;
+
+// 16 bytes of x mirrored (byte k <- byte 15 - k) when sel = kPermRev
+__device__ __forceinline__ void mirror16(uint32_t x[4], uint32_t sel) {
+  const uint32_t y0 = __builtin_amdgcn_perm(x[3], x[0], sel), y1 = __builtin_amdgcn_perm(x[2], x[1], sel);
+  const uint32_t y2 = __builtin_amdgcn_perm(x[1], x[2], sel), y3 = __builtin_amdgcn_perm(x[0], x[3], sel);
+  x[0] = y0;
+  x[1] = y1;
+  x[2] = y2;
+  x[3] = y3;
+}
+
+// slot x 4 of the 16 offsets of a window (lo: codes 0..15, hi: code 16):
+// byte m = U1[code m] + U2[code m + 1]
+__device__ __forceinline__ void lean_ctx(uint64_t lo, uint32_t hi, uint32_t u1lo, uint32_t u1hi, uint32_t u2lo,
+                                         uint32_t u2hi, uint32_t h[4]) {
+  uint32_t s[5];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const uint32_t x = (uint32_t)(lo >> (32 * d));
+    const uint32_t e = x & 0x07070707u, o = (x >> 4) & 0x07070707u;
+    s[2 * d] = __builtin_amdgcn_perm(o, e, 0x05010400u);
+    s[2 * d + 1] = __builtin_amdgcn_perm(o, e, 0x07030602u);
+  }
+  s[4] = hi & 7u;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t b = __builtin_amdgcn_alignbit(s[w + 1], s[w], 8);
+    h[w] = __builtin_amdgcn_perm(u1hi, u1lo, s[w]) + __builtin_amdgcn_perm(u2hi, u2lo, b);
+  }
+}
+
+// the 16 bits of x mirrored (bit p <- bit 15 - p) when rev
+__device__ __forceinline__ uint32_t mirror_bits16(uint32_t x, bool rev) {
+  return rev ? (__builtin_bitreverse32(x) >> 16) : (x & 0xFFFFu);
+}
+
+// bytes k of 16 with klo <= k < khi set to 0xFF (k as byte k & 3 of word k >> 2)
+__device__ __forceinline__ uint32_t byte_range(int w, int klo, int khi) {
+  const int a = min(max(klo - 4 * w, 0), 4), b = min(max(khi - 4 * w, 0), 4);
+  const uint32_t lo = a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+  const uint32_t hi = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+  return lo & hi;
+}
+
+typedef __attribute__((address_space(3))) uint32_t* LdsU32;
+
+// A clean chunk in processing order: both increments of every position, then
+// masked positions moved back out and mismatches added (as observe_clean).
+// a_cyc = LDS byte address of (row 0 - q_lo, cycle cell of position 0), a_ctx
+// of (row 0 - q_lo, context cell 0); q[] holds window rows or the dump row.
+__device__ __forceinline__ void lean_clean(const uint32_t q[4], const uint32_t xo[4], uint32_t a_cyc, uint32_t a_ctx,
+                                           uint32_t w4, uint32_t bm, uint32_t bx, uint32_t mm_off, uint32_t lmasked,
+                                           int q_lo) {
+#pragma unroll
+  for (int p = 0; p < kChunk; ++p) {
+    const uint32_t qv = __builtin_amdgcn_ubfe(q[p >> 2], 8 * (p & 3), 8);
+    const uint32_t xs4 = __builtin_amdgcn_ubfe(xo[p >> 2], 8 * (p & 3), 8);
+    const uint32_t rq = __mul24(qv, w4);
+    __hip_atomic_fetch_add((LdsU32)(uintptr_t)(rq + a_cyc) + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add((LdsU32)(uintptr_t)(rq + xs4 + a_ctx), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  uint32_t mk = bm | bx;
+  if (__builtin_amdgcn_ballot_w64(mk != 0)) {
+    const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
+    const uint64_t q01 = ((uint64_t)q[1] << 32) | q[0], q23 = ((uint64_t)q[3] << 32) | q[2];
+    while (mk) {
+      const int p = __builtin_ctz(mk);
+      mk &= mk - 1;
+      const uint32_t qv = (uint32_t)((p < 8 ? q01 : q23) >> (8 * (p & 7))) & 0xFFu;
+      const uint32_t xs4 = (uint32_t)((p < 8 ? x01 : x23) >> (8 * (p & 7))) & 0xFFu;
+      const uint32_t rq = __mul24(qv, w4);
+      const bool masked = (bm >> p) & 1u;
+      // masked: undo both increments (-1 in the obs window); mismatch: +1 in the mm window
+      const uint32_t off = masked ? 0u : mm_off, val = masked ? ~0u : 1u;
+      lds_add(rq + a_cyc + 4u * (uint32_t)p + off, val);
+      lds_add(rq + a_ctx + xs4 + off, val);
+      if (masked) lds_add(lmasked + 4u * (qv - (uint32_t)q_lo), 1u);
+    }
+  }
+}
+
+// LDS: [obs rows qw + 2 (a pad row, the dump row)][mm rows qw][masked qw][block hist 128]
+// rows of wcells = C + 43 (+ pad to 2 mod 4) words: cycle cells C, context cells 21, junk 22
+__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams P) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
+  const int wcells = P.wcells;
+  uint32_t* w_obs = (uint32_t*)smem;
+  uint32_t* w_mm = w_obs + (qw + 2) * wcells;
+  uint32_t* w_masked = w_mm + qw * wcells;
+  uint32_t* blk_hist = w_masked + qw;
+  const uint32_t lds_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, lds_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = P.n_blocks;
+  const int q_lo = P.w.q_lo, rg_w = P.w.rg_lo;
+  const uint32_t w4 = 4u * (uint32_t)wcells;
+  const uint32_t qoff = (uint32_t)q_lo * w4;
+  const uint32_t a_ctx = lds_obs + 4u * (uint32_t)C - qoff;
+  const uint32_t mm_off = 4u * (uint32_t)((qw + 2) * wcells);
+  const uint32_t dump4 = (uint32_t)(q_lo + qw + 1) * 0x01010101u;
+  const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)(q_lo + qw) * 0x01010101u;
+  constexpr int kSup = kLeanSub * kChunk;
+  constexpr int NW = (kSup + 31) / 32 + 1;
+
+  for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
+  for (int i = tid; i < (2 * qw + 2) * wcells + qw; i += blockDim.x) w_obs[i] = 0;
+  __syncthreads();
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+
+  for (int64_t g0 = wa + 64 * wave; g0 < wb; g0 += 64 * kWaves) {
+    const bool live = g0 + lane < wb;
+    const LaneRead x = lane_read(P.rd, P.info, live ? g0 + lane : 0, live, L);
+    if (x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+    const bool act = x.fl & (kInfoObs | kInfoObsCheck);
+    const bool full = x.fl & kInfoObs;
+    const int n = act ? x.en - x.st : 0;
+    const bool clean_rd = full && x.rg == rg_w;
+    const bool neg = x.fl & kInfoNeg, sec = x.fl & kInfoSecond;
+    const bool rev = x.dir < 0;
+    const uint32_t u1lo = neg ? kT2clo : kT1lo, u2lo = neg ? kT1clo : kT2lo;
+    const uint32_t sel_q = rev ? kPermRev : kPermId, sel_x = sec ? kPermRev : kPermId;
+    const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;
+    const uint8_t* qp = P.rd.qual + x.slot;
+    for (int j0 = jb; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSup) {
+      if (j0 >= n) continue;
+      uint4 qs[kLeanSub];
+      uint3 cr[kLeanSub];
+      uint64_t bw[NW];
+      const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
+#pragma unroll
+      for (int i = 0; i < kLeanSub; ++i) {
+        const bool lv = j0 + kChunk * i < n;
+        const int o0 = x.st + j0 + kChunk * i;
+        qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
+        const int64_t n0 = chunk_n0(x, o0);
+        cr[i] = (lv && full && n0 >= 0) ? *(const uint3*)(P.rd.bases + ((n0 >> 3) << 2)) : make_uint3(0, 0, 0);
+      }
+#pragma unroll
+      for (int w = 0; w < NW; ++w) bw[w] = (full && (w == 0 || 32 * w - 32 < n - j0)) ? P.sbits[(s0 >> 5) + w] : 0ull;
+#pragma clang loop unroll(full)
+      for (int i = 0; i < kLeanSub; ++i) {
+        const int j = j0 + kChunk * i;
+        if (j >= n) continue;
+        const int o0 = x.st + j;
+        // valid offsets k of the chunk: klo <= k < khi
+        const int klo = j < 0 ? -j : 0, khi = min(kChunk, n - j);
+        const uint32_t vmask = (0xFFFFu >> (kChunk - khi)) & (0xFFFFu << klo);
+        uint32_t bm = 0, bx = 0;
+        uint32_t h[4] = {0x10101010u, 0x10101010u, 0x10101010u, 0x10101010u};  // slot 4
+        if (full) {
+          if (P.rd.slots_aligned)
+            sub_bits16<NW>(bw, (uint32_t)(s0 >> 4) & 1u, i, bm, bx);
+          else
+            sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
+          const int64_t n0 = chunk_n0(x, o0);
+          uint64_t clo;
+          uint32_t chi;
+          if (__builtin_expect(n0 >= 0, 1)) {
+            const uint32_t sh = 4u * (uint32_t)(n0 & 7);
+            clo = ((uint64_t)__builtin_amdgcn_alignbit(cr[i].z, cr[i].y, sh) << 32) |
+                  __builtin_amdgcn_alignbit(cr[i].y, cr[i].x, sh);
+            chi = (cr[i].z >> sh) & 0xFu;
+          } else {
+            load_window_head(P.rd.bases, n0, P.rd.n_slots, clo, chi);
+          }
+          lean_ctx(clo, chi, u1lo, kT1hi, u2lo, kT2hi, h);
+        }
+        bm &= vmask;
+        bx &= vmask;
+        // processing order p: offset k = rev ? 15 - p : p
+        uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
+        mirror16(qd, sel_q);
+        mirror16(h, sel_x);
+        if (j <= 0) {  // the read's first visited offset (k = -j): context 0 (slot 4)
+          const int pf = rev ? 15 + j : -j;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t m = (pf >> 2) == w ? 0xFFu << (8 * (pf & 3)) : 0u;
+            h[w] = (h[w] & ~m) | (0x10101010u & m);
+          }
+        }
+        const uint32_t bmp = mirror_bits16(bm, rev), bxp = mirror_bits16(bx, rev);
+        const uint32_t vp = mirror_bits16(vmask, rev);
+        const int plo = rev ? kChunk - khi : klo, phi = rev ? kChunk - klo : khi;
+        // the window cycle cell of position 0 (read order: the window holds every cycle cell)
+        const int cc0 = x.cell0 + __mul24(x.dir, o0);
+        const int cb = rev ? cc0 - (kChunk - 1) : cc0;
+        // clean: the read's group, every valid qual a window row; invalid positions -> the dump row
+        uint32_t qc[4];
+        bool clean = clean_rd;
+        if (__builtin_amdgcn_ballot_w64(vp != 0xFFFFu)) {
+          uint32_t bad = 0;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t vb = byte_range(w, plo, phi);
+            const uint32_t v = (qd[w] & vb) | (lo4 & ~vb);
+            const uint32_t t = v | 0x80808080u;
+            bad |= v | ~(t - lo4) | (t - hi4);
+            qc[w] = (qd[w] & vb) | (dump4 & ~vb);
+          }
+          clean = clean && (bad & 0x80808080u) == 0u;
+        } else {
+          uint32_t bad = 0;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t t = qd[w] | 0x80808080u;
+            bad |= qd[w] | ~(t - lo4) | (t - hi4);
+            qc[w] = qd[w];
+          }
+          clean = clean && (bad & 0x80808080u) == 0u;
+        }
+        const uint32_t a_cyc = lds_obs + 4u * (uint32_t)cb - qoff;
+        uint32_t fastm = 0;
+        if (clean) {
+          lean_clean(qc, h, a_cyc, a_ctx, w4, bmp, bxp, mm_off, lds_masked, q_lo);
+          fastm = 0xFFFFu;
+        } else {
+          // per position: window rows of the read's group; the rest below
+#pragma unroll
+          for (int p = 0; p < kChunk; ++p) {
+            const int q = (int)__builtin_amdgcn_ubfe(qd[p >> 2], 8 * (p & 3), 8);
+            const int row = q - q_lo;
+            const bool f = clean_rd && (unsigned)row < (unsigned)qw && ((vp >> p) & 1u);
+            const bool m = (bmp >> p) & 1u;
+            if (f) {
+              atomicAdd(m ? &w_masked[row] : &w_obs[__mul24(row, wcells) + cb + p], 1u);
+              if (!m) atomicAdd(&w_obs[__mul24(row, wcells) + C + (int)(__builtin_amdgcn_ubfe(h[p >> 2], 8 * (p & 3), 8) >> 2)], 1u);
+            }
+            fastm |= (uint32_t)f << p;
+          }
+          uint32_t mmk = fastm & ~bmp & bxp;
+          if (__builtin_amdgcn_ballot_w64(mmk != 0)) {
+            const uint64_t x01 = ((uint64_t)h[1] << 32) | h[0], x23 = ((uint64_t)h[3] << 32) | h[2];
+            const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
+            while (mmk) {
+              const int p = __builtin_ctz(mmk);
+              mmk &= mmk - 1;
+              const int q = (int)(((p < 8 ? q01 : q23) >> (8 * (p & 7))) & 0xFFu);
+              const int xs = (int)((((p < 8 ? x01 : x23) >> (8 * (p & 7))) & 0xFFu) >> 2);
+              const int base = __mul24(q - q_lo, wcells);
+              atomicAdd(&w_mm[base + cb + p], 1u);
+              atomicAdd(&w_mm[base + C + xs], 1u);
+            }
+          }
+        }
+        uint32_t slow = vp & ~fastm;
+        if (__builtin_amdgcn_ballot_w64(slow != 0)) {
+          const uint64_t x01 = ((uint64_t)h[1] << 32) | h[0], x23 = ((uint64_t)h[3] << 32) | h[2];
+          const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
+          while (slow) {
+            const int p = __builtin_ctz(slow);
+            slow &= slow - 1;
+            const int k = rev ? kChunk - 1 - p : p;
+            const int o = o0 + k;
+            const int q = (int)(int8_t)(((p < 8 ? q01 : q23) >> (8 * (p & 7))) & 0xFFu);
+            if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
+              report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
+            } else if (full) {  // outside the LDS window: straight to the int64 table
+              const bool masked = (bmp >> p) & 1u, mism = (bxp >> p) & 1u;
+              const int ccell = cc0 + __mul24(x.dir, k);
+              const int xs = (int)((((p < 8 ? x01 : x23) >> (8 * (p & 7))) & 0xFFu) >> 2);
+              const int xcell = C + (xs < kCtxSlots ? xs : 4);  // junk slots: an N, context 0
+              atomicAdd(&blk_hist[q], 1u);
+              const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
+              atomicAdd((unsigned long long*)&P.touched[key], 1ull);
+              if (!masked) {
+                atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
+                atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
+                if (mism) {
+                  atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
+                  atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- the window -> the workgroup's slab [obs qw rows][mm qw rows][touched qw]; row totals into the block histogram
+  uint32_t* pb = P.part + (int64_t)blockIdx.x * P.part_stride;
+  const int nw = qw * wcells;
+  for (int i = tid; i < nw; i += blockDim.x) {
+    pb[i] = w_obs[i];
+    pb[nw + i] = w_mm[i];
+  }
+  for (int slot = wave; slot < qw; slot += kWaves) {
+    uint32_t v = 0;
+    for (int c = lane; c < C; c += 64) v += w_obs[slot * wcells + c];  // every unmasked base hits one cycle cell
+    v = wave_sum(v);
+    if (lane == 0) {
+      const uint32_t tot = v + w_masked[slot];
+      pb[2 * nw + slot] = tot;
+      if (tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
+}
+
+}  // namespace bqsr
