@@ -25,6 +25,7 @@ using namespace bqsr;
 // the kernels are compiled in this translation unit (one HIP module)
 #include "bqsr_kernels.hip"
 #include "bqsr_observe_lean.hip"
+#include "bqsr_apply_lean.hip"
 #include "bqsr_fold.hip"
 
 // ------------------------------------------------------------- errors -----
@@ -183,12 +184,22 @@ size_t observe_lds(int qw, int wcells, bool table) {
 // a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
 int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
 size_t apply_lds(int qw, int cw) { return 16 + (size_t)kMkWords * 4 + kCtxTabBytes + (size_t)piece_bytes(qw, cw); }
-// bqsr_observe_lean: obs rows qw + 2 (pad, dump), mm rows qw, masked qw, block histogram
-size_t lean_lds(int qw, int wcells) { return ((size_t)(2 * qw + 2) * wcells + qw + kQBins) * 4; }
-int lean_rows(int wcells) {
-  int qw = kQBins;
-  while (qw > 1 && lean_lds(qw, wcells) > kLdsMax) --qw;
-  return qw;
+// bqsr_observe_lean: obs rows qw of orow words (nc copies of the cycle and the context cells), mm rows
+// qw of wcells, masked qw, block histogram
+int lean_orow(int nc, int cw) {
+  int o = nc * (cw + kCtxCells);
+  while ((o & 3) != 2) ++o;
+  return o;
+}
+size_t lean_lds(int qw, int orow, int wcells) { return ((size_t)qw * (orow + wcells) + qw + kQBins) * 4; }
+// copies of the lean window's counters: the most (<= 4, ADAM_BQSR_LEAN_COPIES caps it) whose rows still
+// hold the batch's qual span
+int lean_copies_max() {
+  static const int v = [] {
+    const char* e = getenv("ADAM_BQSR_LEAN_COPIES");
+    return e ? std::max(1, std::min(4, atoi(e))) : 4;
+  }();
+  return v;
 }
 int observe_rows(int wcells, bool table) {
   int qw = kQBins;
@@ -233,13 +244,21 @@ int observe_form() {
   return v;
 }
 // apply's form: ADAM_BQSR_APPLY=rows (bqsr_apply_rows, lane per offset: SALU-bound, 5.9 ms cfg2 in
-// round 3) (1); unset: the lane-per-chunk walk (bqsr_apply_kernel) (0)
+// round 3) (1), =walk (0), =lean (2, bqsr_apply_lean in read order); unset (-1): the lane-per-chunk
+// walk (bqsr_apply_kernel)
 int apply_form() {
   static const int v = [] {
     const char* e = getenv("ADAM_BQSR_APPLY");
-    return e && strcmp(e, "rows") == 0 ? 1 : 0;
+    return !e ? -1 : strcmp(e, "rows") == 0 ? 1 : strcmp(e, "lean") == 0 ? 2 : 0;
   }();
   return v;
+}
+// bqsr_apply_lean's LDS: the clean-row words and the char table
+size_t apply_lean_lds(int qw, int cw) { return 16 + (size_t)piece_bytes(qw, cw); }
+int apply_lean_rows(int cw) {
+  int qw = kQBins;
+  while (qw > 1 && apply_lean_lds(qw, cw) > kLdsMax) --qw;
+  return qw;
 }
 // known sites as sorted lists only (no position bitmaps): ADAM_BQSR_SITES_BITMAP=0 (A/B)
 bool sites_bitmap_off() {
@@ -473,7 +492,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
                         (const void*)bqsr_observe_rows<4, true>, (const void*)bqsr_observe_rows<2, false>,
                         (const void*)bqsr_observe_rows<4, false>, (const void*)bqsr_apply_rows<2, true>,
                         (const void*)bqsr_apply_rows<4, true>, (const void*)bqsr_apply_rows<2, false>,
-                        (const void*)bqsr_apply_rows<4, false>})
+                        (const void*)bqsr_apply_rows<4, false>, (const void*)bqsr_observe_lean,
+                        (const void*)bqsr_apply_lean})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -638,7 +658,8 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   } else {
     b->bucketed = b->dims.n_rg > 1;
     if (!b->bucketed && b->have_qhist) {
-      const Window w = window_rows(b, apply_rows(geom(b->dims).C));
+      const int cw = geom(b->dims).C;
+      const Window w = window_rows(b, apply_form() == 2 ? apply_lean_rows(cw) : apply_rows(cw));
       int64_t in = 0, all = 0;
       for (int q = 0; q < kQBins; ++q) {
         all += b->qhist[q];
@@ -1303,7 +1324,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
       hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
                          b->d_cursor, b->d_perm);
       HIP_TRY(hipGetLastError());
-      b->gathered = gather_on() && b->rd.slots_aligned && observe_form() <= 0 && apply_form() == 0;
+      b->gathered = gather_on() && b->rd.slots_aligned && observe_form() <= 0 && apply_form() <= 0;
       if (b->gathered) {
         const bqsr_status gst = launch_gather(ctx, b, s);
         if (gst != BQSR_OK) return gst;
@@ -1382,8 +1403,22 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
           if (hc == 0) break;
         }
       P.w = window_rows(b, best_rows);
+    } else if (lean) {
+      const int cw = window_cw(b, P.g), span = qual_span(b);
+      int best_rows = 0;
+      for (int nc = lean_copies_max(); nc >= 1 && best_rows < span; --nc) {
+        const int orow = lean_orow(nc, cw);
+        int qw = kQBins;
+        while (qw > 1 && lean_lds(qw, orow, P.wcells) > kLdsMax) --qw;
+        if (qw > best_rows) {
+          best_rows = qw;
+          P.nc = nc;
+          P.orow = orow;
+        }
+      }
+      P.w = window_rows(b, best_rows);
     } else {
-      P.w = window_rows(b, lean ? lean_rows(P.wcells) : observe_rows(P.wcells, form == 0));
+      P.w = window_rows(b, observe_rows(P.wcells, form == 0));
     }
     P.touched = t->touched();
     P.obs = t->obs();
@@ -1405,7 +1440,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.err = b->d_err + kErrObs;
     P.n_blocks = b->n_blocks;
     const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc)
-                       : lean    ? lean_lds(P.w.qw, P.wcells)
+                       : lean    ? lean_lds(P.w.qw, P.orow, P.wcells)
                                  : observe_lds(P.w.qw, P.wcells, form == 0);
     P.lane_shift = lane_shift(b);
     b->hq_by_observe = form == 3 && b->bucketed;
@@ -1754,7 +1789,10 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.info = b->pass_info();
   P.g = geom(L->dims);
   const int cw = window_cw(b, P.g);
-  P.w = window_rows(b, apply_rows(cw));
+  // the lean lane per read is opt-in (ADAM_BQSR_APPLY=lean): its scattered 16-B result stores ran
+  // 2.34 ms against the walk's 0.84 (cfg2, profiles/r03r_apply_lean_ab.txt)
+  const bool lean = !b->bucketed && apply_form() == 2;
+  P.w = window_rows(b, lean ? apply_lean_rows(cw) : apply_rows(cw));
   P.n_rg = L->dims.n_rg;
   P.s1 = L->s1;
   P.d2 = L->d2;
@@ -1774,6 +1812,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
+  P.probe = getenv("ADAM_BQSR_PROBE") ? atoi(getenv("ADAM_BQSR_PROBE")) : 0;
   if (apply_form() == 1) {
     // bqsr_apply_rows: a packed char table per (read group, mate class) piece,
     // rows of cwp = roundup(L, 32) cycle cells x 6 context groups (dwords)
@@ -1824,9 +1863,11 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_keys * 16, s));
   const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
   hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
-  const size_t lds = apply_lds(P.w.qw, cw);
-  hipLaunchKernelGGL((b->gathered ? bqsr_apply_kernel<true> : bqsr_apply_kernel<false>), dim3(b->n_blocks),
-                     dim3(kBlockThreads), lds, s, P);
+  if (lean)
+    hipLaunchKernelGGL(bqsr_apply_lean, dim3(b->n_blocks), dim3(kBlockThreads), apply_lean_lds(P.w.qw, cw), s, P);
+  else
+    hipLaunchKernelGGL((b->gathered ? bqsr_apply_kernel<true> : bqsr_apply_kernel<false>), dim3(b->n_blocks),
+                       dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
   HIP_TRY(hipGetLastError());
   return ok();
 }

@@ -155,15 +155,25 @@ __device__ void set_sbits(uint64_t* sb, uint64_t lo, uint64_t hi, int half) {
 // (isLowQualityBase: qual <= minQuality = 2, Java signed byte), or 16; with
 // `rev` the bytes are scanned from byte 15 down.
 __device__ __forceinline__ int first_good(const uint4 v, int n, bool rev) {
+  // SWAR: bit 7 of byte b set iff the byte is a qual in [3, 127] ((x & 0x7F) + 0x7D carries into bit 7
+  // from 3 on, never past the byte; a set high bit is a negative Java byte)
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  int first = 16;
+  uint32_t g[4];
 #pragma unroll
-  for (int k = 15; k >= 0; --k) {
-    const int i = rev ? 15 - k : k;
-    const int b = (int)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-    if (k < n && b > 2) first = k;
+  for (int i = 0; i < 4; ++i) g[i] = ((w[i] & 0x7F7F7F7Fu) + 0x7D7D7D7Du) & ~w[i] & 0x80808080u;
+  uint64_t lo = ((uint64_t)g[1] << 32) | g[0], hi = ((uint64_t)g[3] << 32) | g[2];
+  if (n < 16) {  // bytes k >= n (scan order) do not count
+    const int keep = n <= 0 ? 0 : n;
+    if (!rev) {
+      lo &= keep >= 8 ? ~0ull : ((1ull << (8 * keep)) - 1ull);
+      hi &= keep <= 8 ? 0ull : ((1ull << (8 * (keep - 8))) - 1ull);
+    } else {
+      hi &= keep >= 8 ? ~0ull : ~((1ull << (8 * (8 - keep))) - 1ull);
+      lo &= keep <= 8 ? 0ull : ~((1ull << (8 * (16 - keep))) - 1ull);
+    }
   }
-  return first;
+  if (!rev) return lo ? (__builtin_ctzll(lo) >> 3) : hi ? 8 + (__builtin_ctzll(hi) >> 3) : 16;
+  return hi ? (__builtin_clzll(hi) >> 3) : lo ? 8 + (__builtin_clzll(lo) >> 3) : 16;
 }
 
 // ReadCovariates' quality trimming (ReadCovariates.scala:31-39): st = the

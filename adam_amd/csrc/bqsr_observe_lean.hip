@@ -17,9 +17,8 @@
 //    (DiscreteCycle, StandardCovariate.scala:39-48) walks its chunk's quals,
 //    slots and bits mirrored, so the cycle address of position p is one
 //    per-chunk base + 4p, an immediate offset of the ds_add.
-//  * partial chunks (a read's first and last): offsets outside [st, en) get a
-//    dump row (two rows past the window, cycle cells -15 .. C+15 stay inside
-//    them), so every chunk whose quals are window rows takes the clean form.
+//  * partial chunks (a read's first and last) take the clean form too, their
+//    positions outside [st, en) exec-masked.
 //  * the three loads a chunk needs issue for a read's 8 chunks at once (its
 //    cache lines fetched once), bases as 12-B dword-aligned pieces.
 // Masked offsets (clips, insertions, known sites: counted on the key only)
@@ -88,15 +87,22 @@ typedef __attribute__((address_space(3))) uint32_t* LdsU32;
 // A clean chunk in processing order: both increments of every position, then
 // masked positions moved back out and mismatches added (as observe_clean).
 // a_cyc = LDS byte address of (row 0 - q_lo, cycle cell of position 0), a_ctx
-// of (row 0 - q_lo, context cell 0); q[] holds window rows or the dump row.
+// of (row 0 - q_lo, context cell 0); q[] holds window rows at the positions
+// of vp.  kPart: a partial chunk, positions outside vp skipped (exec-masked:
+// a shared dump row for them took 64-way same-address adds, cfg2 observe
+// 0.95 -> 1.16 ms)
+// Mismatches go to the mm window (one copy, rows of w4 bytes): a_mcyc / a_mctx
+// as a_cyc / a_ctx.
+template <bool kPart>
 __device__ __forceinline__ void lean_clean(const uint32_t q[4], const uint32_t xo[4], uint32_t a_cyc, uint32_t a_ctx,
-                                           uint32_t w4, uint32_t bm, uint32_t bx, uint32_t mm_off, uint32_t lmasked,
-                                           int q_lo) {
+                                           uint32_t o4, uint32_t bm, uint32_t bx, uint32_t a_mcyc, uint32_t a_mctx,
+                                           uint32_t w4, uint32_t lmasked, int q_lo, uint32_t vp) {
 #pragma unroll
   for (int p = 0; p < kChunk; ++p) {
+    if (kPart && !((vp >> p) & 1u)) continue;
     const uint32_t qv = __builtin_amdgcn_ubfe(q[p >> 2], 8 * (p & 3), 8);
     const uint32_t xs4 = __builtin_amdgcn_ubfe(xo[p >> 2], 8 * (p & 3), 8);
-    const uint32_t rq = __mul24(qv, w4);
+    const uint32_t rq = __mul24(qv, o4);
     __hip_atomic_fetch_add((LdsU32)(uintptr_t)(rq + a_cyc) + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_fetch_add((LdsU32)(uintptr_t)(rq + xs4 + a_ctx), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
@@ -109,25 +115,28 @@ __device__ __forceinline__ void lean_clean(const uint32_t q[4], const uint32_t x
       mk &= mk - 1;
       const uint32_t qv = (uint32_t)((p < 8 ? q01 : q23) >> (8 * (p & 7))) & 0xFFu;
       const uint32_t xs4 = (uint32_t)((p < 8 ? x01 : x23) >> (8 * (p & 7))) & 0xFFu;
-      const uint32_t rq = __mul24(qv, w4);
       const bool masked = (bm >> p) & 1u;
       // masked: undo both increments (-1 in the obs window); mismatch: +1 in the mm window
-      const uint32_t off = masked ? 0u : mm_off, val = masked ? ~0u : 1u;
-      lds_add(rq + a_cyc + 4u * (uint32_t)p + off, val);
-      lds_add(rq + a_ctx + xs4 + off, val);
+      const uint32_t rq = __mul24(qv, masked ? o4 : w4), val = masked ? ~0u : 1u;
+      lds_add(rq + (masked ? a_cyc : a_mcyc) + 4u * (uint32_t)p, val);
+      lds_add(rq + (masked ? a_ctx : a_mctx) + xs4, val);
       if (masked) lds_add(lmasked + 4u * (qv - (uint32_t)q_lo), 1u);
     }
   }
 }
 
-// LDS: [obs rows qw + 2 (a pad row, the dump row)][mm rows qw][masked qw][block hist 128]
-// rows of wcells = C + 43 (+ pad to 2 mod 4) words: cycle cells C, context cells 21, junk 22
+// LDS: [obs rows qw][mm rows qw][masked qw][block hist 128]
+// obs rows of P.orow words: nc copies of the C cycle cells, then nc copies of
+// the 43 context cells (21 contexts, 22 junk), padded to 2 mod 4; lane l adds
+// to copy l % nc (same-address adds of a wavefront's lanes -- same qual, same
+// cycle -- split nc ways).  mm rows (rare adds): one copy, wcells = C + 43
+// padded, the slab layout.
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
-  const int wcells = P.wcells;
+  const int wcells = P.wcells, orow = P.orow, nc = P.nc;
   uint32_t* w_obs = (uint32_t*)smem;
-  uint32_t* w_mm = w_obs + (qw + 2) * wcells;
+  uint32_t* w_mm = w_obs + qw * orow;
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
   const uint32_t lds_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, lds_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
@@ -135,17 +144,18 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = P.n_blocks;
   const int q_lo = P.w.q_lo, rg_w = P.w.rg_lo;
-  const uint32_t w4 = 4u * (uint32_t)wcells;
-  const uint32_t qoff = (uint32_t)q_lo * w4;
-  const uint32_t a_ctx = lds_obs + 4u * (uint32_t)C - qoff;
-  const uint32_t mm_off = 4u * (uint32_t)((qw + 2) * wcells);
-  const uint32_t dump4 = (uint32_t)(q_lo + qw + 1) * 0x01010101u;
+  const uint32_t w4 = 4u * (uint32_t)wcells, o4 = 4u * (uint32_t)orow;
+  const uint32_t copy = (uint32_t)(lane % nc);
+  const uint32_t qoff = (uint32_t)q_lo * o4;
+  const uint32_t a_ctx = lds_obs + 4u * ((uint32_t)(nc * C) + copy * kCtxCells) - qoff;
+  const uint32_t lds_mm = (uint32_t)(uintptr_t)(LdsWords)w_mm;
+  const uint32_t a_mctx = lds_mm + 4u * (uint32_t)C - (uint32_t)q_lo * w4;
   const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)(q_lo + qw) * 0x01010101u;
   constexpr int kSup = kLeanSub * kChunk;
   constexpr int NW = (kSup + 31) / 32 + 1;
 
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
-  for (int i = tid; i < (2 * qw + 2) * wcells + qw; i += blockDim.x) w_obs[i] = 0;
+  for (int i = tid; i < qw * (orow + wcells) + qw; i += blockDim.x) w_obs[i] = 0;
   __syncthreads();
   const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
 
@@ -227,35 +237,32 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
         // the window cycle cell of position 0 (read order: the window holds every cycle cell)
         const int cc0 = x.cell0 + __mul24(x.dir, o0);
         const int cb = rev ? cc0 - (kChunk - 1) : cc0;
-        // clean: the read's group, every valid qual a window row; invalid positions -> the dump row
-        uint32_t qc[4];
+        // clean: the read's group, every valid qual a window row
+        const bool part = __builtin_amdgcn_ballot_w64(vp != 0xFFFFu) != 0;
         bool clean = clean_rd;
-        if (__builtin_amdgcn_ballot_w64(vp != 0xFFFFu)) {
+        {
           uint32_t bad = 0;
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
-            const uint32_t vb = byte_range(w, plo, phi);
-            const uint32_t v = (qd[w] & vb) | (lo4 & ~vb);
+            uint32_t v = qd[w];
+            if (part) {  // positions outside [plo, phi) tested as q_lo
+              const uint32_t vb = byte_range(w, plo, phi);
+              v = (v & vb) | (lo4 & ~vb);
+            }
             const uint32_t t = v | 0x80808080u;
             bad |= v | ~(t - lo4) | (t - hi4);
-            qc[w] = (qd[w] & vb) | (dump4 & ~vb);
-          }
-          clean = clean && (bad & 0x80808080u) == 0u;
-        } else {
-          uint32_t bad = 0;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const uint32_t t = qd[w] | 0x80808080u;
-            bad |= qd[w] | ~(t - lo4) | (t - hi4);
-            qc[w] = qd[w];
           }
           clean = clean && (bad & 0x80808080u) == 0u;
         }
-        const uint32_t a_cyc = lds_obs + 4u * (uint32_t)cb - qoff;
+        const uint32_t a_cyc = lds_obs + 4u * (copy * (uint32_t)C + (uint32_t)cb) - qoff;
+        const uint32_t a_mcyc = lds_mm + 4u * (uint32_t)cb - (uint32_t)q_lo * w4;
         uint32_t fastm = 0;
         if (clean) {
-          lean_clean(qc, h, a_cyc, a_ctx, w4, bmp, bxp, mm_off, lds_masked, q_lo);
-          fastm = 0xFFFFu;
+          if (part)
+            lean_clean<true>(qd, h, a_cyc, a_ctx, o4, bmp, bxp, a_mcyc, a_mctx, w4, lds_masked, q_lo, vp);
+          else
+            lean_clean<false>(qd, h, a_cyc, a_ctx, o4, bmp, bxp, a_mcyc, a_mctx, w4, lds_masked, q_lo, vp);
+          fastm = vp;
         } else {
           // per position: window rows of the read's group; the rest below
 #pragma unroll
@@ -265,8 +272,12 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
             const bool f = clean_rd && (unsigned)row < (unsigned)qw && ((vp >> p) & 1u);
             const bool m = (bmp >> p) & 1u;
             if (f) {
-              atomicAdd(m ? &w_masked[row] : &w_obs[__mul24(row, wcells) + cb + p], 1u);
-              if (!m) atomicAdd(&w_obs[__mul24(row, wcells) + C + (int)(__builtin_amdgcn_ubfe(h[p >> 2], 8 * (p & 3), 8) >> 2)], 1u);
+              const int ob = __mul24(row, orow);
+              atomicAdd(m ? &w_masked[row] : &w_obs[ob + (int)copy * C + cb + p], 1u);
+              if (!m)
+                atomicAdd(&w_obs[ob + nc * C + (int)copy * kCtxCells +
+                                 (int)(__builtin_amdgcn_ubfe(h[p >> 2], 8 * (p & 3), 8) >> 2)],
+                          1u);
             }
             fastm |= (uint32_t)f << p;
           }
@@ -324,12 +335,19 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   uint32_t* pb = P.part + (int64_t)blockIdx.x * P.part_stride;
   const int nw = qw * wcells;
   for (int i = tid; i < nw; i += blockDim.x) {
-    pb[i] = w_obs[i];
+    const int r = i / wcells, c = i - r * wcells;
+    const uint32_t* ro = w_obs + r * orow;
+    uint32_t v = 0;
+    if (c < C)
+      for (int k = 0; k < nc; ++k) v += ro[k * C + c];
+    else if (c < C + kCtxCells)
+      for (int k = 0; k < nc; ++k) v += ro[nc * C + k * kCtxCells + (c - C)];
+    pb[i] = v;
     pb[nw + i] = w_mm[i];
   }
   for (int slot = wave; slot < qw; slot += kWaves) {
     uint32_t v = 0;
-    for (int c = lane; c < C; c += 64) v += w_obs[slot * wcells + c];  // every unmasked base hits one cycle cell
+    for (int c = lane; c < nc * C; c += 64) v += w_obs[slot * orow + c];  // every unmasked base hits one cycle cell
     v = wave_sum(v);
     if (lane == 0) {
       const uint32_t tot = v + w_masked[slot];

@@ -229,5 +229,5 @@ def test_two_ranks_raise_the_jobs_first_error_and_parity_leg(tmp_path, bad_rank)
     first = min(shard_bounds(6000, r, WORLD)[0] + res[r]["bad_local"] for r in range(WORLD))
     for z in res:
         p = z["parity"]
-        assert p["ok"] and p["reads_checked"] == 6000, p
+        assert p["ok"] and p["reads_checked"] == 6000, json.dumps(p)
         assert z["raised"] == ["MD_PARSE", first], (z["raised"], first)
