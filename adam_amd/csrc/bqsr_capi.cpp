@@ -348,6 +348,7 @@ struct bqsr_batch {
   int32_t q_lo = 0, rg_lo = 0;  // LDS window choice
   bool have_qhist = false;      // q_lo follows qhist at each launch's window width
   int64_t qhist[kQBins] = {0};
+  int64_t qhigh = 0;            // quals >= 128 (negative Java bytes) in the batch
   std::vector<void*> allocs;
   std::vector<size_t> staged_cnt;  // column element counts (bqsr_batch_create_staged)
   uint8_t* d_bases2 = nullptr;     // staged: the uploaded 2-bit base codes
@@ -818,6 +819,7 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
   b->q_lo = best_q_lo(P.qhist, 40);
   b->have_qhist = true;
   for (int q = 0; q < kQBins; ++q) b->qhist[q] = P.qhist[q];
+  for (int q = kQBins; q < 256; ++q) b->qhigh += P.qhist[q];
   ReadMeta* meta;
   ReadAlign* align;
   uint8_t *qual, *bases, *md;
@@ -922,6 +924,7 @@ struct bqsr_staged {
   bqsr_dims dims{1, 1};
   int32_t rg_lo = 0, q_lo = 0;
   int64_t qhist[kQBins] = {0};
+  int64_t qhigh = 0;
   ~bqsr_staged() {
     if (host) (void)hipHostFree(host);
   }
@@ -992,6 +995,7 @@ bqsr_status bqsr_stage_records(bqsr_context* ctx, const bqsr_records* R, bqsr_st
     if (P.rghist[(size_t)i] > P.rghist[(size_t)s->rg_lo]) s->rg_lo = i;  // as bqsr_batch_create
   s->q_lo = best_q_lo(P.qhist, 40);
   for (int q = 0; q < kQBins; ++q) s->qhist[q] = P.qhist[q];
+  for (int q = kQBins; q < 256; ++q) s->qhigh += P.qhist[q];
   *out = s.release();
   return ok();
 }
@@ -1016,6 +1020,7 @@ bqsr_status bqsr_batch_create_staged(bqsr_context* ctx, const bqsr_staged* S_, b
   b->q_lo = S_->q_lo;
   b->have_qhist = true;
   for (int q = 0; q < kQBins; ++q) b->qhist[q] = S_->qhist[q];
+  b->qhigh = S_->qhigh;
   ReadMeta* meta;
   ReadAlign* align;
   uint8_t *qual, *bases, *md;
@@ -1417,6 +1422,10 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
         }
       }
       P.w = window_rows(b, best_rows);
+      // every qual of the batch a window row: the kernel skips the per-chunk row test
+      P.rows_all = b->have_qhist && b->qhigh == 0;
+      for (int q = 0; q < kQBins && P.rows_all; ++q)
+        if (b->qhist[q] && (q < P.w.q_lo || q >= P.w.q_lo + P.w.qw)) P.rows_all = 0;
     } else {
       P.w = window_rows(b, observe_rows(P.wcells, form == 0));
     }

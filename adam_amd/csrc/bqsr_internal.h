@@ -210,6 +210,7 @@ struct ObserveParams {
   int32_t orow;        // bqsr_observe_rows: LDS obs row words ([ctx copies 21 * nc][cycle cells cw][pad]), 0 mod 32
   int32_t nc;          // bqsr_observe_rows: copies of a row's context counters (power of 2, <= 16)
   int32_t hc;          // bqsr_observe_rows, bucketed: copies of a wavefront's fold-block qual histogram
+  int32_t rows_all;    // bqsr_observe_lean: every qual of the batch is a window row (host histogram)
 };
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----

@@ -1214,6 +1214,16 @@ __device__ __forceinline__ void chunk_ctx(const ReadsDev& rd, bool neg, int64_t 
   ctx_lookup(lo, hi, neg ? tb + 2u * kCtxTab : tb, neg, xo);
 }
 
+// 16 bytes of x mirrored (byte k <- byte 15 - k) when sel = 0x04050607 (0x03020100: as is)
+__device__ __forceinline__ void mirror16(uint32_t x[4], uint32_t sel) {
+  const uint32_t y0 = __builtin_amdgcn_perm(x[3], x[0], sel), y1 = __builtin_amdgcn_perm(x[2], x[1], sel);
+  const uint32_t y2 = __builtin_amdgcn_perm(x[1], x[2], sel), y3 = __builtin_amdgcn_perm(x[0], x[3], sel);
+  x[0] = y0;
+  x[1] = y1;
+  x[2] = y2;
+  x[3] = y3;
+}
+
 // ------------------------------------------------------- lane per chunk ----
 //
 // The per-base passes' wavefront walk: every lane takes one 16-offset chunk

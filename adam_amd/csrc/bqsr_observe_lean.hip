@@ -39,16 +39,6 @@ constexpr uint32_t kT2lo = 0x100C0804u, kT2hi = 0x00000054u;   // (idx(b) + 1) x
 constexpr uint32_t kT1clo = 0x10203040u, kT2clo = 0x04080C10u;  // complemented (A<->T, C<->G)
 constexpr uint32_t kPermId = 0x03020100u, kPermRev = 0x04050607u;
 
-// 16 bytes of x mirrored (byte k <- byte 15 - k) when sel = kPermRev
-__device__ __forceinline__ void mirror16(uint32_t x[4], uint32_t sel) {
-  const uint32_t y0 = __builtin_amdgcn_perm(x[3], x[0], sel), y1 = __builtin_amdgcn_perm(x[2], x[1], sel);
-  const uint32_t y2 = __builtin_amdgcn_perm(x[1], x[2], sel), y3 = __builtin_amdgcn_perm(x[0], x[3], sel);
-  x[0] = y0;
-  x[1] = y1;
-  x[2] = y2;
-  x[3] = y3;
-}
-
 // slot x 4 of the 16 offsets of a window (lo: codes 0..15, hi: code 16):
 // byte m = U1[code m] + U2[code m + 1]
 __device__ __forceinline__ void lean_ctx(uint64_t lo, uint32_t hi, uint32_t u1lo, uint32_t u1hi, uint32_t u2lo,
@@ -240,7 +230,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
         // clean: the read's group, every valid qual a window row
         const bool part = __builtin_amdgcn_ballot_w64(vp != 0xFFFFu) != 0;
         bool clean = clean_rd;
-        {
+        if (!P.rows_all) {  // (every qual of the batch a window row: nothing to test)
           uint32_t bad = 0;
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
