@@ -493,7 +493,7 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
                         (const void*)bqsr_observe_rows<4, true>, (const void*)bqsr_observe_rows<2, false>,
                         (const void*)bqsr_observe_rows<4, false>, (const void*)bqsr_apply_rows<2, true>,
                         (const void*)bqsr_apply_rows<4, true>, (const void*)bqsr_apply_rows<2, false>,
-                        (const void*)bqsr_apply_rows<4, false>, (const void*)bqsr_observe_lean,
+                        (const void*)bqsr_apply_rows<4, false>, (const void*)bqsr_observe_lean<true>, (const void*)bqsr_observe_lean<false>,
                         (const void*)bqsr_apply_lean})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
@@ -1372,9 +1372,10 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     // words: 7.6 ms observe; 225: 5.8; cfg2 222 against 223 / 224: 0.94 /
     // 1.00 / 1.25 ms).  ADAM_BQSR_WMOD=r pads to r mod 32 instead (A/B), -1
     // not at all.  Pad words stay 0.
-    // the lean lane per read (read order) is the default; ADAM_BQSR_OBSERVE=read / superchunk / rows /
-    // chunks select the others
-    const int form = observe_form() >= 0 && !(observe_form() == 4 && b->bucketed) ? observe_form()
+    // the lean lane per read is the default in read order; bucketed batches take the chunk walk
+    // (cfg4 observe 4.51 ms against lean's 6.42, profiles/r03w_cfg4_lean_bucketed_ab.txt; lean there
+    // with ADAM_BQSR_OBSERVE=lean); ADAM_BQSR_OBSERVE=read / superchunk / rows / chunks select the others
+    const int form = observe_form() >= 0 && !(observe_form() == 4 && b->gathered) ? observe_form()
                      : b->bucketed                                               ? 0
                                                                                  : 4;
     const bool lean = form == 4;
@@ -1455,7 +1456,8 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     b->hq_by_observe = form == 3 && b->bucketed;
     if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
     if (lean) {
-      hipLaunchKernelGGL(bqsr_observe_lean, dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+      hipLaunchKernelGGL((b->bucketed ? bqsr_observe_lean<false> : bqsr_observe_lean<true>), dim3(b->n_blocks),
+                         dim3(kBlockThreads), lds, s, P);
     } else if (form == 3) {
       const bool wide = b->dims.max_len > 128;
       if (b->bucketed)

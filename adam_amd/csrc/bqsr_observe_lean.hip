@@ -121,6 +121,7 @@ __device__ __forceinline__ void lean_clean(const uint32_t q[4], const uint32_t x
 // to copy l % nc (same-address adds of a wavefront's lanes -- same qual, same
 // cycle -- split nc ways).  mm rows (rare adds): one copy, wcells = C + 43
 // padded, the slab layout.
+template <bool kIdent>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -133,25 +134,38 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = P.n_blocks;
-  const int q_lo = P.w.q_lo, rg_w = P.w.rg_lo;
+  const int q_lo = P.w.q_lo;
   const uint32_t w4 = 4u * (uint32_t)wcells, o4 = 4u * (uint32_t)orow;
   const uint32_t copy = (uint32_t)(lane % nc);
   const uint32_t qoff = (uint32_t)q_lo * o4;
-  const uint32_t a_ctx = lds_obs + 4u * ((uint32_t)(nc * C) + copy * kCtxCells) - qoff;
   const uint32_t lds_mm = (uint32_t)(uintptr_t)(LdsWords)w_mm;
-  const uint32_t a_mctx = lds_mm + 4u * (uint32_t)C - (uint32_t)q_lo * w4;
   const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)(q_lo + qw) * 0x01010101u;
   constexpr int kSup = kLeanSub * kChunk;
   constexpr int NW = (kSup + 31) / 32 + 1;
-
+  // read order: one piece, every cycle cell in the window; bucketed batches
+  // (OrderDev): a piece per key (read group, mate class) the workgroup's sorted
+  // range meets, its window holding the key's half of the cycle cells
+  constexpr bool ident = kIdent;  // P.ord.perm == nullptr
+  const int nk = kIdent ? 1 : order_keys(P.ord);
+  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
+
+  for (int key = kIdent ? 0 : (wa < wb ? key_at(P.ord, wa) : nk); key < nk; ++key) {
+  const int64_t p0 = kIdent ? wa : max(wa, key_begin(P.ord, P.rd.n_reads, key));
+  const int64_t p1 = kIdent ? wb : min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
+  if (!kIdent && p0 >= wb) break;
+  if (!kIdent && p0 >= p1) continue;
+  const int rg_w = kIdent ? P.w.rg_lo : key_rg(P.ord, key, P.w.rg_lo);  // the read group of the window rows
+  const WinGeom gm = kIdent ? WinGeom{0, C} : win_geom(P.ord, P.g, key);
+  const int c_lo = gm.c_lo, cw = gm.cw;  // window cycle cell c = table cell c_lo + c
+  const uint32_t a_ctx = lds_obs + 4u * ((uint32_t)(nc * cw) + copy * kCtxCells) - qoff;
+  const uint32_t a_mctx = lds_mm + 4u * (uint32_t)cw - (uint32_t)q_lo * w4;
   for (int i = tid; i < qw * (orow + wcells) + qw; i += blockDim.x) w_obs[i] = 0;
   __syncthreads();
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
 
-  for (int64_t g0 = wa + 64 * wave; g0 < wb; g0 += 64 * kWaves) {
-    const bool live = g0 + lane < wb;
-    const LaneRead x = lane_read(P.rd, P.info, live ? g0 + lane : 0, live, L);
+  for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
+    const bool live = g0 + lane < p1;
+    const LaneRead x = lane_read(P.rd, P.info, live ? (kIdent ? g0 + lane : order_read(P.ord, g0 + lane)) : 0, live, L);
     if (x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
     const bool act = x.fl & (kInfoObs | kInfoObsCheck);
     const bool full = x.fl & kInfoObs;
@@ -226,7 +240,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
         const int plo = rev ? kChunk - khi : klo, phi = rev ? kChunk - klo : khi;
         // the window cycle cell of position 0 (read order: the window holds every cycle cell)
         const int cc0 = x.cell0 + __mul24(x.dir, o0);
-        const int cb = rev ? cc0 - (kChunk - 1) : cc0;
+        const int cb = (rev ? cc0 - (kChunk - 1) : cc0) - c_lo;  // window cycle cell of position 0
         // clean: the read's group, every valid qual a window row
         const bool part = __builtin_amdgcn_ballot_w64(vp != 0xFFFFu) != 0;
         bool clean = clean_rd;
@@ -244,7 +258,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
           }
           clean = clean && (bad & 0x80808080u) == 0u;
         }
-        const uint32_t a_cyc = lds_obs + 4u * (copy * (uint32_t)C + (uint32_t)cb) - qoff;
+        const uint32_t a_cyc = lds_obs + 4u * (copy * (uint32_t)cw + (uint32_t)cb) - qoff;
         const uint32_t a_mcyc = lds_mm + 4u * (uint32_t)cb - (uint32_t)q_lo * w4;
         uint32_t fastm = 0;
         if (clean) {
@@ -263,9 +277,9 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
             const bool m = (bmp >> p) & 1u;
             if (f) {
               const int ob = __mul24(row, orow);
-              atomicAdd(m ? &w_masked[row] : &w_obs[ob + (int)copy * C + cb + p], 1u);
+              atomicAdd(m ? &w_masked[row] : &w_obs[ob + (int)copy * cw + cb + p], 1u);
               if (!m)
-                atomicAdd(&w_obs[ob + nc * C + (int)copy * kCtxCells +
+                atomicAdd(&w_obs[ob + nc * cw + (int)copy * kCtxCells +
                                  (int)(__builtin_amdgcn_ubfe(h[p >> 2], 8 * (p & 3), 8) >> 2)],
                           1u);
             }
@@ -282,7 +296,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
               const int xs = (int)((((p < 8 ? x01 : x23) >> (8 * (p & 7))) & 0xFFu) >> 2);
               const int base = __mul24(q - q_lo, wcells);
               atomicAdd(&w_mm[base + cb + p], 1u);
-              atomicAdd(&w_mm[base + C + xs], 1u);
+              atomicAdd(&w_mm[base + cw + xs], 1u);
             }
           }
         }
@@ -303,7 +317,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
               const int ccell = cc0 + __mul24(x.dir, k);
               const int xs = (int)((((p < 8 ? x01 : x23) >> (8 * (p & 7))) & 0xFFu) >> 2);
               const int xcell = C + (xs < kCtxSlots ? xs : 4);  // junk slots: an N, context 0
-              atomicAdd(&blk_hist[q], 1u);
+              if (ident) atomicAdd(&blk_hist[q], 1u);
               const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
               atomicAdd((unsigned long long*)&P.touched[key], 1ull);
               if (!masked) {
@@ -321,32 +335,37 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
     }
   }
   __syncthreads();
-  // ---- the window -> the workgroup's slab [obs qw rows][mm qw rows][touched qw]; row totals into the block histogram
-  uint32_t* pb = P.part + (int64_t)blockIdx.x * P.part_stride;
+  // ---- the window -> the piece's slab [obs qw rows][mm qw rows][touched qw]; row totals into the block histogram
+  uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
   const int nw = qw * wcells;
   for (int i = tid; i < nw; i += blockDim.x) {
     const int r = i / wcells, c = i - r * wcells;
     const uint32_t* ro = w_obs + r * orow;
     uint32_t v = 0;
-    if (c < C)
-      for (int k = 0; k < nc; ++k) v += ro[k * C + c];
-    else if (c < C + kCtxCells)
-      for (int k = 0; k < nc; ++k) v += ro[nc * C + k * kCtxCells + (c - C)];
+    if (c < cw)
+      for (int k = 0; k < nc; ++k) v += ro[k * cw + c];
+    else if (c < cw + kCtxCells)
+      for (int k = 0; k < nc; ++k) v += ro[nc * cw + k * kCtxCells + (c - cw)];
     pb[i] = v;
     pb[nw + i] = w_mm[i];
   }
   for (int slot = wave; slot < qw; slot += kWaves) {
     uint32_t v = 0;
-    for (int c = lane; c < nc * C; c += 64) v += w_obs[slot * orow + c];  // every unmasked base hits one cycle cell
+    for (int c = lane; c < nc * cw; c += 64) v += w_obs[slot * orow + c];  // every unmasked base hits one cycle cell
     v = wave_sum(v);
     if (lane == 0) {
       const uint32_t tot = v + w_masked[slot];
       pb[2 * nw + slot] = tot;
-      if (tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
+      if (ident && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
     }
   }
   __syncthreads();
-  for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
+  }  // pieces
+  if (ident)
+    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
 }
+
+template __global__ void bqsr_observe_lean<true>(ObserveParams);
+template __global__ void bqsr_observe_lean<false>(ObserveParams);
 
 }  // namespace bqsr
