@@ -16,11 +16,6 @@
 
 namespace bqsr {
 
-// T[code] for codes 0..7 (A C G T N other), unscaled: slot = T1[a] + T2[b]
-constexpr uint32_t kA1lo = 0x100C0804u, kA1hi = 0x00000015u;  // 4 (idx + 1); N 21
-constexpr uint32_t kA2lo = 0x04030201u, kA2hi = 0x00000015u;  // idx + 1
-constexpr uint32_t kA1clo = 0x04080C10u, kA2clo = 0x01020304u;  // complemented
-
 // bit k of the result: byte k of the 16 (4 words) has its high bit set
 __device__ __forceinline__ uint32_t byte_flags16(const uint32_t f[4]) {
   uint32_t m = 0;

@@ -1194,6 +1194,32 @@ __device__ __forceinline__ void ctx_lookup(uint64_t lo, uint32_t hi, uint32_t tb
 #pragma unroll
   for (int w = 0; w < 4; ++w) xo[w] = __builtin_amdgcn_perm(X[3 - w], X[w], sel);
 }
+// Context slots by byte tables (bqsr_observe_lean, the arithmetic apply
+// form): byte m of h = U1[code m] + U2[code m + 1] of a window (lo: codes
+// 0..15, hi: code 16); U = v_perm tables {lo: codes 0..3, hi: codes 4..7}
+__device__ __forceinline__ void lean_ctx(uint64_t lo, uint32_t hi, uint32_t u1lo, uint32_t u1hi, uint32_t u2lo,
+                                         uint32_t u2hi, uint32_t h[4]) {
+  uint32_t s[5];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const uint32_t x = (uint32_t)(lo >> (32 * d));
+    const uint32_t e = x & 0x07070707u, o = (x >> 4) & 0x07070707u;
+    s[2 * d] = __builtin_amdgcn_perm(o, e, 0x05010400u);
+    s[2 * d + 1] = __builtin_amdgcn_perm(o, e, 0x07030602u);
+  }
+  s[4] = hi & 7u;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t b = __builtin_amdgcn_alignbit(s[w + 1], s[w], 8);
+    h[w] = __builtin_amdgcn_perm(u1hi, u1lo, s[w]) + __builtin_amdgcn_perm(u2hi, u2lo, b);
+  }
+}
+
+// T[code] for codes 0..7 (A C G T N other), unscaled: slot = T1[a] + T2[b]
+constexpr uint32_t kA1lo = 0x100C0804u, kA1hi = 0x00000015u;  // 4 (idx + 1); N 21
+constexpr uint32_t kA2lo = 0x04030201u, kA2hi = 0x00000015u;  // idx + 1
+constexpr uint32_t kA1clo = 0x04080C10u, kA2clo = 0x01020304u;  // complemented
+
 // a chunk's 16 context slots from its raw 16-B bases load: the 17-code window
 // (forward), the read's first offset given context 0, the table lookups
 __device__ __forceinline__ void chunk_ctx(const ReadsDev& rd, bool neg, int64_t n0, uint4 v, int j, uint32_t tb,
@@ -1211,6 +1237,8 @@ __device__ __forceinline__ void chunk_ctx(const ReadsDev& rd, bool neg, int64_t 
     const int t = neg ? 16 + j : -j;
     if (t < 16) lo = window_first(lo, t); else hi = kCodeN;
   }
+  // (the byte-table form of bqsr_observe_lean here, junk slots fixed to 4 in
+  // SWAR: cfg2 apply 793 -> 825 us, cfg4 5948 -> 6011 us; not taken)
   ctx_lookup(lo, hi, neg ? tb + 2u * kCtxTab : tb, neg, xo);
 }
 

@@ -39,26 +39,6 @@ constexpr uint32_t kT2lo = 0x100C0804u, kT2hi = 0x00000054u;   // (idx(b) + 1) x
 constexpr uint32_t kT1clo = 0x10203040u, kT2clo = 0x04080C10u;  // complemented (A<->T, C<->G)
 constexpr uint32_t kPermId = 0x03020100u, kPermRev = 0x04050607u;
 
-// slot x 4 of the 16 offsets of a window (lo: codes 0..15, hi: code 16):
-// byte m = U1[code m] + U2[code m + 1]
-__device__ __forceinline__ void lean_ctx(uint64_t lo, uint32_t hi, uint32_t u1lo, uint32_t u1hi, uint32_t u2lo,
-                                         uint32_t u2hi, uint32_t h[4]) {
-  uint32_t s[5];
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {
-    const uint32_t x = (uint32_t)(lo >> (32 * d));
-    const uint32_t e = x & 0x07070707u, o = (x >> 4) & 0x07070707u;
-    s[2 * d] = __builtin_amdgcn_perm(o, e, 0x05010400u);
-    s[2 * d + 1] = __builtin_amdgcn_perm(o, e, 0x07030602u);
-  }
-  s[4] = hi & 7u;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const uint32_t b = __builtin_amdgcn_alignbit(s[w + 1], s[w], 8);
-    h[w] = __builtin_amdgcn_perm(u1hi, u1lo, s[w]) + __builtin_amdgcn_perm(u2hi, u2lo, b);
-  }
-}
-
 // the 16 bits of x mirrored (bit p <- bit 15 - p) when rev
 __device__ __forceinline__ uint32_t mirror_bits16(uint32_t x, bool rev) {
   return rev ? (__builtin_bitreverse32(x) >> 16) : (x & 0xFFFFu);

@@ -1,0 +1,39 @@
+"""GPU parity of the kernel forms that are not the defaults (the library reads
+ADAM_BQSR_OBSERVE / ADAM_BQSR_APPLY once per process, so each form runs in a
+child process): the round-2 lane-per-read observe, the lean observe on
+bucketed batches, the lean apply.  Each child checks a read-order and a
+bucketed job against the oracle (tests/_parity.check: table words,
+expectedMismatch bits, every output char)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import os, sys
+sys.path.insert(0, {root!r}); sys.path.insert(0, os.path.join({root!r}, "tests")); sys.path.insert(0, os.path.join({root!r}, "oracle"))
+from _parity import check
+from adam_amd import synth
+b = synth.generate(12000, (100,), 1, seed=61)
+check([b.slice(0, 5000), b.slice(5000, 12000)], synth.known_sites(2_000_000, seed=5))
+os.environ["ADAM_BQSR_ORDER"] = "group"
+b = synth.generate(6000, (150, 250), 8, seed=62)
+check([b.slice(0, 2000), b.slice(2000, 6000)], synth.known_sites(2_000_000, seed=5))
+os.environ["ADAM_BQSR_ORDER"] = "read"
+b = synth.generate(6000, (60, 100, 140), 3, seed=63)
+check([b])
+print("forms ok")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("observe,apply", [("read", "walk"), ("lean", "lean"), ("chunks", "walk")])
+def test_kernel_forms(observe, apply):
+    env = dict(os.environ, ADAM_BQSR_OBSERVE=observe, ADAM_BQSR_APPLY=apply)
+    r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=env, capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0 and "forms ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
