@@ -192,12 +192,8 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_lean(ApplyParams P) 
             }
           }
         }
-        if ((app || pass) && !(P.probe & 1)) {
-          if (P.probe & 2) {
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 v = {out[0], out[1], out[2], out[3]};
-            __builtin_nontemporal_store(v, (u32x4*)(op + o0));
-          } else if (j + kChunk <= n || P.rd.slots_aligned) {  // aligned: the chunk's other bytes are this read's scratch
+        if (app || pass) {
+          if (j + kChunk <= n || P.rd.slots_aligned) {  // aligned: the chunk's other bytes are this read's scratch
             *(uint4*)(op + o0) = make_uint4(out[0], out[1], out[2], out[3]);
           } else {
 #pragma unroll

@@ -1823,7 +1823,6 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
-  P.probe = getenv("ADAM_BQSR_PROBE") ? atoi(getenv("ADAM_BQSR_PROBE")) : 0;
   if (apply_form() == 1) {
     // bqsr_apply_rows: a packed char table per (read group, mate class) piece,
     // rows of cwp = roundup(L, 32) cycle cells x 6 context groups (dwords)

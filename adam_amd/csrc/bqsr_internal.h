@@ -304,7 +304,6 @@ struct ApplyParams {
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
   int32_t cwp;            // bqsr_apply_rows: cycle cells per packed row (the half window's L, padded to 32)
-  int32_t probe;          // bqsr_apply_lean: measurement variants (ADAM_BQSR_PROBE), 0 in production
 };
 
 // finalize results read back by the host
