@@ -217,7 +217,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
   // run's first block holds the summed increment and cidx = -(run length)
   // (a run adds less than 2^53 units: its integer sum is exact)
   __shared__ unsigned long long rsum[kMaxFoldBlocks];
-  __shared__ int32_t rkey[kMaxFoldBlocks], rfirst[kMaxFoldBlocks], rlen[kMaxFoldBlocks];
+  __shared__ int32_t rkey[kMaxFoldBlocks], rlen[kMaxFoldBlocks];
   __syncthreads();
   const bool blive = tid < nb;
   FoldBlock mine{};

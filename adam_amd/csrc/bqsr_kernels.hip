@@ -1164,10 +1164,10 @@ __device__ __forceinline__ uint32_t ctx_slot(uint32_t a, uint32_t b) {
 }
 __device__ __forceinline__ uint32_t comp_code(uint32_t c) { return c < 4u ? c ^ 3u : c; }
 __device__ __forceinline__ void ctx_table_fill(uint16_t* t, int tid, int nthreads) {
-  for (int i = tid; i < 2 * kCtxTab; i += nthreads) {
+  for (int i = tid; i < (int)(2 * kCtxTab); i += nthreads) {
     const uint32_t e = (uint32_t)i & (kCtxTab - 1u);
     const uint32_t c0 = e & 15u, c1 = (e >> 4) & 15u, c2 = e >> 8;
-    t[i] = (uint16_t)(i < kCtxTab ? ctx_slot(c0, c1) | ctx_slot(c1, c2) << 8
+    t[i] = (uint16_t)((uint32_t)i < kCtxTab ? ctx_slot(c0, c1) | ctx_slot(c1, c2) << 8
                                   : ctx_slot(comp_code(c1), comp_code(c0)) |
                                         ctx_slot(comp_code(c2), comp_code(c1)) << 8);
   }
