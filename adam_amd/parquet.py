@@ -1,0 +1,260 @@
+"""ADAM's own storage: ADAMRecord Parquet in and out.
+
+The reference stores reads as Avro-Parquet ADAMRecords
+(adam-format/src/main/resources/avro/adam.avdl:4-68) and loads them with
+``adamLoad`` -> ``adamParquetLoad`` (core/rdd/AdamContext.scala:139-161,
+318-331), optionally with an Avro projection (AvroParquetInputFormat.
+setRequestedProjection, :150; core/projections/Projection.scala:10-34 over
+ADAMRecordField.scala:28-71); ``adamSave`` writes them back
+(core/rdd/AdamRDDFunctions.scala:37-56).
+
+Here the Parquet pages are decoded by Arrow's C++ reader on host threads --
+they come out columnar already: a string column is an offsets buffer and one
+byte buffer, the ``bqsr_records`` layout itself -- and only the columns BQSR
+reads are requested (:data:`BQSR_PROJECTION`).  The conversion to a
+:class:`RecordBatch` is vectorized (flags from the boolean columns, CIGAR
+strings to BAM elements with TextCigarCodec's rules in numpy); the batch then
+goes to the device like a SAM or BAM parse.
+
+Semantics kept: an Avro null is "field absent" (the HAS_* bits, the
+reference's NPEs / NullPointer paths); strings are UTF-8 in Parquet and Java
+strings in the reference, so a qual char c enters as the byte c & 0xFF (BQSR
+uses ``(c - 33).toByte``, which only sees those 8 bits) and a sequence or MD
+char above 0xFF as the byte 0xFF (no base, no MD digit or letter).  A null
+boolean is read as false (the reference unboxes it: an NPE -- parity
+unpinned, as is every comparison against files ADAM itself wrote: the
+reference cannot run here, so the reader is checked against its own writer
+and the SAM fixtures' columns).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .records import (CigarParseError, F_DUPLICATE, F_HAS_CIGAR, F_HAS_MD, F_HAS_QUAL, F_HAS_REFNAME, F_HAS_RG,
+                      F_HAS_SEQ, F_HAS_START, F_MAPPED, F_NEG_STRAND, F_PAIRED, F_PRIMARY, F_SECOND_OF_PAIR,
+                      RecordBatch, cigar_to_text)
+
+# the ADAMRecord fields BQSR reads (RecalibrateBaseQualities, ReadCovariates, RichADAMRecord, MdTag)
+BQSR_PROJECTION = ("referenceName", "start", "sequence", "qual", "cigar", "recordGroupId", "mismatchingPositions",
+                   "readPaired", "readMapped", "readNegativeStrand", "secondOfPair", "primaryAlignment",
+                   "duplicateRead")
+# ... and MarkDuplicates (MarkDuplicates.scala:24-111, SingleReadBucket, ReferencePositionPair)
+MARKDUP_PROJECTION = ("readName", "recordGroupLibrary", "mateMapped", "referenceId")
+
+_BOOL_BITS = (("readPaired", F_PAIRED), ("readMapped", F_MAPPED), ("readNegativeStrand", F_NEG_STRAND),
+              ("secondOfPair", F_SECOND_OF_PAIR), ("primaryAlignment", F_PRIMARY), ("duplicateRead", F_DUPLICATE))
+
+_CIGAR_OP = np.full(256, -1, dtype=np.int64)
+for _i, _c in enumerate("MIDNSHP=X"):
+    _CIGAR_OP[ord(_c)] = _i
+
+
+def _pa():
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import pyarrow.parquet as pq
+    return pa, pc, pq
+
+
+def _string_column(col, kind: str) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(present, offsets u64 [n+1], bytes u8) of a nullable string column;
+    kind 'qual' / 'seq' / 'md' decides how chars above 0x7F become bytes."""
+    pa, pc, _ = _pa()
+    present = np.asarray(pc.is_valid(col).to_numpy(zero_copy_only=False), dtype=bool)
+    arr = pc.fill_null(col, "").cast(pa.large_binary())
+    if isinstance(arr, pa.ChunkedArray):
+        arr = arr.combine_chunks()
+    n = len(arr)
+    bufs = arr.buffers()
+    off = np.frombuffer(bufs[1], dtype=np.int64, count=arr.offset + n + 1)[arr.offset:] if n else np.zeros(1, np.int64)
+    data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
+    data = data[int(off[0]):int(off[-1])]
+    off = (off - off[0]).astype(np.uint64)
+    if data.size and int(data.max()) >= 0x80:  # UTF-8 beyond ASCII: one byte per char, rebuilt per string
+        strs = [bytes(data[int(off[r]):int(off[r + 1])]).decode("utf-8") for r in range(n)]
+        if kind == "qual":
+            enc = [bytes(ord(c) & 0xFF for c in s) for s in strs]
+        else:
+            enc = [bytes(min(ord(c), 0xFF) for c in s) for s in strs]
+        lens = np.fromiter((len(b) for b in enc), dtype=np.uint64, count=n)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=off[1:])
+        data = np.frombuffer(b"".join(enc), dtype=np.uint8)
+    return present, off, np.ascontiguousarray(data)
+
+
+def parse_cigars(present: np.ndarray, off: np.ndarray, data: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """CIGAR strings (offsets / bytes) -> (element offsets [n+1], BAM elements
+    len << 4 | op), samtools TextCigarCodec.decode's rules vectorized: "*" is
+    the empty CIGAR, every op is preceded by 1..9 digits (a length below
+    2^28), a string ends with an op, ops are MIDNSHP=X.  Raises
+    CigarParseError as records.parse_cigar does."""
+    n = len(off) - 1
+    lens = np.diff(off.astype(np.int64))
+    first = data[np.minimum(off[:-1].astype(np.int64), data.size - 1)] if data.size else np.zeros(n, np.uint8)
+    star = (lens == 1) & (first == ord("*"))
+    use = present & ~star & (lens > 0)
+    d = data.astype(np.int64)
+    isdig = (d >= 48) & (d <= 57)
+    owner = np.repeat(np.arange(n), lens)  # read of each byte
+    keep = use[owner] if owner.size else np.zeros(0, bool)
+    pos = np.nonzero(~isdig & keep)[0]  # op bytes of the parsed strings
+    if np.any(_CIGAR_OP[d[pos]] < 0):
+        raise CigarParseError("Malformed CIGAR string (bad op)")
+    rd = owner[pos]
+    seg0 = np.maximum(np.concatenate([[-1], pos[:-1]]) + 1, off[:-1].astype(np.int64)[rd]) if pos.size else pos
+    nd = pos - seg0
+    if np.any(nd < 1) or np.any(nd > 9):
+        raise CigarParseError("Malformed CIGAR string (op without a length, or length too long)")
+    # every parsed string ends with an op
+    last = off[1:].astype(np.int64) - 1
+    if np.any(isdig[last[use]]):
+        raise CigarParseError("Malformed CIGAR string (ends in a digit)")
+    val = np.zeros(pos.size, dtype=np.int64)
+    for k in range(1, 10):
+        m = nd >= k
+        val[m] += (d[pos[m] - k] - 48) * (10 ** (k - 1))
+    if np.any(val >= (1 << 28)):
+        raise CigarParseError("CIGAR element too long")
+    elems = ((val << 4) | _CIGAR_OP[d[pos]]).astype(np.uint32)
+    counts = np.bincount(rd, minlength=n).astype(np.uint64) if n else np.zeros(0, np.uint64)
+    coff = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(counts, out=coff[1:])
+    return coff, elems
+
+
+def table_to_batch(t) -> RecordBatch:
+    """An Arrow table of ADAMRecord columns (BQSR_PROJECTION) -> RecordBatch."""
+    pa, pc, _ = _pa()
+    n = t.num_rows
+    names = set(t.column_names)
+
+    def col(name, typ):
+        return t.column(name) if name in names else pa.nulls(n, typ)
+
+    flags = np.zeros(n, dtype=np.uint32)
+    for name, bit in _BOOL_BITS:
+        v = pc.fill_null(col(name, pa.bool_()), False).to_numpy(zero_copy_only=False)
+        flags |= np.where(np.asarray(v, dtype=bool), np.uint32(bit), np.uint32(0))
+    s_present, s_off, s_data = _string_column(col("sequence", pa.string()), "seq")
+    q_present, q_off, q_data = _string_column(col("qual", pa.string()), "qual")
+    m_present, m_off, m_data = _string_column(col("mismatchingPositions", pa.string()), "md")
+    c_present, c_off, c_data = _string_column(col("cigar", pa.string()), "cigar")
+    cig_off, cig = parse_cigars(c_present, c_off, c_data)
+    rgc = col("recordGroupId", pa.int32())
+    rg_present = np.asarray(pc.is_valid(rgc).to_numpy(zero_copy_only=False), bool)
+    rg = np.asarray(pc.fill_null(rgc, 0).to_numpy(zero_copy_only=False), dtype=np.int32)
+    stc = col("start", pa.int64())
+    st_present = np.asarray(pc.is_valid(stc).to_numpy(zero_copy_only=False), bool)
+    start = np.asarray(pc.fill_null(stc, 0).to_numpy(zero_copy_only=False), dtype=np.int64)
+    refc = col("referenceName", pa.string())
+    ref_present = np.asarray(pc.is_valid(refc).to_numpy(zero_copy_only=False), bool)
+    # referenceName -> index in first-appearance order (RecordBatch.ref_names)
+    enc = pc.fill_null(refc, "").combine_chunks() if isinstance(refc, pa.ChunkedArray) else pc.fill_null(refc, "")
+    dic = enc.dictionary_encode()
+    codes = np.asarray(dic.indices.to_numpy(zero_copy_only=False), dtype=np.int64)
+    dict_names = dic.dictionary.to_pylist()
+    order: Dict[int, int] = {}
+    ref_names: List[str] = []
+    for c in codes[ref_present]:
+        if int(c) not in order:
+            order[int(c)] = len(ref_names)
+            ref_names.append(dict_names[int(c)])
+    remap = np.full(max(1, len(dict_names)), -1, dtype=np.int32)
+    for c, i in order.items():
+        remap[c] = i
+    ref_index = np.where(ref_present, remap[codes] if codes.size else codes, -1).astype(np.int32)
+    for present, bit in ((rg_present, F_HAS_RG), (m_present, F_HAS_MD), (q_present, F_HAS_QUAL),
+                         (s_present, F_HAS_SEQ), (c_present, F_HAS_CIGAR), (st_present, F_HAS_START),
+                         (ref_present, F_HAS_REFNAME)):
+        flags |= np.where(present, np.uint32(bit), np.uint32(0))
+    return RecordBatch(flags, rg, ref_index, ref_names, start, s_off, s_data, q_off, q_data, cig_off, cig, m_off,
+                       m_data)
+
+
+def read_table(path: str, columns: Optional[Sequence[str]] = None):
+    """The ADAMRecord Parquet file (or directory of part files) at `path`, the
+    requested columns only (those the file lacks are left out)."""
+    _, _, pq = _pa()
+    f = pq.ParquetDataset(path)
+    have = set(f.schema.names)
+    cols = None if columns is None else [c for c in columns if c in have]
+    return f.read(columns=cols, use_threads=True)
+
+
+def read_parquet(path: str) -> RecordBatch:
+    """adamLoad with a BQSR projection: the reads of `path` as one RecordBatch."""
+    return table_to_batch(read_table(path, BQSR_PROJECTION))
+
+
+def _strings_of(present: np.ndarray, off: np.ndarray, data: np.ndarray):
+    pa, _, _ = _pa()
+    n = len(present)
+    if n == 0:
+        return pa.array([], pa.string())
+    arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(off.astype(np.int64)), pa.py_buffer(data.tobytes()),
+                                           pa.py_buffer(np.packbits(present, bitorder="little").tobytes()))
+    return arr.cast(pa.string())
+
+
+def batch_to_table(b: RecordBatch, read_name: Optional[Sequence[Optional[str]]] = None):
+    """RecordBatch -> Arrow table of ADAMRecord columns (adam.avdl field names and
+    types; HAS_* bits off = null).  Strings are the batch's bytes as Latin-1."""
+    pa, _, _ = _pa()
+    f = b.flags
+    has = lambda bit: (f & bit) != 0
+
+    def strcol(present, off, data):
+        if data.size and int(data.max()) >= 0x80:
+            strs = [bytes(data[int(off[r]):int(off[r + 1])]).decode("latin-1") if present[r] else None
+                    for r in range(len(present))]
+            return pa.array(strs, pa.string())
+        return _strings_of(present, off, data)
+
+    cig = [cigar_to_text(b.cigar[int(b.cigar_offset[r]):int(b.cigar_offset[r + 1])]) if has(F_HAS_CIGAR)[r] else None
+           for r in range(b.n_reads)]
+    cols = {
+        "referenceName": pa.array([b.ref_names[i] if h else None for i, h in zip(b.ref_index, has(F_HAS_REFNAME))],
+                                  pa.string()),
+        "start": pa.array(b.start, pa.int64(), mask=~has(F_HAS_START)),
+        "readName": pa.array(list(read_name) if read_name is not None else [None] * b.n_reads, pa.string()),
+        "sequence": strcol(has(F_HAS_SEQ), b.seq_offset, b.seq),
+        "cigar": pa.array(cig, pa.string()),
+        "qual": strcol(has(F_HAS_QUAL), b.qual_offset, b.qual),
+        "recordGroupId": pa.array(b.rg_id, pa.int32(), mask=~has(F_HAS_RG)),
+    }
+    for name, bit in _BOOL_BITS:
+        cols[name] = pa.array(has(bit), pa.bool_())
+    cols["mismatchingPositions"] = strcol(has(F_HAS_MD), b.md_offset, b.md)
+    return pa.table(cols)
+
+
+def write_parquet(b: RecordBatch, path: str, read_name: Optional[Sequence[Optional[str]]] = None) -> None:
+    """adamSave of a RecordBatch's ADAMRecord fields (one Parquet file)."""
+    _, _, pq = _pa()
+    pq.write_table(batch_to_table(b, read_name), path)
+
+
+def recalibrated_qual_column(parts, n_reads: int):
+    """The qual column after BQSR: per read the recalibrated Java chars
+    (bqsr.Partition: chars[qo[r] : qo[r] + out_len[r]]), null where the input
+    had none; UTF-8 as Avro writes Java strings (chars above 0x7F take 2-3
+    bytes, RecalUtil's `toChar` of values beyond Latin-1 included)."""
+    pa, _, _ = _pa()
+    out: List[Optional[str]] = []
+    for p in parts:
+        b = p.batch
+        has_q = (b.flags & F_HAS_QUAL) != 0
+        ch = p.chars
+        ascii_only = not ch.size or int(ch.max()) < 0x80
+        for r in range(b.n_reads):
+            if not has_q[r] and not p.out_len[r]:
+                out.append(None)
+                continue
+            o, ln = int(b.qual_offset[r]), int(p.out_len[r])
+            seg = ch[o:o + ln]
+            out.append(seg.astype(np.uint8).tobytes().decode("ascii") if ascii_only else "".join(map(chr, seg)))
+    assert len(out) == n_reads
+    return pa.array(out, pa.string())

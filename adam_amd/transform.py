@@ -1,8 +1,15 @@
-"""`adam transform` for SAM in, SAM out: the CLI harness around the device
-path (adam-cli/.../cli/Transform.scala:38-110).
+"""`adam transform`: the CLI harness around the device path
+(adam-cli/.../cli/Transform.scala:38-110).
 
     python -m adam_amd.transform INPUT.sam OUTPUT.sam [-mark_duplicate_reads]
         [-recalibrate_base_qualities] [-dbsnp_sites SITES.vcf]
+    python -m adam_amd.transform INPUT.{adam,parquet,sam} OUTPUT.{adam,parquet} [...]
+
+SAM in, SAM out is the device path described below.  ADAMRecord Parquet
+(ADAM's own format) in or out goes through ``transform_parquet``: Arrow
+decodes the Parquet columns on host threads, MarkDuplicates runs over host
+columns, BQSR on the device, and the records are written back as Parquet
+with the qual (and duplicateRead) columns replaced (adamSave).
 
 Steps in Transform.run's order (:66-90): load (the SAM text parsed on the
 device, SAMRecordConverter semantics), MarkDuplicates (`adamMarkDuplicates`),
@@ -37,6 +44,8 @@ import os
 import sys
 import time
 from typing import Dict, List, Optional, Tuple
+
+import numpy as np
 
 from . import _capi, bqsr
 from . import distributed as D
@@ -154,9 +163,76 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
     return {"reads": n_reads, "partitions": len(ranges)}
 
 
+def is_parquet(path: str) -> bool:
+    """ADAM's own format: a Parquet file (magic PAR1) or a directory of part
+    files (what adamSave writes), or a .adam / .parquet name."""
+    if path.endswith((".adam", ".parquet")) or os.path.isdir(path):
+        return True
+    try:
+        with open(path, "rb") as fh:
+            return fh.read(4) == b"PAR1"
+    except OSError:
+        return False
+
+
+def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
+                      dbsnp: Optional[str] = None, device: int = 0) -> Dict[str, float]:
+    """`transform` with ADAMRecord Parquet output (adamSave,
+    core/rdd/AdamRDDFunctions.scala:37-56): the input -- Parquet (adamLoad,
+    AdamContext.scala:318-331, every column kept and written back) or SAM
+    (parsed on the host) -- MarkDuplicates over host columns
+    (bqsr_mark_duplicates), BQSR on the device, the qual (and duplicateRead)
+    columns replaced."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    from . import parquet as P
+    from . import sam as S
+    from .records import F_DUPLICATE, RecordBatch, read_sam_records
+    t0 = time.perf_counter()
+    if is_parquet(inp):
+        table = P.read_table(inp)
+        batch = P.table_to_batch(table.select([c for c in P.BQSR_PROJECTION if c in table.column_names]))
+    else:
+        if mark_duplicates:  # (the host SAM parse carries no library / mateMapped: use SAM output or ADAM input)
+            raise ValueError("-mark_duplicate_reads with SAM input and ADAM output is not supported")
+        recs = read_sam_records(inp)
+        batch = RecordBatch.from_records(recs)
+        table = P.batch_to_table(batch, [r.read_name for r in recs])
+    n = batch.n_reads
+    stats: Dict[str, float] = {"reads": n}
+    if mark_duplicates:
+        col = lambda name: table.column(name).to_pylist() if name in table.column_names else [None] * n
+        names, libs = col("readName"), col("recordGroupLibrary")
+        mate = np.asarray([bool(v) for v in col("mateMapped")], dtype=np.uint8)
+        ref_id = np.asarray([-1 if v is None else v for v in col("referenceId")], dtype=np.int32)
+        if "referenceId" not in table.column_names:  # the reference index, as the SAM converter sets it
+            ref_id = batch.ref_index.astype(np.int32)
+        dup = S.mark_duplicates(names, libs, batch.flags, mate, batch.rg_id, ref_id, batch.start,
+                                batch.qual_offset, batch.qual, batch.cigar_offset, batch.cigar)
+        batch.flags = np.where(dup, batch.flags | F_DUPLICATE, batch.flags & ~np.uint32(F_DUPLICATE)).astype(np.uint32)
+        dcol = pa.array(dup, pa.bool_())
+        table = (table.set_column(table.column_names.index("duplicateRead"), "duplicateRead", dcol)
+                 if "duplicateRead" in table.column_names else table.append_column("duplicateRead", dcol))
+        stats["duplicates"] = int(dup.sum())
+    if recalibrate:
+        snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
+        parts = bqsr.adam_bqsr([batch], snp if snp.table else None, bqsr.Context.get(device))
+        qcol = P.recalibrated_qual_column(parts, n)
+        table = (table.set_column(table.column_names.index("qual"), "qual", qcol)
+                 if "qual" in table.column_names else table.append_column("qual", qcol))
+    tmp = out + ".partial"
+    pq.write_table(table, tmp)
+    os.replace(tmp, out)
+    stats["seconds"] = time.perf_counter() - t0
+    return stats
+
+
 def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
               dbsnp: Optional[str] = None, device: int = 0,
               partition_bytes: int = DEFAULT_PARTITION_BYTES) -> Dict[str, float]:
+    if is_parquet(inp) or out.endswith((".adam", ".parquet")):
+        return transform_parquet(inp, out, mark_duplicates, recalibrate, dbsnp, device)
     t0 = time.perf_counter()
     ctx = bqsr.Context.get(device)
     if recalibrate and not mark_duplicates and os.path.getsize(inp) > 0:
