@@ -213,11 +213,13 @@ def batch_to_table(b: RecordBatch, read_name: Optional[Sequence[Optional[str]]] 
             return pa.array(strs, pa.string())
         return _strings_of(present, off, data)
 
-    cig = [cigar_to_text(b.cigar[int(b.cigar_offset[r]):int(b.cigar_offset[r + 1])]) if has(F_HAS_CIGAR)[r] else None
-           for r in range(b.n_reads)]
+    has_cig = has(F_HAS_CIGAR)
+    co = b.cigar_offset.astype(np.int64)
+    cig = [cigar_to_text(b.cigar[co[r]:co[r + 1]]) if has_cig[r] else None for r in range(b.n_reads)]
     cols = {
-        "referenceName": pa.array([b.ref_names[i] if h else None for i, h in zip(b.ref_index, has(F_HAS_REFNAME))],
-                                  pa.string()),
+        "referenceName": pa.DictionaryArray.from_arrays(
+            pa.array(np.where(has(F_HAS_REFNAME), b.ref_index, 0).astype(np.int32), mask=~has(F_HAS_REFNAME)),
+            pa.array(b.ref_names if b.ref_names else [""], pa.string())).cast(pa.string()),
         "start": pa.array(b.start, pa.int64(), mask=~has(F_HAS_START)),
         "readName": pa.array(list(read_name) if read_name is not None else [None] * b.n_reads, pa.string()),
         "sequence": strcol(has(F_HAS_SEQ), b.seq_offset, b.seq),
