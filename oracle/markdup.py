@@ -11,7 +11,9 @@ bqsr_mark_duplicates (adam_amd/csrc/mark_duplicates.cpp).  It follows:
 
 Pinned by the cases of core/.../rdd/MarkDuplicatesSuite.scala (ported in
 tests/test_markdup.py).  Group iteration order in Spark is its shuffle's; here
-buckets keep first-appearance order, and sortBy is stable as Scala's is.
+buckets keep first-appearance order, and sortBy is stable as Scala's is.  So
+which of several equally scored best buckets stays unmarked is unpinned
+against the reference: `equivalent_marks` accepts any choice among them.
 
 A read is a dict: name, library, rg (None = no recordGroupId), mapped,
 primary, paired, mate_mapped, neg, ref, start, qual (str), cigar (list of
@@ -56,7 +58,10 @@ def score(r) -> int:
     return s
 
 
-def mark_duplicates(reads: List[dict]) -> List[bool]:
+def mark_duplicates(reads: List[dict], ties: Optional[list] = None) -> List[bool]:
+    """MarkDuplicates.apply (:100-111).  `ties`, when a list, receives per
+    scoreAndMarkReads call whose best score is shared the primary-read index
+    lists of the tied best buckets (the first of them kept here)."""
     dup = [False] * len(reads)
     # SingleReadBucket.apply: groupBy (recordGroupId, readName); partition mapped / primary
     buckets: Dict[tuple, dict] = {}
@@ -90,6 +95,9 @@ def mark_duplicates(reads: List[dict]) -> List[bool]:
 
     def score_and_mark(bs):  # scoreAndMarkReads
         scored = sorted(((sum(score(reads[i]) for i in b["prim"]), b) for b in bs), key=lambda t: -t[0])
+        best = [b["prim"] for s, b in scored if s == scored[0][0]]
+        if ties is not None and len(best) > 1:
+            ties.append(best)
         for k, (_, b) in enumerate(scored):
             for i in b["prim"]:
                 dup[i] = k != 0
@@ -120,3 +128,22 @@ def mark_duplicates(reads: List[dict]) -> List[bool]:
         elif fragments:
             score_and_mark(fragments)
     return dup
+
+
+def equivalent_marks(reads: List[dict], got) -> Tuple[bool, str]:
+    """Whether a marking equals mark_duplicates' up to the choice among tied
+    best buckets: reads outside the ties must match exactly; in each tie
+    exactly one bucket's primaries are all unmarked and every other tied
+    bucket's primaries are all marked."""
+    ties: list = []
+    want = mark_duplicates(reads, ties)
+    got = [bool(x) for x in got]
+    tied = {i for t in ties for b in t for i in b}
+    for i, (g, w) in enumerate(zip(got, want)):
+        if g != w and i not in tied:
+            return False, "read %d: %s, expected %s (not in a tie)" % (i, g, w)
+    for t in ties:
+        kept = [b for b in t if not any(got[i] for i in b)]
+        if len(kept) != 1 or any(not all(got[i] for i in b) for b in t if b is not kept[0]):
+            return False, "tie of %d buckets: %d kept" % (len(t), len(kept))
+    return True, ""

@@ -139,3 +139,21 @@ def test_random_reads_against_restatement(seed):
                  cigar=cig)
         reads.append(r)
     run(reads)
+
+
+def test_tied_best_buckets_equivalent():
+    """Equally scored best buckets (MarkDuplicates.scala:67-92 sortBy over a
+    Spark group, whose order is the shuffle's): any one of them may stay
+    unmarked.  The library keeps the first in input order, as the oracle."""
+    reads = [mapped(1, 42, phred=30, name="a"), mapped(1, 42, phred=30, name="b"), mapped(1, 42, name="c")]
+    d = run(reads)
+    assert list(d) == [False, True, True]
+    ok, why = M.equivalent_marks(reads, [True, False, True])  # the other tied bucket kept
+    assert ok, why
+    assert not M.equivalent_marks(reads, [False, False, True])[0]  # both kept
+    assert not M.equivalent_marks(reads, [True, True, True])[0]    # none kept
+    assert not M.equivalent_marks(reads, [True, False, False])[0]  # the poorer read is no tie
+    pairs = pair(0, 10, 0, 210, name="p", phred=30) + pair(0, 10, 0, 210, name="q", phred=30)
+    run(pairs)
+    assert M.equivalent_marks(pairs, [True, True, False, False])[0]
+    assert not M.equivalent_marks(pairs, [True, False, False, True])[0]  # a bucket split
