@@ -281,6 +281,34 @@ bool gather_on() {
   }();
   return v;
 }
+// Fronts of a bucketed batch (OrderDev::n_base), for the chunk-walk passes:
+// the sorted order becomes (front, read group, mate class), a front being a
+// contiguous share of the read indices, and each key a workgroup of its own.
+// Keyed ranges cut anywhere left every workgroup at its own point of the
+// read-index space, so each cache line of the qual / base / bitmap columns,
+// records and ReadInfo was fetched once per key whose reads it holds (PMC
+// 2.1x algorithmic on cfg4, the MALL catching some); the workgroups of one
+// front now start together and sweep the same range.  About eight pieces per
+// CU (cfg4, 192 base keys: apply 5.7 -> 4.2 / 3.9 / 3.9 / 4.1 ms at 4 / 8 / 12
+// / 32 fronts, observe 4.4 -> 4.0 ms), pieces of at least 8192 reads; none
+// when that leaves fewer pieces than CUs or there are more base keys than 4
+// per CU.  ADAM_BQSR_FRONTS=f forces f fronts, 0 turns them off (A/B).
+int fronts(int n_base, int n_cu, int64_t n_reads) {
+  static const int forced = [] {
+    const char* e = getenv("ADAM_BQSR_FRONTS");
+    return e ? std::max(0, atoi(e)) : -1;
+  }();
+  if (forced == 0) return 0;
+  int f = forced;
+  if (f < 0) {
+    if (n_base > 4 * n_cu) return 0;
+    f = (int)std::min<int64_t>((8 * n_cu + n_base - 1) / n_base, n_reads / (8192 * (int64_t)n_base));
+    if ((int64_t)std::max(f, 1) * n_base < n_cu) return 0;
+    f = std::max(f, 1);
+  }
+  while (f > 1 && (int64_t)f * n_base > 4096) --f;  // keys kept in the sort's LDS
+  return f;
+}
 // bqsr_observe_rows' LDS: obs rows [qw][orow], mm rows [qw][wcells], masked, block histogram, context tables
 size_t rows_lds(int qw, int orow, int wcells, int hc) {
   return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes +
@@ -378,14 +406,19 @@ struct bqsr_batch {
   // read-group buckets (OrderDev): several read groups -> the per-base passes
   // walk the reads grouped by read group
   bool bucketed = false;
-  int32_t n_keys = 1;
+  int32_t n_keys = 1;   // n_base * fronts
+  int32_t n_base = 1;   // 2 * read group + mate class
+  int32_t fronts = 0;   // > 0: front-ordered pieces, a chunk-walk workgroup per key (OrderDev::n_base)
   uint32_t* d_perm = nullptr;
   int64_t* d_key_off = nullptr;
   uint32_t* d_key_cnt = nullptr;
   uint32_t* d_cursor = nullptr;
   OrderDev order() const {
-    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, gathered ? d_oslot : nullptr} : OrderDev{nullptr, nullptr, 1};
+    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, gathered ? d_oslot : nullptr, fronts > 0 ? n_base : 0}
+                    : OrderDev{nullptr, nullptr, 1};
   }
+  // workgroups of the chunk-walk passes: a piece each with fronts, else the fold's blocks
+  int32_t pass_blocks() const { return bucketed && fronts > 0 ? n_keys : n_blocks; }
   // bucket-major copies (bqsr_bucket_gather; valid once prepped with `gathered`):
   // the per-base passes' ReadsDev / ReadInfo in sorted order
   bool gathered = false;
@@ -670,7 +703,9 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
     }
   }
   if (b->bucketed) {
-    b->n_keys = 2 * std::max<int32_t>(1, b->dims.n_rg);  // 2 * read group + mate class
+    b->n_base = 2 * std::max<int32_t>(1, b->dims.n_rg);  // 2 * read group + mate class
+    b->fronts = (observe_form() <= 0 && apply_form() <= 0 && !gather_on()) ? fronts(b->n_base, b->ctx->n_cu, n) : 0;
+    b->n_keys = b->n_base * std::max(1, b->fronts);
     if ((st = dalloc(b->allocs, &b->d_perm, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_off, (size_t)b->n_keys + 1)) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_cnt, (size_t)b->n_keys)) != BQSR_OK) return st;
@@ -1322,12 +1357,12 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
       HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
       const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
       hipLaunchKernelGGL(bqsr_key_count, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
-                         b->d_key_cnt);
+                         b->n_base, std::max(1, b->fronts), b->d_key_cnt);
       hipLaunchKernelGGL(bqsr_key_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)b->d_key_cnt, b->n_keys,
                          b->d_key_off, b->d_cursor);
       const unsigned sb = (unsigned)std::min<int64_t>((n + 4095) / 4096, (int64_t)ctx->n_cu * 8);
       hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
-                         b->d_cursor, b->d_perm);
+                         b->n_base, std::max(1, b->fronts), b->d_cursor, b->d_perm);
       HIP_TRY(hipGetLastError());
       b->gathered = gather_on() && b->rd.slots_aligned && observe_form() <= 0 && apply_form() <= 0;
       if (b->gathered) {
@@ -1434,7 +1469,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.obs = t->obs();
     P.mm = t->mm();
     P.part_stride = 2 * P.w.qw * P.wcells + P.w.qw;
-    const size_t need = (size_t)P.part_stride * (b->n_blocks + b->n_keys - 1);  // slabs w + key
+    const size_t need = (size_t)P.part_stride * (b->pass_blocks() + b->n_keys - 1);  // slabs w + key
     if (b->part_words < need) {  // grows with the table geometry; kept across calls
       if (b->d_part) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -1448,7 +1483,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.part = b->d_part;
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
-    P.n_blocks = b->n_blocks;
+    P.n_blocks = form == 0 ? b->pass_blocks() : b->n_blocks;  // (fronts: only with the chunk walk, form 0)
     const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc)
                        : lean    ? lean_lds(P.w.qw, P.orow, P.wcells)
                                  : observe_lds(P.w.qw, P.wcells, form == 0);
@@ -1467,17 +1502,17 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
         hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, true> : bqsr_observe_rows<2, true>), dim3(b->n_blocks),
                            dim3(kBlockThreads), lds, s, P);
     } else if (form == 0)
-      hipLaunchKernelGGL((b->gathered ? bqsr_observe_chunks<true> : bqsr_observe_chunks<false>), dim3(b->n_blocks),
+      hipLaunchKernelGGL((b->gathered ? bqsr_observe_chunks<true> : bqsr_observe_chunks<false>), dim3(P.n_blocks),
                          dim3(kBlockThreads), lds, s, P);
     else if (form == 2 || chunk_lanes(b->bucketed))
       hipLaunchKernelGGL((bqsr_observe_kernel<true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     else
       hipLaunchKernelGGL((bqsr_observe_kernel<false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
-    const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_keys : 1) + 255) / 256);
+    const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_base : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb, ry), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
-                       b->n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0);
+                       P.n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
@@ -1857,7 +1892,8 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     return ok();
   }
   P.piece_stride = piece_bytes(P.w.qw, cw);
-  const size_t need = (size_t)P.piece_stride * (size_t)b->n_keys + (size_t)b->n_keys * 16;  // + rowbad
+  // a char table per base key (fronts share their read group's)
+  const size_t need = (size_t)P.piece_stride * (size_t)b->n_base + (size_t)b->n_base * 16;  // + rowbad
   if (b->chars_bytes < need) {  // grows with the window; kept across calls
     if (b->d_chars) {
       HIP_TRY(hipStreamSynchronize(s));
@@ -1869,14 +1905,14 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     b->chars_bytes = need;
   }
   P.chars = b->d_chars;
-  P.rowbad = (uint32_t*)(b->d_chars + (size_t)P.piece_stride * (size_t)b->n_keys);
-  HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_keys * 16, s));
+  P.rowbad = (uint32_t*)(b->d_chars + (size_t)P.piece_stride * (size_t)b->n_base);
+  HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_base * 16, s));
   const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
   hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
   if (lean)
     hipLaunchKernelGGL(bqsr_apply_lean, dim3(b->n_blocks), dim3(kBlockThreads), apply_lean_lds(P.w.qw, cw), s, P);
   else
-    hipLaunchKernelGGL((b->gathered ? bqsr_apply_kernel<true> : bqsr_apply_kernel<false>), dim3(b->n_blocks),
+    hipLaunchKernelGGL((b->gathered ? bqsr_apply_kernel<true> : bqsr_apply_kernel<false>), dim3(b->pass_blocks()),
                        dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
   HIP_TRY(hipGetLastError());
   return ok();

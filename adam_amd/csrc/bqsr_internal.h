@@ -187,6 +187,12 @@ struct OrderDev {
   // codes copied bucket-major); oslot[i] = the read's slot in the batch (slot
   // bitmap, outputs), perm[i] its index.  nullptr: records are read indices.
   const uint64_t* oslot = nullptr;
+  // fronts (n_base > 0): keys are (front, base key) = front * n_base + base
+  // key, a front being a contiguous share of the read indices, and workgroup
+  // w of the chunk-walk passes takes key w whole -- so the workgroups of one
+  // front sweep the same read range together and share its cache lines
+  // (bqsr_capi.cpp fronts()).  0: keys are base keys, ranges by wg_begin.
+  int32_t n_base = 0;
 };
 
 struct ObserveParams {

@@ -1034,12 +1034,21 @@ __device__ __forceinline__ int key_at(const OrderDev& o, int64_t p) {
   }
   return lo;
 }
+// the chunk-walk passes' workgroup ranges: piece w itself with fronts, else wg_begin
+__device__ __forceinline__ int64_t pass_begin(const ReadsDev& rd, const OrderDev& o, int64_t w, int G) {
+  return o.n_base ? o.key_off[min((int64_t)o.n_keys, w)] : wg_begin(rd, w, G);
+}
 __device__ __forceinline__ int64_t order_read(const OrderDev& o, int64_t i) { return o.perm ? (int64_t)o.perm[i] : i; }
 // the record of sorted position i in the passes' columns: i itself when the
 // batch's columns were gathered into sorted order (bqsr_bucket_gather)
 __device__ __forceinline__ int64_t order_rec(const OrderDev& o, int64_t i) { return o.oslot ? i : order_read(o, i); }
 // the read group of a key's window rows
-__device__ __forceinline__ int key_rg(const OrderDev& o, int key, int rg_lo) { return o.perm ? key >> 1 : rg_lo; }
+__device__ __forceinline__ int key_rg(const OrderDev& o, int key, int rg_lo) {
+  return o.perm ? (o.n_base ? key % o.n_base : key) >> 1 : rg_lo;
+}
+// the base key (read group, mate class) of a key: what the apply char tables are per
+__device__ __forceinline__ int base_key(const OrderDev& o, int key) { return o.n_base ? key % o.n_base : key; }
+__device__ __forceinline__ int order_base_keys(const OrderDev& o) { return o.perm ? (o.n_base ? o.n_base : o.n_keys) : 1; }
 // the cycle cells a piece's windows hold: all of them in read order, the
 // key's mate-class half when bucketed (OrderDev)
 struct WinGeom {
@@ -1047,7 +1056,7 @@ struct WinGeom {
 };
 __device__ __forceinline__ WinGeom win_geom(const OrderDev& o, const TableGeom& g, int key) {
   if (!o.perm) return WinGeom{0, g.C};
-  return (key & 1) ? WinGeom{0, g.L} : WinGeom{g.L + 1, g.L};
+  return (key & 1) ? WinGeom{0, g.L} : WinGeom{g.L + 1, g.L};  // (n_base is even: key & 1 is the mate class)
 }
 
 
@@ -1782,7 +1791,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
   const bool ident = P.ord.perm == nullptr;
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
   ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+  const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -2207,27 +2216,37 @@ template __global__ void bqsr_observe_rows<4, false>(ObserveParams);
 extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd, OrderDev ord, int32_t n_blocks,
                                               int32_t stride, int32_t wcells, Window w, TableGeom g, int64_t* touched,
                                               int64_t* obs, int64_t* mm, int32_t junk) {
-  const int nk = order_keys(ord);
+  // fronts: a thread per (base key, word) sums the base key's pieces (slab
+  // 2 key of workgroup key), one atomic per table word as without fronts
+  const int nk = order_base_keys(ord);
   const int nc = w.qw * wcells;
   const int64_t total = (int64_t)nk * stride;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int key = (int)(t / stride);
     const int i = (int)(t - (int64_t)key * stride);
-    const int64_t k0 = key_begin(ord, rd.n_reads, key), k1 = key_begin(ord, rd.n_reads, key + 1);
-    if (k0 >= k1) continue;
-    // grid y: thread y takes the groups y, y + gridDim.y, ... of kRedSlabs
-    // slabs of the key's range
-    const int64_t wk1 = wg_of(rd, k1 - 1, n_blocks);
     uint64_t s = 0;
-    for (int64_t w0 = wg_of(rd, k0, n_blocks) + (int64_t)blockIdx.y * kRedSlabs; w0 <= wk1;
-         w0 += (int64_t)gridDim.y * kRedSlabs) {
-      const int64_t w1 = min(wk1, w0 + kRedSlabs - 1);
+    if (ord.n_base) {
+#pragma unroll 4
+      for (int kf = key; kf < ord.n_keys; kf += ord.n_base) {
+        const uint32_t v = part[2 * (int64_t)kf * stride + i];
+        if (ord.key_off[kf] < ord.key_off[kf + 1]) s += v;
+      }
+    } else {
+      const int64_t k0 = key_begin(ord, rd.n_reads, key), k1 = key_begin(ord, rd.n_reads, key + 1);
+      if (k0 >= k1) continue;
+      // grid y: thread y takes the groups y, y + gridDim.y, ... of kRedSlabs
+      // slabs of the key's range
+      const int64_t wk1 = wg_of(rd, k1 - 1, n_blocks);
+      for (int64_t w0 = wg_of(rd, k0, n_blocks) + (int64_t)blockIdx.y * kRedSlabs; w0 <= wk1;
+           w0 += (int64_t)gridDim.y * kRedSlabs) {
+        const int64_t w1 = min(wk1, w0 + kRedSlabs - 1);
 #pragma unroll 8
-      for (int64_t b = w0; b <= w1; ++b) {
-        // a workgroup with an empty range in between wrote no slab (its words
-        // are read but not added: the loads stay independent)
-        const uint32_t v = part[(b + (ord.perm ? key : 0)) * stride + i];
-        if (max(k0, wg_begin(rd, b, n_blocks)) < min(k1, wg_begin(rd, b + 1, n_blocks))) s += v;
+        for (int64_t b = w0; b <= w1; ++b) {
+          // a workgroup with an empty range in between wrote no slab (its words
+          // are read but not added: the loads stay independent)
+          const uint32_t v = part[(b + (ord.perm ? key : 0)) * stride + i];
+          if (max(k0, wg_begin(rd, b, n_blocks)) < min(k1, wg_begin(rd, b + 1, n_blocks))) s += v;
+        }
       }
     }
     if (!s) continue;
@@ -2267,21 +2286,24 @@ constexpr int kSortThreads = 256;
 constexpr int kSortPer = 16;             // reads per thread in the scatter
 constexpr int kSortLdsKeys = 4096;       // keys kept in LDS; more go straight to global atomics
 
-// key = 2 * read group + mate class (OrderDev); n_keys = 2 * n_rg
-__device__ __forceinline__ int sort_key(const ReadMeta& m, int n_keys) {
+// key = front * n_base + 2 * read group + mate class (OrderDev); n_base = 2 *
+// n_rg, front = read r's share of [0, n) when there are `fronts` of them
+__device__ __forceinline__ int sort_key(const ReadMeta& m, int64_t r, int64_t n, int n_base, int fronts) {
   const int cls = ((m.flags & BQSR_F_PAIRED) && (m.flags & BQSR_F_SECOND_OF_PAIR)) ? 1 : 0;
-  return 2 * min((int)m.rg, n_keys / 2 - 1) + cls;
+  const int f = fronts > 1 ? (int)((r * fronts) / n) : 0;
+  return f * n_base + 2 * min((int)m.rg, n_base / 2 - 1) + cls;
 }
 
 extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_count(const ReadMeta* meta, int64_t n,
-                                                                            int32_t n_keys, uint32_t* counts) {
+                                                                            int32_t n_keys, int32_t n_base,
+                                                                            int32_t fronts, uint32_t* counts) {
   __shared__ uint32_t h[kSortLdsKeys];
   const bool lds = n_keys <= kSortLdsKeys;
   if (lds)
     for (int i = threadIdx.x; i < n_keys; i += blockDim.x) h[i] = 0;
   __syncthreads();
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    const int k = sort_key(meta[r], n_keys);
+    const int k = sort_key(meta[r], r, n, n_base, fronts);
     if (lds) atomicAdd(&h[k], 1u); else atomicAdd(&counts[k], 1u);
   }
   __syncthreads();
@@ -2320,7 +2342,8 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_key_scan(const uint32_t*
 }
 
 extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(const ReadMeta* meta, int64_t n,
-                                                                              int32_t n_keys, uint32_t* cursor,
+                                                                              int32_t n_keys, int32_t n_base,
+                                                                              int32_t fronts, uint32_t* cursor,
                                                                               uint32_t* perm) {
   __shared__ uint32_t h[kSortLdsKeys];
   const bool lds = n_keys <= kSortLdsKeys;
@@ -2330,7 +2353,7 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
     if (!lds) {
       for (int i = 0; i < kSortPer; ++i) {
         const int64_t r = c0 + (int64_t)i * kSortThreads + tid;
-        if (r < n) perm[atomicAdd(&cursor[sort_key(meta[r], n_keys)], 1u)] = (uint32_t)r;
+        if (r < n) perm[atomicAdd(&cursor[sort_key(meta[r], r, n, n_base, fronts)], 1u)] = (uint32_t)r;
       }
       continue;
     }
@@ -2341,7 +2364,7 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
 #pragma unroll
     for (int i = 0; i < kSortPer; ++i) {
       const int64_t r = c0 + (int64_t)i * kSortThreads + tid;
-      key[i] = r < n ? sort_key(meta[r], n_keys) : -1;
+      key[i] = r < n ? sort_key(meta[r], r, n, n_base, fronts) : -1;
     }
 #pragma unroll
     for (int i = 0; i < kSortPer; ++i) rank[i] = key[i] >= 0 ? atomicAdd(&h[key[i]], 1u) : 0u;
@@ -2871,7 +2894,7 @@ constexpr int kApplyU = 4;  // chunks in flight per lane
 // piece's table into LDS (it used to compute it itself: 65 us of a 0.87 ms
 // cfg2 launch with every workgroup repeating the same 156K entries).
 extern "C" __global__ void bqsr_apply_chars(ApplyParams P, uint8_t* chars) {
-  const int nk = order_keys(P.ord), qw = P.w.qw, q_lo = P.w.q_lo;
+  const int nk = order_base_keys(P.ord), qw = P.w.qw, q_lo = P.w.q_lo;
   const int64_t total = (int64_t)nk * P.piece_stride;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int key = (int)(t / P.piece_stride);
@@ -2918,7 +2941,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
   uint32_t* mk = mk_all + wave * 64;
   const int q_lo = P.w.q_lo;
   const int G = gridDim.x;
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+  const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
   ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
 
@@ -2932,13 +2955,13 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     __syncthreads();  // the previous piece is done with the table
     // ---- the piece's char table (bqsr_apply_chars) into LDS, 16 B a thread ----
     {
-      const uint4* src = (const uint4*)(P.chars + (int64_t)key * P.piece_stride);
+      const uint4* src = (const uint4*)(P.chars + (int64_t)base_key(P.ord, key) * P.piece_stride);
       uint4* dst = (uint4*)lut;
       const int n16 = (int)(P.piece_stride >> 4);
       for (int i = tid; i < n16; i += blockDim.x) dst[i] = src[i];
     }
     if (tid == 0) {  // the longest run of rows without a 0 entry: quals there need no per-entry check
-      const uint4 rb = *(const uint4*)(P.rowbad + key * 4);  // one load, not one per row
+      const uint4 rb = *(const uint4*)(P.rowbad + base_key(P.ord, key) * 4);  // one load, not one per row
       const uint32_t rw[4] = {rb.x, rb.y, rb.z, rb.w};
       int best_lo = 0, best_n = 0, run = 0;
       for (int r = 0; r < qw; ++r) {

@@ -1,7 +1,8 @@
 """GPU parity of the kernel forms that are not the defaults (the library reads
 ADAM_BQSR_OBSERVE / ADAM_BQSR_APPLY once per process, so each form runs in a
 child process): the round-2 lane-per-read observe, the lean observe on
-bucketed batches, the lean apply.  Each child checks a read-order and a
+bucketed batches, the lean apply, the chunk walk on bucketed batches with
+front-ordered pieces forced on (5 fronts) and off.  Each child checks a read-order and a
 bucketed job against the oracle (tests/_parity.check: table words,
 expectedMismatch bits, every output char)."""
 import os
@@ -31,9 +32,13 @@ print("forms ok")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("observe,apply", [("read", "walk"), ("lean", "lean"), ("chunks", "walk")])
-def test_kernel_forms(observe, apply):
+@pytest.mark.parametrize("observe,apply,fronts", [("read", "walk", None), ("lean", "lean", None),
+                                                   ("chunks", "walk", None), ("chunks", "walk", "5"),
+                                                   ("chunks", "walk", "0")])
+def test_kernel_forms(observe, apply, fronts):
     env = dict(os.environ, ADAM_BQSR_OBSERVE=observe, ADAM_BQSR_APPLY=apply)
+    if fronts is not None:  # front-ordered pieces of the bucketed jobs forced on / off (bqsr_capi.cpp fronts())
+        env["ADAM_BQSR_FRONTS"] = fronts
     r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=env, capture_output=True, text=True,
                        timeout=280)
     assert r.returncode == 0 and "forms ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -15,5 +15,5 @@ for envs in "$@"; do
   env $envs timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/s$i" -o run --output-format csv -- \
     python3 "$R/bench.py" --config "$CFG" --no-cpu-baseline --no-parity --steps 5 --warmup 1 > "$O/s$i.log" 2>&1
   echo "== $envs"
-  find "$O/s$i" -name "*kernel_stats.csv" -exec grep -E "prep|observe|apply" {} \; | cut -d, -f1,4
+  find "$O/s$i" -name "*kernel_stats.csv" -exec grep -E "prep|observe|apply|reduce|fold_hist" {} \; | cut -d, -f1,4
 done
