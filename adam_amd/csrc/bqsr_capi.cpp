@@ -704,7 +704,9 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   }
   if (b->bucketed) {
     b->n_base = 2 * std::max<int32_t>(1, b->dims.n_rg);  // 2 * read group + mate class
-    b->fronts = (observe_form() <= 0 && apply_form() <= 0 && !gather_on()) ? fronts(b->n_base, b->ctx->n_cu, n) : 0;
+    b->fronts = ((observe_form() <= 0 || observe_form() == 4) && apply_form() <= 0 && !gather_on())
+                    ? fronts(b->n_base, b->ctx->n_cu, n)
+                    : 0;
     b->n_keys = b->n_base * std::max(1, b->fronts);
     if ((st = dalloc(b->allocs, &b->d_perm, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_off, (size_t)b->n_keys + 1)) != BQSR_OK) return st;
@@ -1483,7 +1485,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.part = b->d_part;
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
-    P.n_blocks = form == 0 ? b->pass_blocks() : b->n_blocks;  // (fronts: only with the chunk walk, form 0)
+    P.n_blocks = (form == 0 || (lean && b->bucketed)) ? b->pass_blocks() : b->n_blocks;  // (fronts: chunk walk or lean)
     const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc)
                        : lean    ? lean_lds(P.w.qw, P.orow, P.wcells)
                                  : observe_lds(P.w.qw, P.wcells, form == 0);
@@ -1491,7 +1493,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     b->hq_by_observe = form == 3 && b->bucketed;
     if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
     if (lean) {
-      hipLaunchKernelGGL((b->bucketed ? bqsr_observe_lean<false> : bqsr_observe_lean<true>), dim3(b->n_blocks),
+      hipLaunchKernelGGL((b->bucketed ? bqsr_observe_lean<false> : bqsr_observe_lean<true>), dim3(P.n_blocks),
                          dim3(kBlockThreads), lds, s, P);
     } else if (form == 3) {
       const bool wide = b->dims.max_len > 128;

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   // range meets, its window holding the key's half of the cycle cells
   constexpr bool ident = kIdent;  // P.ord.perm == nullptr
   const int nk = kIdent ? 1 : order_keys(P.ord);
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
+  const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
 
   for (int key = kIdent ? 0 : (wa < wb ? key_at(P.ord, wa) : nk); key < nk; ++key) {

@@ -34,7 +34,7 @@ print("forms ok")
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("observe,apply,fronts", [("read", "walk", None), ("lean", "lean", None),
                                                    ("chunks", "walk", None), ("chunks", "walk", "5"),
-                                                   ("chunks", "walk", "0")])
+                                                   ("chunks", "walk", "0"), ("lean", "walk", "5")])
 def test_kernel_forms(observe, apply, fronts):
     env = dict(os.environ, ADAM_BQSR_OBSERVE=observe, ADAM_BQSR_APPLY=apply)
     if fronts is not None:  # front-ordered pieces of the bucketed jobs forced on / off (bqsr_capi.cpp fronts())
