@@ -261,17 +261,23 @@ bqsr_status bgzf_inflate(const uint8_t* data, int64_t n, std::vector<uint8_t>& o
   while (p < n) {
     if (n - p < 18 || data[p] != 31 || data[p + 1] != 139 || data[p + 2] != 8 || !(data[p + 3] & 4))
       return fail(BQSR_ERR_SAM_PARSE, "BAM: not a BGZF block at byte " + std::to_string(p));
+    // an untrusted file: every field is bounds-checked before it is read
     const int64_t xlen = data[p + 10] | (data[p + 11] << 8);
+    const int64_t xend = p + 12 + xlen;
+    if (xend > n) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated BGZF header at byte " + std::to_string(p));
     int64_t bsize = -1;
-    for (int64_t q = p + 12; q + 4 <= p + 12 + xlen;) {  // the BC subfield holds BSIZE
+    for (int64_t q = p + 12; q + 4 <= xend;) {  // the BC subfield holds BSIZE
       const int64_t sl = data[q + 2] | (data[q + 3] << 8);
+      if (q + 4 + sl > xend) return fail(BQSR_ERR_SAM_PARSE, "BAM: BGZF extra subfield overruns its header");
       if (data[q] == 'B' && data[q + 1] == 'C' && sl == 2) bsize = data[q + 4] | (data[q + 5] << 8);
       q += 4 + sl;
     }
     if (bsize < 0 || p + bsize + 1 > n) return fail(BQSR_ERR_SAM_PARSE, "BAM: BGZF block without BSIZE");
     const int64_t blen = bsize + 1;
     const int64_t hdr = 12 + xlen;
+    if (blen < hdr + 8) return fail(BQSR_ERR_SAM_PARSE, "BAM: BGZF BSIZE smaller than its header");
     const int64_t isize = le32(data + p + blen - 4);
+    if (isize > 65536) return fail(BQSR_ERR_SAM_PARSE, "BAM: BGZF ISIZE above 64 KiB");
     blks.push_back(Blk{p + hdr, blen - hdr - 8, total, isize});
     total += isize;
     p += blen;
@@ -293,8 +299,10 @@ bqsr_status bgzf_inflate(const uint8_t* data, int64_t n, std::vector<uint8_t>& o
       zs.next_out = (Bytef*)(out.data() + k.dst);
       zs.avail_out = (uInt)k.isize;
       const int rc = inflate(&zs, Z_FINISH);
-      if (rc != Z_STREAM_END || zs.total_out != (uLong)k.isize) bad = 1;
+      const bool ok_len = rc == Z_STREAM_END && zs.total_out == (uLong)k.isize;
       inflateEnd(&zs);
+      // the block's CRC32 of its uncompressed bytes (the 4 bytes before ISIZE)
+      if (!ok_len || crc32(0L, out.data() + k.dst, (uInt)k.isize) != le32(data + k.src + k.csize)) bad = 1;
     }
   };
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)std::thread::hardware_concurrency(),
@@ -302,7 +310,7 @@ bqsr_status bgzf_inflate(const uint8_t* data, int64_t n, std::vector<uint8_t>& o
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t) th.emplace_back(work);
   for (auto& t : th) t.join();
-  if (bad) return fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate");
+  if (bad) return fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate or fails its CRC32");
   out.resize((size_t)total);
   return BQSR_OK;
 }

@@ -379,6 +379,7 @@ struct bqsr_batch {
   int64_t qhigh = 0;            // quals >= 128 (negative Java bytes) in the batch
   std::vector<void*> allocs;
   std::vector<size_t> staged_cnt;  // column element counts (bqsr_batch_create_staged)
+  const bqsr_staged* staged_src = nullptr;  // the one staged partition this batch uploads
   uint8_t* d_bases2 = nullptr;     // staged: the uploaded 2-bit base codes
   uint64_t* d_bexc = nullptr;      //         and their exceptions
   uint64_t* d_qcodes = nullptr;    // staged: the uploaded qual chunks (codes, base bytes)
@@ -1082,15 +1083,19 @@ bqsr_status bqsr_batch_create_staged(bqsr_context* ctx, const bqsr_staged* S_, b
     return st;
   if ((st = finish_batch(b.get(), S_->max_slot)) != BQSR_OK) return st;
   b->staged_cnt.assign(S_->cnt, S_->cnt + kStagedCols);
+  b->staged_src = S_;
   *out = b.release();
   return ok();
 }
 
 bqsr_status bqsr_batch_upload_async(bqsr_batch* b, const bqsr_staged* S_, void* stream) {
   if (!b || !S_) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: bad arguments");
-  if (b->staged_cnt.size() != kStagedCols || !std::equal(b->staged_cnt.begin(), b->staged_cnt.end(), S_->cnt) ||
-      b->rd.n_reads != S_->n_reads)
-    return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: batch was not created from a partition of this shape");
+  // the batch's launch parameters (quality window, qual histogram, read-group
+  // order) were derived from the staged partition it was created from: any
+  // other partition, even one of the same shape, is refused
+  if (b->staged_src != S_ || b->staged_cnt.size() != kStagedCols ||
+      !std::equal(b->staged_cnt.begin(), b->staged_cnt.end(), S_->cnt) || b->rd.n_reads != S_->n_reads)
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_upload_async: batch was not created from this staged partition");
   HIP_TRY(hipSetDevice(b->ctx->device));
   void* dst[kStagedCols] = {(void*)b->rd.meta,  (void*)b->rd.align,  nullptr,           nullptr,
                             (void*)b->rd.md,    (void*)b->rd.cigar,  (void*)b->d_bases2, (void*)b->d_bexc,
@@ -2092,11 +2097,10 @@ bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64
   const bool vec = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
   const int64_t n16 = vec ? bytes / 16 : 0;
   const int64_t head = 16 * n16, tail = bytes - head;
-  if (tail > 1 << 20) return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_async: unaligned buffers above 1 MiB");
   const int64_t need = std::max<int64_t>((n16 + 255) / 256, (tail + 255) / 256);
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, copy_blocks(ctx)));
   hipLaunchKernelGGL(bqsr_copy16, dim3(g), dim3(256), 0, S(stream), (const uint4*)src, (uint4*)dst, n16,
-                     (const uint8_t*)src + head, (uint8_t*)dst + head, (int32_t)tail);
+                     (const uint8_t*)src + head, (uint8_t*)dst + head, tail);
   HIP_TRY(hipGetLastError());
   return ok();
 }

@@ -3383,12 +3383,12 @@ extern "C" __global__ void bqsr_quals_exceptions(const uint64_t* exc, int64_t n,
 // D2H by a kernel runs beside the DMA engines' H2D at once, where two DMA
 // copies share the link (tools/link_probe.hip: DMA H2D 58 + kernel D2H
 // concurrently 85 GB/s in total, two DMA copies 57).  16-B pieces, then the
-// tail bytes.
+// tail bytes (all of an unaligned buffer), both grid-stride.
 extern "C" __global__ void bqsr_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16,
-                                       const uint8_t* __restrict__ tsrc, uint8_t* __restrict__ tdst, int32_t ntail) {
+                                       const uint8_t* __restrict__ tsrc, uint8_t* __restrict__ tdst, int64_t ntail) {
   const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = t0; i < n16; i += step) dst[i] = src[i];
-  if (t0 < ntail) tdst[t0] = tsrc[t0];
+  for (int64_t i = t0; i < ntail; i += step) tdst[i] = tsrc[i];
 }
 
 // --------------------------------------------------------- table merge -----

@@ -47,6 +47,21 @@ def _host_coll(t: torch.Tensor) -> bool:
     return t.device.type != "cpu" and dist.get_backend() == "gloo"
 
 
+def allreduce(t: torch.Tensor, op=None) -> torch.Tensor:
+    """In-place all-reduce of `t` (SUM by default) on any backend: RCCL on
+    device tensors, gloo on a host copy.  For the bench's timing and parity
+    reductions (not on the data path)."""
+    op = dist.ReduceOp.SUM if op is None else op
+    if _multi():
+        if _host_coll(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
+    return t
+
+
 def allreduce_table(words: torch.Tensor) -> torch.Tensor:
     """Exact int64 sum of the ranks' count tables, in place (RecalTable.++ on counts)."""
     if words.dtype != torch.int64:

@@ -37,9 +37,10 @@ class ResidentJob:
     STAGES = ("prep", "observe", "fold", "apply")
 
     def __init__(self, batch: RecordBatch, dims, snp: Optional["bqsr.SnpTable"] = None, device: int = 0,
-                 max_exc: int = 1 << 16, read_base: int = 0):
+                 max_exc: int = 1 << 16, read_base: Optional[int] = None):
         """read_base: global index of the shard's first read (reads of the
-        ranks before this one): errors are reported in global read order."""
+        ranks before this one): errors are reported in global read order.
+        Required when several ranks run the job."""
         import torch
         self.torch = torch
         self.L = L = _capi.lib()
@@ -70,7 +71,9 @@ class ResidentJob:
         self.em_part = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self.lut = ctypes.c_void_p()
         self.world = D.dist.get_world_size() if D._multi() else 1
-        self.read_base = int(read_base)
+        if read_base is None and self.world > 1:
+            raise ValueError("several ranks: read_base (reads of the ranks before this one) is required")
+        self.read_base = int(read_base or 0)
         self.err_keys = torch.empty(2, dtype=torch.int64, device=self.dev)
         self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         self.kt: Dict[str, List[float]] = {k: [] for k in self.STAGES}

@@ -46,10 +46,12 @@ class StreamedShard:
     """Partitions of one rank's shard: pinned host copies + device batches."""
 
     def __init__(self, ctx, parts: Sequence, dims, sites_handle=None, device: int = 0, max_exc: int = 1 << 16,
-                 site_contigs: Optional[Sequence[str]] = None, read_base: int = 0, zero_copy: bool = False,
+                 site_contigs: Optional[Sequence[str]] = None, read_base: Optional[int] = None,
+                 zero_copy: bool = False,
                  d2h: str = "kernel"):
         """read_base: global index of the shard's first read (reads of the
-        ranks before this one): multi-rank errors are raised in global order."""
+        ranks before this one): multi-rank errors are raised in global order;
+        required when several ranks run the job."""
         import torch
         self.torch = torch
         self.L = L = _capi.lib()
@@ -64,7 +66,9 @@ class StreamedShard:
         self.n_bases = 0
         self.staged_bytes = 0
         self.site_contigs = site_contigs
-        self.read_base = int(read_base)
+        if read_base is None and D._multi():
+            raise ValueError("several ranks: read_base (reads of the ranks before this one) is required")
+        self.read_base = int(read_base or 0)
         # zero_copy: apply writes its outputs straight into the pinned host
         # buffers (device stores over PCIe, no download copies)
         self.zero_copy = bool(zero_copy)
@@ -129,6 +133,7 @@ class StreamedShard:
         self.ev_up = [torch.cuda.Event() for _ in range(n)]
         self.ev_ap = [torch.cuda.Event() for _ in range(n)]
         self.ev_dl = [torch.cuda.Event() for _ in range(2)]
+        self.ev_exc = [torch.cuda.Event() for _ in range(n)]  # partition i's exception list copied back
         self.dl_used = [False, False]
         self.ev_status = [torch.cuda.Event() for _ in range(2)]
         self.ev_done = [torch.cuda.Event() for _ in range(2)]
@@ -144,8 +149,10 @@ class StreamedShard:
         uploads start as soon as the previous job's apply is done with each
         partition, while its results still move back on the other copy
         stream.  At most two jobs may be pending; ``finish`` raises a job's
-        errors and makes its results (host_qual / host_start / host_len)
-        valid until the next ``run``."""
+        errors.  The host results (host_qual / host_start / host_len /
+        host_exc) are shared by the jobs: they hold the last job's results
+        once no job is pending (``exceptions`` / ``qual_chars`` refuse to read
+        them before), since a pending job's apply and copies overwrite them."""
         torch, L = self.torch, self.L
         if len(self.pending) >= 2:
             raise RuntimeError("two jobs pending: finish() one first")
@@ -187,6 +194,8 @@ class StreamedShard:
                 if self.dl_used[k]:
                     comp.wait_event(self.ev_dl[k])  # output buffer k drained to the host
                 oq, os_, ol = self.out_qual[k], self.out_start[k], self.out_len[k]
+            if self.jobs:
+                comp.wait_event(self.ev_exc[i])  # the previous job's exception list of partition i is on the host
             if record_apply:
                 self.ev_apply_t[i][0].record(comp)
             exc_i = ctypes.c_void_p(self.exc.data_ptr() + 8 * i * self.max_exc)
@@ -213,6 +222,7 @@ class StreamedShard:
                     for h, d in pairs:
                         h.copy_(d, non_blocking=True)
             self.ev_dl[k].record(dn)
+            self.ev_exc[i].record(dn)
             self.dl_used[k] = True
         # (4) several ranks: the job's first error in global read order on every rank
         if D._multi():
@@ -275,8 +285,13 @@ class StreamedShard:
             check(L.bqsr_job_errors_import_async(bh, ctypes.c_void_p((red if i == 0 else none).data_ptr()), sp))
         self._err_keep = (keys, red, none)
 
+    def _results_ready(self):
+        if self.pending:
+            raise RuntimeError("a job is pending: its apply and copies overwrite the host results; finish() it first")
+
     def exceptions(self, i: int):
         """Partition i's chars above 0xFF of the last job: (slot, Java char) pairs."""
+        self._results_ready()
         a = self.host_exc[i * self.max_exc: i * self.max_exc + self.n_exc[i]].numpy()
         return [(int(v) >> 16, int(v) & 0xFFFF) for v in a]
 
@@ -285,6 +300,7 @@ class StreamedShard:
         (uint16), given its packed slot: the u8 output with the partition's
         exceptions applied."""
         import numpy as np
+        self._results_ready()
         st, ln = int(self.host_start[i][r]), int(self.host_len[i][r])
         out = self.host_qual[i][slot + st: slot + st + ln].numpy().astype(np.uint16)
         for s, code in self.exceptions(i):

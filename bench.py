@@ -39,9 +39,14 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Without WORLD_SIZE in the environment and N > 1 this process "
+                         "launches the N ranks itself; under torch.distributed.run it must equal WORLD_SIZE")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend (nccl = RCCL over xGMI; gloo: host collectives, ranks may "
+                         "share a GPU -- tests)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
@@ -59,11 +64,75 @@ def parse():
                          "apply writing into pinned host memory")
     ap.add_argument("--d2h", default="kernel", choices=("kernel", "dma"),
                     help="cfg5: results copied back by a kernel (beside the DMA uploads) or by DMA copies")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, child_argv, poll_s: float = 0.2, out=None) -> int:
+    """Start `n` ranks of `child_argv` (a command list) as fresh child
+    processes -- RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+    set, the way torch.distributed.run would -- wait for all of them, relay
+    rank 0's stdout (the JSON line) and return 0, or the first failing rank's
+    exit status (the other ranks are then terminated: a rank left waiting in
+    a collective would never return).  The launcher itself never touches the
+    GPU (it does not import torch)."""
+    import subprocess
+    import tempfile
+    out = out or sys.stdout
+    port = _free_port()
+    procs = []
+    line0 = tempfile.TemporaryFile()
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(child_argv, env=env, stdout=line0 if r == 0 else 2))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    line0.seek(0)
+    text = line0.read().decode()
+    line0.close()
+    if rc == 0:
+        out.write(text)
+        out.flush()
+    else:
+        sys.stderr.write(text)
+        print("bench: a rank failed (exit status %d); no result line" % rc, file=sys.stderr, flush=True)
+    return rc
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        # bench.py --gpus N without a launcher: start the N ranks here
+        sys.exit(launch(args.gpus, [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -72,16 +141,32 @@ def main():
     from adam_amd import distributed as D
     from adam_amd._capi import Dims, check
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # a rank per GPU; with gloo (tests) ranks beyond the device count share GPUs.
+    # device_count() does not initialise the GPU on this runtime.
+    n_dev = torch.cuda.device_count()
+    if n_dev < 1:
+        raise SystemExit("bench: no HIP device")
+    if world > n_dev and args.backend == "nccl":
+        raise SystemExit("bench: %d ranks over RCCL need %d GPUs (%d visible); use --backend gloo to share" %
+                         (world, world, n_dev))
+    dev_index = local % n_dev
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            torch.zeros(1, device=dev)  # torch's HIP runtime up before the library's
+            dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise SystemExit("bench: process group has %d ranks, expected %d" % (dist.get_world_size(), world))
     L = _capi.lib()
-    ctx = bqsr.Context.get(local)
+    ctx = bqsr.Context.get(dev_index)
 
     cfg = dict(synth.CONFIGS[args.config])
     if args.config == "cfg5":
@@ -105,7 +190,7 @@ def main():
     n_bases = batch.n_bases
 
     from adam_amd.job import ResidentJob
-    job = ResidentJob(batch, Dims(cfg["n_rg"], max(cfg["lens"])), snp, local, read_base=r0)
+    job = ResidentJob(batch, Dims(cfg["n_rg"], max(cfg["lens"])), snp, dev_index, read_base=r0)
 
     for _ in range(args.warmup):
         job.step(False)
@@ -127,10 +212,10 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        D.allreduce(t, dist.ReduceOp.MAX)
         elapsed = float(t.item())
         nb = torch.tensor([n_bases], dtype=torch.int64, device=dev)
-        dist.all_reduce(nb)
+        D.allreduce(nb)
         total_bases = int(nb.item())
     else:
         total_bases = n_bases
@@ -291,9 +376,9 @@ def parity_multi(job, cfg, batch, sites, world, rank, dev):
     first_g = (job.read_base + first) if bad else np.iinfo(np.int64).max
     red = torch.tensor([bad, int(not table_ok), int(not em_ok), len(exc), batch.n_reads], dtype=torch.int64,
                        device=dev)
-    dist.all_reduce(red)
+    D.allreduce(red)
     fr = torch.tensor([first_g], dtype=torch.int64, device=dev)
-    dist.all_reduce(fr, op=dist.ReduceOp.MIN)
+    D.allreduce(fr, dist.ReduceOp.MIN)
     red = red.cpu().tolist()
     fr = int(fr.item())
     return {"checked": True, "ok": red[0] == 0 and red[1] == 0 and red[2] == 0,
@@ -325,11 +410,14 @@ def main_stream(args, cfg, world, rank, dev, ctx):
     pr = max(1, args.part_reads)
     dims = Dims(cfg["n_rg"], max(cfg["lens"]))
     t_gen = time.time()
-    sh = StreamedShard(ctx, [], dims, None, dev.index, zero_copy=args.stream_mode == "zerocopy", d2h=args.d2h)
+    # rank r holds reads [r*n, (r+1)*n) of the one 600M-read dataset (the
+    # generator is indexed by global read), as partitions of `pr` reads
+    base = rank * n_reads
+    sh = StreamedShard(ctx, [], dims, None, dev.index, zero_copy=args.stream_mode == "zerocopy", d2h=args.d2h,
+                       read_base=base)
     first = None
     for i, r0 in enumerate(range(0, n_reads, pr)):
-        part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"],
-                              cfg["seed"] + 1_000_003 * rank + 7919 * i)
+        part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"], cfg["seed"], first_read=base + r0)
         sh.add_partition(part)
         if first is None:
             first = part
@@ -371,13 +459,16 @@ def main_stream(args, cfg, world, rank, dev, ctx):
     n_bases = sh.n_bases
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        D.allreduce(t, dist.ReduceOp.MAX)
         elapsed = float(t.item())
         nb = torch.tensor([n_bases], dtype=torch.int64, device=dev)
-        dist.all_reduce(nb)
+        D.allreduce(nb)
         total_bases = int(nb.item())
     else:
         total_bases = n_bases
+    parity = None
+    if not args.no_parity:  # every rank (collectives inside)
+        parity = parity_stream(cfg, sh, table_t, n_reads, pr, rank, world, dims, dev)
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         parts_n = len(sh.batches)
@@ -431,45 +522,62 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         if world == 1 and not args.no_cpu_baseline:
             args.cpu_reads = min(args.cpu_reads, 2_000_000)
             line["cpu_baseline"] = cpu_baseline(args, cfg, first, None)[0]
-        if world == 1 and not args.no_parity:
-            line["parity"] = parity_stream(cfg, sh, table_t, n_reads, pr, rank, dims)
+        if parity is not None:
+            line["parity"] = parity
         print(json.dumps(line), flush=True)
     sh.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def parity_stream(cfg, sh, table_t, n_reads, pr, rank, dims):
-    """cfg5: the last job's table words and expectedMismatch against the oracle
-    over every partition (each observed as one partition, the tables summed
-    and the expectedMismatch values folded in partition order), and the
-    recalibrated chars of the first and last partitions (outside the timed
-    region; partitions regenerated from their seeds)."""
+def parity_stream(cfg, sh, table_t, n_reads, pr, rank, world, dims, dev):
+    """cfg5 (called on every rank): the last job's table words and
+    expectedMismatch against the oracle over every partition of every rank
+    (each observed as one partition; the tables summed across ranks, the
+    expectedMismatch values folded in global partition order -- rank 0's
+    partitions first), and the recalibrated chars of each rank's first and
+    last partitions (outside the timed region; partitions regenerated from
+    the dataset's global read indices).  Counts and equalities are reduced
+    to every rank."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
+    import torch
+    import torch.distributed as dist
     import oracle as O
+    from adam_amd import distributed as D
     from adam_amd import synth
     t = time.perf_counter()
     cores, _ = host_cores()
     d = O.Dims(dims.n_rg, dims.max_len)
     words = np.zeros(O.table_words(d), dtype=np.int64)
-    em = 0.0
+    base = rank * n_reads
     starts = list(range(0, n_reads, pr))
     sampled = {0, len(starts) - 1}
     keep = {}
+    ems = []
     for i, r0 in enumerate(starts):
-        part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"], cfg["seed"] + 1_000_003 * rank + 7919 * i)
+        part = synth.generate(min(pr, n_reads - r0), cfg["lens"], cfg["n_rg"], cfg["seed"], first_read=base + r0)
         w, e = O.observe_mt(part, None, d, n_parts=cores, nthreads=cores, fold1=True)
         words += w
-        em = em + e
+        ems.append(e)
         if i in sampled:
             keep[i] = part
         del part
+    if world > 1:
+        wt = torch.from_numpy(words).to(dev)
+        D.allreduce_table(wt)
+        words = wt.cpu().numpy()
+        all_ems = D.gather_partition_ems(torch.tensor(ems, dtype=torch.float64, device=dev)).cpu().tolist()
+    else:
+        all_ems = ems
+    em = 0.0
+    for e in all_ems:  # ((0.0 + e_0) + e_1) + ... in global partition order
+        em = em + e
     gw = table_t.cpu().numpy()
     gem = float(sh._em_keep.cpu()[0])
     table_ok = bool(np.array_equal(gw, words))
     em_ok = gem == em
-    bad_total, checked, first_bad = 0, 0, -1
+    bad_total, checked, first_bad = 0, 0, np.iinfo(np.int64).max
     for i, part in sorted(keep.items()):
         out, out_len = O.apply_mt(part, d, words, em, n_parts=cores, nthreads=cores)
         ns, nr = sh.n_slots[i], sh.n_reads[i]
@@ -479,14 +587,21 @@ def parity_stream(cfg, sh, table_t, n_reads, pr, rank, dims):
                                              exc if len(exc) else None, nthreads=cores)
         bad_total += bad
         checked += part.n_reads
-        if bad and first_bad < 0:
-            first_bad = sum(sh.n_reads[:i]) + first
-    return {"checked": True, "ok": bool(table_ok and em_ok and bad_total == 0), "table_words_equal": table_ok,
-            "expected_mismatch_equal": bool(em_ok), "expected_mismatch": float(gem).hex(),
-            "reads_checked": checked, "partitions_checked": sorted(keep), "reads_differing": bad_total,
-            "first_differing_read": first_bad,
-            "against": "oracle/ (C++ restatement of ADAM BQSR): table and expectedMismatch over every partition "
-                       "(merged in partition order), chars of the first and last partitions",
+        if bad:
+            first_bad = min(first_bad, base + sum(sh.n_reads[:i]) + first)
+    red = torch.tensor([bad_total, int(not table_ok), int(not em_ok), checked], dtype=torch.int64, device=dev)
+    D.allreduce(red)
+    fr = torch.tensor([first_bad], dtype=torch.int64, device=dev)
+    D.allreduce(fr, dist.ReduceOp.MIN)
+    red = red.cpu().tolist()
+    fr = int(fr.item())
+    return {"checked": True, "ok": red[0] == 0 and red[1] == 0 and red[2] == 0, "table_words_equal": red[1] == 0,
+            "expected_mismatch_equal": red[2] == 0, "expected_mismatch": float(gem).hex(),
+            "reads_checked": red[3], "partitions_checked_per_rank": sorted(keep), "reads_differing": red[0],
+            "first_differing_read": fr if red[0] else -1, "ranks": world,
+            "against": "oracle/ (C++ restatement of ADAM BQSR): table and expectedMismatch over every partition of "
+                       "every rank (tables summed, expectedMismatch folded in global partition order), chars of "
+                       "each rank's first and last partitions",
             "check_s": time.perf_counter() - t}
 
 

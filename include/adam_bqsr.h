@@ -184,7 +184,9 @@ bqsr_status bqsr_batch_wrap_device(bqsr_context* ctx, const bqsr_device_reads* d
  * device columns (no copy); bqsr_batch_upload_async enqueues the H2D copies on
  * `stream` without a host sync (the caller orders its compute stream after it
  * with an event).  A batch may be re-uploaded from the same staged partition
- * any number of times; each upload invalidates the batch's prep results. */
+ * any number of times; each upload invalidates the batch's prep results.  Any
+ * other staged partition (even one of the same shape) is refused with
+ * BQSR_ERR_INVALID_ARG: the batch's launch parameters come from its own. */
 typedef struct bqsr_staged bqsr_staged;
 bqsr_status bqsr_stage_records(bqsr_context* ctx, const bqsr_records* recs, bqsr_staged** out);
 void bqsr_staged_destroy(bqsr_staged* s);
@@ -332,8 +334,8 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin);
 /* A copy by a kernel on `stream` (either side may be pinned host memory the
  * device can address): the streamed path's D2H of results, which then runs
  * beside the DMA engines' H2D of the next partitions instead of sharing them
- * (tools/link_probe.hip).  16-B aligned buffers of any size, or unaligned
- * ones up to 1 MiB.  Replaces, for the JNI side, the memcpy of a partition's
+ * (tools/link_probe.hip).  Any size; 16-B aligned buffers move in 16-B
+ * pieces, unaligned ones byte by byte.  Replaces, for the JNI side, the memcpy of a partition's
  * output buffers back into the executor's direct buffers. */
 bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64_t bytes, void* stream);
 

@@ -74,7 +74,8 @@ def _rank_main(rank, port, out_dir):
         dims = bqsr.dims_of([batch])
         shard, parts = _rank_parts(batch, rank)
         # ---- bench.py's step: the shard as one partition ----
-        job = ResidentJob(shard, dims, snp, 0)
+        r0 = sum(_rank_parts(batch, r)[0].n_reads for r in range(rank))
+        job = ResidentJob(shard, dims, snp, 0, read_base=r0)
         for _ in range(2):  # steady state: the second job reuses every buffer
             job.step(False)
         words, em, q, st, ln, exc = job.results()
@@ -85,7 +86,7 @@ def _rank_main(rank, port, out_dir):
         words_t = torch.zeros(int(L.bqsr_table_words(dims)), dtype=torch.int64, device=dev)
         th = ctypes.c_void_p()
         _capi.check(L.bqsr_table_create(ctx.handle, dims, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
-        sh = StreamedShard(ctx, parts, dims, snp.handle(ctx), 0, site_contigs=snp.contigs)
+        sh = StreamedShard(ctx, parts, dims, snp.handle(ctx), 0, site_contigs=snp.contigs, read_base=r0)
         try:
             for _ in range(2):
                 em_s = sh.run(th, words_t)
@@ -173,6 +174,7 @@ def _rank_err_main(rank, port, out_dir, bad_rank):
     from adam_amd import _capi, bqsr, synth
     from adam_amd.distributed import shard_bounds
     from adam_amd.job import ResidentJob
+    from adam_amd.stream import StreamedShard
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -194,10 +196,16 @@ def _rank_err_main(rank, port, out_dir, bad_rank):
         job.close()
         # errors: the first bad read of the job in global read order
         shard = synth.generate(r1 - r0, cfg["lens"], 1, 31337, first_read=r0)
-        k = 100 if rank == bad_rank else 2000
-        while not _bad_md(shard, k):
-            k += 1
-        out["bad_local"] = k
+        # bad_rank 0: both ranks hold a bad read, rank 0's comes first in
+        # global order; bad_rank 1: only rank 1 holds one (its global index
+        # = read_base + local index).  Both past the stream's first partition
+        # (1000 reads).
+        out["bad_local"] = None
+        if rank == bad_rank or bad_rank == 0:
+            k = 2100 if rank == bad_rank else 2900
+            while not _bad_md(shard, k):
+                k += 1
+            out["bad_local"] = k
         job = ResidentJob(shard, dims, None, 0, read_base=r0)
         try:
             job.step(False)
@@ -205,6 +213,32 @@ def _rank_err_main(rank, port, out_dir, bad_rank):
         except _capi.BQSRError as e:
             out["raised"] = [e.name, e.read]
         job.close()
+        # the streamed path: the same shard as two partitions, the bad read in
+        # the second one -- the error key is rebased by read_base + the reads
+        # of the partitions before (stream.py _exchange_errors)
+        import ctypes
+        L = _capi.lib()
+        ctx = bqsr.Context.get(0)
+        half = shard.n_reads // 3
+        parts = [shard.slice(0, half), shard.slice(half, shard.n_reads)]
+        words_t = torch.zeros(int(L.bqsr_table_words(dims)), dtype=torch.int64, device=dev)
+        th = ctypes.c_void_p()
+        _capi.check(L.bqsr_table_create(ctx.handle, dims, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
+        sh = StreamedShard(ctx, parts, dims, None, 0, read_base=r0)
+        try:
+            sh.run(th, words_t)
+            sh.finish()
+            out["raised_stream"] = None
+        except _capi.BQSRError as e:
+            out["raised_stream"] = [e.name, e.read]
+        finally:
+            while sh.pending:
+                try:
+                    sh.finish()
+                except _capi.BQSRError:
+                    pass
+            sh.close()
+            L.bqsr_table_destroy(th)
         with open(os.path.join(out_dir, "err%d.json" % rank), "w") as fh:
             json.dump(out, fh)
     finally:
@@ -226,8 +260,11 @@ def test_two_ranks_raise_the_jobs_first_error_and_parity_leg(tmp_path, bad_rank)
         pytest.fail("ranks did not finish")
     res = [json.load(open(tmp_path / ("err%d.json" % r))) for r in range(WORLD)]
     from adam_amd.distributed import shard_bounds
-    first = min(shard_bounds(6000, r, WORLD)[0] + res[r]["bad_local"] for r in range(WORLD))
+    first = min(shard_bounds(6000, r, WORLD)[0] + res[r]["bad_local"] for r in range(WORLD)
+                if res[r]["bad_local"] is not None)
+    assert first >= 3000 if bad_rank == 1 else first < 3000
     for z in res:
         p = z["parity"]
         assert p["ok"] and p["reads_checked"] == 6000, json.dumps(p)
         assert z["raised"] == ["MD_PARSE", first], (z["raised"], first)
+        assert z["raised_stream"] == ["MD_PARSE", first], (z["raised_stream"], first)

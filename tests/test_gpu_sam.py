@@ -440,3 +440,41 @@ def test_bam_ingest_synthetic_and_mark_duplicates(tmp_path):
     finally:
         a.close()
         b.close()
+
+
+def _bgzf_corruptions(bam):
+    """Damaged copies of a BAM's first BGZF block (an untrusted file): each
+    must fail with SAM_PARSE, never read outside the input or allocate from
+    a forged size."""
+    import struct
+    xlen = bam[10] | (bam[11] << 8)
+    bsize = bam[16] | (bam[17] << 8)
+    out = {"truncated_header": bam[:14], "truncated_block": bam[:bsize // 2]}
+    b = bytearray(bam)
+    b[10:12] = struct.pack("<H", 60000)  # XLEN past the end of the block / file
+    out["xlen_overrun"] = bytes(b[:200])
+    b = bytearray(bam)
+    b[14:16] = struct.pack("<H", 5000)  # the BC subfield's SLEN overruns the extra field
+    out["subfield_overrun"] = bytes(b)
+    b = bytearray(bam)
+    b[16:18] = struct.pack("<H", 1)  # BSIZE smaller than the header: negative compressed size
+    out["bsize_small"] = bytes(b)
+    b = bytearray(bam)
+    blen = bsize + 1
+    b[blen - 4:blen] = struct.pack("<I", 1 << 31)  # forged ISIZE: a multi-GB output buffer
+    out["isize_huge"] = bytes(b)
+    b = bytearray(bam)
+    b[12 + xlen + 2] ^= 0xFF  # compressed bytes damaged
+    out["deflate_damaged"] = bytes(b)
+    return out
+
+
+def test_bam_ingest_rejects_damaged_bgzf():
+    from adam_amd.bam_writer import sam_to_bam
+    with open(os.path.join(GOLD, FIXTURES[0]), "rb") as fh:
+        bam = sam_to_bam(fh.read())
+    assert bam[12:14] == b"BC"
+    for name, data in _bgzf_corruptions(bam).items():
+        with pytest.raises(_capi.BQSRError) as e:
+            SamText(data, bam=True).close()
+        assert e.value.status == _capi.SAM_PARSE, (name, e.value)

@@ -91,3 +91,29 @@ def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy, d2h)
     finally:
         sh.close()
         L.bqsr_table_destroy(th)
+
+
+def test_upload_refuses_another_staged_partition():
+    """A batch uploads only the staged partition it was created from: its
+    quality window and histogram came from that partition, so another one --
+    even of the same shape, here the same reads staged twice -- is refused."""
+    import torch
+    L = _capi.lib()
+    ctx = bqsr.Context.get(0)
+    part = synth.generate(3000, (100,), 1, 4321)
+    s, keep = part.c_struct(None)
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    _capi.check(L.bqsr_stage_records(ctx.handle, ctypes.byref(s), ctypes.byref(a)))
+    _capi.check(L.bqsr_stage_records(ctx.handle, ctypes.byref(s), ctypes.byref(b)))
+    bh = ctypes.c_void_p()
+    try:
+        _capi.check(L.bqsr_batch_create_staged(ctx.handle, a, ctypes.byref(bh)))
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _capi.check(L.bqsr_batch_upload_async(bh, a, sp))
+        assert L.bqsr_batch_upload_async(bh, b, sp) == _capi.INVALID_ARG
+        torch.cuda.synchronize()
+    finally:
+        if bh:
+            L.bqsr_batch_destroy(bh)
+        L.bqsr_staged_destroy(a)
+        L.bqsr_staged_destroy(b)
