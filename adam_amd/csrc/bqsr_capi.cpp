@@ -4,7 +4,6 @@
 // (bqsr_internal.h), launches the kernels of bqsr_kernels.hip and maps device
 // error words back to the reference's exception classes.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <array>
@@ -25,7 +24,6 @@ using namespace bqsr;
 // the kernels are compiled in this translation unit (one HIP module)
 #include "bqsr_kernels.hip"
 #include "bqsr_observe_lean.hip"
-#include "bqsr_apply_lean.hip"
 #include "bqsr_fold.hip"
 
 // ------------------------------------------------------------- errors -----
@@ -192,92 +190,20 @@ int lean_orow(int nc, int cw) {
   return o;
 }
 size_t lean_lds(int qw, int orow, int wcells) { return ((size_t)qw * (orow + wcells) + qw + kQBins) * 4; }
-// copies of the lean window's counters: the most (<= 4, ADAM_BQSR_LEAN_COPIES caps it) whose rows still
-// hold the batch's qual span
-int lean_copies_max() {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_LEAN_COPIES");
-    return e ? std::max(1, std::min(4, atoi(e))) : 4;
-  }();
-  return v;
-}
+// copies of the lean window's counters: the most (<= 4) whose rows still hold the batch's qual span
+constexpr int kLeanCopiesMax = 4;
 int observe_rows(int wcells, bool table) {
   int qw = kQBins;
   while (qw > 1 && observe_lds(qw, wcells, table) > kLdsMax) --qw;
   return qw;
 }
-// 16-aligned packed layout (ReadsDev::slots_aligned); ADAM_BQSR_ALIGN=0 packs reads back to back
-bool align_slots() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_ALIGN");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
-// per-base passes with lanes per super-chunk or a lane per read (kCL):
-// apply always takes the former, observe the former for bucketed batches
-// (measured: a lane per read is faster for observe in read order, where its
-// LDS window counts dominate); ADAM_BQSR_LANES=read / chunk forces either
-bool chunk_lanes(bool dflt) {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_LANES");
-    return !e ? -1 : strcmp(e, "read") == 0 ? 0 : 1;
-  }();
-  return v < 0 ? dflt : v != 0;
-}
-// lanes per read of the lane-per-super-chunk passes: 2^s >= the super-chunks
-// (64 offsets) of the batch's longest read (at most 64; longer reads loop)
-int lane_shift(const bqsr_batch* b);
-// observe's form: ADAM_BQSR_OBSERVE=chunk (bqsr_observe_chunks, the lane-per-chunk walk), read
-// (bqsr_observe_kernel: lane per read, or lanes per super-chunk when bucketed), superchunk; unset:
-// chunk for bucketed batches, read otherwise (-1)
-int observe_form() {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_OBSERVE");
-    return !e                            ? -1
-           : strcmp(e, "read") == 0       ? 1
-           : strcmp(e, "superchunk") == 0 ? 2
-           : strcmp(e, "rows") == 0       ? 3
-           : strcmp(e, "lean") == 0       ? 4
-                                          : 0;
-  }();
-  return v;
-}
-// apply's form: ADAM_BQSR_APPLY=rows (bqsr_apply_rows, lane per offset: SALU-bound, 5.9 ms cfg2 in
-// round 3) (1), =walk (0), =lean (2, bqsr_apply_lean in read order); unset (-1): the lane-per-chunk
-// walk (bqsr_apply_kernel)
-int apply_form() {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_APPLY");
-    return !e ? -1 : strcmp(e, "rows") == 0 ? 1 : strcmp(e, "lean") == 0 ? 2 : 0;
-  }();
-  return v;
-}
-// bqsr_apply_lean's LDS: the clean-row words and the char table
-size_t apply_lean_lds(int qw, int cw) { return 16 + (size_t)piece_bytes(qw, cw); }
-int apply_lean_rows(int cw) {
-  int qw = kQBins;
-  while (qw > 1 && apply_lean_lds(qw, cw) > kLdsMax) --qw;
-  return qw;
-}
+// the host-packed layout is 16-aligned (ReadsDev::slots_aligned); device batches may be either
+constexpr bool align_slots() { return true; }
 // known sites as sorted lists only (no position bitmaps): ADAM_BQSR_SITES_BITMAP=0 (A/B)
 bool sites_bitmap_off() {
   static const bool v = [] {
     const char* e = getenv("ADAM_BQSR_SITES_BITMAP");
     return e && strcmp(e, "0") == 0;
-  }();
-  return v;
-}
-// bucket-major copies of bucketed batches (bqsr_bucket_gather), opt-in with
-// ADAM_BQSR_GATHER=1 (chunk-walk passes only).  Measured (round 3, cfg4, one
-// box): the passes over the copies ran faster (apply 5.37 -> 3.91 ms, observe
-// 4.47 -> 3.77 ms, no bqsr_fold_hist: -3.6 ms), but the copy itself -- each
-// read's spans written at its sorted slot, random 128-256 B writes -- took
-// 6.54 ms (+0.59 ms for the inverse permutation): 12.97 -> 16.91 ms a job.
-bool gather_on() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_GATHER");
-    return e && strcmp(e, "1") == 0;
   }();
   return v;
 }
@@ -308,28 +234,6 @@ int fronts(int n_base, int n_cu, int64_t n_reads) {
   }
   while (f > 1 && (int64_t)f * n_base > 4096) --f;  // keys kept in the sort's LDS
   return f;
-}
-// bqsr_observe_rows' LDS: obs rows [qw][orow], mm rows [qw][wcells], masked, block histogram, context tables
-size_t rows_lds(int qw, int orow, int wcells, int hc) {
-  return (size_t)qw * orow * 4 + (size_t)qw * wcells * 4 + (size_t)qw * 4 + kQBins * 4 + kLutBytes +
-         (size_t)kWaves * qw * hc * 4;
-}
-int rows_orow(int nc, int cw) { return (kCtxSlots * nc + cw + 31) & ~31; }
-// prep's word stores (PrepParams::store_words); ADAM_BQSR_PREP_ATOMIC=1 turns them off (A/B)
-bool store_words_off() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_PREP_ATOMIC");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-// observe's window row length mod 32: ADAM_BQSR_WMOD=r pads it to r, -1 leaves it; unset: 2 mod 4 (-2)
-int window_mod() {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_WMOD");
-    return !e ? -2 : atoi(e) < 0 ? -1 : (atoi(e) & 31);
-  }();
-  return v;
 }
 int apply_rows(int cw) {
   int qw = kQBins;
@@ -403,7 +307,6 @@ struct bqsr_batch {
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
   int32_t n_blocks = 0;
-  bool hq_by_observe = false;  // bucketed: the observe kernel wrote the fold's read-order block histograms
   // read-group buckets (OrderDev): several read groups -> the per-base passes
   // walk the reads grouped by read group
   bool bucketed = false;
@@ -415,30 +318,12 @@ struct bqsr_batch {
   uint32_t* d_key_cnt = nullptr;
   uint32_t* d_cursor = nullptr;
   OrderDev order() const {
-    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, gathered ? d_oslot : nullptr, fronts > 0 ? n_base : 0}
-                    : OrderDev{nullptr, nullptr, 1};
+    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0} : OrderDev{nullptr, nullptr, 1};
   }
   // workgroups of the chunk-walk passes: a piece each with fronts, else the fold's blocks
   int32_t pass_blocks() const { return bucketed && fronts > 0 ? n_keys : n_blocks; }
-  // bucket-major copies (bqsr_bucket_gather; valid once prepped with `gathered`):
-  // the per-base passes' ReadsDev / ReadInfo in sorted order
-  bool gathered = false;
-  ReadsDev grd{};
-  uint32_t* d_inv = nullptr;     // read -> sorted position
-  uint64_t* d_gspan = nullptr;   // sorted position -> slot span, then
-  uint64_t* d_gslot = nullptr;   //   its slot in the copies (exclusive scan)
-  ReadMeta* d_gmeta = nullptr;
-  ReadInfo* d_ginfo = nullptr;
-  uint64_t* d_oslot = nullptr;
-  uint8_t* d_gqual = nullptr;
-  uint8_t* d_gbases = nullptr;
-  void* d_scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
-  const ReadsDev& pass_rd() const { return gathered ? grd : rd; }
-  ReadInfo* pass_info() const { return gathered ? d_ginfo : d_info; }
   uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
   ~bqsr_batch() {
-    if (d_scan_tmp) (void)hipFree(d_scan_tmp);
     if (d_part) (void)hipFree(d_part);
     if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
@@ -520,21 +405,11 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMalloc(&c->d_qbq, kQbN * sizeof(int16_t));
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
-  for (const void* f : {(const void*)bqsr_observe_kernel<false>, (const void*)bqsr_observe_kernel<true>,
-                        (const void*)bqsr_apply_kernel<false>, (const void*)bqsr_apply_kernel<true>,
-                        (const void*)bqsr_observe_chunks<false>, (const void*)bqsr_observe_chunks<true>,
-                        (const void*)bqsr_observe_rows<2, true>,
-                        (const void*)bqsr_observe_rows<4, true>, (const void*)bqsr_observe_rows<2, false>,
-                        (const void*)bqsr_observe_rows<4, false>, (const void*)bqsr_apply_rows<2, true>,
-                        (const void*)bqsr_apply_rows<4, true>, (const void*)bqsr_apply_rows<2, false>,
-                        (const void*)bqsr_apply_rows<4, false>, (const void*)bqsr_observe_lean<true>, (const void*)bqsr_observe_lean<false>,
-                        (const void*)bqsr_apply_lean})
+  for (const void* f : {(const void*)bqsr_apply_kernel, (const void*)bqsr_observe_chunks,
+                        (const void*)bqsr_observe_lean<true>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)bqsr_bucket_gather, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)fold_hist_lds());
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)chain_lds(kMaxFoldBlocks));
@@ -694,7 +569,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
     b->bucketed = b->dims.n_rg > 1;
     if (!b->bucketed && b->have_qhist) {
       const int cw = geom(b->dims).C;
-      const Window w = window_rows(b, apply_form() == 2 ? apply_lean_rows(cw) : apply_rows(cw));
+      const Window w = window_rows(b, apply_rows(cw));
       int64_t in = 0, all = 0;
       for (int q = 0; q < kQBins; ++q) {
         all += b->qhist[q];
@@ -705,9 +580,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   }
   if (b->bucketed) {
     b->n_base = 2 * std::max<int32_t>(1, b->dims.n_rg);  // 2 * read group + mate class
-    b->fronts = ((observe_form() <= 0 || observe_form() == 4) && apply_form() <= 0 && !gather_on())
-                    ? fronts(b->n_base, b->ctx->n_cu, n)
-                    : 0;
+    b->fronts = fronts(b->n_base, b->ctx->n_cu, n);
     b->n_keys = b->n_base * std::max(1, b->fronts);
     if ((st = dalloc(b->allocs, &b->d_perm, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_off, (size_t)b->n_keys + 1)) != BQSR_OK) return st;
@@ -1297,40 +1170,6 @@ bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
 //   BQSR_STAGE_FOLD    the expectedMismatch fold kernel
 // Exposed separately so a caller can bracket one kernel with HIP events.
 namespace {
-// bucket-major copies of a bucketed batch (bqsr_bucket_gather), after the key sort
-bqsr_status launch_gather(bqsr_context* ctx, bqsr_batch* b, hipStream_t s) {
-  const int64_t n = b->rd.n_reads;
-  bqsr_status st;
-  if (!b->d_inv) {  // once per batch
-    const size_t nr = (size_t)std::max<int64_t>(1, n);
-    if ((st = dalloc(b->allocs, &b->d_inv, nr)) != BQSR_OK || (st = dalloc(b->allocs, &b->d_gspan, nr)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &b->d_gslot, nr)) != BQSR_OK || (st = dalloc(b->allocs, &b->d_gmeta, nr)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &b->d_ginfo, nr)) != BQSR_OK || (st = dalloc(b->allocs, &b->d_oslot, nr)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &b->d_gqual, (size_t)b->rd.n_slots + 64)) != BQSR_OK ||
-        (st = dalloc(b->allocs, &b->d_gbases, (size_t)(b->rd.n_slots + 1) / 2 + 64)) != BQSR_OK)
-      return st;
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, b->d_gspan, b->d_gslot, (int)n, s));
-    HIP_TRY(hipMalloc(&b->d_scan_tmp, std::max<size_t>(tb, 16)));
-    b->scan_tmp_bytes = std::max<size_t>(tb, 16);
-    b->grd = b->rd;
-    b->grd.meta = b->d_gmeta;
-    b->grd.qual = b->d_gqual;
-    b->grd.bases = b->d_gbases;
-  }
-  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8);
-  hipLaunchKernelGGL(bqsr_key_inverse, dim3(g), dim3(256), 0, s, (const uint32_t*)b->d_perm,
-                     (const ReadMeta*)b->rd.meta, n, b->d_inv, b->d_gspan);
-  size_t tb = b->scan_tmp_bytes;
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(b->d_scan_tmp, tb, b->d_gspan, b->d_gslot, (int)n, s));
-  HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
-  hipLaunchKernelGGL(bqsr_bucket_gather, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd,
-                     b->d_info, (const uint32_t*)b->d_inv, (const uint64_t*)b->d_gslot, b->n_blocks, lane_shift(b),
-                     b->d_hq, b->d_gmeta, b->d_ginfo, b->d_oslot, b->d_gqual, b->d_gbases);
-  HIP_TRY(hipGetLastError());
-  return BQSR_OK;
-}
-
 bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
   HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
   if (b->rd.n_reads > 0) {
@@ -1341,7 +1180,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     // word (no zeroing pass, no read-modify-write atomics: cfg3 prep 3.0 ->
     // 2.2 ms); without sites the few mismatch bits as atomics onto a zeroed
     // bitmap cost less (cfg2: 0.25 + 0.03 ms against 0.30)
-    P.store_words = b->dims.max_len <= 128 && P.sites.n_contigs > 0 && !store_words_off();
+    P.store_words = b->dims.max_len <= 128 && P.sites.n_contigs > 0;
     P.bnd = b->d_bnd;
     if (!P.store_words) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
     P.info = b->d_info;
@@ -1371,11 +1210,6 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
       hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
                          b->n_base, std::max(1, b->fronts), b->d_cursor, b->d_perm);
       HIP_TRY(hipGetLastError());
-      b->gathered = gather_on() && b->rd.slots_aligned && observe_form() <= 0 && apply_form() <= 0;
-      if (b->gathered) {
-        const bqsr_status gst = launch_gather(ctx, b, s);
-        if (gst != BQSR_OK) return gst;
-      }
     }
   }
   b->prepped = true;
@@ -1403,58 +1237,28 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     return fail(BQSR_ERR_INVALID_ARG, "observe kernel before the prep stage (or with other known sites)");
   if (stages & BQSR_STAGE_KERNEL) {
     ObserveParams P{};
-    P.rd = b->pass_rd();
+    P.rd = b->rd;
     P.ord = b->order();
-    P.info = b->pass_info();
+    P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.g = geom(t->dims);
     // window row length padded to 2 mod 4 words: the lanes of a wavefront add
     // to one cycle cell of many rows at once, which a row length sharing a
     // factor 4 or more with the 32 banks folds onto few banks (cfg3, 224
     // words: 7.6 ms observe; 225: 5.8; cfg2 222 against 223 / 224: 0.94 /
-    // 1.00 / 1.25 ms).  ADAM_BQSR_WMOD=r pads to r mod 32 instead (A/B), -1
-    // not at all.  Pad words stay 0.
-    // the lean lane per read is the default in read order; bucketed batches take the chunk walk
-    // (cfg4 observe 4.51 ms against lean's 6.42, profiles/r03w_cfg4_lean_bucketed_ab.txt; lean there
-    // with ADAM_BQSR_OBSERVE=lean); ADAM_BQSR_OBSERVE=read / superchunk / rows / chunks select the others
-    const int form = observe_form() >= 0 && !(observe_form() == 4 && b->gathered) ? observe_form()
-                     : b->bucketed                                               ? 0
-                                                                                 : 4;
-    const bool lean = form == 4;
+    // 1.00 / 1.25 ms).  Pad words stay 0.
+    // Read order: the lean lane per read (bqsr_observe_lean.hip); bucketed
+    // batches: the lane-per-chunk walk (cfg4 observe 4.51 ms against the lean
+    // form's 6.42, profiles/r03w_cfg4_lean_bucketed_ab.txt).  Measured and
+    // removed (round 3, in git history): the round-2 lane per read, lanes per
+    // super-chunk and the lane-per-offset rows kernel (SALU-bound, 6.0 ms cfg2).
+    const bool lean = !b->bucketed;
     P.wcells = window_cw(b, P.g) + (lean ? kCtxCells : kCtxSlots);
-    if (window_mod() == -2)
-      while ((P.wcells & 3) != 2) ++P.wcells;
-    else if (window_mod() >= 0)
-      while ((P.wcells & 31) != window_mod()) ++P.wcells;
-    // measured (cfg2 / cfg4 / cfg3): the chunk walk wins on bucketed batches (4.63 vs 5.03 ms),
-    // the lane per read on read order (1.00 vs 1.16 ms cfg2; 7.11 vs 7.25 cfg3)
-    // measured (round 3, cfg2 / cfg4): the lane-per-offset rows kernel is SALU-bound (2.7e9 scalar
-    // instructions per cfg2 launch, 6.0 ms) -- opt-in only; the chunk walk wins on bucketed batches
-    // (4.63 vs 5.03 ms cfg4), the lane per read on read order (1.00 vs 1.16 ms cfg2)
-    if (form == 3) {
-      // bqsr_observe_rows: the most context copies (and, bucketed, fold
-      // histogram copies) whose rows still hold the batch's qual span (fewer
-      // rows than the span: the rest take the global atomics)
+    while ((P.wcells & 3) != 2) ++P.wcells;
+    if (lean) {
       const int cw = window_cw(b, P.g), span = qual_span(b);
       int best_rows = 0;
-      for (int nc = 16; nc >= 1 && best_rows < span; nc >>= 1)
-        for (int hc = b->bucketed ? 16 : 0; hc >= (b->bucketed ? 1 : 0) && best_rows < span; hc = hc > 1 ? hc >> 1 : -1) {
-          const int orow = rows_orow(nc, cw);
-          int qw = kQBins;
-          while (qw > 1 && rows_lds(qw, orow, P.wcells, hc) > kLdsMax) --qw;
-          if (qw > best_rows) {
-            best_rows = qw;
-            P.nc = nc;
-            P.orow = orow;
-            P.hc = hc;
-          }
-          if (hc == 0) break;
-        }
-      P.w = window_rows(b, best_rows);
-    } else if (lean) {
-      const int cw = window_cw(b, P.g), span = qual_span(b);
-      int best_rows = 0;
-      for (int nc = lean_copies_max(); nc >= 1 && best_rows < span; --nc) {
+      for (int nc = kLeanCopiesMax; nc >= 1 && best_rows < span; --nc) {
         const int orow = lean_orow(nc, cw);
         int qw = kQBins;
         while (qw > 1 && lean_lds(qw, orow, P.wcells) > kLdsMax) --qw;
@@ -1470,7 +1274,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       for (int q = 0; q < kQBins && P.rows_all; ++q)
         if (b->qhist[q] && (q < P.w.q_lo || q >= P.w.q_lo + P.w.qw)) P.rows_all = 0;
     } else {
-      P.w = window_rows(b, observe_rows(P.wcells, form == 0));
+      P.w = window_rows(b, observe_rows(P.wcells, true));
     }
     P.touched = t->touched();
     P.obs = t->obs();
@@ -1490,31 +1294,12 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.part = b->d_part;
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
-    P.n_blocks = (form == 0 || (lean && b->bucketed)) ? b->pass_blocks() : b->n_blocks;  // (fronts: chunk walk or lean)
-    const size_t lds = form == 3 ? rows_lds(P.w.qw, P.orow, P.wcells, P.hc)
-                       : lean    ? lean_lds(P.w.qw, P.orow, P.wcells)
-                                 : observe_lds(P.w.qw, P.wcells, form == 0);
-    P.lane_shift = lane_shift(b);
-    b->hq_by_observe = form == 3 && b->bucketed;
-    if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
-    if (lean) {
-      hipLaunchKernelGGL((b->bucketed ? bqsr_observe_lean<false> : bqsr_observe_lean<true>), dim3(P.n_blocks),
-                         dim3(kBlockThreads), lds, s, P);
-    } else if (form == 3) {
-      const bool wide = b->dims.max_len > 128;
-      if (b->bucketed)
-        hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, false> : bqsr_observe_rows<2, false>), dim3(b->n_blocks),
-                           dim3(kBlockThreads), lds, s, P);
-      else
-        hipLaunchKernelGGL((wide ? bqsr_observe_rows<4, true> : bqsr_observe_rows<2, true>), dim3(b->n_blocks),
-                           dim3(kBlockThreads), lds, s, P);
-    } else if (form == 0)
-      hipLaunchKernelGGL((b->gathered ? bqsr_observe_chunks<true> : bqsr_observe_chunks<false>), dim3(P.n_blocks),
-                         dim3(kBlockThreads), lds, s, P);
-    else if (form == 2 || chunk_lanes(b->bucketed))
-      hipLaunchKernelGGL((bqsr_observe_kernel<true>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+    P.n_blocks = lean ? b->n_blocks : b->pass_blocks();  // (fronts: a chunk-walk workgroup per piece)
+    const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true);
+    if (lean)
+      hipLaunchKernelGGL(bqsr_observe_lean<true>, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     else
-      hipLaunchKernelGGL((bqsr_observe_kernel<false>), dim3(b->n_blocks), dim3(kBlockThreads), lds, s, P);
+      hipLaunchKernelGGL(bqsr_observe_chunks, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_base : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
@@ -1523,7 +1308,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-    if (b->bucketed && !b->hq_by_observe && !b->gathered) {  // the observe kernel did not walk the fold's blocks: their histograms
+    if (b->bucketed) {  // the observe kernel did not walk the fold's blocks: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
                          b->n_blocks, lane_shift(b), b->d_hq);
@@ -1837,15 +1622,14 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   if (b->rd.n_reads == 0 || !(stages & BQSR_STAGE_KERNEL)) return ok();
   ApplyParams P{};
-  P.rd = b->pass_rd();
+  P.rd = b->rd;
   P.ord = b->order();
-  P.info = b->pass_info();
+  P.info = b->d_info;
   P.g = geom(L->dims);
   const int cw = window_cw(b, P.g);
-  // the lean lane per read is opt-in (ADAM_BQSR_APPLY=lean): its scattered 16-B result stores ran
-  // 2.34 ms against the walk's 0.84 (cfg2, profiles/r03r_apply_lean_ab.txt)
-  const bool lean = !b->bucketed && apply_form() == 2;
-  P.w = window_rows(b, lean ? apply_lean_rows(cw) : apply_rows(cw));
+  // (measured and removed, round 3: a lean lane per read, 2.34 ms against the walk's 0.84 cfg2 --
+  // its scattered 16-B result stores -- and a lane-per-offset rows kernel, SALU-bound at 5.9 ms)
+  P.w = window_rows(b, apply_rows(cw));
   P.n_rg = L->dims.n_rg;
   P.s1 = L->s1;
   P.d2 = L->d2;
@@ -1865,39 +1649,6 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   P.max_exc = exceptions ? max_exceptions : 0;
   P.n_exc = b->d_err + kNExc;
   P.err = b->d_err + kErrAppKern;
-  if (apply_form() == 1) {
-    // bqsr_apply_rows: a packed char table per (read group, mate class) piece,
-    // rows of cwp = roundup(L, 32) cycle cells x 6 context groups (dwords)
-    P.cwp = (P.g.L + 31) & ~31;
-    const int n_pieces = b->bucketed ? b->n_keys : 2;
-    int qw = kQBins;
-    while (qw > 1 && (size_t)qw * 24 * P.cwp + 2 * kLutBytes > kLdsMax) --qw;
-    P.w = window_rows(b, qw);
-    const size_t need = (size_t)n_pieces * P.w.qw * 24 * P.cwp;
-    if (b->chars_bytes < need) {
-      if (b->d_chars) {
-        HIP_TRY(hipStreamSynchronize(s));
-        (void)hipFree(b->d_chars);
-        b->d_chars = nullptr;
-        b->chars_bytes = 0;
-      }
-      HIP_TRY(hipMalloc((void**)&b->d_chars, need));
-      b->chars_bytes = need;
-    }
-    P.chars = b->d_chars;
-    const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need / 4 + 255) / 256, (int64_t)ctx->n_cu * 16);
-    hipLaunchKernelGGL(bqsr_apply_chars_rows, dim3(cb), dim3(256), 0, s, P, n_pieces, (uint32_t*)b->d_chars);
-    const size_t lds = (size_t)P.w.qw * 24 * P.cwp + 2 * kLutBytes;
-    const bool wide = b->dims.max_len > 128;
-    if (b->bucketed)
-      hipLaunchKernelGGL((wide ? bqsr_apply_rows<4, false> : bqsr_apply_rows<2, false>), dim3(b->n_blocks),
-                         dim3(kBlockThreads), lds, s, P);
-    else
-      hipLaunchKernelGGL((wide ? bqsr_apply_rows<4, true> : bqsr_apply_rows<2, true>), dim3(b->n_blocks),
-                         dim3(kBlockThreads), lds, s, P);
-    HIP_TRY(hipGetLastError());
-    return ok();
-  }
   P.piece_stride = piece_bytes(P.w.qw, cw);
   // a char table per base key (fronts share their read group's)
   const size_t need = (size_t)P.piece_stride * (size_t)b->n_base + (size_t)b->n_base * 16;  // + rowbad
@@ -1916,11 +1667,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_base * 16, s));
   const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
   hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
-  if (lean)
-    hipLaunchKernelGGL(bqsr_apply_lean, dim3(b->n_blocks), dim3(kBlockThreads), apply_lean_lds(P.w.qw, cw), s, P);
-  else
-    hipLaunchKernelGGL((b->gathered ? bqsr_apply_kernel<true> : bqsr_apply_kernel<false>), dim3(b->pass_blocks()),
-                       dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
+  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
   HIP_TRY(hipGetLastError());
   return ok();
 }

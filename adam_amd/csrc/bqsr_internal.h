@@ -182,11 +182,6 @@ struct OrderDev {
   const uint32_t* perm;    // [n_reads] or nullptr (identity, one piece per workgroup, group = Window::rg_lo)
   const int64_t* key_off;  // [n_keys + 1]
   int32_t n_keys;          // 2 * n_rg when bucketed
-  // gathered (bqsr_bucket_gather): the passes' ReadsDev / ReadInfo hold the
-  // reads in sorted order (record i = sorted position i, its quals and base
-  // codes copied bucket-major); oslot[i] = the read's slot in the batch (slot
-  // bitmap, outputs), perm[i] its index.  nullptr: records are read indices.
-  const uint64_t* oslot = nullptr;
   // fronts (n_base > 0): keys are (front, base key) = front * n_base + base
   // key, a front being a contiguous share of the read indices, and workgroup
   // w of the chunk-walk passes takes key w whole -- so the workgroups of one
@@ -213,9 +208,8 @@ struct ObserveParams {
   int32_t n_blocks;
   int32_t wcells;      // window row length: WinGeom::cw + 21
   int32_t lane_shift;  // lane-per-chunk kernels: log2(lanes per read)
-  int32_t orow;        // bqsr_observe_rows: LDS obs row words ([ctx copies 21 * nc][cycle cells cw][pad]), 0 mod 32
-  int32_t nc;          // bqsr_observe_rows: copies of a row's context counters (power of 2, <= 16)
-  int32_t hc;          // bqsr_observe_rows, bucketed: copies of a wavefront's fold-block qual histogram
+  int32_t orow;        // bqsr_observe_lean: LDS obs row words (nc copies of the cycle and 43 context cells), 2 mod 4
+  int32_t nc;          // bqsr_observe_lean: copies of a row's counters (<= 4)
   int32_t rows_all;    // bqsr_observe_lean: every qual of the batch is a window row (host histogram)
 };
 
@@ -309,7 +303,6 @@ struct ApplyParams {
   const uint8_t* chars;   // [n_keys][piece_stride] the pieces' char tables (bqsr_apply_chars)
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
-  int32_t cwp;            // bqsr_apply_rows: cycle cells per packed row (the half window's L, padded to 32)
 };
 
 // finalize results read back by the host

@@ -1,28 +1,22 @@
 // bqsr_kernels.hip -- gfx950 kernels of the BQSR path.
 //
-//   bqsr_prep_kernel      per read: ReadCovariates' constructor + the per-read
-//                         parts of next() (trimming, CIGAR, MD, known sites)
-//   bqsr_observe_kernel   RecalibrateBaseQualities.computeTable, one partition
-//   bqsr_fold_kernel      expectedMismatch: the partition's sequential fold
+//   bqsr_prep_kernel / _complex  per read: ReadCovariates' constructor + the
+//                         per-read parts of next() (trimming, CIGAR, MD, known
+//                         sites) -> ReadInfo + the 2-bit slot bitmap
+//   bqsr_observe_chunks   RecalTable.+= over bucketed batches (several read
+//                         groups): a lane per 16-offset chunk (chunk_walk)
+//                         (read order: bqsr_observe_lean.hip)
+//   bqsr_window_reduce    the workgroups' LDS windows -> the int64 table
+//   bqsr_key_*            counting sort of reads by (front, read group, mate)
+//   bqsr_fold_hist        the expectedMismatch fold's per-block quality
+//                         histograms of bucketed batches (bqsr_fold.hip folds)
 //   bqsr_final_*          RecalTable.finalizeTable + the apply tables
-//   bqsr_apply_kernel     RecalUtil.recalibrate over every eligible read
+//   bqsr_apply_chars / bqsr_apply_kernel  RecalUtil.recalibrate over every
+//                         eligible read (char tables, then the chunk walk)
 //   bqsr_table_add        RecalTable.++ (int64 counts)
+//   staged expand / copies / job status  the streamed path's plumbing
 //
-// Structure (DESIGN.md has the full account):
-//  * prep: one thread per read, full occupancy.  The serial, branchy work
-//    (quality trimming, CIGAR walk, MD parse, known-site lookup, the JVM's
-//    exception order) happens once per read and leaves an 8-B ReadInfo plus
-//    two per-read bitmaps {masked, mismatch} over read offsets -- the "2-bit
-//    structural mask" of SURVEY.md 8d.
-//  * observe / apply: one 1024-thread workgroup per CU owning a contiguous
-//    range of read tiles; a wavefront takes one tile (<= 64 reads, <= 4096
-//    base slots) at a time and its lanes walk the slots one base per lane per
-//    step.  A lane finds its read by a popcount over a per-tile read-start
-//    bitmap, so there is no per-lane serial loop and no divergence beyond the
-//    trimmed ends.  observe accumulates a u32 LDS-privatised window of the
-//    covariate table (flushed with int64 atomics at the end); apply reads the
-//    window's double tables from LDS and turns p into a phred score with two
-//    LDS loads (bucketed threshold table).
+// DESIGN.md section 3 has the account of each kernel and its measurements.
 // Compiled with -ffp-contract=off: the double arithmetic must round exactly
 // as the JVM's.
 #include <hip/hip_runtime.h>
@@ -939,32 +933,12 @@ __device__ __forceinline__ void load_window_head(const uint8_t* bases, int64_t n
   }
 }
 
-__device__ __forceinline__ uint32_t nibrev32(uint32_t u) {
-  u = __builtin_bswap32(u);
-  return ((u >> 4) & 0x0F0F0F0Fu) | ((u << 4) & 0xF0F0F0F0u);
-}
-
-// reverse strand: R.nib(k) = complement(W.nib(16 - k)), k = 0..16; A<->T, C<->G
-// (index 3 - index), N stays N (BaseContext.simpleReverseComplement).
-__device__ __forceinline__ void revcomp_window(uint64_t& lo, uint32_t& hi) {
-  const uint64_t z = (uint64_t)nibrev32((uint32_t)(lo >> 32)) | ((uint64_t)nibrev32((uint32_t)lo) << 32);
-  uint64_t rlo = (z << 4) | (hi & 0xFu);
-  uint32_t rhi = (uint32_t)(z >> 60);
-  const uint64_t m = (~rlo >> 2) & 0x1111111111111111ull;  // nibbles holding A/C/G/T
-  rlo ^= m | (m << 1);
-  const uint32_t mh = (~rhi >> 2) & 1u;
-  rhi ^= mh | (mh << 1);
-  lo = rlo;
-  hi = rhi;
-}
-
-
 // Per-lane read decode shared by observe and apply.
 struct LaneRead {
   int64_t r;      // record index (into rd.meta / info)
-  int64_t ro;     // the read's index in the batch (errors, per-read outputs): r, or perm[r] when gathered
+  int64_t ro;     // the read's index in the batch (errors, per-read outputs): r
   uint64_t slot;  // first base slot of rd's qual / base columns
-  uint64_t oslot; // its slot in the batch (slot bitmap, output): slot, or OrderDev::oslot[r] when gathered
+  uint64_t oslot; // its slot in the batch (slot bitmap, output): slot
   int st, en;     // visited offsets [st, en)
   int fl;         // kInfo* bits
   bool trimmed;   // st / en computed here (kInfoTrim): observe writes the ReadInfo back
@@ -1039,9 +1013,6 @@ __device__ __forceinline__ int64_t pass_begin(const ReadsDev& rd, const OrderDev
   return o.n_base ? o.key_off[min((int64_t)o.n_keys, w)] : wg_begin(rd, w, G);
 }
 __device__ __forceinline__ int64_t order_read(const OrderDev& o, int64_t i) { return o.perm ? (int64_t)o.perm[i] : i; }
-// the record of sorted position i in the passes' columns: i itself when the
-// batch's columns were gathered into sorted order (bqsr_bucket_gather)
-__device__ __forceinline__ int64_t order_rec(const OrderDev& o, int64_t i) { return o.oslot ? i : order_read(o, i); }
 // the read group of a key's window rows
 __device__ __forceinline__ int key_rg(const OrderDev& o, int key, int rg_lo) {
   return o.perm ? (o.n_base ? key % o.n_base : key) >> 1 : rg_lo;
@@ -1071,29 +1042,11 @@ __device__ __forceinline__ int64_t chunk_n0(const LaneRead& x, int o0) {
 __device__ __forceinline__ uint4 chunk_raw(const ReadsDev& rd, int64_t n0) {
   return n0 >= 0 ? *(const uint4*)(rd.bases + (n0 >> 1)) : make_uint4(0, 0, 0, 0);
 }
-// (bqsr_observe_kernel's lane per read: the arithmetic form below, whose
-// registers it has; the other passes take the table lookup, chunk_ctx)
-__device__ __forceinline__ void chunk_finish(const ReadsDev& rd, const LaneRead& x, int64_t n0, uint4 v, uint64_t& lo,
-                                             uint32_t& hi) {
-  if (__builtin_expect(n0 >= 0, 1)) {
-    const uint32_t sh = (uint32_t)(n0 & 1) * 4u;
-    const uint32_t d0 = __builtin_amdgcn_alignbit(v.y, v.x, sh);
-    const uint32_t d1 = __builtin_amdgcn_alignbit(v.z, v.y, sh);
-    const uint32_t d2 = __builtin_amdgcn_alignbit(v.w, v.z, sh);
-    lo = ((uint64_t)d1 << 32) | d0;
-    hi = d2 & 0xFu;
-  } else {
-    load_window_head(rd.bases, n0, rd.n_slots, lo, hi);
-  }
-  if (x.fl & kInfoNeg) revcomp_window(lo, hi);
-}
-
 // Offsets per super-chunk: the loads of kSub chunks of one read are issued
 // together, so the few cache lines a read spans are fetched once while hot
 // instead of once per chunk.
 constexpr int kSub = 4;
 constexpr int kSuper = kSub * kChunk;
-constexpr int kObsSub = 8;  // observe, lane per read: chunks per step
 
 // 16 masked / mismatch bits of sub-chunk i from a step's NW bitmap words
 // (w[0] holds the slot of the step's first offset at bit b0)
@@ -1121,31 +1074,6 @@ __device__ __forceinline__ void sub_bits16(const uint64_t* w, uint32_t h, int i,
   const uint32_t sh = 16u * ((h + (uint32_t)i) & 1u);
   masked = (uint32_t)v >> sh;
   mism = (uint32_t)(v >> 32) >> sh;
-}
-
-// Context slots (ctx + 4) of the 16 offsets of a chunk, one per byte
-// (xo[k >> 2] byte k & 3), from its 17-code window: with A = idx(a) + 1 and
-// B = idx(b) + 1 (0 for 'other'), ctx + 4 = 4A + B, and 4 when either base is
-// N.  The per-byte lookups are v_perm byte selects on the 3-bit codes.
-__device__ __forceinline__ void spread8(uint32_t x, uint32_t& s0, uint32_t& s1) {
-  const uint32_t e = x & 0x0F0F0F0Fu, o = (x >> 4) & 0x0F0F0F0Fu;
-  s0 = __builtin_amdgcn_perm(o, e, 0x05010400u);  // nibbles 0..3 -> bytes
-  s1 = __builtin_amdgcn_perm(o, e, 0x07030602u);  // nibbles 4..7 -> bytes
-}
-__device__ __forceinline__ void ctx_slots(uint64_t lo, uint32_t hi, uint32_t xo[4]) {
-  uint32_t as[4], bs[4];
-  spread8((uint32_t)lo, as[0], as[1]);
-  spread8((uint32_t)(lo >> 32), as[2], as[3]);
-  spread8((uint32_t)(lo >> 4), bs[0], bs[1]);
-  spread8((uint32_t)(lo >> 36) | (hi << 28), bs[2], bs[3]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t A = __builtin_amdgcn_perm(0u, 0x04030201u, as[i]);  // A0 C1 G2 T3 -> 1..4, N/other -> 0
-    const uint32_t B = __builtin_amdgcn_perm(0u, 0x04030201u, bs[i]);
-    const uint32_t N = __builtin_amdgcn_perm(0x000000FFu, 0u, as[i]) | __builtin_amdgcn_perm(0x000000FFu, 0u, bs[i]);
-    const uint32_t v = (A << 2) + B;
-    xo[i] = (v & ~N) | (0x04040404u & N);
-  }
 }
 
 // the read's first visited offset k has context 0 (slot 4): its predecessor
@@ -1314,17 +1242,13 @@ constexpr uint32_t kPkRev = 0x8000u;  // packed flags: cycle direction -1
 // (fchunk(x, j, n, on, ld)), so a lane has kU chunks' loads in flight; x
 // holds r, slot, st, en, fl, rg, cell0 and dir of the chunk's read, j = jb +
 // 16k, n = en - st.
-template <uint32_t kAct, int kU, class LD, bool kG, class FRead, class FLoad, class FChunk>
+template <uint32_t kAct, int kU, class LD, class FRead, class FLoad, class FChunk>
 __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* info, const OrderDev& ord, int64_t q0,
                                            int64_t q1, int64_t qstep, int L, int lane, uint32_t* mk, FRead&& fread,
                                            FLoad&& fload, FChunk&& fchunk) {
   for (int64_t wb = q0; wb < q1; wb += qstep) {
     const bool live = wb + lane < q1;
-    LaneRead x = lane_read(rd, info, live ? (kG ? wb + lane : order_read(ord, wb + lane)) : 0, live, L);
-    if (kG) {  // gathered columns (OrderDev::oslot): the read's own index and slot
-      x.ro = live ? order_read(ord, wb + lane) : rd.n_reads;
-      x.oslot = live ? ord.oslot[wb + lane] : 0;
-    }
+    LaneRead x = lane_read(rd, info, live ? order_read(ord, wb + lane) : 0, live, L);
     fread(x, live);
     const int n = (live && (x.fl & kAct)) ? x.en - x.st : 0;
     const int jb = rd.slots_aligned ? -(x.st & 15) : 0;
@@ -1332,8 +1256,6 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
     const uint32_t pe = wave_incl_add(nch), ps = pe - nch;
     const uint32_t total = __builtin_amdgcn_readlane(pe, 63);
     const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
-    const uint32_t p_ro = kG ? (uint32_t)x.ro : 0u, p_oslo = kG ? (uint32_t)x.oslot : 0u,
-                   p_oshi = kG ? (uint32_t)(x.oslot >> 32) : 0u;
     const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
     const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
     const uint32_t p_rg = (uint32_t)x.rg;
@@ -1357,13 +1279,8 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
         const int ri = (int)wave_incl_max(v);
         c[u].r = bperm(ri, p_r);
         c[u].slot = ((uint64_t)bperm(ri, p_shi) << 32) | bperm(ri, p_slo);
-        if (kG) {
-          c[u].ro = bperm(ri, p_ro);
-          c[u].oslot = ((uint64_t)bperm(ri, p_oshi) << 32) | bperm(ri, p_oslo);
-        } else {
-          c[u].ro = c[u].r;
-          c[u].oslot = c[u].slot;
-        }
+        c[u].ro = c[u].r;
+        c[u].oslot = c[u].slot;
         const uint32_t se = bperm(ri, p_se), fl = bperm(ri, p_fl);
         c[u].st = (int)(se & 0xFFFFu);
         c[u].en = (int)(se >> 16);
@@ -1386,283 +1303,14 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
 // ------------------------------------------------------------ observe ------
 
 typedef __attribute__((address_space(3))) uint32_t* LdsWords;
+typedef __attribute__((address_space(3))) const uint8_t* LdsBytes;
 __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
   __hip_atomic_fetch_add((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// SWAR: every byte of a chunk's 16 quals is a window row, q_lo <= q < hi
-// (hi = q_lo + qw <= 128; a byte >= 128 is a negative Java byte, never a row)
-__device__ __forceinline__ bool quals_in_rows(const uint32_t qd[4], int q_lo, int hi) {
-  const uint32_t lo4 = (uint32_t)q_lo * 0x01010101u, hi4 = (uint32_t)hi * 0x01010101u;
-  uint32_t bad = 0;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const uint32_t v = qd[w] | 0x80808080u;  // per byte no borrow: v >= 128 >= lo, hi
-    bad |= qd[w] | ~(v - lo4) | (v - hi4);   // high bit: q >= 128, q < lo, q >= hi
-  }
-  return (bad & 0x80808080u) == 0u;
-}
-
-// A clean chunk (a read of the window's read group, all 16 offsets visited,
-// every qual a window row): both increments of every offset without a
-// predicate -- per offset a row address, the cycle cell (cb stepping by the
-// cycle direction) and the context cell -- then the masked offsets, counted
-// on the key only (RecalTable.+=), are moved back out: their two increments
-// undone, the row's masked count raised.  The unconditional form issues
-// about a third of the predicated loop's VALU and none of its exec-mask
-// juggling.
-// The fix-ups of masked offsets and the mismatch increments (unmasked
-// mismatches: both cells of the mm window, qw * wcells words on) share one
-// loop, so a wavefront pays for the larger of the two counts, not their sum.
-__device__ __forceinline__ void observe_clean(uint32_t lb, const uint32_t qd[4], const uint32_t xo[4], uint32_t bm,
-                                              uint32_t bx, int wc0, int dir, int q_lo, int qw, int wcells, int cw,
-                                              uint32_t lmasked) {
-  const uint32_t w4 = 4u * (uint32_t)wcells;
-  const uint32_t qoff = 4u * (uint32_t)(q_lo * wcells);
-  const uint32_t cb0 = lb + 4u * (uint32_t)wc0 - qoff;
-  const uint32_t xb = lb + 4u * (uint32_t)cw - qoff;
-  const uint32_t d4 = 4u * (uint32_t)dir;
-  uint32_t cb = cb0;
-#pragma unroll
-  for (int k = 0; k < kChunk; ++k) {
-    const uint32_t q = __builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
-    const uint32_t xs = __builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8);
-    const uint32_t rq = __mul24(q, w4);
-    lds_add(rq + cb, 1u);
-    lds_add(rq + xb + 4u * xs, 1u);
-    cb += d4;
-  }
-  uint32_t mk = (bm | bx) & 0xFFFFu;
-  if (__builtin_amdgcn_ballot_w64(mk != 0)) {  // masked (clips, insertions, known sites) or mismatch
-    const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-    const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
-    const uint32_t mm_off = 4u * (uint32_t)(qw * wcells);
-    while (mk) {
-      const int k = __builtin_ctz(mk);
-      mk &= mk - 1;
-      const uint32_t q = (uint32_t)((k < 8 ? q01 : q23) >> (8 * (k & 7))) & 0xFFu;
-      const uint32_t xs = (uint32_t)((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu;
-      const uint32_t rq = __mul24(q, w4);
-      const bool masked = (bm >> k) & 1u;
-      // masked: undo both increments (add ~0u = -1 in the obs window); mismatch: +1 in the mm window
-      const uint32_t off = masked ? 0u : mm_off, val = masked ? ~0u : 1u;
-      lds_add(rq + cb0 + d4 * (uint32_t)k + off, val);
-      lds_add(rq + xb + 4u * xs + off, val);
-      if (masked) lds_add(lmasked + 4u * (q - (uint32_t)q_lo), 1u);
-    }
-  }
-}
-
-// LDS: [obs window qw*wcells u32][mm window qw*wcells u32][masked qw u32][block hist 128 u32]
-// The window holds a piece's counts for rows (rg, q_lo..q_lo+qw-1) where rg is
-// the piece's read group; other keys go straight to the int64 table.  Each
-// piece's window is written to its slab of `part` and summed into the table by
-// bqsr_window_reduce.
-// kCL: lanes per super-chunk (see kCL below), else a lane per read.
-// (Tried: visiting a clean chunk's offsets in eight lane-dependent orders so
-// that lanes of one qual stop piling onto one cycle cell halved
-// SQ_LDS_ADDR_CONFLICT but the byte shuffles and their registers cost more:
-// cfg2 0.92 -> 1.58 ms; an odd or 32-aligned row length: 0.94 -> 1.00 /
-// 1.25 ms.)
-template <bool kCL>
-__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_kernel(ObserveParams P) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
-  const int wcells = P.wcells;  // window row: [cycle cells cw][contexts 21]
-  uint32_t* w_obs = (uint32_t*)smem;  // (no context table: observe_lds without it)
-  uint32_t* w_mm = w_obs + qw * wcells;
-  uint32_t* w_masked = w_mm + qw * wcells;
-  uint32_t* blk_hist = w_masked + qw;
-  const uint32_t lds_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, lds_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = P.n_blocks;
-  const bool ident = P.ord.perm == nullptr;
-  for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, G), wb = wg_begin(P.rd, blockIdx.x + 1, G);
-  const int q_lo = P.w.q_lo;
-  const int nk = order_keys(P.ord);
-  // kCL (lane per super-chunk): a wavefront step takes 64 >> ls reads with
-  // 2^ls lanes each, lane `sub` of a read taking its super-chunks (kSub
-  // chunks, 64 offsets) sub, sub + 2^ls, ...: the lanes of a read cover
-  // neighbouring 64-B pieces of its columns, so a wavefront's loads and
-  // stores fill whole cache lines at once.  Otherwise a lane per read walks
-  // all its super-chunks.
-  const int ls = kCL ? P.lane_shift : 6;
-  const int sub = kCL ? lane & ((1 << ls) - 1) : 0, rl = kCL ? lane >> ls : lane, rpw = kCL ? 64 >> ls : 64;
-  // lane per read: a read's 8 chunks (128 offsets) per step, so all its
-  // cache lines are fetched while hot (with 4 chunks a step, half of a
-  // 100-bp read's lines were fetched again a step later: PMC FETCH 2.0x ->
-  // 1.25x the algorithmic bytes); lane per super-chunk: 4
-  constexpr int NS = kCL ? kSub : kObsSub;
-  constexpr int kSup = NS * kChunk;
-  constexpr int NW = (kSup + 31) / 32 + 1;  // sbits words of a step (first slot at bit 0..31)
-  const int jstep = kSup << (kCL ? ls : 0);
-
-  for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
-    const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
-    const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
-    if (p0 >= wb) break;
-    if (p0 >= p1) continue;
-    const int rg_w = key_rg(P.ord, key, P.w.rg_lo);  // the read group of the window rows
-    const WinGeom gm = win_geom(P.ord, P.g, key);
-    const int c_lo = gm.c_lo, cw = gm.cw;
-    const bool all_cycles = c_lo == 0 && cw == C;  // read order: the window holds every cycle cell
-    for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
-    __syncthreads();
-
-    for (int64_t g0 = p0 + (int64_t)rpw * wave; g0 < p1; g0 += (int64_t)rpw * kWaves) {
-      const bool live = g0 + rl < p1;
-      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, g0 + rl) : 0, live, L);
-      if (x.trimmed && sub == 0) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
-      const bool act = x.fl & (kInfoObs | kInfoObsCheck);
-      const bool full = x.fl & kInfoObs;
-      const int n = act ? x.en - x.st : 0;
-      const bool full_rg = full && x.rg == rg_w;
-      // chunks start at offset st, or at st rounded down to 16 in the aligned
-      // layout (then the first chunk's offsets below st are not visited)
-      const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;
-      const uint8_t* qp = P.rd.qual + x.slot;
-      for (int j0 = jb + kSup * sub; __builtin_amdgcn_ballot_w64(j0 < n); j0 += jstep) {
-        if (j0 >= n) continue;
-        // issue every load of the super-chunk first
-        uint4 qs[NS], cr[NS];
-        uint64_t bw[NW];
-        const uint64_t s0 = x.slot + (uint64_t)(x.st + j0);
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-          const bool lv = j0 + kChunk * i < n;
-          const int o0 = x.st + j0 + kChunk * i;
-          qs[i] = lv ? *(const uint4*)(qp + o0) : make_uint4(0, 0, 0, 0);
-          cr[i] = (lv && full) ? chunk_raw(P.rd, chunk_n0(x, o0)) : make_uint4(0, 0, 0, 0);
-        }
-        // word w holds slots from bit 32 w - (s0 & 31) on: needed while that is below n - j0
-#pragma unroll
-        for (int w = 0; w < NW; ++w) bw[w] = (full && (w == 0 || 32 * w - 32 < n - j0)) ? P.sbits[(s0 >> 5) + w] : 0ull;
-#pragma clang loop unroll(full)
-        for (int i = 0; i < NS; ++i) {
-          const int j = j0 + kChunk * i;
-          if (j >= n) continue;
-          const int o0 = x.st + j;
-          const uint32_t qd[4] = {qs[i].x, qs[i].y, qs[i].z, qs[i].w};
-          uint32_t bm = 0, bx = 0;
-          uint32_t xo[4] = {4u, 4u, 4u, 4u};
-          if (full) {
-            if (P.rd.slots_aligned)
-              sub_bits16<NW>(bw, (uint32_t)(s0 >> 4) & 1u, i, bm, bx);
-            else
-              sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
-            uint64_t clo;
-            uint32_t chi;
-            chunk_finish(P.rd, x, chunk_n0(x, o0), cr[i], clo, chi);
-            if (j <= 0) clo = window_first(clo, -j);  // the read's first visited offset: context 0
-            ctx_slots(clo, chi, xo);
-          }
-          const int cc0 = x.cell0 + __mul24(x.dir, o0);  // table cycle cell of offset k: cc0 + dir * k
-          const int wc0 = cc0 - c_lo;                     // ... and window cycle cell
-          // the cycle cells of the chunk's valid offsets inside the window
-          // (monotone in k: both ends)
-          const uint32_t nv = (uint32_t)min(kChunk, n - j);
-          const int klo = j < 0 ? -j : 0;  // chunk offsets klo .. nv-1 are visited
-          const bool cok = full_rg && (all_cycles || ((unsigned)(wc0 + __mul24(klo, x.dir)) < (unsigned)cw &&
-                                                     (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)cw));
-          const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
-          // fast path: window rows of the piece's read group; offsets it skips
-          // are redone below
-          uint32_t fastm = 0;
-          if (cok && vmask == 0xFFFFu && quals_in_rows(qd, q_lo, q_lo + qw)) {
-            observe_clean(lds_obs, qd, xo, bm, bx, wc0, x.dir, q_lo, qw, wcells, cw, lds_masked);
-            bx = 0;  // its mismatches are counted
-            fastm = 0xFFFFu;
-          } else {
-            const uint32_t* qr = qd;
-            const uint32_t* xr = xo;
-            const uint32_t bmr = bm & 0xFFFFu, vr = vmask;
-#pragma unroll
-            for (int k = 0; k < kChunk; ++k) {
-              const int kk = k;
-              const int q = (int)((qr[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-              const int row = q - q_lo;
-              const bool f = cok && (unsigned)row < (unsigned)qw && ((vr >> k) & 1u);
-              const bool m = (bmr >> k) & 1u;
-              const int base = __mul24(row, wcells);  // 24-bit: full rate (v_mul_lo_u32 is quarter rate)
-              if (f) {
-                atomicAdd(m ? &w_masked[row] : &w_obs[base + wc0 + x.dir * kk], 1u);
-                if (!m) atomicAdd(&w_obs[base + cw + (int)((xr[k >> 2] >> (8 * (k & 3))) & 0xFFu)], 1u);
-              }
-              fastm |= (uint32_t)f << kk;
-            }
-          }
-          uint32_t slow = vmask & ~fastm;
-          uint32_t mmk = fastm & ~bm & bx;
-          if (__builtin_amdgcn_ballot_w64(mmk != 0)) {  // mismatches (about 1 base in 100)
-            const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-            const uint64_t q01 = ((uint64_t)qd[1] << 32) | qd[0], q23 = ((uint64_t)qd[3] << 32) | qd[2];
-            while (mmk) {
-              const int k = __builtin_ctz(mmk);
-              mmk &= mmk - 1;
-              // the qual from the chunk's registers (a byte load here is a
-              // memory round trip in nearly every chunk: 1 base in 100 of 1024)
-              const int q = (int)(int8_t)(((k < 8 ? q01 : q23) >> (8 * (k & 7))) & 0xFFu);
-              const int base = __mul24(q - q_lo, wcells);
-              atomicAdd(&w_mm[base + wc0 + __mul24(x.dir, k)], 1u);
-              atomicAdd(&w_mm[base + cw + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu)], 1u);
-            }
-          }
-          if (__builtin_amdgcn_ballot_w64(slow != 0)) {
-            const uint64_t x01 = ((uint64_t)xo[1] << 32) | xo[0], x23 = ((uint64_t)xo[3] << 32) | xo[2];
-            while (slow) {
-              const int k = __builtin_ctz(slow);
-              slow &= slow - 1;
-              const int o = o0 + k;
-              const int q = (int)(int8_t)qp[o];
-              if (q < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-                report(P.err, err_key((uint64_t)x.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
-              } else if (full) {  // outside the LDS window: straight to the int64 table
-                const bool masked = (bm >> k) & 1u, mism = (bx >> k) & 1u;
-                const int ccell = cc0 + __mul24(x.dir, k);
-                const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
-                if (ident) atomicAdd(&blk_hist[q], 1u);
-                const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
-                atomicAdd((unsigned long long*)&P.touched[key], 1ull);
-                if (!masked) {
-                  atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
-                  atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
-                  if (mism) {
-                    atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
-                    atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
-                  }
-                }
-              }
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ---- the piece's window -> its slab; window rows into the block histogram ----
-    uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
-    for (int i = tid; i < 2 * qw * wcells; i += blockDim.x) pb[i] = w_obs[i];
-    for (int slot = wave; slot < qw; slot += kWaves) {
-      uint32_t v = 0;
-      for (int c = lane; c < cw; c += 64) v += w_obs[slot * wcells + c];  // every unmasked base hits one cycle cell
-      v = wave_sum(v);
-      if (lane == 0) {
-        const uint32_t tot = v + w_masked[slot];
-        pb[2 * qw * wcells + slot] = tot;
-        if (ident && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
-      }
-    }
-    __syncthreads();
-  }
-  if (ident)
-    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
-}
-
 // Lane per chunk (chunk_walk): the same counts, each lane one 16-offset
 // chunk of the wavefront's reads laid end to end.  LDS: the window as in
-// bqsr_observe_kernel, then the walk's kMkWords markers.
+// bqsr_observe_lean's slab layout, then the walk's kMkWords markers.
 struct ObsChunkLoads {
   uint4 qs, cr;
   uint64_t bw0, bw1;  // sbits words of the chunk's first slot and the next
@@ -1771,10 +1419,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
 
 constexpr int kObserveU = 2;  // chunks in flight per lane
 
-// kG: the batch's columns gathered into sorted order (OrderDev::oslot; a
-// kernel of its own: the gathered walk's extra fields cost registers)
-template <bool kG>
-__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObserveParams P) {
+extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, L = P.g.L;
   const int wcells = P.wcells;
@@ -1810,7 +1455,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) {
       observe_chunk(P, pc, x, j, n, on, ld);
     };
-    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, kG>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
                                                                       64 * kWaves, L, lane, mk, fread, fload, fchunk);
     __syncthreads();
     // ---- the piece's window -> its slab; window rows into the block histogram ----
@@ -1831,383 +1476,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(ObservePara
   if (ident)
     for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
 }
-
-// ------------------------------------------------- observe: lane per offset --
-//
-// bqsr_observe_rows: a wavefront takes its reads one at a time and lane l the
-// read's offset o0 + l (rows of 64 offsets), so everything per read is
-// wavefront-uniform (SGPRs: read_lane fields), the read's trimmed range and
-// its masked / mismatch bits are 64-bit lane masks (the mismatch and masked
-// bits straight from the slot bitmap) used as exec masks, and per base a lane
-// has: its qual byte (one byte load per row), the two base codes of its
-// context (one u16 load: Q9's mirrored pair for reverse reads), the context
-// slot from a 512-B LDS table, and two LDS adds (RecalTable.+=,
-// RecalTable.scala:55-62 / ErrorCount.+= :195-201).  About 5 VALU per base
-// against 27 of the lane-per-read walk, and the adds no longer pile up:
-//  * the 64 cycle-cell adds of a row go to 64 consecutive cells of the
-//    lanes' qual rows; the LDS row length is 0 mod 32 words, so their banks
-//    are the cells' and differ whatever the quals (the walk's wavefront added
-//    to ONE cell per mate class in many rows: same-address and bank conflicts);
-//  * a row's context counters have `nc` copies (copy = lane & (nc - 1), the
-//    copies of one context adjacent), so lanes of one qual and context add
-//    to different words and nearly always different banks; the slab write
-//    sums the copies.
-// The obs window row is [context copies 21 * nc][cycle cells cw][pad]; the mm
-// window (mismatches, about 1 base in 100) and the slab keep the
-// [cycle cells cw][contexts 21][pad] rows of bqsr_window_reduce.  R rows of
-// G = 16 / R reads have their loads issued before the first is used.
-constexpr int kLutBytes = 512;
-
-__device__ __forceinline__ uint64_t lane_range(int lo, int hi) {  // lanes [lo, hi) of 64, clamped
-  lo = max(lo, 0);
-  hi = min(hi, 64);
-  if (lo >= hi) return 0ull;
-  const uint64_t h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-  return h & ~((1ull << lo) - 1ull);
-}
-
-struct URead {  // one read, wavefront-uniform
-  int64_t r;
-  uint64_t slot;
-  int st, en, fl, cell0, dir, rg;
-};
-
-struct RowsLane {  // per-lane constants of bqsr_observe_rows
-  uint32_t kl;     // LDS address of (qual row q, context copy of the lane) = q * row4 + kl
-  uint32_t bound;  // kl + q * row4 < bound <=> q is a window row
-  uint32_t row4, nc4;
-  int32_t cyc_a, cyc_b;  // cycle cell term of the lane for dir +1 / -1, minus its copy offset
-  uint32_t sh_f, sh_e;   // bit offset of a lane's code pair in its u16 (forward / reverse, E even)
-  uint32_t vo_f, vo_re, vo_ro;  // byte offset of a lane's u16 (forward / reverse, E even / odd)
-};
-
-__device__ __forceinline__ URead uread(int j, uint32_t p_r, uint32_t p_slo, uint32_t p_shi, uint32_t p_se,
-                                       uint32_t p_fl, uint32_t p_rg) {
-  URead u;
-  u.r = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)p_r, j);
-  u.slot = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)p_shi, j) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)p_slo, j);
-  const uint32_t se = (uint32_t)__builtin_amdgcn_readlane((int)p_se, j);
-  const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)p_fl, j);
-  u.st = (int)(se & 0xFFFFu);
-  u.en = (int)(se >> 16);
-  u.fl = (int)(fl & 0x7FFFu);
-  u.dir = (fl & kPkRev) ? -1 : 1;
-  u.cell0 = (int)(fl >> 16);
-  u.rg = __builtin_amdgcn_readlane((int)p_rg, j);
-  return u;
-}
-
-// issue a row's loads: quals, context code pairs, the bitmap words of its slots
-__device__ __forceinline__ void row_load(const ObserveParams& P, const URead& u, int o0, int lane, const RowsLane& c,
-                                         uint32_t& q, uint32_t& pr, uint64_t& bw) {
-  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
-  const bool full = u.fl & kInfoObs;
-  if (__builtin_amdgcn_inverse_ballot_w64(valid)) q = P.rd.qual[u.slot + (uint64_t)(o0 + lane)];
-  if (!full) return;
-  const int kf = u.st - o0;  // the read's first visited offset: context 0, no pair needed
-  const uint64_t pm = valid & ~((kf >= 0 && kf < 64) ? (1ull << kf) : 0ull);
-  if (!(u.fl & kInfoNeg)) {
-    // offset o: codes o-1 (low nibble of the pair) and o
-    const uint8_t* b = P.rd.bases + (((u.slot + (uint64_t)o0) >> 1) - 1);
-    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + c.vo_f);
-  } else {
-    // offset o = st + k: codes at E - o and E - o + 1 (E = st + en - 1), complemented by the table (Q9)
-    const int e = u.st + u.en - 1;
-    const int64_t x = (int64_t)u.slot + e - o0;
-    const uint8_t* b = P.rd.bases + ((x - 63) >> 1);
-    const uint32_t vo = (e & 1) ? c.vo_ro : c.vo_re;
-    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + vo);
-  }
-  const uint64_t s0 = u.slot + (uint64_t)o0;
-  const int hi = min(u.en - o0, 64);
-  const int nw = (int)(((s0 & 31) + (uint64_t)hi + 31) >> 5);
-  if (lane < nw) bw = P.sbits[(s0 >> 5) + (uint64_t)lane];
-}
-
-template <bool kIdent>
-__device__ __forceinline__ void row_slow(const ObserveParams& P, const URead& u, int o, uint32_t q, uint32_t slot,
-                                         bool masked, bool mism, uint32_t* blk_hist) {
-  const int qs = (int)(int8_t)(uint8_t)q;
-  if (qs < 0) {  // RecalTable.+= : phredToErrorProbabilityCache(qual)
-    report(P.err, err_key((uint64_t)u.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
-    return;
-  }
-  if (kIdent) atomicAdd(&blk_hist[qs], 1u);
-  const int cells = P.g.cells;
-  const int64_t key = (int64_t)qs + (int64_t)kMaxQ * u.rg;
-  atomicAdd((unsigned long long*)&P.touched[key], 1ull);
-  if (masked) return;
-  const int ccell = u.cell0 + u.dir * o, xcell = P.g.C + (int)slot;
-  atomicAdd((unsigned long long*)&P.obs[key * cells + ccell], 1ull);
-  atomicAdd((unsigned long long*)&P.obs[key * cells + xcell], 1ull);
-  if (mism) {
-    atomicAdd((unsigned long long*)&P.mm[key * cells + ccell], 1ull);
-    atomicAdd((unsigned long long*)&P.mm[key * cells + xcell], 1ull);
-  }
-}
-
-
-typedef __attribute__((address_space(3))) const uint8_t* LdsBytes;
-
-// Bucketed batches: the fold needs per-block qual histograms of the folded
-// bases in READ order (fold blocks = read-order ranges, wg_begin), which the
-// bucketed walk does not follow.  Each wavefront keeps the histogram of the
-// block of the read it is on in LDS (`hc` copies, copy lane & (hc - 1)) and
-// adds it to hq_block with global atomics when a read of another block comes
-// (a key's reads come in runs of one sort chunk, nearly always one block).
-struct FoldHist {
-  uint32_t* wh;         // the wavefront's [qw][hc] counters
-  int64_t blk, lo, hi;  // its block and that block's reads [lo, hi)
-};
-__device__ __forceinline__ void hist_flush(const ObserveParams& P, FoldHist& h, int qw, int hc, int q_lo, int lane) {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  if (h.blk >= 0)
-    for (int t = lane; t < qw; t += 64) {
-      uint32_t s = 0;
-      for (int k = 0; k < hc; ++k) {
-        s += h.wh[t * hc + k];
-        h.wh[t * hc + k] = 0;
-      }
-      if (s) atomicAdd(&P.hq_block[h.blk * kQBins + q_lo + t], s);
-    }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-__device__ __forceinline__ void hist_block(const ObserveParams& P, FoldHist& h, int64_t r, int qw, int hc, int q_lo,
-                                           int lane) {
-  if (r >= h.lo && r < h.hi) return;
-  hist_flush(P, h, qw, hc, q_lo, lane);
-  h.blk = wg_of(P.rd, r, P.n_blocks);
-  h.lo = wg_begin(P.rd, h.blk, P.n_blocks);
-  h.hi = wg_begin(P.rd, h.blk + 1, P.n_blocks);
-}
-
-template <bool kIdent>
-__device__ __forceinline__ void row_proc(const ObserveParams& P, const URead& u, int o0, int lane, const RowsLane& c,
-                                         uint32_t q, uint32_t pr, uint64_t bw, int rg_w, int c_lo, int cw, int q_lo,
-                                         int nc, uint32_t a_mm, uint32_t a_masked, uint32_t a_lut,
-                                         uint32_t* blk_hist, FoldHist& fh, int hc) {
-  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
-  if (!(u.fl & kInfoObs)) {  // usable but failing at `en` (prep reported it): quals before it only checked
-    const uint64_t bad = __builtin_amdgcn_ballot_w64(__builtin_amdgcn_inverse_ballot_w64(valid) && q >= 128u);
-    if (bad && lane == 0) report(P.err, err_key((uint64_t)u.r, (uint32_t)(o0 + __builtin_ctzll(bad)), kRankTable,
-                                                BQSR_ERR_QUAL_RANGE));
-    return;
-  }
-  // masked (refPos None / outside the read / known site) and mismatch bits of the row's 64 slots
-  const uint32_t sh = (uint32_t)((u.slot + (uint64_t)o0) & 31);
-  const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bw, 0);
-  const uint32_t m1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bw, 1);
-  const uint32_t m2 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bw, 2);
-  const uint32_t x0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bw >> 32), 0);
-  const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bw >> 32), 1);
-  const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bw >> 32), 2);
-  uint64_t masked, mism;
-  if (sh == 0) {
-    masked = (uint64_t)m0 | ((uint64_t)m1 << 32);
-    mism = (uint64_t)x0 | ((uint64_t)x1 << 32);
-  } else {  // 16-aligned slots: the row starts at bit 16
-    masked = (uint64_t)(m0 >> 16) | ((uint64_t)m1 << 16) | ((uint64_t)m2 << 48);
-    mism = (uint64_t)(x0 >> 16) | ((uint64_t)x1 << 16) | ((uint64_t)x2 << 48);
-  }
-  const bool neg = u.fl & kInfoNeg;
-  const uint32_t sh_p = (neg && !((u.st + u.en - 1) & 1)) ? c.sh_e : c.sh_f;
-  uint32_t pair = __builtin_amdgcn_ubfe(pr, sh_p, 8);
-  if (lane == u.st - o0) pair = 0xFFu;  // the read's first visited offset: context 0 (BaseContext k == 0)
-  const uint32_t slot = *(LdsBytes)(uintptr_t)(a_lut + (neg ? 256u : 0u) + pair);
-  const uint32_t trl = __mul24(q, c.row4) + c.kl;
-  const bool inrow = trl < c.bound && u.rg == rg_w;
-  const int cellrow = u.cell0 + u.dir * o0 - c_lo;  // window cycle cell of lane 0
-  const uint32_t cyc = trl + (uint32_t)(4 * (kCtxSlots * nc + cellrow) + (u.dir > 0 ? c.cyc_a : c.cyc_b));
-  const uint32_t ctx = __mul24(slot, c.nc4) + trl;
-  const uint64_t em = valid & ~masked;
-  if (inrow && __builtin_amdgcn_inverse_ballot_w64(em)) {
-    lds_add(cyc, 1u);
-    lds_add(ctx, 1u);
-  }
-  const uint64_t mx = em & mism;
-  if (mx) {
-    if (inrow && __builtin_amdgcn_inverse_ballot_w64(mx)) {
-      const uint32_t mrow = a_mm + 4u * __mul24(q - (uint32_t)q_lo, (uint32_t)P.wcells);
-      lds_add(mrow + 4u * (uint32_t)(cellrow + u.dir * lane), 1u);
-      lds_add(mrow + 4u * ((uint32_t)cw + slot), 1u);
-    }
-  }
-  const uint64_t mk = valid & masked;
-  if (mk) {
-    if (inrow && __builtin_amdgcn_inverse_ballot_w64(mk)) lds_add(a_masked + 4u * (q - (uint32_t)q_lo), 1u);
-  }
-  if (!kIdent) {  // the folded bases' quals into the read's read-order block histogram
-    hist_block(P, fh, u.r, P.w.qw, hc, q_lo, lane);
-    if (inrow && __builtin_amdgcn_inverse_ballot_w64(valid))
-      lds_add((uint32_t)(uintptr_t)(LdsWords)fh.wh + 4u * (__mul24(q - (uint32_t)q_lo, (uint32_t)hc) +
-                                                        ((uint32_t)lane & (uint32_t)(hc - 1))), 1u);
-  }
-  if (__builtin_amdgcn_ballot_w64(!inrow && __builtin_amdgcn_inverse_ballot_w64(valid))) {
-    if (!inrow && __builtin_amdgcn_inverse_ballot_w64(valid)) {
-      row_slow<kIdent>(P, u, o0 + lane, q, slot, (masked >> lane) & 1u, (mism >> lane) & 1u, blk_hist);
-      if (!kIdent && q < (uint32_t)kQBins) atomicAdd(&P.hq_block[fh.blk * kQBins + q], 1u);
-    }
-  }
-}
-
-// LDS: [obs qw * orow][mm qw * wcells][masked qw][block hist 128][context tables 512 B]
-//      (bucketed: [per wavefront fold-block histograms kWaves * qw * hc])
-template <int R, bool kIdent>
-__global__ void __launch_bounds__(kBlockThreads) bqsr_observe_rows(ObserveParams P) {
-  constexpr int G = 8 / R;  // reads per group: G * R rows' loads in flight per wavefront
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int qw = P.w.qw, wcells = P.wcells, orow = P.orow, nc = P.nc, L = P.g.L;
-  uint32_t* w_obs = (uint32_t*)smem;
-  uint32_t* w_mm = w_obs + qw * orow;
-  uint32_t* w_masked = w_mm + qw * wcells;
-  uint32_t* blk_hist = w_masked + qw;
-  uint8_t* lut = (uint8_t*)(blk_hist + kQBins);
-  const uint32_t a_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, a_mm = (uint32_t)(uintptr_t)(LdsWords)w_mm;
-  const uint32_t a_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
-  const uint32_t a_lut = (uint32_t)(uintptr_t)(LdsWords)(uint32_t*)lut;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hc = kIdent ? 1 : P.hc;
-  FoldHist fh{(uint32_t*)(lut + kLutBytes) + wave * qw * hc, -1, 0, 0};
-  for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
-  if (!kIdent)
-    for (int i = tid; i < kWaves * qw * hc; i += blockDim.x) ((uint32_t*)(lut + kLutBytes))[i] = 0;
-  // context slot (ctx + 4) of a code pair: forward (previous | current << 4),
-  // reverse (the mirrored pair, complemented: BaseContext.simpleReverseComplement);
-  // 0xFF: a read's first visited offset (context 0)
-  for (int i = tid; i < kLutBytes; i += blockDim.x) {
-    const uint32_t e = (uint32_t)i & 255u, lo = e & 15u, hi = e >> 4;
-    lut[i] = (uint8_t)(e == 0xFFu ? 4u : i < 256 ? ctx_slot(lo, hi) : ctx_slot(comp_code(hi), comp_code(lo)));
-  }
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, P.n_blocks), wb = wg_begin(P.rd, blockIdx.x + 1, P.n_blocks);
-  const int q_lo = P.w.q_lo;
-  const int nk = order_keys(P.ord);
-  RowsLane c;
-  c.row4 = 4u * (uint32_t)orow;
-  c.nc4 = 4u * (uint32_t)nc;
-  const uint32_t lanepart = 4u * ((uint32_t)lane & (uint32_t)(nc - 1));
-  c.kl = a_obs + lanepart - (uint32_t)q_lo * c.row4;
-  c.bound = a_obs + (uint32_t)qw * c.row4;
-  c.cyc_a = 4 * lane - (int)lanepart;
-  c.cyc_b = -4 * lane - (int)lanepart;
-  c.sh_f = 4u * (uint32_t)((lane + 1) & 1);
-  c.sh_e = 4u * (uint32_t)(lane & 1);
-  c.vo_f = (uint32_t)((lane + 1) >> 1);
-  c.vo_re = 32u - (uint32_t)((lane + 1) >> 1);
-  c.vo_ro = 31u - (uint32_t)(lane >> 1);
-
-  for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
-    const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
-    const int64_t p1 = min(wb, key_begin(P.ord, P.rd.n_reads, key + 1));
-    if (p0 >= wb) break;
-    if (p0 >= p1) continue;
-    const int rg_w = key_rg(P.ord, key, P.w.rg_lo);
-    const WinGeom gm = win_geom(P.ord, P.g, key);
-    for (int i = tid; i < qw * orow + qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
-    __syncthreads();
-    for (int64_t pb = p0 + 64 * wave; pb < p1; pb += 64 * kWaves) {
-      const bool live = pb + lane < p1;
-      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, pb + lane) : 0, live, L);
-      if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
-      const bool act = live && (x.fl & (kInfoObs | kInfoObsCheck)) && x.en > x.st;
-      const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
-      const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
-      const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
-      const uint32_t p_rg = (uint32_t)x.rg;
-      uint64_t todo = __builtin_amdgcn_ballot_w64(act), tail = 0;
-      while (todo) {
-        URead u[G];
-        bool has[G];
-        int jj[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          has[g] = todo != 0;
-          jj[g] = has[g] ? (int)__builtin_ctzll(todo) : 0;
-          todo &= todo - 1;
-          u[g] = uread(jj[g], p_r, p_slo, p_shi, p_se, p_fl, p_rg);
-        }
-        uint32_t q[G][R], pr[G][R];
-        uint64_t bw[G][R];
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            q[g][i] = 0;
-            pr[g][i] = 0;
-            bw[g][i] = 0;
-            const int o0 = (u[g].st & ~63) + 64 * i;
-            if (has[g] && o0 < u[g].en) row_load(P, u[g], o0, lane, c, q[g][i], pr[g][i], bw[g][i]);
-          }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            const int o0 = (u[g].st & ~63) + 64 * i;
-            if (has[g] && o0 < u[g].en)
-              row_proc<kIdent>(P, u[g], o0, lane, c, q[g][i], pr[g][i], bw[g][i], rg_w, gm.c_lo, gm.cw, q_lo, nc,
-                               a_mm, a_masked, a_lut, blk_hist, fh, hc);
-          }
-        // reads longer than the R rows held: their remaining rows below
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-          if (has[g] && (u[g].st & ~63) + 64 * R < u[g].en) tail |= 1ull << jj[g];
-      }
-      // rows past the R held ones, one at a time
-      while (tail) {
-        const int j = (int)__builtin_ctzll(tail);
-        tail &= tail - 1;
-        const URead v = uread(j, p_r, p_slo, p_shi, p_se, p_fl, p_rg);
-        for (int o0 = (v.st & ~63) + 64 * R; o0 < v.en; o0 += 64) {
-          uint32_t q1 = 0, pr1 = 0;
-          uint64_t bw1 = 0;
-          row_load(P, v, o0, lane, c, q1, pr1, bw1);
-          row_proc<kIdent>(P, v, o0, lane, c, q1, pr1, bw1, rg_w, gm.c_lo, gm.cw, q_lo, nc, a_mm, a_masked, a_lut,
-                           blk_hist, fh, hc);
-        }
-      }
-    }
-    if (!kIdent) {
-      hist_flush(P, fh, qw, hc, q_lo, lane);
-      fh.blk = -1;
-      fh.lo = fh.hi = 0;
-    }
-    __syncthreads();
-    // ---- the piece's window -> its slab ([cycle cells][contexts 21][pad] rows; the copies summed) ----
-    uint32_t* pb = P.part + (int64_t)(blockIdx.x + (kIdent ? 0 : key)) * P.part_stride;
-    const int cw = gm.cw, cx = kCtxSlots * nc;
-    for (int i = tid; i < qw * wcells; i += blockDim.x) {
-      const int t = i / wcells, cc = i - t * wcells;
-      const uint32_t* row = w_obs + t * orow;
-      uint32_t v = 0;
-      if (cc < cw) {
-        v = row[cx + cc];
-      } else if (cc < cw + kCtxSlots) {
-        const uint32_t* cp = row + (cc - cw) * nc;
-        for (int k = 0; k < nc; ++k) v += cp[k];
-      }
-      pb[i] = v;
-      pb[qw * wcells + i] = w_mm[i];
-    }
-    for (int slot = wave; slot < qw; slot += kWaves) {
-      uint32_t v = 0;
-      for (int cc = lane; cc < cw; cc += 64) v += w_obs[slot * orow + cx + cc];  // every unmasked base: one cycle cell
-      v = wave_sum(v);
-      if (lane == 0) {
-        const uint32_t tot = v + w_masked[slot];
-        pb[2 * qw * wcells + slot] = tot;
-        if (kIdent && tot && q_lo + slot < kQBins) atomicAdd(&blk_hist[q_lo + slot], tot);
-      }
-    }
-    __syncthreads();
-  }
-  if (kIdent)
-    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
-}
-template __global__ void bqsr_observe_rows<2, true>(ObserveParams);
-template __global__ void bqsr_observe_rows<4, true>(ObserveParams);
-template __global__ void bqsr_observe_rows<2, false>(ObserveParams);
-template __global__ void bqsr_observe_rows<4, false>(ObserveParams);
 
 // Sum the pieces' window counts into the int64 table: one thread per (key,
 // window cell, slab group), over the slabs (w + key) of the workgroups whose
@@ -2482,107 +1750,6 @@ __device__ __forceinline__ bool err_prob(int64_t obs, int64_t mm, double mre, do
 }
 
 // one workgroup: groups, globals, average, then a2 per (rg, q)
-// ---- bucket-major copies of a bucketed batch (cfg4: several read groups) ----
-// The bucketed passes visit reads in key order, where a read's neighbours in
-// memory belong to other keys and are visited at other times: most of every
-// cache line a pass touches was fetched for one read (PMC fetch 2.2x apply,
-// 3.1x observe the algorithmic bytes on cfg4, against 1.3x in read order).
-// So once per job the reads' quals, base codes, records and ReadInfo are
-// copied into sorted order (record p = sorted position p), and both passes
-// stream through them; the slot bitmap and the outputs stay in the batch's
-// layout (OrderDev::oslot).
-// Sorted position p -> the read's index (perm) and slot span; read r -> p.
-extern "C" __global__ void bqsr_key_inverse(const uint32_t* perm, const ReadMeta* meta, int64_t n, uint32_t* inv,
-                                            uint64_t* span) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = perm[p];
-    const ReadMeta m = meta[r];
-    inv[r] = (uint32_t)p;
-    span[p] = slot_span(m.lq, m.ls);
-  }
-}
-
-// In read order (coalesced reads; each read's spans written whole at its
-// sorted slot gslot[inv[r]]): a read's quals and base codes, its record with
-// the new slot, its ReadInfo with the trimming resolved (also written back in
-// place for the fold), and -- bqsr_fold_hist's work, which this replaces --
-// the fold's per-block quality histograms of the folded bases.  Lanes as in
-// bqsr_fold_hist: 2^ls lanes per read, 64 slots each.  Aligned layout only
-// (every read's span a multiple of 16 slots).
-extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_bucket_gather(
-    ReadsDev rd, ReadInfo* info, const uint32_t* inv, const uint64_t* gslot, int32_t n_blocks, int32_t ls,
-    uint32_t* hq_block, ReadMeta* gmeta, ReadInfo* ginfo, uint64_t* oslot, uint8_t* gqual, uint8_t* gbases) {
-  extern __shared__ uint32_t fh_smem[];
-  uint32_t* hist = fh_smem;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < kFhWaves * kFhCopies * kFhStride; i += blockDim.x) hist[i] = 0;
-  __syncthreads();
-  const int blk = blockIdx.x / kFhSplit, part = blockIdx.x - blk * kFhSplit;
-  const int64_t b0 = wg_begin(rd, blk, n_blocks), b1 = wg_begin(rd, blk + 1, n_blocks);
-  const int64_t r0 = b0 + (b1 - b0) * part / kFhSplit, r1 = b0 + (b1 - b0) * (part + 1) / kFhSplit;
-  uint32_t* hw = hist + (wv * kFhCopies + (lane & (kFhCopies - 1))) * kFhStride;
-  const int sub = lane & ((1 << ls) - 1), rl = lane >> ls, rpw = 64 >> ls;
-  for (int64_t g0 = r0 + (int64_t)rpw * wv; g0 < r1; g0 += (int64_t)rpw * kFhWaves) {
-    const int64_t r = g0 + rl;
-    int span = 0, st = 0, en = 0;
-    uint64_t src = 0, dst = 0;
-    if (r < r1) {
-      const ReadMeta m = rd.meta[r];
-      const ReadInfo raw = info[r];
-      const ReadInfo inf = resolve_info(rd, raw, m.slot, m.lq);
-      const uint32_t p = inv[r];
-      src = m.slot;
-      dst = gslot[p];
-      span = (int)slot_span(m.lq, m.ls);
-      if ((inf.fl & kInfoObs) && inf.en > inf.st) {
-        st = inf.st;
-        en = inf.en;
-      }
-      if (sub == 0) {
-        ReadMeta gm = m;
-        gm.slot = dst;
-        gmeta[p] = gm;
-        ginfo[p] = inf;
-        oslot[p] = m.slot;
-        if (raw.fl & kInfoTrim) info[r] = inf;  // the fold reads the trimmed range
-      }
-    }
-    for (int j0 = kSuper * sub; __builtin_amdgcn_ballot_w64(j0 < span); j0 += kSuper << ls) {
-      if (j0 >= span) continue;
-      uint4 v[kSub];
-      uint2 b[kSub];
-#pragma unroll
-      for (int i = 0; i < kSub; ++i) {
-        const int o = j0 + kChunk * i;
-        v[i] = o < span ? *(const uint4*)(rd.qual + src + o) : make_uint4(0, 0, 0, 0);
-        b[i] = o < span ? *(const uint2*)(rd.bases + ((src + o) >> 1)) : make_uint2(0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < kSub; ++i) {
-        const int o = j0 + kChunk * i;
-        if (o >= span) continue;
-        *(uint4*)(gqual + dst + o) = v[i];
-        *(uint2*)(gbases + ((dst + o) >> 1)) = b[i];
-        // folded bases: offsets [st, en) of usable reads
-        const int lo = max(st - o, 0), hi = min(en - o, kChunk);
-        const uint32_t vm = hi > lo ? ((hi >= 16 ? 0xFFFFu : (1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
-        if (__builtin_amdgcn_ballot_w64(vm != 0)) {
-          const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-          for (int k = 0; k < kChunk; ++k)  // (an offset outside adds 0: no branch per byte)
-            atomicAdd(&hw[__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 7)], __builtin_amdgcn_ubfe(vm, k, 1));
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < kQBins; q += blockDim.x) {
-    uint32_t s = 0;
-    for (int i = 0; i < kFhWaves * kFhCopies; ++i) s += hist[i * kFhStride + q];
-    if (s) atomicAdd(&hq_block[(int64_t)blk * kQBins + q], s);
-  }
-}
-
 extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_t* touched, const int64_t* qk_obs,
                                                                       const int64_t* qk_mm, TableGeom g, int32_t n_rg,
                                                                       double em_host, const double* em_dev,
@@ -2924,8 +2091,7 @@ extern "C" __global__ void bqsr_apply_chars(ApplyParams P, uint8_t* chars) {
   }
 }
 
-template <bool kG>  // (as bqsr_observe_chunks)
-__global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
+extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
   // LDS: [clean rows 16 B][walk markers][context table][char table]
@@ -2992,283 +2158,12 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(ApplyParams P
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
       apply_chunk(P, &P, pc, x, j, n, on, ld);
     };
-    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, kG>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
                                                                              64 * kWaves, L, lane, mk, fread, fload,
                                                                              fchunk);
   }  // pieces
 }
 
-// ------------------------------------------------- apply: lane per offset --
-//
-// bqsr_apply_rows: RecalUtil.recalibrate (RecalUtil.scala:31-42) with the
-// read-per-wavefront, lane-per-offset walk of bqsr_observe_rows.  A piece is
-// one read group and mate class (readPaired && secondOfPair decides the sign
-// of DiscreteCycle, so a piece's reads use one half of the cycle cells, L
-// cells): in read order a workgroup walks its reads twice, class 0 then
-// class 1, with that class's char table in LDS; bucketed batches have a
-// piece per key.  The char table is packed for the walk: dword (row q,
-// context group x >> 2, cycle cell c) holds the chars of contexts 4 (x >> 2)
-// .. +3, rows of cwp = roundup(L, 32) dwords, so the 64 lanes of a row --
-// consecutive cycle cells, any quals and contexts -- read 64 different banks'
-// worth of dwords in consecutive banks: no bank conflicts whatever the quals
-// (the lane-per-chunk walk's byte reads conflicted 60 % of their cycles).
-// A char 0 (key not in the table, a char above 0xFF) and quals outside the
-// rows take the exact checked path.
-
-// context slot (ctx + 4) of a code pair: forward (previous | current << 4),
-// reverse (the mirrored pair, complemented: BaseContext.simpleReverseComplement);
-// 0xFF: a read's first visited offset (context 0)
-__device__ __forceinline__ uint32_t pair_slot(uint32_t e, bool rev) {
-  const uint32_t lo = e & 15u, hi = e >> 4;
-  return e == 0xFFu ? 4u : !rev ? ctx_slot(lo, hi) : ctx_slot(comp_code(hi), comp_code(lo));
-}
-
-// a piece's packed char table: (class, read group, cycle cells c_lo .. c_lo + L - 1)
-struct ApplyRowsPiece {
-  int rg, c_lo, cls;
-};
-__device__ __forceinline__ ApplyRowsPiece apply_rows_piece(const ApplyParams& P, int pi) {
-  const bool ident = P.ord.perm == nullptr;
-  const int cls = ident ? pi : (pi & 1);
-  return ApplyRowsPiece{ident ? P.w.rg_lo : (pi >> 1), cls ? 0 : P.g.L + 1, cls};
-}
-
-// Every piece's packed char table, once per apply launch: a thread per dword.
-extern "C" __global__ void bqsr_apply_chars_rows(ApplyParams P, int32_t n_pieces, uint32_t* chars) {
-  const int qw = P.w.qw, q_lo = P.w.q_lo, cwp = P.cwp, L = P.g.L;
-  const int64_t per = (int64_t)qw * 6 * cwp;
-  const int64_t total = (int64_t)n_pieces * per;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int pi = (int)(t / per);
-    const int64_t e = t - (int64_t)pi * per;
-    const int row = (int)(e / (6 * cwp));
-    const int rem = (int)(e - (int64_t)row * 6 * cwp), xg = rem / cwp, c = rem - xg * cwp;
-    const ApplyRowsPiece pc = apply_rows_piece(P, pi);
-    const int64_t rq = (int64_t)pc.rg * kQBins + q_lo + row;
-    uint32_t v = 0;
-    if (c < L && pc.rg < P.n_rg && q_lo + row < kQBins && P.rq_ok[rq]) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int x = 4 * xg + k;
-        if (x >= kCtxSlots) break;
-        // RecalUtil.recalibrate: (((e + rgD) + qD) + cycD) + ctxD = (a2 + cycD) + ctxD
-        const int32_t Q = phred_q(P.s1[rq * P.g.C + pc.c_lo + c] + P.d2[rq * kCtxSlots + x], P.qb_thr, P.qb_q, P.thr,
-                                  P.thr_qmin, P.thr_n);
-        const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-        v |= (code <= 0xFFu ? code : 0u) << (8 * k);
-      }
-    }
-    chars[t] = v;
-  }
-}
-
-// the checked path of one offset (apply_slow's body): key checks, QUAL_RANGE,
-// the exact char, exceptions above 0xFF; returns the output byte
-__device__ __forceinline__ uint32_t apply_one(const ApplyParams& P, const URead& u, int o, uint32_t qb, uint32_t xs) {
-  const int q = (int)(int8_t)(uint8_t)qb;
-  const int64_t key = (int64_t)q + (int64_t)kMaxQ * u.rg;
-  const int64_t gr = (key - 1) / kMaxQ;
-  const bool grp = (gr + 1) >= 0 && (gr + 1) < P.n_groups && P.grp_ok[gr + 1];
-  const bool kok = key >= 0 && key < P.g.K && P.key_ok[key];
-  if (!grp || !kok) {
-    report(P.err, err_key((uint64_t)u.r, (uint32_t)o, kRankTable, BQSR_ERR_MISSING_KEY));
-    return 0;
-  }
-  if (q < 0) {
-    report(P.err, err_key((uint64_t)u.r, (uint32_t)o, kRankTable, BQSR_ERR_QUAL_RANGE));
-    return 0;
-  }
-  if (!(u.fl & kInfoApp)) return 0;
-  const int64_t rq = (int64_t)u.rg * kQBins + q;
-  const int ccell = u.cell0 + u.dir * o;
-  const double p = P.s1[rq * P.g.C + ccell] + P.d2[rq * kCtxSlots + xs];
-  const int32_t Q = phred_q(p, P.qb_thr, P.qb_q, P.thr, P.thr_qmin, P.thr_n);
-  const uint32_t code = ((uint32_t)Q + 33u) & 0xFFFFu;  // (Q + 33).toChar
-  if (code > 0xFFu) {
-    const unsigned long long e = atomicAdd(P.n_exc, 1ull);
-    if ((int64_t)e < P.max_exc) P.exc[e] = ((u.slot + (uint64_t)o) << 16) | code;
-  }
-  return code & 0xFFu;
-}
-
-struct ApplyLane {
-  uint32_t kt, bound, rowb;  // row address of qual q: q * rowb + kt (< bound: a table row)
-  uint32_t sh_f, sh_e, vo_f, vo_re, vo_ro;
-};
-
-__device__ __forceinline__ void apply_row_load(const ApplyParams& P, const URead& u, int o0, int lane,
-                                               const ApplyLane& c, uint32_t& q, uint32_t& pr) {
-  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
-  if (__builtin_amdgcn_inverse_ballot_w64(valid)) q = P.rd.qual[u.slot + (uint64_t)(o0 + lane)];
-  if (u.fl & kInfoPass) return;
-  const int kf = u.st - o0;
-  const uint64_t pm = valid & ~((kf >= 0 && kf < 64) ? (1ull << kf) : 0ull);
-  if (!(u.fl & kInfoNeg)) {
-    const uint8_t* b = P.rd.bases + (((u.slot + (uint64_t)o0) >> 1) - 1);
-    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + c.vo_f);
-  } else {
-    const int e = u.st + u.en - 1;
-    const int64_t x = (int64_t)u.slot + e - o0;
-    const uint8_t* b = P.rd.bases + ((x - 63) >> 1);
-    const uint32_t vo = (e & 1) ? c.vo_ro : c.vo_re;
-    if (__builtin_amdgcn_inverse_ballot_w64(pm)) pr = *(const uint16_t*)(b + vo);
-  }
-}
-
-typedef __attribute__((address_space(3))) const uint16_t* LdsHalfs;
-
-__device__ __forceinline__ void apply_row_proc(const ApplyParams& P, const URead& u, int o0, int lane,
-                                               const ApplyLane& c, uint32_t q, uint32_t pr, int rg_p, int c_lo,
-                                               uint32_t a_lut) {
-  const uint64_t valid = lane_range(u.st - o0, u.en - o0);
-  uint8_t* op = P.out_qual + u.slot + (uint64_t)o0;
-  if (u.fl & kInfoPass) {  // the original chars: qual + 33 (Java byte -> char)
-    if (__builtin_amdgcn_inverse_ballot_w64(valid)) op[lane] = (uint8_t)(((q & 0x7Fu) + 0x21u) ^ (q & 0x80u));
-    return;
-  }
-  const bool neg = u.fl & kInfoNeg;
-  const uint32_t sh_p = (neg && !((u.st + u.en - 1) & 1)) ? c.sh_e : c.sh_f;
-  uint32_t pair = __builtin_amdgcn_ubfe(pr, sh_p, 8);
-  if (lane == u.st - o0) pair = 0xFFu;  // the read's first visited offset: context 0
-  // context slot and its packed-table offset ((x >> 2) * 4 cwp + (x & 3)): one u16 entry
-  const uint32_t xe = *(LdsHalfs)(uintptr_t)(a_lut + 2u * ((neg ? 256u : 0u) + pair));  // (no conflicts:
-  // pairs other than 0xFF and those of an N or other base lie in the first 64 entries)
-  const uint32_t at = __mul24(q, c.rowb) + c.kt;
-  const bool inrow = at < c.bound && u.rg == rg_p && (u.fl & kInfoApp);
-  const int cellrow = u.cell0 + u.dir * o0 - c_lo;
-  const uint32_t addr = at + (uint32_t)(4 * (cellrow + u.dir * lane)) + xe;
-  uint32_t ch = 0;
-  if (inrow && __builtin_amdgcn_inverse_ballot_w64(valid)) ch = *(LdsBytes)(uintptr_t)addr;
-  const bool fast = inrow && ch != 0u;
-  if (__builtin_amdgcn_ballot_w64(!fast && __builtin_amdgcn_inverse_ballot_w64(valid))) {
-    if (!fast && __builtin_amdgcn_inverse_ballot_w64(valid)) ch = apply_one(P, u, o0 + lane, q, pair_slot(pair, neg));
-  }
-  if ((u.fl & kInfoApp) && __builtin_amdgcn_inverse_ballot_w64(valid)) op[lane] = (uint8_t)ch;
-}
-
-// LDS: [the piece's packed char table qw * 6 * cwp dwords][context tables 2 * 256 u16]
-template <int R, bool kIdent>
-__global__ void __launch_bounds__(kBlockThreads) bqsr_apply_rows(ApplyParams P) {
-  constexpr int G = 8 / R;
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int qw = P.w.qw, cwp = P.cwp, L = P.g.L;
-  uint32_t* tab = (uint32_t*)smem;
-  uint16_t* lut = (uint16_t*)(tab + (int64_t)qw * 6 * cwp);
-  const uint32_t a_tab = (uint32_t)(uintptr_t)(LdsWords)tab;
-  const uint32_t a_lut = (uint32_t)(uintptr_t)(LdsWords)(uint32_t*)lut;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // packed-table offset (x >> 2) * 4 cwp + (x & 3) of the context slot x of
-  // a code pair (forward / reverse; 0xFF: a read's first offset, context 0)
-  for (int i = tid; i < kLutBytes; i += blockDim.x) {
-    const uint32_t x = pair_slot((uint32_t)i & 255u, i >= 256);
-    lut[i] = (uint16_t)((x >> 2) * 4u * (uint32_t)cwp + (x & 3u));
-  }
-  ApplyLane c;
-  c.rowb = 4u * 6u * (uint32_t)cwp;
-  c.kt = a_tab - (uint32_t)P.w.q_lo * c.rowb;
-  c.bound = a_tab + (uint32_t)qw * c.rowb;
-  c.sh_f = 4u * (uint32_t)((lane + 1) & 1);
-  c.sh_e = 4u * (uint32_t)(lane & 1);
-  c.vo_f = (uint32_t)((lane + 1) >> 1);
-  c.vo_re = 32u - (uint32_t)((lane + 1) >> 1);
-  c.vo_ro = 31u - (uint32_t)(lane >> 1);
-  const int G_blocks = gridDim.x;
-  const int64_t wa = wg_begin(P.rd, blockIdx.x, G_blocks), wb = wg_begin(P.rd, blockIdx.x + 1, G_blocks);
-  const int nk = order_keys(P.ord);
-  const int64_t tab_words = (int64_t)qw * 6 * cwp;
-  // pieces: read order -> class 0, class 1 over the workgroup's range; bucketed -> its keys
-  const int pi0 = kIdent ? 0 : (wa < wb ? key_at(P.ord, wa) : nk), pi1 = kIdent ? (wa < wb ? 2 : 0) : nk;
-  for (int pi = pi0; pi < pi1; ++pi) {
-    const int64_t p0 = kIdent ? wa : max(wa, key_begin(P.ord, P.rd.n_reads, pi));
-    const int64_t p1 = kIdent ? wb : min(wb, key_begin(P.ord, P.rd.n_reads, pi + 1));
-    if (p0 >= wb) break;
-    if (p0 >= p1) continue;
-    const ApplyRowsPiece pc = apply_rows_piece(P, pi);
-    __syncthreads();  // the previous piece is done with the table
-    {
-      const uint4* src = (const uint4*)(P.chars + (int64_t)pi * tab_words * 4);
-      uint4* dst = (uint4*)tab;
-      for (int64_t i = tid; i < tab_words / 4; i += blockDim.x) dst[i] = src[i];
-    }
-    __syncthreads();
-    for (int64_t pb = p0 + 64 * wave; pb < p1; pb += 64 * kWaves) {
-      const bool live = pb + lane < p1;
-      const LaneRead x = lane_read(P.rd, P.info, live ? order_read(P.ord, pb + lane) : 0, live, L);
-      const bool pass = x.fl & kInfoPass;
-      // read order: class pass 0 takes class-0 reads and every pass-through read
-      const bool mine = !kIdent || (pass ? pi == 0 : ((x.fl & kInfoSecond) ? 1 : 0) == pi);
-      if (live && mine) {
-        if (pass) {  // quality string passed through
-          P.out_start[x.r] = 0;
-          P.out_len[x.r] = (uint32_t)x.en;
-        } else {
-          P.out_start[x.r] = (uint32_t)x.st;
-          P.out_len[x.r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
-        }
-      }
-      const bool act = live && mine && (x.fl & (kInfoApp | kInfoAppCheck | kInfoPass)) && x.en > x.st;
-      const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
-      const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
-      const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
-      const uint32_t p_rg = (uint32_t)x.rg;
-      uint64_t todo = __builtin_amdgcn_ballot_w64(act), tail = 0;
-      while (todo) {
-        URead u[G];
-        bool has[G];
-        int jj[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          has[g] = todo != 0;
-          jj[g] = has[g] ? (int)__builtin_ctzll(todo) : 0;
-          todo &= todo - 1;
-          u[g] = uread(jj[g], p_r, p_slo, p_shi, p_se, p_fl, p_rg);
-        }
-        uint32_t q[G][R], pr[G][R];
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            q[g][i] = 0;
-            pr[g][i] = 0;
-            const int o0 = (u[g].st & ~63) + 64 * i;
-            if (has[g] && o0 < u[g].en) apply_row_load(P, u[g], o0, lane, c, q[g][i], pr[g][i]);
-          }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int i = 0; i < R; ++i) {
-            const int o0 = (u[g].st & ~63) + 64 * i;
-            if (has[g] && o0 < u[g].en) apply_row_proc(P, u[g], o0, lane, c, q[g][i], pr[g][i], pc.rg, pc.c_lo, a_lut);
-          }
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-          if (has[g] && (u[g].st & ~63) + 64 * R < u[g].en) tail |= 1ull << jj[g];
-      }
-      while (tail) {
-        const int j = (int)__builtin_ctzll(tail);
-        tail &= tail - 1;
-        const URead v = uread(j, p_r, p_slo, p_shi, p_se, p_fl, p_rg);
-        for (int o0 = (v.st & ~63) + 64 * R; o0 < v.en; o0 += 64) {
-          uint32_t q1 = 0, pr1 = 0;
-          apply_row_load(P, v, o0, lane, c, q1, pr1);
-          apply_row_proc(P, v, o0, lane, c, q1, pr1, pc.rg, pc.c_lo, a_lut);
-        }
-      }
-    }
-  }
-}
-template __global__ void bqsr_apply_rows<2, true>(ApplyParams);
-template __global__ void bqsr_apply_rows<4, true>(ApplyParams);
-template __global__ void bqsr_apply_rows<2, false>(ApplyParams);
-template __global__ void bqsr_apply_rows<4, false>(ApplyParams);
-
-template __global__ void bqsr_observe_kernel<false>(ObserveParams);
-template __global__ void bqsr_observe_kernel<true>(ObserveParams);
-template __global__ void bqsr_observe_chunks<false>(ObserveParams);
-template __global__ void bqsr_observe_chunks<true>(ObserveParams);
-template __global__ void bqsr_apply_kernel<false>(ApplyParams);
-template __global__ void bqsr_apply_kernel<true>(ApplyParams);
 
 // RecalTable.++ over partitions in a declared order (RecalTable.scala:90-108):
 // expectedMismatch = ((0.0 + e_0) + e_1) + ... -- one lane, each `+` one IEEE

@@ -346,6 +346,5 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
 }
 
 template __global__ void bqsr_observe_lean<true>(ObserveParams);
-template __global__ void bqsr_observe_lean<false>(ObserveParams);
 
 }  // namespace bqsr

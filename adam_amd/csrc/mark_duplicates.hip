@@ -25,7 +25,7 @@
 // Included by bqsr_capi.cpp after mark_duplicates.cpp (the host path, kept
 // for bqsr_mark_duplicates on host columns and as the collision fallback).
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 namespace mdupd {
 
@@ -337,8 +337,8 @@ bqsr_status mark_duplicates_device(bqsr_sam* s, int64_t* n_duplicates, std::vect
       (e = alloc(&d_rglib, rg_lib.size())) || (e = alloc(&bad, 1)) || (e = alloc(&ndup, 1)))
     return e;
   size_t tb = 0, tb2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, idx, idx2, (int)n, 0, 64, st));
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, head, incl, (int)n, st));
+  HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, key, key2, idx, idx2, (size_t)n, 0, 64, st));
+  HIP_TRY(rocprim::inclusive_scan(nullptr, tb2, head, incl, (size_t)n, rocprim::plus<uint32_t>(), st));
   void* temp = nullptr;
   if ((e = dalloc(tmp, (uint8_t**)&temp, std::max(tb, tb2)))) return e;
   tb = std::max(tb, tb2);
@@ -352,10 +352,10 @@ bqsr_status mark_duplicates_device(bqsr_sam* s, int64_t* n_duplicates, std::vect
   // 1. buckets: (rg, QNAME) keys sorted with the read index
   hipLaunchKernelGGL(mdup_keys, dim3(g), dim3(kThreads), 0, st, S, key, idx);
   size_t t1 = tb;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, t1, key, key2, idx, idx2, (int)n, 0, 64, st));
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t1, key, key2, idx, idx2, (size_t)n, 0, 64, st));
   hipLaunchKernelGGL(mdup_heads, dim3(g), dim3(kThreads), 0, st, (const uint64_t*)key2, n, head);
   size_t t2 = tb;
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(temp, t2, head, incl, (int)n, st));
+  HIP_TRY(rocprim::inclusive_scan(temp, t2, head, incl, (size_t)n, rocprim::plus<uint32_t>(), st));
   hipLaunchKernelGGL(mdup_head_pos, dim3(g), dim3(kThreads), 0, st, (const uint32_t*)head, (const uint32_t*)incl, n,
                      hpos);
   hipLaunchKernelGGL(mdup_verify, dim3(g), dim3(kThreads), 0, st, S, (const uint32_t*)idx2, (const uint32_t*)incl,
@@ -371,13 +371,13 @@ bqsr_status mark_duplicates_device(bqsr_sam* s, int64_t* n_duplicates, std::vect
   // 3. bucket order: first appearance, then right position, then (left, library) -- stable passes
   hipLaunchKernelGGL(mdup_first_keys, dim3(gb), dim3(kThreads), 0, st, (const uint32_t*)first, nb, ka, ord2);
   size_t t3 = tb;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, t3, ka, kb, ord2, ord, (int)nb, 0, 32, st));
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t3, ka, kb, ord2, ord, (size_t)nb, 0, 32, st));
   hipLaunchKernelGGL(mdup_gather, dim3(gb), dim3(kThreads), 0, st, (const uint64_t*)kr, (const uint32_t*)ord, nb, ka);
   t3 = tb;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, t3, ka, kb, ord, ord2, (int)nb, 0, 52, st));
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t3, ka, kb, ord, ord2, (size_t)nb, 0, 52, st));
   hipLaunchKernelGGL(mdup_gather, dim3(gb), dim3(kThreads), 0, st, (const uint64_t*)kll, (const uint32_t*)ord2, nb, ka);
   t3 = tb;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(temp, t3, ka, kb, ord2, ord, (int)nb, 0, 64, st));
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t3, ka, kb, ord2, ord, (size_t)nb, 0, 64, st));
   // 4. groups; 5. flags
   hipLaunchKernelGGL(mdup_groups, dim3(gb), dim3(kThreads), 0, st, (const uint32_t*)ord, (const uint64_t*)kll,
                      (const uint64_t*)kr, (const int32_t*)score, nb, outcome);

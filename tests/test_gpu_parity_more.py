@@ -265,30 +265,3 @@ def test_char_table_row_gap(read_order):
     keep = q <= 33 + 2  # leave the Q2 tails (trimming) as they are
     b.qual = np.where(keep, q, pick).astype(q.dtype)
     check([b.slice(0, 5000), b.slice(5000, 12000)])
-
-
-_ROWS_SCRIPT = r"""
-import sys, numpy as np
-sys.path.insert(0, %r); sys.path.insert(0, %r); sys.path.insert(0, %r)
-from _parity import check
-from adam_amd import synth
-b = synth.generate(9000, (101,), 1, seed=12)
-check([b.slice(0, 4000), b.slice(4000, 9000)], synth.known_sites(2_000_000, seed=3))
-b = synth.generate(6000, (150, 250), 8, seed=13)
-check([b])
-print("rows OK")
-"""
-
-
-def test_rows_kernels_parity_opt_in():
-    """The lane-per-offset kernels (ADAM_BQSR_OBSERVE=rows, ADAM_BQSR_APPLY=rows:
-    opt-in, SALU-bound on MI355X -- DESIGN.md) stay bit-exact against the oracle
-    (a subprocess: the forms are read once per process)."""
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    root = os.path.dirname(here)
-    env = dict(os.environ, ADAM_BQSR_OBSERVE="rows", ADAM_BQSR_APPLY="rows")
-    r = subprocess.run([sys.executable, "-c", _ROWS_SCRIPT % (root, here, os.path.join(root, "oracle"))], env=env,
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "rows OK" in r.stdout, r.stdout + r.stderr
