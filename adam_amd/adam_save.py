@@ -1,0 +1,305 @@
+"""adamSave from the device: ADAMRecord Parquet part files built from a SAM /
+BAM parse on the GPU.
+
+The reference's `transform` always ends in ``adamSave``
+(adam-cli/.../cli/Transform.scala:95-96 -> core/rdd/AdamRDDFunctions.scala:
+37-56): Avro-Parquet ADAMRecords (adam-format/.../avro/adam.avdl:4-68), one
+part file per RDD partition, GZIP-compressed by default, dictionary encoding
+on.  The records are SAMRecordConverter's (core/converters/
+SAMRecordConverter.scala:26-144).
+
+Here the record-level columns come from the device (``bqsr_sam_adam_prepare``
+/ ``bqsr_sam_adam_columns``, adam_amd/csrc/adam_out.hip): Arrow offsets,
+bytes, validity and flag bitmaps, copied to host memory and wrapped by
+pyarrow without a per-record step.  The columns that depend only on the read
+group or the @SQ entry are looked up by index from the header
+(:class:`HeaderInfo`).  Part files are written by a pool of host threads
+while the device builds the next one.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import shutil
+from concurrent.futures import ThreadPoolExecutor
+from datetime import datetime, timedelta, timezone
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _capi
+from ._capi import check
+
+# adam.avdl:4-68, in order: (name, arrow type name)
+ADAM_FIELDS: List[Tuple[str, str]] = [
+    ("referenceName", "string"), ("referenceId", "int32"), ("start", "int64"), ("mapq", "int32"),
+    ("readName", "string"), ("sequence", "string"), ("mateReference", "string"), ("mateAlignmentStart", "int64"),
+    ("cigar", "string"), ("qual", "string"), ("recordGroupName", "string"), ("recordGroupId", "int32"),
+    ("readPaired", "bool"), ("properPair", "bool"), ("readMapped", "bool"), ("mateMapped", "bool"),
+    ("readNegativeStrand", "bool"), ("mateNegativeStrand", "bool"), ("firstOfPair", "bool"),
+    ("secondOfPair", "bool"), ("primaryAlignment", "bool"), ("failedVendorQualityChecks", "bool"),
+    ("duplicateRead", "bool"), ("mismatchingPositions", "string"), ("attributes", "string"),
+    ("recordGroupSequencingCenter", "string"), ("recordGroupDescription", "string"),
+    ("recordGroupRunDateEpoch", "int64"), ("recordGroupFlowOrder", "string"), ("recordGroupKeySequence", "string"),
+    ("recordGroupLibrary", "string"), ("recordGroupPredictedMedianInsertSize", "int32"),
+    ("recordGroupPlatform", "string"), ("recordGroupPlatformUnit", "string"), ("recordGroupSample", "string"),
+    ("mateReferenceId", "int32"), ("referenceLength", "int64"), ("referenceUrl", "string"),
+    ("mateReferenceLength", "int64"), ("mateReferenceUrl", "string"),
+]
+STR_COLS = ("readName", "sequence", "cigar", "qual", "mismatchingPositions", "attributes")  # bqsr_adam_host order
+I32_COLS = ("referenceId", "mapq", "mateReferenceId", "recordGroupId")
+I64_COLS = ("start", "mateAlignmentStart")
+BOOL_COLS = ("readPaired", "properPair", "readMapped", "mateMapped", "readNegativeStrand", "mateNegativeStrand",
+             "firstOfPair", "secondOfPair", "primaryAlignment", "failedVendorQualityChecks", "duplicateRead")
+# the read group's header fields (SAMReadGroupRecord getters, SAMRecordConverter.scala:123-141)
+RG_TAGS = (("recordGroupSequencingCenter", "CN"), ("recordGroupDescription", "DS"), ("recordGroupFlowOrder", "FO"),
+           ("recordGroupKeySequence", "KS"), ("recordGroupLibrary", "LB"), ("recordGroupPlatform", "PL"),
+           ("recordGroupPlatformUnit", "PU"), ("recordGroupSample", "SM"))
+
+
+class AdamSizes(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_int64), ("str_bytes", ctypes.c_int64 * 6), ("bitmap_words", ctypes.c_int64)]
+
+
+class AdamHost(ctypes.Structure):
+    _fields_ = [("str_offsets", ctypes.c_void_p * 6), ("str_bytes", ctypes.c_void_p * 6),
+                ("str_valid", ctypes.c_void_p * 6), ("i32", ctypes.c_void_p * 4), ("i64", ctypes.c_void_p * 2),
+                ("int_valid", ctypes.c_void_p * 6), ("bools", ctypes.c_void_p * 11)]
+
+
+_bound = False
+
+
+def _lib():
+    global _bound
+    from . import sam as S
+    L = S._lib()
+    if not _bound:
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.bqsr_sam_adam_prepare.restype = ctypes.c_int
+        L.bqsr_sam_adam_prepare.argtypes = [vp, vp, i64, i64, vp, ctypes.POINTER(AdamSizes)]
+        L.bqsr_sam_adam_columns.restype = ctypes.c_int
+        L.bqsr_sam_adam_columns.argtypes = [vp, vp, ctypes.POINTER(AdamHost), vp]
+        L.bqsr_sam_header_text.restype = ctypes.c_int
+        L.bqsr_sam_header_text.argtypes = [vp, ctypes.c_char_p, i64, ctypes.POINTER(i64)]
+        _bound = True
+    return L
+
+
+def _iso8601_epoch_ms(v: str) -> Optional[int]:
+    """SAMReadGroupRecord.getRunDate (ISO 8601) -> epoch milliseconds; a
+    value without a zone is read as UTC (htsjdk takes the JVM's zone: parity
+    unpinned); None when it does not parse."""
+    m = re.fullmatch(r"(\d{4})-(\d{2})-(\d{2})(?:[T ](\d{2}):(\d{2})(?::(\d{2})(?:\.(\d{1,3})\d*)?)?"
+                     r"(Z|[+-]\d{2}:?\d{2})?)?", v.strip())
+    if not m:
+        return None
+    y, mo, d, hh, mi, ss, ms, tz = m.groups()
+    try:
+        dt = datetime(int(y), int(mo), int(d), int(hh or 0), int(mi or 0), int(ss or 0),
+                      int((ms or "0").ljust(3, "0")) * 1000, tzinfo=timezone.utc)
+    except ValueError:
+        return None
+    if tz and tz != "Z":
+        sign = 1 if tz[0] == "+" else -1
+        t = tz[1:].replace(":", "")
+        dt -= sign * timedelta(hours=int(t[:2]), minutes=int(t[2:]))
+    return int(dt.timestamp() * 1000)
+
+
+class HeaderInfo:
+    """The header's @RG and @SQ records, by the ids the device columns carry:
+    recordGroupId = the index in the sorted @RG IDs (RecordGroupDictionary.
+    scala:36-43, a repeated ID taking its last index), referenceId = the @SQ
+    line index (the first line of a name)."""
+
+    def __init__(self, text: str):
+        rg_lines: Dict[str, Dict[str, str]] = {}
+        rg_ids: List[str] = []
+        self.sq: List[Dict[str, str]] = []
+        for line in text.split("\n"):
+            line = line.rstrip("\r")
+            if not line.startswith("@"):
+                continue
+            f = line.split("\t")
+            kv = dict(t.split(":", 1) for t in f[1:] if ":" in t)
+            if f[0] == "@RG" and "ID" in kv:
+                rg_ids.append(kv["ID"])
+                rg_lines[kv["ID"]] = kv  # the last line of an ID
+            elif f[0] == "@SQ" and "SN" in kv:
+                self.sq.append(kv)
+        names = sorted(rg_ids)
+        self.rg: List[Optional[Dict[str, str]]] = [None] * len(names)
+        for i, nm in enumerate(names):
+            if i + 1 < len(names) and names[i + 1] == nm:
+                continue
+            self.rg[i] = dict(rg_lines[nm], ID=nm)
+
+    def rg_column(self, key: str, kind: str = "str"):
+        vals = []
+        for r in self.rg:
+            v = None if r is None else r.get(key)
+            if v is not None and kind == "int":
+                try:
+                    v = int(v)
+                except ValueError:
+                    v = None
+            elif v is not None and kind == "date":
+                v = _iso8601_epoch_ms(v)
+            vals.append(v)
+        return vals
+
+    def sq_column(self, key: str, kind: str = "str"):
+        out = []
+        for r in self.sq:
+            v = r.get(key)
+            if v is not None and kind == "int":
+                try:
+                    v = int(v)
+                except ValueError:
+                    v = None
+            out.append(v)
+        return out
+
+
+def header_info(sam) -> HeaderInfo:
+    L = _lib()
+    n = ctypes.c_int64()
+    check(L.bqsr_sam_header_text(sam.h, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(max(1, n.value))
+    check(L.bqsr_sam_header_text(sam.h, buf, n.value, ctypes.byref(n)))
+    return HeaderInfo(buf.raw[:n.value].decode("latin-1"))
+
+
+def schema():
+    import pyarrow as pa
+    t = {"string": pa.string(), "int32": pa.int32(), "int64": pa.int64(), "bool": pa.bool_()}
+    return pa.schema([pa.field(n, t[k], nullable=True) for n, k in ADAM_FIELDS])
+
+
+def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
+    """The ADAMRecord table of records [r0, r0 + n) of a parse (SamText), from
+    its current text (after ``rewrite``: recalibrated qual, MarkDuplicates'
+    flag)."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    L = _lib()
+    ctx = sam.ctx
+    sz = AdamSizes()
+    check(L.bqsr_sam_adam_prepare(ctx.handle, sam.h, r0, n, stream, ctypes.byref(sz)))
+    W = sz.bitmap_words
+    keep = []
+
+    def buf(count, dtype):
+        a = np.empty(max(1, count), dtype=dtype)
+        keep.append(a)
+        return a
+
+    soff = [buf(n + 1, np.int32) for _ in range(6)]
+    sbytes = [buf(sz.str_bytes[c], np.uint8) for c in range(6)]
+    svalid = [buf(W, np.uint64) for _ in range(6)]
+    i32 = [buf(n, np.int32) for _ in range(4)]
+    i64 = [buf(n, np.int64) for _ in range(2)]
+    ivalid = [buf(W, np.uint64) for _ in range(6)]
+    bools = [buf(W, np.uint64) for _ in range(11)]
+    H = AdamHost()
+    for c in range(6):
+        H.str_offsets[c] = soff[c].ctypes.data
+        H.str_bytes[c] = sbytes[c].ctypes.data if sz.str_bytes[c] else None
+        H.str_valid[c] = svalid[c].ctypes.data
+        H.int_valid[c] = ivalid[c].ctypes.data
+    for c in range(4):
+        H.i32[c] = i32[c].ctypes.data
+    for c in range(2):
+        H.i64[c] = i64[c].ctypes.data
+    for c in range(11):
+        H.bools[c] = bools[c].ctypes.data
+    check(L.bqsr_sam_adam_columns(ctx.handle, sam.h, ctypes.byref(H), stream))
+    pb = lambda a: pa.py_buffer(a)  # noqa: E731 (zero-copy views of the host buffers)
+    cols = {}
+    for c, name in enumerate(STR_COLS):
+        cols[name] = pa.StringArray.from_buffers(n, pb(soff[c]), pb(sbytes[c][:sz.str_bytes[c]]), pb(svalid[c]))
+    ints = {}
+    for c, name in enumerate(I32_COLS):
+        ints[name] = pa.Array.from_buffers(pa.int32(), n, [pb(ivalid[c]), pb(i32[c][:n])])
+    for c, name in enumerate(I64_COLS):
+        ints[name] = pa.Array.from_buffers(pa.int64(), n, [pb(ivalid[4 + c]), pb(i64[c][:n])])
+    cols.update(ints)
+    for c, name in enumerate(BOOL_COLS):
+        cols[name] = pa.Array.from_buffers(pa.bool_(), n, [None, pb(bools[c])])
+    # by index: the @SQ entry of referenceId / mateReferenceId, the @RG record of recordGroupId
+    ref, mref, rgi = ints["referenceId"], ints["mateReferenceId"], ints["recordGroupId"]
+
+    def take(values, idx, typ):
+        return pc.take(pa.array(values if values else [None], typ), idx)
+
+    sq_name = [r["SN"] for r in hdr.sq]
+    sq_len, sq_url = hdr.sq_column("LN", "int"), hdr.sq_column("UR")
+    cols["referenceName"] = take(sq_name, ref, pa.string())
+    cols["referenceLength"] = take(sq_len, ref, pa.int64())
+    cols["referenceUrl"] = take(sq_url, ref, pa.string())
+    cols["mateReference"] = take(sq_name, mref, pa.string())
+    cols["mateReferenceLength"] = take(sq_len, mref, pa.int64())
+    cols["mateReferenceUrl"] = take(sq_url, mref, pa.string())
+    cols["recordGroupName"] = take(hdr.rg_column("ID"), rgi, pa.string())
+    for name, key in RG_TAGS:
+        cols[name] = take(hdr.rg_column(key), rgi, pa.string())
+    cols["recordGroupRunDateEpoch"] = take(hdr.rg_column("DT", "date"), rgi, pa.int64())
+    cols["recordGroupPredictedMedianInsertSize"] = take(hdr.rg_column("PI", "int"), rgi, pa.int32())
+    t = pa.table([cols[name] for name, _ in ADAM_FIELDS], schema=schema())
+    t._adam_keep = keep  # (the host buffers back the arrays)
+    return t
+
+
+class AdamWriter:
+    """adamSave's output: a directory of part files, written by host threads
+    as the tables arrive (``OUT.partial`` renamed to ``OUT`` on ``close``)."""
+
+    def __init__(self, path: str, compression: str = "gzip", threads: Optional[int] = None):
+        self.path = path
+        self.tmp = path + ".partial"
+        if os.path.exists(self.tmp):
+            shutil.rmtree(self.tmp)
+        os.makedirs(self.tmp)
+        self.compression = None if compression in (None, "none") else compression
+        nth = threads or max(1, min(16, len(os.sched_getaffinity(0))))
+        self.pool = ThreadPoolExecutor(max_workers=nth)
+        self.futures = []
+        self.parts = 0
+        self.rows = 0
+
+    def _write(self, table, name):
+        import pyarrow.parquet as pq
+        pq.write_table(table, os.path.join(self.tmp, name), compression=self.compression, use_dictionary=True)
+
+    def add(self, table):
+        name = "part-r-%05d.parquet" % self.parts
+        self.parts += 1
+        self.rows += table.num_rows
+        self.futures.append(self.pool.submit(self._write, table, name))
+        if len(self.futures) > 64:  # bound the tables held in memory
+            self.futures.pop(0).result()
+
+    def emit(self, sam, part_reads: int = 1 << 20, stream=None):
+        """Every record of a parse, part_reads records per part file."""
+        hdr = header_info(sam)
+        n = sam.counts().n_reads
+        for r0 in range(0, max(n, 1), max(1, part_reads)):
+            self.add(adam_table(sam, r0, min(part_reads, n - r0) if n else 0, hdr, stream))
+
+    def close(self, ok: bool = True):
+        try:
+            for f in self.futures:
+                f.result()
+        finally:
+            self.pool.shutdown(wait=True)
+        if ok:
+            open(os.path.join(self.tmp, "_SUCCESS"), "wb").close()
+            if os.path.isdir(self.path):
+                shutil.rmtree(self.path)
+            elif os.path.exists(self.path):
+                os.remove(self.path)
+            os.replace(self.tmp, self.path)
+        else:
+            shutil.rmtree(self.tmp, ignore_errors=True)

@@ -24,223 +24,216 @@
 namespace bamk {
 
 struct BamParams {
-  const uint8_t* buf;       // the decompressed BAM
+  const uint8_t* buf;       // the decompressed BAM records
   const uint64_t* rec;      // [n + 1] record offsets (block_size field of record r at rec[r])
   int64_t n;
-  const int32_t* ref_sq;    // [n_ref] BAM refID -> @SQ header index (-1: not a header name)
+  const uint8_t* ref_blob;  // the binary reference list's names: ref_blob[ref_off[i], ref_off[i + 1])
+  const uint64_t* ref_off;
   int32_t n_ref;
-  samk::NameTable rg;
-  uint64_t* len;            // [4][n]: seq, qual, cigar ops, md bytes
-  uint64_t* off;            // [4][n + 1] exclusive scans of len
+  uint64_t* len;            // [n] SAM line bytes of record r, '\n' included (pass 1)
+  const uint64_t* off;      // [n + 1] their exclusive scan (pass 2)
+  uint8_t* out;             // the SAM text: the header at [0, hdr), record r's line at hdr + off[r]
+  int64_t hdr;
   unsigned long long* err;  // (record << 8) | code, the smallest wins
-  // columns (bqsr_sam)
-  uint32_t* flags;
-  int32_t* rg_id;
-  int32_t* ref;
-  int32_t* sq_id;
-  uint32_t* raw_flag;
-  int64_t* start;
-  uint64_t *seq_off, *qual_off, *cig_off, *md_off;
-  uint8_t *seq, *qual, *md;
-  uint32_t* cig;
-  uint64_t* line_span;      // the read name's bytes (MarkDuplicates' QNAME)
 };
 
-enum : uint32_t { kBamOk = 0, kBamRecord = 1, kBamTag = 2, kBamTagType = 3 };
+enum : uint32_t { kBamOk = 0, kBamRecord = 1, kBamTag = 2 };
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 __device__ __forceinline__ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
-// the text of an integer tag value (htsjdk's attribute value toString)
-__device__ __forceinline__ int int_text(int64_t v, uint8_t* out) {
-  uint8_t b[24];
-  int n = 0;
-  const bool neg = v < 0;
-  uint64_t u = neg ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
-  do {
-    b[n++] = (uint8_t)('0' + u % 10);
-    u /= 10;
-  } while (u);
-  int k = 0;
-  if (neg) out[k++] = '-';
-  while (n) out[k++] = b[--n];
-  return k;
-}
-
-struct TagVal {
-  int64_t a = -1, n = 0;  // Z: bytes [a, a + n) of the record
-  int kind = 0;           // 0 none, 1 Z / A (bytes), 2 integer (value)
-  int64_t v = 0;
+// writes (or, out == nullptr, counts) bytes at out[n]
+struct Put {
+  uint8_t* out;
+  int64_t n;
+  __device__ __forceinline__ void c(uint8_t v) {
+    if (out) out[n] = v;
+    ++n;
+  }
+  __device__ __forceinline__ void bytes(const uint8_t* p, int64_t k) {
+    if (out)
+      for (int64_t i = 0; i < k; ++i) out[n + i] = p[i];
+    n += k;
+  }
+  __device__ void integer(int64_t v) {  // decimal text (Java's Integer / Long toString)
+    uint8_t b[24];
+    int m = 0;
+    const bool neg = v < 0;
+    uint64_t u = neg ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+    do {
+      b[m++] = (uint8_t)('0' + u % 10);
+      u /= 10;
+    } while (u);
+    if (neg) c('-');
+    while (m) c(b[--m]);
+  }
+  __device__ void real(float f) { n += samk::java_float_text(f, out ? out + n : nullptr); }
 };
 
-// one record: lengths (kWrite false) or the columns of read r
+// One BAM record as its SAM text line (htsjdk's SAMRecord of the record, as
+// the SAM text of the same record would parse; the SAM spec's field order):
+// QNAME FLAG RNAME POS MAPQ CIGAR RNEXT PNEXT TLEN SEQ QUAL, then every tag
+// TG:TYPE:VALUE in record order -- integer types (c C s S i I) as "i", floats
+// by Java's Float.toString, B arrays as "B:t,v,...".  The line then goes
+// through the SAM record parser, so BAM and SAM input share one parse, the
+// QUAL rewrite and the ADAM columns.
 template <bool kWrite>
-__device__ void bam_record(const BamParams& P, int64_t r) {
+__device__ void bam_line(const BamParams& P, int64_t r) {
   const uint8_t* b = P.buf + P.rec[r];
   const int64_t bs = (int64_t)rd32(b);
   const int64_t end = 4 + bs;
-  if (bs < 32) {
-    if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamRecord);
-    return;
-  }
   const int32_t refid = (int32_t)rd32(b + 4);
   const int32_t pos = (int32_t)rd32(b + 8);
   const int l_name = b[12];
+  const int mapq = b[13];
   const int n_cig = rd16(b + 16);
   const uint32_t flag = rd16(b + 18);
   const int64_t l_seq = (int64_t)(int32_t)rd32(b + 20);
+  const int32_t next_ref = (int32_t)rd32(b + 24);
+  const int32_t next_pos = (int32_t)rd32(b + 28);
+  const int32_t tlen = (int32_t)rd32(b + 32);
   const int64_t o_name = 36, o_cig = o_name + l_name, o_seq = o_cig + 4 * (int64_t)n_cig;
   const int64_t o_qual = o_seq + (l_seq + 1) / 2, o_tag = o_qual + l_seq;
-  if (l_seq < 0 || o_tag > end || l_name < 1) {
-    if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamRecord);
+  if (!kWrite && (bs < 32 || l_seq < 0 || o_tag > end || l_name < 1)) {
+    atomicMin(P.err, ((unsigned long long)r << 8) | kBamRecord);
+    P.len[r] = 0;
     return;
   }
-  // tags: the last MD and RG win
-  TagVal md, rg;
+  Put o{kWrite ? P.out + P.hdr + P.off[r] : nullptr, 0};
+  auto ref_name = [&](int32_t id) {
+    if (id >= 0 && id < P.n_ref) o.bytes(P.ref_blob + P.ref_off[id], (int64_t)(P.ref_off[id + 1] - P.ref_off[id]));
+    else o.c('*');
+  };
+  o.bytes(b + o_name, l_name - 1);
+  o.c('\t');
+  o.integer(flag);
+  o.c('\t');
+  ref_name(refid);
+  o.c('\t');
+  o.integer((int64_t)pos + 1);
+  o.c('\t');
+  o.integer(mapq);
+  o.c('\t');
+  if (n_cig == 0) {
+    o.c('*');
+  } else {
+    const char kOps[] = "MIDNSHP=X";
+    for (int k = 0; k < n_cig; ++k) {
+      const uint32_t e = rd32(b + o_cig + 4 * k);
+      o.integer(e >> 4);
+      o.c((e & 15u) < 9u ? (uint8_t)kOps[e & 15u] : (uint8_t)'?');
+    }
+  }
+  o.c('\t');
+  if (next_ref >= 0 && next_ref == refid) o.c('=');
+  else ref_name(next_ref);
+  o.c('\t');
+  o.integer((int64_t)next_pos + 1);
+  o.c('\t');
+  o.integer(tlen);
+  o.c('\t');
+  if (l_seq == 0) {
+    o.c('*');
+  } else {
+    const char kCodes[] = "=ACMGRSVTWYHKDBN";
+    for (int64_t k = 0; k < l_seq; ++k) o.c((uint8_t)kCodes[(b[o_seq + (k >> 1)] >> ((k & 1) ? 0 : 4)) & 15]);
+  }
+  o.c('\t');
+  if (l_seq == 0 || b[o_qual] == 0xFF) {
+    o.c('*');
+  } else {
+    for (int64_t k = 0; k < l_seq; ++k) o.c((uint8_t)(b[o_qual + k] + 33));
+  }
   for (int64_t p = o_tag; p < end;) {
     if (p + 3 > end) {
       if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamTag);
-      return;
+      break;
     }
-    const uint8_t t0 = b[p], t1 = b[p + 1], ty = b[p + 2];
-    p += 3;
-    TagVal v;
-    int64_t sz = 0;
+    const uint8_t ty = b[p + 2];
+    const int64_t v = p + 3;
+    int64_t sz;
     switch (ty) {
-      case 'A': v.kind = 1; v.a = p; v.n = 1; sz = 1; break;
-      case 'c': v.kind = 2; v.v = (int8_t)b[p]; sz = 1; break;
-      case 'C': v.kind = 2; v.v = b[p]; sz = 1; break;
-      case 's': v.kind = 2; v.v = (int16_t)rd16(b + p); sz = 2; break;
-      case 'S': v.kind = 2; v.v = rd16(b + p); sz = 2; break;
-      case 'i': v.kind = 2; v.v = (int32_t)rd32(b + p); sz = 4; break;
-      case 'I': v.kind = 2; v.v = rd32(b + p); sz = 4; break;
-      case 'f': sz = 4; v.kind = -1; break;  // float: its text is Java's Float.toString (not decoded)
-      case 'Z':
-      case 'H': {
-        int64_t q = p;
+      case 'A': case 'c': case 'C': sz = 1; break;
+      case 's': case 'S': sz = 2; break;
+      case 'i': case 'I': case 'f': sz = 4; break;
+      case 'Z': case 'H': {
+        int64_t q = v;
         while (q < end && b[q]) ++q;
-        if (q >= end) {
-          if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamTag);
-          return;
-        }
-        v.kind = ty == 'Z' ? 1 : -1;
-        v.a = p;
-        v.n = q - p;
-        sz = q - p + 1;
+        sz = q - v + 1;
         break;
       }
       case 'B': {
-        if (p + 5 > end) {
-          if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamTag);
-          return;
-        }
-        const uint8_t st = b[p];
-        const int64_t cnt = rd32(b + p + 1);
-        const int es = (st == 'c' || st == 'C') ? 1 : (st == 's' || st == 'S') ? 2 : 4;
-        sz = 5 + cnt * es;
-        v.kind = -1;
+        const uint8_t st = v + 5 <= end ? b[v] : 0;
+        const int es = (st == 'c' || st == 'C') ? 1 : (st == 's' || st == 'S') ? 2 : (st == 'i' || st == 'I' || st == 'f') ? 4 : 0;
+        sz = es && v + 5 <= end ? 5 + (int64_t)rd32(b + v + 1) * es : end;  // (unknown subtype: overruns below)
         break;
       }
-      default:
-        if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamTag);
-        return;
+      default: sz = end; break;
     }
-    if (p + sz > end) {
+    if (v + sz > end) {
       if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamTag);
-      return;
+      break;
     }
-    if (t0 == 'M' && t1 == 'D') md = v;
-    if (t0 == 'R' && t1 == 'G') rg = v;
-    p += sz;
-  }
-  if (md.kind < 0 || rg.kind < 0) {  // an MD / RG value whose text is not decoded here
-    if (!kWrite) atomicMin(P.err, ((unsigned long long)r << 8) | kBamTagType);
-    return;
-  }
-  uint8_t ibuf[24];
-  int64_t md_n = md.kind == 1 ? md.n : md.kind == 2 ? int_text(md.v, ibuf) : 0;
-  const int64_t seq_n = l_seq ? l_seq : 1;  // "*"
-  const bool no_qual = l_seq == 0 || b[o_qual] == 0xFF;
-  const int64_t qual_n = no_qual ? 1 : l_seq;
-  if (!kWrite) {
-    P.len[r] = (uint64_t)seq_n;
-    P.len[P.n + r] = (uint64_t)qual_n;
-    P.len[2 * P.n + r] = (uint64_t)n_cig;
-    P.len[3 * P.n + r] = (uint64_t)md_n;
-    return;
-  }
-  const int32_t sq = (refid >= 0 && refid < P.n_ref) ? P.ref_sq[refid] : -1;
-  int32_t rgv = -1;
-  if (rg.kind == 1) {
-    rgv = samk::name_lookup(P.rg, b + rg.a, rg.n);
-  } else if (rg.kind == 2) {
-    const int k = int_text(rg.v, ibuf);
-    rgv = samk::name_lookup(P.rg, ibuf, k);
-  }
-  uint32_t f = BQSR_F_HAS_SEQ | BQSR_F_HAS_QUAL | BQSR_F_HAS_CIGAR;
-  if (flag != 0) {  // SAMRecordConverter.scala:72-108: flags only when the word is non-zero (Q2)
-    if (flag & 0x1) {
-      f |= BQSR_F_PAIRED;
-      if (flag & 0x80) f |= BQSR_F_SECOND_OF_PAIR;
+    o.c('\t');
+    o.c(b[p]);
+    o.c(b[p + 1]);
+    o.c(':');
+    switch (ty) {
+      case 'A': o.c('A'); o.c(':'); o.c(b[v]); break;
+      case 'c': o.c('i'); o.c(':'); o.integer((int8_t)b[v]); break;
+      case 'C': o.c('i'); o.c(':'); o.integer(b[v]); break;
+      case 's': o.c('i'); o.c(':'); o.integer((int16_t)rd16(b + v)); break;
+      case 'S': o.c('i'); o.c(':'); o.integer(rd16(b + v)); break;
+      case 'i': o.c('i'); o.c(':'); o.integer((int32_t)rd32(b + v)); break;
+      case 'I': o.c('i'); o.c(':'); o.integer(rd32(b + v)); break;
+      case 'f': {
+        const uint32_t w = rd32(b + v);
+        float fv;
+        __builtin_memcpy(&fv, &w, 4);
+        o.c('f'); o.c(':'); o.real(fv);
+        break;
+      }
+      case 'Z': case 'H': o.c(ty); o.c(':'); o.bytes(b + v, sz - 1); break;
+      case 'B': {
+        const uint8_t st = b[v];
+        const int64_t cnt = rd32(b + v + 1);
+        o.c('B'); o.c(':'); o.c(st);
+        for (int64_t k = 0; k < cnt; ++k) {
+          const uint8_t* e = b + v + 5;
+          o.c(',');
+          switch (st) {
+            case 'c': o.integer((int8_t)e[k]); break;
+            case 'C': o.integer(e[k]); break;
+            case 's': o.integer((int16_t)rd16(e + 2 * k)); break;
+            case 'S': o.integer(rd16(e + 2 * k)); break;
+            case 'i': o.integer((int32_t)rd32(e + 4 * k)); break;
+            case 'I': o.integer(rd32(e + 4 * k)); break;
+            default: {
+              const uint32_t w = rd32(e + 4 * k);
+              float fv;
+              __builtin_memcpy(&fv, &w, 4);
+              o.real(fv);
+            }
+          }
+        }
+        break;
+      }
     }
-    if (flag & 0x400) f |= BQSR_F_DUPLICATE;
-    if (flag & 0x10) f |= BQSR_F_NEG_STRAND;
-    if (!(flag & 0x100)) f |= BQSR_F_PRIMARY;
-    if (!(flag & 0x4)) f |= BQSR_F_MAPPED;
+    p = v + sz;
   }
-  const bool has_start = sq >= 0 && pos != -1;  // SAM POS = pos + 1: a start when POS != 0
-  if (sq >= 0) f |= BQSR_F_HAS_REFNAME;
-  if (has_start) f |= BQSR_F_HAS_START;
-  if (md.kind > 0) f |= BQSR_F_HAS_MD;
-  if (rgv >= 0) f |= BQSR_F_HAS_RG;
-  const uint64_t os = P.off[r], oq = P.off[(P.n + 1) + r], oc = P.off[2 * (P.n + 1) + r],
-                 om = P.off[3 * (P.n + 1) + r];
-  P.flags[r] = f;
-  P.rg_id[r] = rgv >= 0 ? rgv : 0;
-  P.ref[r] = sq;
-  P.sq_id[r] = sq;
-  P.raw_flag[r] = flag;
-  P.start[r] = has_start ? (int64_t)pos : 0;
-  P.seq_off[r] = os;
-  P.qual_off[r] = oq;
-  P.cig_off[r] = oc;
-  P.md_off[r] = om;
-  for (int k = 0; k < n_cig; ++k) P.cig[oc + k] = rd32(b + o_cig + 4 * k);
-  const char kCodes[] = "=ACMGRSVTWYHKDBN";
-  if (l_seq == 0) {
-    P.seq[os] = '*';
-  } else {
-    for (int64_t k = 0; k < l_seq; ++k) P.seq[os + k] = (uint8_t)kCodes[(b[o_seq + (k >> 1)] >> ((k & 1) ? 0 : 4)) & 15];
-  }
-  if (no_qual) {
-    P.qual[oq] = '*';
-  } else {
-    for (int64_t k = 0; k < l_seq; ++k) P.qual[oq + k] = (uint8_t)(b[o_qual + k] + 33);
-  }
-  if (md.kind == 1)
-    for (int64_t k = 0; k < md_n; ++k) P.md[om + k] = b[md.a + k];
-  else if (md.kind == 2)
-    for (int64_t k = 0; k < md_n; ++k) P.md[om + k] = ibuf[k];
-  P.line_span[2 * r] = P.rec[r] + o_name;
-  P.line_span[2 * r + 1] = P.rec[r] + o_name + l_name - 1;  // the name without its NUL
+  o.c('\n');
+  if (!kWrite) P.len[r] = (uint64_t)o.n;
 }
 
-extern "C" __global__ void bam_records_len(BamParams P) {
+extern "C" __global__ void bam_lines_len(BamParams P) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.n; r += (int64_t)gridDim.x * blockDim.x)
-    bam_record<false>(P, r);
+    bam_line<false>(P, r);
 }
-extern "C" __global__ void bam_records_write(BamParams P) {
+extern "C" __global__ void bam_lines_write(BamParams P) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.n; r += (int64_t)gridDim.x * blockDim.x)
-    bam_record<true>(P, r);
-}
-extern "C" __global__ void bam_offsets_close(BamParams P) {
-  const int64_t n1 = P.n + 1;
-  P.seq_off[P.n] = P.off[P.n];
-  P.qual_off[P.n] = P.off[n1 + P.n];
-  P.cig_off[P.n] = P.off[2 * n1 + P.n];
-  P.md_off[P.n] = P.off[3 * n1 + P.n];
+    bam_line<true>(P, r);
 }
 
 }  // namespace bamk
@@ -337,16 +330,16 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   int64_t p = 8 + l_text;
   const int64_t n_ref = (int32_t)le32(u + p);
   p += 4;
-  std::map<std::string, int32_t> sq_index;
-  for (size_t i = 0; i < H.sq_names.size(); ++i) sq_index.emplace(H.sq_names[i], (int32_t)i);
-  std::vector<int32_t> ref_sq;
+  // the binary reference list's names: a record's RNAME / RNEXT text
+  // (referenceName then only for a header @SQ name, as for SAM text)
+  std::vector<uint8_t> ref_blob;
+  std::vector<uint64_t> ref_off(1, 0);
   for (int64_t i = 0; i < n_ref; ++i) {
     if (p + 4 > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated reference list");
     const int64_t l_name = (int32_t)le32(u + p);
     if (l_name < 1 || p + 4 + l_name + 4 > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: bad reference name");
-    const std::string name((const char*)u + p + 4, (size_t)(l_name - 1));
-    auto it = sq_index.find(name);  // referenceName only for a header @SQ name (records.read_sam)
-    ref_sq.push_back(it == sq_index.end() ? -1 : it->second);
+    ref_blob.insert(ref_blob.end(), u + p + 4, u + p + 4 + (l_name - 1));
+    ref_off.push_back(ref_blob.size());
     p += 4 + l_name + 4;
   }
   // records: offsets by their block_size fields
@@ -361,22 +354,10 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   }
   const int64_t nr = (int64_t)rec.size();
   rec.push_back((uint64_t)(m - body));
-
-  std::unique_ptr<bqsr_sam> S_(new bqsr_sam);
-  bqsr_sam* o = S_.get();
-  o->ctx = ctx;
-  o->from_bam = true;
-  o->n_rg = (int32_t)H.rgh.value.size();
-  o->rg_library.assign(H.rg_names.size(), std::string());
-  o->rg_has_lb.assign(H.rg_names.size(), 0);
-  for (size_t i = 0; i < H.rg_names.size(); ++i) {
-    const auto& v = H.rg_lb[H.rg_names[i]];
-    o->rg_has_lb[i] = v.first ? 1 : 0;
-    o->rg_library[i] = v.second;
-  }
-  o->header = 0;
-  o->n_text = m - body;
-  HIP_TRY(hipMalloc(&o->d_text, (size_t)o->n_text + 64));
+  // the header text, newline-terminated, then the records' SAM lines
+  std::string hdr((const char*)u + 8, (size_t)lt);
+  if (!hdr.empty() && hdr.back() != '\n') hdr.push_back('\n');
+  H.body = (int64_t)hdr.size();
   std::vector<void*> tmp;
   struct Free {
     std::vector<void*>& v;
@@ -384,112 +365,56 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
       for (void* q : v) (void)hipFree(q);
     }
   } free_tmp{tmp};
-  if (o->n_text > 0) HIP_TRY(hipMemcpyAsync(o->d_text, u + body, (size_t)o->n_text, hipMemcpyHostToDevice, s));
   bamk::BamParams P{};
-  P.buf = o->d_text;
+  uint8_t* d_rec;
+  if ((st = sam_alloc(tmp, &d_rec, (size_t)(m - body) + 64)) != BQSR_OK) return st;
+  if (m > body) HIP_TRY(hipMemcpyAsync(d_rec, u + body, (size_t)(m - body), hipMemcpyHostToDevice, s));
+  P.buf = d_rec;
   P.n = nr;
-  P.n_ref = (int32_t)ref_sq.size();
+  P.n_ref = (int32_t)n_ref;
+  P.hdr = H.body;
   if ((st = sam_upload(tmp, (uint64_t**)&P.rec, rec, s)) != BQSR_OK) return st;
-  if ((st = sam_upload(tmp, (int32_t**)&P.ref_sq, ref_sq.empty() ? std::vector<int32_t>{-1} : ref_sq, s)) != BQSR_OK)
+  if ((st = sam_upload(tmp, (uint8_t**)&P.ref_blob, ref_blob.empty() ? std::vector<uint8_t>{0} : ref_blob, s)) != BQSR_OK)
     return st;
-  if ((st = sam_names_upload(o->allocs, H.rgh, &P.rg, s)) != BQSR_OK) return st;
+  if ((st = sam_upload(tmp, (uint64_t**)&P.ref_off, ref_off, s)) != BQSR_OK) return st;
   if ((st = sam_alloc(tmp, &P.err, 1)) != BQSR_OK) return st;
   HIP_TRY(hipMemsetAsync(P.err, 0xFF, 8, s));
-  if ((st = sam_alloc(tmp, &P.len, (size_t)(4 * nr))) != BQSR_OK) return st;
-  if ((st = sam_alloc(tmp, &P.off, (size_t)(4 * (nr + 1)))) != BQSR_OK) return st;
+  uint64_t *len, *off, *part;
+  if ((st = sam_alloc(tmp, &len, (size_t)nr)) != BQSR_OK || (st = sam_alloc(tmp, &off, (size_t)nr + 1)) != BQSR_OK ||
+      (st = sam_alloc(tmp, &part, (size_t)(nr / samk::kScanChunk + 2))) != BQSR_OK)
+    return st;
+  P.len = len;
+  P.off = off;
   const unsigned g = sam_grid(nr, 256, ctx->n_cu * 16);
-  if (nr > 0) hipLaunchKernelGGL(bamk::bam_records_len, dim3(g), dim3(256), 0, s, P);
+  if (nr > 0) hipLaunchKernelGGL(bamk::bam_lines_len, dim3(g), dim3(256), 0, s, P);
   HIP_TRY(hipGetLastError());
+  if ((st = sam_scan(len, nr, off, part, s)) != BQSR_OK) return st;
   unsigned long long e_word = ~0ull;
+  uint64_t body_bytes = 0;
   HIP_TRY(hipMemcpyAsync(&e_word, P.err, 8, hipMemcpyDeviceToHost, s));
+  if (nr > 0) HIP_TRY(hipMemcpyAsync(&body_bytes, off + nr, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (e_word != ~0ull) {
     const uint32_t code = (uint32_t)(e_word & 0xFF);
     char buf[160];
     snprintf(buf, sizeof buf, "BAM record %lld: %s", (long long)(e_word >> 8),
-             code == bamk::kBamTagType ? "MD / RG tag of a type whose text is not decoded (f, H, B)"
-             : code == bamk::kBamTag   ? "malformed optional field"
-                                       : "malformed record");
-    return fail(code == bamk::kBamTagType ? BQSR_ERR_UNSUPPORTED : BQSR_ERR_SAM_PARSE, buf);
+             code == bamk::kBamTag ? "malformed optional field" : "malformed record");
+    return fail(BQSR_ERR_SAM_PARSE, buf);
   }
-  uint64_t* part;
-  if ((st = sam_alloc(tmp, &part, (size_t)(nr / samk::kScanChunk + 2))) != BQSR_OK) return st;
-  for (int c = 0; c < 4; ++c)
-    if ((st = sam_scan(P.len + (size_t)c * nr, nr, P.off + (size_t)c * (nr + 1), part, s)) != BQSR_OK) return st;
-  uint64_t tot[4] = {0, 0, 0, 0};
-  for (int c = 0; c < 4 && nr > 0; ++c)
-    HIP_TRY(hipMemcpyAsync(&tot[c], P.off + (size_t)c * (nr + 1) + nr, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  o->n_reads = nr;
-  o->seq_bytes = (int64_t)tot[0];
-  o->qual_bytes = (int64_t)tot[1];
-  o->cig_ops = (int64_t)tot[2];
-  o->md_bytes = (int64_t)tot[3];
-  const size_t n1 = (size_t)nr;
-  if ((st = sam_alloc(o->allocs, &o->flags, n1)) != BQSR_OK || (st = sam_alloc(o->allocs, &o->rg_id, n1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->ref, n1)) != BQSR_OK || (st = sam_alloc(o->allocs, &o->start, n1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->sq_id, n1)) != BQSR_OK || (st = sam_alloc(o->allocs, &o->raw_flag, n1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->seq_off, n1 + 1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->seq, (size_t)o->seq_bytes)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->qual_off, n1 + 1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->qual, (size_t)o->qual_bytes)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->cig_off, n1 + 1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->cig, (size_t)o->cig_ops)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->md_off, n1 + 1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->md, (size_t)o->md_bytes)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->line_span, 2 * n1)) != BQSR_OK ||
-      (st = sam_alloc(o->allocs, &o->qual_span, 2 * n1)) != BQSR_OK)
-    return st;
-  P.flags = o->flags;
-  P.rg_id = o->rg_id;
-  P.ref = o->ref;
-  P.sq_id = o->sq_id;
-  P.raw_flag = o->raw_flag;
-  P.start = o->start;
-  P.seq_off = o->seq_off;
-  P.seq = o->seq;
-  P.qual_off = o->qual_off;
-  P.qual = o->qual;
-  P.cig_off = o->cig_off;
-  P.cig = o->cig;
-  P.md_off = o->md_off;
-  P.md = o->md;
-  P.line_span = o->line_span;
-  if (nr > 0) {
-    hipLaunchKernelGGL(bamk::bam_records_write, dim3(g), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(bamk::bam_offsets_close, dim3(1), dim3(1), 0, s, P);
-  } else {
-    HIP_TRY(hipMemsetAsync(o->seq_off, 0, 8, s));
-    HIP_TRY(hipMemsetAsync(o->qual_off, 0, 8, s));
-    HIP_TRY(hipMemsetAsync(o->cig_off, 0, 8, s));
-    HIP_TRY(hipMemsetAsync(o->md_off, 0, 8, s));
+  const int64_t n_text = H.body + (int64_t)body_bytes;
+  uint8_t* d_text = nullptr;
+  HIP_TRY(hipMalloc(&d_text, (size_t)n_text + 64));
+  hipError_t e = hipMemsetAsync(d_text + n_text, 0, 64, s);
+  if (e == hipSuccess && H.body > 0) e = hipMemcpyAsync(d_text, hdr.data(), hdr.size(), hipMemcpyHostToDevice, s);
+  P.out = d_text;
+  if (e == hipSuccess && nr > 0) {
+    hipLaunchKernelGGL(bamk::bam_lines_write, dim3(g), dim3(256), 0, s, P);
+    e = hipGetLastError();
   }
-  HIP_TRY(hipGetLastError());
-  // referenceName ids: first appearance order (as bqsr_sam_parse)
-  const size_t nsq = H.sq_names.size();
-  if (nsq > 0 && nr > 0) {
-    unsigned long long* first;
-    int32_t* rank_d;
-    if ((st = sam_alloc(tmp, &first, nsq)) != BQSR_OK) return st;
-    HIP_TRY(hipMemsetAsync(first, 0xFF, nsq * 8, s));
-    hipLaunchKernelGGL(samk::sam_ref_first, dim3(g), dim3(256), 0, s, (const int32_t*)o->ref, nr, first);
-    std::vector<unsigned long long> fh(nsq);
-    HIP_TRY(hipMemcpyAsync(fh.data(), first, nsq * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    std::vector<int32_t> order;
-    for (size_t i = 0; i < nsq; ++i)
-      if (fh[i] != ~0ull) order.push_back((int32_t)i);
-    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return fh[a] < fh[b]; });
-    std::vector<int32_t> rank(nsq, -1);
-    for (size_t k = 0; k < order.size(); ++k) {
-      rank[order[k]] = (int32_t)k;
-      o->ref_names.push_back(H.sq_names[order[k]]);
-    }
-    if ((st = sam_upload(tmp, &rank_d, rank, s)) != BQSR_OK) return st;
-    hipLaunchKernelGGL(samk::sam_ref_remap, dim3(g), dim3(256), 0, s, o->ref, nr, (const int32_t*)rank_d);
-    HIP_TRY(hipGetLastError());
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // (the header copy reads `hdr`)
+  if (e != hipSuccess) {
+    (void)hipFree(d_text);
+    return fail(BQSR_ERR_DEVICE, std::string("bqsr_bam_parse: ") + hipGetErrorString(e));
   }
-  HIP_TRY(hipStreamSynchronize(s));
-  *out = S_.release();
-  return ok();
+  return sam_parse_device(ctx, H, hdr.data(), d_text, n_text, s, true, out);  // (owns d_text from here)
 }

@@ -1879,3 +1879,4 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
 #include "sam_ingest.hip"
 #include "bam_ingest.hip"
 #include "mark_duplicates.cpp"
+#include "adam_out.hip"

@@ -256,6 +256,179 @@ extern "C" __global__ void __launch_bounds__(kScanThreads) scan_apply(const uint
   if (blockIdx.x == gridDim.x - 1 && tid == 0) out[n] = part[gridDim.x];
 }
 
+// ---- Java float text (tag values of type 'f') ----
+// java.lang.Float.toString: the fewest significant digits (at most 9) that
+// read back as the same float; plain notation for 1e-3 <= |f| < 1e7
+// ("100.0", "0.00125"), else "d.dddE[-]n" ("1.0E7", "1.5E-4"); "NaN",
+// "Infinity", "0.0" / "-0.0".  Powers of ten and the read-back are double
+// arithmetic: exact for the float's digits except at decimal ties (parity
+// unpinned).  out == nullptr: the length only.
+__device__ double pow10_d(int k) {
+  const double kP[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                         1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  double v = 1.0;
+  int a = k < 0 ? -k : k;
+  while (a > 22) {
+    v *= 1e22;
+    a -= 22;
+  }
+  v *= kP[a];
+  return k < 0 ? 1.0 / v : v;
+}
+__device__ int put_text(uint8_t* out, int n, const char* t) {
+  int k = 0;
+  for (; t[k]; ++k)
+    if (out) out[n + k] = (uint8_t)t[k];
+  return n + k;
+}
+__device__ int java_float_text(float f, uint8_t* out) {
+  int n = 0;
+  if (f != f) return put_text(out, 0, "NaN");
+  if (__builtin_signbit(f)) n = put_text(out, n, "-");
+  const double x = fabs((double)f);
+  if (isinf(x)) return put_text(out, n, "Infinity");
+  if (x == 0.0) return put_text(out, n, "0.0");
+  int k = (int)floor(log10(x));
+  while (k > -60 && pow10_d(k) > x) --k;
+  while (k < 60 && pow10_d(k + 1) <= x) ++k;
+  uint32_t dig = 0;
+  int e = k, p = 1;
+  for (; p <= 9; ++p) {
+    const int sh = p - 1 - k;
+    const double y = sh >= 0 ? x * pow10_d(sh) : x / pow10_d(-sh);
+    const double d = rint(y);
+    const double v = sh >= 0 ? d / pow10_d(sh) : d * pow10_d(-sh);
+    if ((float)v == fabsf(f) || p == 9) {
+      dig = (uint32_t)d;
+      e = k;
+      if (d >= pow10_d(p)) {  // rounded up to 10^p: one more decade
+        dig /= 10u;
+        e = k + 1;
+      }
+      break;
+    }
+  }
+  uint8_t D[10];
+  int nd = 0;
+  {
+    uint8_t t[10];
+    int m = 0;
+    do {
+      t[m++] = (uint8_t)('0' + dig % 10u);
+      dig /= 10u;
+    } while (dig);
+    for (int i = 0; i < m; ++i) D[i] = t[m - 1 - i];
+    nd = m;
+    while (nd > 1 && D[nd - 1] == '0') --nd;  // digits without trailing zeros
+  }
+  auto put = [&](uint8_t c) {
+    if (out) out[n] = c;
+    ++n;
+  };
+  if (e >= -3 && e < 7) {
+    if (e >= 0) {
+      for (int i = 0; i <= e; ++i) put(i < nd ? D[i] : (uint8_t)'0');
+      put('.');
+      if (nd > e + 1)
+        for (int i = e + 1; i < nd; ++i) put(D[i]);
+      else
+        put('0');
+    } else {
+      put('0');
+      put('.');
+      for (int i = 0; i < -e - 1; ++i) put('0');
+      for (int i = 0; i < nd; ++i) put(D[i]);
+    }
+  } else {
+    put(D[0]);
+    put('.');
+    if (nd > 1)
+      for (int i = 1; i < nd; ++i) put(D[i]);
+    else
+      put('0');
+    put('E');
+    int a = e;
+    if (a < 0) {
+      put('-');
+      a = -a;
+    }
+    uint8_t t[4];
+    int m = 0;
+    do {
+      t[m++] = (uint8_t)('0' + a % 10);
+      a /= 10;
+    } while (a);
+    while (m) put(t[--m]);
+  }
+  return n;
+}
+// java.lang.Float.parseFloat of t[a, b) (decimal forms, NaN / Infinity);
+// false when it would throw NumberFormatException
+__device__ bool java_parse_float(const uint8_t* t, int64_t a, int64_t b, float* v) {
+  while (a < b && t[a] <= ' ') ++a;  // String.trim
+  while (b > a && t[b - 1] <= ' ') --b;
+  bool neg = false;
+  if (a < b && (t[a] == '+' || t[a] == '-')) {
+    neg = t[a] == '-';
+    ++a;
+  }
+  auto is = [&](const char* w) {
+    int64_t i = 0;
+    for (; w[i]; ++i)
+      if (a + i >= b || t[a + i] != (uint8_t)w[i]) return false;
+    return a + i == b;
+  };
+  if (is("NaN")) {
+    *v = __builtin_nanf("");
+    return true;
+  }
+  if (is("Infinity")) {
+    *v = neg ? -__builtin_inff() : __builtin_inff();
+    return true;
+  }
+  uint64_t m = 0;
+  int nd = 0, dexp = 0;
+  bool any = false, dot = false;
+  int64_t i = a;
+  for (; i < b; ++i) {
+    const uint8_t c = t[i];
+    if (c >= '0' && c <= '9') {
+      any = true;
+      if (nd < 19) {
+        if (m || c != '0') {
+          m = m * 10 + (c - '0');
+          ++nd;
+        }
+        if (dot) --dexp;
+      } else if (!dot) {
+        ++dexp;
+      }
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      break;
+    }
+  }
+  if (!any) return false;
+  if (i < b && (t[i] == 'e' || t[i] == 'E')) {
+    ++i;
+    bool en = false;
+    if (i < b && (t[i] == '+' || t[i] == '-')) en = t[i++] == '-';
+    if (i >= b) return false;
+    int x = 0;
+    for (; i < b && t[i] >= '0' && t[i] <= '9'; ++i) x = x < 100000 ? x * 10 + (t[i] - '0') : x;
+    dexp += en ? -x : x;
+  }
+  if (i < b && (t[i] == 'f' || t[i] == 'F' || t[i] == 'd' || t[i] == 'D')) ++i;  // Java's type suffixes
+  if (i != b) return false;
+  double d = (double)m;
+  if (dexp < -340) d = 0.0;
+  else if (dexp > 0) d *= pow10_d(dexp > 320 ? 320 : dexp);
+  else if (dexp < 0) d /= pow10_d(-dexp > 320 ? 320 : -dexp);
+  *v = neg ? -(float)d : (float)d;
+  return true;
+}
+
 // ---- the record parser ----
 __device__ __forceinline__ void sam_error(const SamParams& P, int64_t line, uint32_t code) {
   atomicMin(P.err, (unsigned long long)(((uint64_t)line << 8) | code));
@@ -717,12 +890,12 @@ struct bqsr_sam {
   uint64_t* line_span = nullptr;
   uint64_t* qual_span = nullptr;
   bool dup_marked = false;  // bqsr_sam_mark_duplicates ran: FLAG 0x400 rewritten on output
-  bool from_bam = false;    // bqsr_bam_parse: d_text holds the BAM records (no SAM text to rewrite)
+  bool from_bam = false;    // bqsr_bam_parse: d_text holds the records converted to SAM text on the device
+  samk::NameTable sq_tab{}, rg_tab{};  // @SQ / @RG name tables on the device (ADAM columns)
+  std::string header_text;  // the header lines (host copy)
+  void* adam = nullptr;     // ADAM column buffers (adam_out.hip), freed with the handle
   std::vector<void*> allocs;
-  ~bqsr_sam() {
-    for (void* p : allocs) (void)hipFree(p);
-    if (d_text) (void)hipFree(d_text);
-  }
+  ~bqsr_sam();
 };
 
 namespace {
@@ -875,23 +1048,25 @@ bqsr_status parse_sam_header(const char* text, int64_t n, SamHeader* H) {
 
 }  // namespace
 
-bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void* stream, bqsr_sam** out) {
-  if (!ctx || !out || n < 0 || (n > 0 && !text)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_parse: bad arguments");
-  HIP_TRY(hipSetDevice(ctx->device));
-  hipStream_t s = S(stream);
-  // ---- header (host): @RG IDs sorted (RecordGroupDictionary), @SQ names ----
-  SamHeader H;
-  bqsr_status hst = parse_sam_header(text, n, &H);
-  if (hst != BQSR_OK) return hst;
+namespace {
+// The record parse of a SAM text already on the device (d_text: n bytes +
+// 64 readable, owned by the result; the header lines parsed into H, the
+// records from H.body): bqsr_sam_parse's text, or bqsr_bam_parse's records
+// converted to SAM lines on the device.
+bqsr_status sam_parse_device(bqsr_context* ctx, SamHeader& H, const char* header, uint8_t* d_text, int64_t n,
+                             hipStream_t s, bool from_bam, bqsr_sam** out) {
+  std::unique_ptr<bqsr_sam> S_(new bqsr_sam);
+  bqsr_sam* o = S_.get();
+  o->d_text = d_text;
+  o->from_bam = from_bam;
   const int64_t body = H.body;
+  o->header_text.assign(header, (size_t)body);
   std::vector<std::string>& rg_names = H.rg_names;
   std::vector<std::string>& sq_names = H.sq_names;
   std::map<std::string, std::pair<bool, std::string>>& rg_lb = H.rg_lb;
   HostNames& rgh = H.rgh;
   HostNames& sqh = H.sqh;
 
-  std::unique_ptr<bqsr_sam> S_(new bqsr_sam);
-  bqsr_sam* o = S_.get();
   o->ctx = ctx;
   o->n_rg = (int32_t)rgh.value.size();
   o->rg_library.assign(rg_names.size(), std::string());
@@ -903,9 +1078,6 @@ bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void*
   }
   o->header = body;
   o->n_text = n;
-  HIP_TRY(hipMalloc(&o->d_text, (size_t)n + 64));
-  HIP_TRY(hipMemsetAsync(o->d_text + n, 0, 64, s));
-  if (n > 0) HIP_TRY(hipMemcpyAsync(o->d_text, text, (size_t)n, hipMemcpyHostToDevice, s));
   std::vector<void*> tmp;  // per-line temporaries
   struct Free {
     std::vector<void*>& v;
@@ -920,6 +1092,8 @@ bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void*
   bqsr_status st;
   if ((st = sam_names_upload(o->allocs, sqh, &P.sq, s)) != BQSR_OK) return st;
   if ((st = sam_names_upload(o->allocs, rgh, &P.rg, s)) != BQSR_OK) return st;
+  o->sq_tab = P.sq;
+  o->rg_tab = P.rg;
   // ---- newline positions ----
   const int64_t nb = std::max<int64_t>(1, (n - body + samk::kNlChunk - 1) / samk::kNlChunk);
   uint64_t* cnt;
@@ -1048,6 +1222,26 @@ bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void*
   *out = S_.release();
   return ok();
 }
+}  // namespace
+
+bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void* stream, bqsr_sam** out) {
+  if (!ctx || !out || n < 0 || (n > 0 && !text)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_parse: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = S(stream);
+  // ---- header (host): @RG IDs sorted (RecordGroupDictionary), @SQ names ----
+  SamHeader H;
+  bqsr_status hst = parse_sam_header(text, n, &H);
+  if (hst != BQSR_OK) return hst;
+  uint8_t* d_text = nullptr;
+  HIP_TRY(hipMalloc(&d_text, (size_t)n + 64));
+  hipError_t e = hipMemsetAsync(d_text + n, 0, 64, s);
+  if (e == hipSuccess && n > 0) e = hipMemcpyAsync(d_text, text, (size_t)n, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) {
+    (void)hipFree(d_text);
+    return fail(BQSR_ERR_DEVICE, std::string("bqsr_sam_parse: ") + hipGetErrorString(e));
+  }
+  return sam_parse_device(ctx, H, text, d_text, n, s, false, out);  // (owns d_text from here)
+}
 
 void bqsr_sam_destroy(bqsr_sam* s) { delete s; }
 
@@ -1100,7 +1294,6 @@ bqsr_status bqsr_sam_rewrite_quals(bqsr_context* ctx, bqsr_sam* sm, const bqsr_b
                                    int64_t n_exc, void* stream) {
   if (!ctx || !sm || (b && (!out_qual || !out_start || !out_len)) || n_exc < 0 || (n_exc > 0 && !exceptions))
     return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_rewrite_quals: bad arguments");
-  if (sm->from_bam) return fail(BQSR_ERR_UNSUPPORTED, "bqsr_sam_rewrite_quals: BAM input has no SAM text to rewrite");
   if (b && b->rd.n_reads != sm->n_reads) return fail(BQSR_ERR_INVALID_ARG, "batch and SAM read counts differ");
   if (b && !b->prepped) return fail(BQSR_ERR_INVALID_ARG, "the batch has not been through apply");
   if (!b) {  // QUAL fields kept (only FLAG rewritten, after MarkDuplicates)
@@ -1184,7 +1377,6 @@ bqsr_status bqsr_sam_rewrite_quals(bqsr_context* ctx, bqsr_sam* sm, const bqsr_b
 
 bqsr_status bqsr_sam_text_download(const bqsr_sam* s, char* dst) {
   if (!s || (!dst && s->n_text > 0)) return fail(BQSR_ERR_INVALID_ARG, "null");
-  if (s->from_bam) return fail(BQSR_ERR_UNSUPPORTED, "bqsr_sam_text_download: BAM input has no SAM text");
   HIP_TRY(hipSetDevice(s->ctx->device));
   if (s->n_text > 0) HIP_TRY(hipMemcpy(dst, s->d_text, (size_t)s->n_text, hipMemcpyDeviceToHost));
   return ok();

@@ -77,10 +77,11 @@ def sam_partitions(data, partition_bytes: int) -> Tuple[bytes, List[Tuple[int, i
     return bytes(data[:pos]), ranges
 
 
-def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ctx, device: int, out_fh,
+def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ctx, device: int, emit,
                      max_exc: int = 1 << 16) -> Dict[str, float]:
     """BQSR over several partitions of one SAM input (see the module doc);
-    writes the recalibrated text to out_fh in partition order."""
+    emit(i, sam) gets every partition's parse with its QUAL fields rewritten,
+    in partition order."""
     import torch
     L = _capi.lib()
     dev = torch.device("cuda", device)
@@ -146,10 +147,9 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
             try:
                 check(L.bqsr_sam_rewrite_quals(h, sam.h, bh, ptr(out_qual), ptr(out_start), ptr(out_len), ptr(exc),
                                                nexc.value, sp))
-                text = sam.text()
+                emit(i, sam)
             finally:
                 sam.close()
-            out_fh.write(text if i == 0 else text[len(header):])
             L.bqsr_batch_destroy(bh)
             batches[i] = None
     finally:
@@ -228,58 +228,113 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
     return stats
 
 
+class _SamOut:
+    """SAM text output (records appended partition by partition; the file
+    appears when the job succeeds)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.tmp = path + ".partial"
+        self.fh = open(self.tmp, "wb")
+        self.first = True
+
+    def emit(self, i, sam):
+        text = sam.text()
+        self.fh.write(text if self.first else text[self._header_len(sam):])
+        self.first = False
+
+    @staticmethod
+    def _header_len(sam) -> int:
+        from .adam_save import _lib
+        n = ctypes.c_int64()
+        check(_lib().bqsr_sam_header_text(sam.h, None, 0, ctypes.byref(n)))
+        return int(n.value)
+
+    def close(self, ok: bool = True):
+        self.fh.close()
+        if ok:
+            os.replace(self.tmp, self.path)
+        elif os.path.exists(self.tmp):
+            os.remove(self.tmp)
+
+
+class _AdamOut:
+    """ADAM output (adamSave): part files of `part_reads` records each."""
+
+    def __init__(self, path: str, compression: str, part_reads: int):
+        from .adam_save import AdamWriter
+        self.w = AdamWriter(path, compression)
+        self.part_reads = part_reads
+
+    def emit(self, i, sam):
+        self.w.emit(sam, self.part_reads)
+
+    def close(self, ok: bool = True):
+        self.w.close(ok)
+
+
+def is_bam(data) -> bool:
+    return bytes(data[:4]) == b"\x1f\x8b\x08\x04"
+
+
 def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
-              dbsnp: Optional[str] = None, device: int = 0,
-              partition_bytes: int = DEFAULT_PARTITION_BYTES) -> Dict[str, float]:
-    if is_parquet(inp) or out.endswith((".adam", ".parquet")):
+              dbsnp: Optional[str] = None, device: int = 0, partition_bytes: int = DEFAULT_PARTITION_BYTES,
+              compression: str = "gzip", part_reads: int = 1 << 20) -> Dict[str, float]:
+    """Transform.run (cli/Transform.scala:62-97) over SAM or BAM input: the
+    records parsed on the device (a BAM's records become SAM lines there),
+    MarkDuplicates, BQSR, then adamSave (OUT.adam / .parquet / a directory:
+    ADAMRecord Parquet part files, adam_save.py) or SAM text.  ADAM Parquet
+    input goes through transform_parquet (Arrow reads it on the host)."""
+    if is_parquet(inp):
         return transform_parquet(inp, out, mark_duplicates, recalibrate, dbsnp, device)
     t0 = time.perf_counter()
     ctx = bqsr.Context.get(device)
-    if recalibrate and not mark_duplicates and os.path.getsize(inp) > 0:
-        with open(inp, "rb") as fh:
-            data = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
-            try:
-                header, ranges = sam_partitions(data, partition_bytes)
-                if len(ranges) > 1 and data[:4] != b"\x1f\x8b\x08\x04":
-                    snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
-                    tmp = out + ".partial"
-                    try:
-                        with open(tmp, "wb") as ofh:
-                            stats = _bqsr_partitions(data, header, ranges, snp if snp.table else None, ctx, device,
-                                                     ofh)
-                        os.replace(tmp, out)
-                    finally:
-                        if os.path.exists(tmp):
-                            os.remove(tmp)
-                    stats["seconds"] = time.perf_counter() - t0
-                    return stats
-            finally:
-                data.close()
-    with open(inp, "rb") as fh:
-        data = fh.read()
-    sam = SamText(data, ctx)
-    stats: Dict[str, float] = {"reads": sam.counts().n_reads}
+    adam_out = out.endswith((".adam", ".parquet")) or os.path.isdir(out)
+    sink = _AdamOut(out, compression, part_reads) if adam_out else _SamOut(out)
+    ok = False
+    stats: Dict[str, float] = {}
     try:
-        if mark_duplicates:
-            stats["duplicates"] = sam.mark_duplicates()
-        job = None
-        if recalibrate:
-            from .job import ResidentJob
-            snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
-            batch = sam.batch()
-            job = ResidentJob(batch, bqsr.dims_of([batch]), snp if snp.table else None, device)
+        with open(inp, "rb") as fh:
+            data = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ) if os.path.getsize(inp) else b""
             try:
-                job.step()
-                sam.rewrite(job)
+                bam = is_bam(data)
+                ranges = None
+                if recalibrate and not mark_duplicates and not bam and len(data):
+                    header, ranges = sam_partitions(data, partition_bytes)
+                if ranges is not None and len(ranges) > 1:
+                    # BQSR over partitions streamed through the device
+                    snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
+                    stats = _bqsr_partitions(data, header, ranges, snp if snp.table else None, ctx, device,
+                                             sink.emit)
+                else:
+                    sam = SamText(bytes(data), ctx, bam=bam)
+                    try:
+                        stats["reads"] = sam.counts().n_reads
+                        if mark_duplicates:
+                            stats["duplicates"] = sam.mark_duplicates()
+                        if recalibrate:
+                            from .job import ResidentJob
+                            snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
+                            batch = sam.batch()
+                            job = ResidentJob(batch, bqsr.dims_of([batch]), snp if snp.table else None, device)
+                            try:
+                                job.step()
+                                sam.rewrite(job)
+                            finally:
+                                job.close()
+                        elif mark_duplicates:
+                            sam.rewrite(None)
+                        sink.emit(0, sam)
+                    finally:
+                        sam.close()
             finally:
-                job.close()
-        elif mark_duplicates:
-            sam.rewrite(None)
-        text = sam.text()
+                if isinstance(data, mmap.mmap):
+                    data.close()
+        ok = True
     finally:
-        sam.close()
-    with open(out, "wb") as fh:
-        fh.write(text)
+        sink.close(ok)
+    if adam_out:
+        stats["parts"] = sink.w.parts
     stats["seconds"] = time.perf_counter() - t0
     return stats
 
@@ -296,11 +351,14 @@ def main(argv=None) -> int:
     ap.add_argument("-coalesce", type=int, default=-1)
     ap.add_argument("-partition_bytes", type=int, default=DEFAULT_PARTITION_BYTES,
                     help="records per streamed partition, in bytes of SAM text (BQSR without MarkDuplicates)")
+    ap.add_argument("-parquet_compression", default="gzip", choices=("gzip", "snappy", "zstd", "none"),
+                    help="ADAM output: the part files' codec (adamSave's default: GZIP)")
+    ap.add_argument("-part_reads", type=int, default=1 << 20, help="ADAM output: records per part file")
     a = ap.parse_args(argv)
     if a.sort_reads or a.realignIndels or a.coalesce != -1:
         ap.error("-sort_reads / -coalesce / -realignIndels are outside this build")
     st = transform(a.input, a.output, a.mark_duplicate_reads, a.recalibrate_base_qualities, a.dbsnp_sites,
-                   partition_bytes=a.partition_bytes)
+                   partition_bytes=a.partition_bytes, compression=a.parquet_compression, part_reads=a.part_reads)
     print(" ".join("%s=%s" % kv for kv in st.items()), file=sys.stderr)
     return 0
 

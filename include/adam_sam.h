@@ -43,13 +43,14 @@ typedef struct bqsr_sam bqsr_sam;
  * the first record and lone '\r' bytes. */
 bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n_bytes, void* stream, bqsr_sam** out);
 void bqsr_sam_destroy(bqsr_sam* s);
-/* BAM bytes (BGZF) -> the same device columns bqsr_sam_parse builds from the
- * SAM text of the same records (AdamContext.scala:122-137 adamBamLoad,
- * SAMRecordConverter.scala:26-144): BGZF blocks inflated by host threads,
- * records decoded on the device.  The result serves bqsr_sam_get_counts,
- * bqsr_sam_download / device_columns and bqsr_sam_mark_duplicates; there is
- * no SAM text to rewrite (bqsr_sam_rewrite_quals / text_download:
- * BQSR_ERR_UNSUPPORTED).  MD / RG values of type f, H or B: UNSUPPORTED. */
+/* BAM bytes (BGZF) -> the same parse bqsr_sam_parse builds from the SAM
+ * text of the same records (AdamContext.scala:122-137 adamBamLoad,
+ * SAMRecordConverter.scala:26-144): BGZF blocks inflated (and their CRC32
+ * checked) by host threads; on the device every record becomes its SAM text
+ * line (integer tag types as "i", floats by Java's Float.toString, arrays as
+ * B:t,...) and the lines go through the SAM record parser.  So every call
+ * on a SAM parse -- rewrite, text download, MarkDuplicates, ADAM columns --
+ * serves BAM input too. */
 bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* bam, int64_t n_bytes, void* stream, bqsr_sam** out);
 
 typedef struct bqsr_sam_counts {
@@ -103,6 +104,47 @@ bqsr_status bqsr_sam_rewrite_quals(bqsr_context* ctx, bqsr_sam* s, const bqsr_ba
                                    int64_t n_exceptions, void* stream);
 /* copy the (rewritten) SAM text to host memory of at least counts.text_bytes */
 bqsr_status bqsr_sam_text_download(const bqsr_sam* s, char* dst);
+
+/* ADAMRecord columns (§8 f2: adamSave of SAMRecordConverter's records,
+ * core/rdd/AdamRDDFunctions.scala:37-56, converters/SAMRecordConverter.scala:
+ * 26-144) of records [r0, r0 + n) of the parse, from its current text (after
+ * bqsr_sam_rewrite_quals: the recalibrated QUAL and MarkDuplicates' FLAG).
+ * Record-level columns in Arrow layout, built on the device:
+ *   strings (int32 offsets [n+1], bytes, validity bitmap): readName, sequence,
+ *     cigar (re-encoded, "*" when empty), qual, mismatchingPositions (MD),
+ *     attributes (every tag but MD as TG:T:value, descending binary tag,
+ *     tab-joined; "" without tags);
+ *   int32 (+ validity): referenceId, mapq, mateReferenceId, recordGroupId;
+ *   int64 (+ validity): start, mateAlignmentStart;
+ *   bitmaps: readPaired, properPair, readMapped, mateMapped,
+ *     readNegativeStrand, mateNegativeStrand, firstOfPair, secondOfPair,
+ *     primaryAlignment, failedVendorQualityChecks, duplicateRead.
+ * Bitmaps are Arrow's (bit r of word r / 64, LSB first).  The columns that
+ * depend only on the read group or the @SQ entry (referenceName,
+ * recordGroup*, referenceLength / Url, mate*) come from the header text by
+ * index (bqsr_sam_header_text).  An H or B tag, or an 'i' tag outside Int,
+ * gives BQSR_ERR_UNSUPPORTED (the reference's attribute conversion throws).
+ * prepare: pass 1 and the sizes; columns: pass 2 and the copies into the
+ * caller's host buffers (NULL pointers skip a column). */
+typedef struct bqsr_adam_sizes {
+  int64_t n_reads;
+  int64_t str_bytes[6];
+  int64_t bitmap_words; /* u64 words of each bitmap */
+} bqsr_adam_sizes;
+typedef struct bqsr_adam_host {
+  int32_t* str_offsets[6];
+  uint8_t* str_bytes[6];
+  uint64_t* str_valid[6];
+  int32_t* i32[4];
+  int64_t* i64[2];
+  uint64_t* int_valid[6]; /* referenceId, mapq, mateReferenceId, recordGroupId, start, mateAlignmentStart */
+  uint64_t* bools[11];
+} bqsr_adam_host;
+bqsr_status bqsr_sam_adam_prepare(bqsr_context* ctx, bqsr_sam* s, int64_t r0, int64_t n, void* stream,
+                                  bqsr_adam_sizes* out);
+bqsr_status bqsr_sam_adam_columns(bqsr_context* ctx, bqsr_sam* s, const bqsr_adam_host* dst, void* stream);
+/* the header lines of the parse (SAM input, or a BAM's header text) */
+bqsr_status bqsr_sam_header_text(const bqsr_sam* s, char* dst, int64_t cap, int64_t* len);
 
 /* MarkDuplicates (§8 f3): adam-core/.../rdd/MarkDuplicates.scala:24-111 over
  * SingleReadBucket (models/SingleReadBucket.scala:27-37: reads grouped by
