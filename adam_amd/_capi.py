@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ADAM_BQSR_LIB") or os.path.join(_HERE, "libadam_bqsr.so")
 
 BQSR_OK = 0
-STAGE_RESET, STAGE_KERNEL, STAGE_FOLD, STAGE_PREP = 1, 2, 4, 8
+STAGE_RESET, STAGE_KERNEL, STAGE_FOLD, STAGE_PREP, STAGE_LUT, STAGE_NO_LUT = 1, 2, 4, 8, 16, 32
 STATUS_NAMES = ["OK", "NULL_RG", "MD_PARSE", "CIGAR_SHORT", "BAD_REVCOMP_BASE", "EMPTY_TABLE", "MISSING_KEY",
                 "QUAL_RANGE", "NULL_FIELD", "SEQ_SHORT", "CIGAR_INVALID", "INVALID_ARG", "DEVICE", "UNSUPPORTED",
                 "SAM_PARSE"]

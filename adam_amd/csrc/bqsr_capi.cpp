@@ -303,6 +303,7 @@ struct bqsr_batch {
   uint32_t* d_part = nullptr;      // per-block window counts
   size_t part_words = 0;
   uint8_t* d_chars = nullptr;      // apply: the pieces' char tables (ApplyParams::chars)
+  const bqsr_lut* chars_lut = nullptr;  // the LUT they were built from (BQSR_STAGE_LUT)
   size_t chars_bytes = 0;
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
@@ -1620,7 +1621,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     bqsr_status st = launch_prep(ctx, b, nullptr, s);
     if (st != BQSR_OK) return st;
   }
-  if (b->rd.n_reads == 0 || !(stages & BQSR_STAGE_KERNEL)) return ok();
+  if (b->rd.n_reads == 0 || !(stages & (BQSR_STAGE_KERNEL | BQSR_STAGE_LUT))) return ok();
   ApplyParams P{};
   P.rd = b->rd;
   P.ord = b->order();
@@ -1661,13 +1662,21 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     }
     HIP_TRY(hipMalloc((void**)&b->d_chars, need));
     b->chars_bytes = need;
+    b->chars_lut = nullptr;
   }
   P.chars = b->d_chars;
   P.rowbad = (uint32_t*)(b->d_chars + (size_t)P.piece_stride * (size_t)b->n_base);
-  HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_base * 16, s));
-  const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
-  hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
-  hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
+  const bool lut_stage = (stages & BQSR_STAGE_LUT) || ((stages & BQSR_STAGE_KERNEL) && !(stages & BQSR_STAGE_NO_LUT));
+  if (lut_stage) {
+    HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_base * 16, s));
+    const unsigned cb = (unsigned)std::min<int64_t>(((int64_t)need + 255) / 256, (int64_t)ctx->n_cu * 16);
+    hipLaunchKernelGGL(bqsr_apply_chars, dim3(cb), dim3(256), 0, s, P, b->d_chars);
+    b->chars_lut = L;
+  }
+  if (stages & BQSR_STAGE_KERNEL) {
+    if (b->chars_lut != L) return fail(BQSR_ERR_INVALID_ARG, "apply kernel before the LUT stage of this LUT");
+    hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
+  }
   HIP_TRY(hipGetLastError());
   return ok();
 }

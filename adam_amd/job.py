@@ -111,9 +111,13 @@ class ResidentJob:
         check(L.bqsr_finalize_device(ctx, th, em_ptr, ctypes.byref(self.lut), sp))
         args = (ctx, bh, self.lut, self._ptr(self.out_qual), self._ptr(self.out_start), self._ptr(self.out_len),
                 self._ptr(self.exc), self.max_exc)
-        mark(3)
-        check(L.bqsr_apply_stage(*args, _capi.STAGE_KERNEL, sp))
-        mark(4)
+        if record:  # the char tables first, so the bracket holds the apply kernel alone
+            check(L.bqsr_apply_stage(*args, _capi.STAGE_LUT, sp))
+            mark(3)
+            check(L.bqsr_apply_stage(*args, _capi.STAGE_KERNEL | _capi.STAGE_NO_LUT, sp))
+            mark(4)
+        else:
+            check(L.bqsr_apply_stage(*args, _capi.STAGE_KERNEL, sp))
         if self.world > 1:
             check(L.bqsr_job_errors_export_async(bh, self.read_base, self._ptr(self.err_keys), sp))
             D.allreduce_error_keys(self.err_keys)

@@ -242,19 +242,30 @@ def main():
         R = batch.n_reads
         # algorithmic bytes: observe 1.75 B/base + 16 B/read, apply 2.5 B/base + 16 B/read
         alg = {"observe": 1.75 * n_bases + 16 * R, "apply": 2.5 * n_bases + 16 * R}
-        dom = "observe" if ms.get("observe", 0) >= ms.get("apply", 0) else "apply"
-        achieved = alg[dom] / (ms[dom] * 1e-3) / 1e9 if dom in ms else None
-        traffic = None
-        kname = "bqsr_%s_kernel" % dom
         tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.config)
-        try:  # PMC bytes of the same kernel on the same workload (tools/make_traffic.py)
-            with open(tpath) as fh:
-                tr = json.load(fh)
-            if tr.get("config") == args.config and tr.get("reads_per_gpu") == R:
-                traffic = tr["kernels"].get(dom, {}).get("hbm_bytes_per_launch")
-                kname = tr["kernels"].get(dom, {}).get("kernel", kname)
-        except (OSError, ValueError, KeyError):
-            traffic = None
+        tr = _profile_json(tpath, args.config, R)  # PMC bytes per launch (tools/make_traffic.py)
+        kpath = os.path.join(ROOT, "profiles", "kernel_stats_%s.json" % args.config)
+        ks = _profile_json(kpath, args.config, R)  # rocprofv3 kernel averages (tools/make_kstats.py)
+        # the dominant kernel: the longer one by rocprof's kernel-only averages of
+        # this tree's committed profile; by the live HIP events without one
+        rp = {k: ks["kernels"][k]["avg_ms"] for k in alg if ks and k in ks["kernels"]}
+        src = rp if len(rp) == 2 else ms
+        dom = "observe" if src.get("observe", 0) >= src.get("apply", 0) else "apply"
+        kernels = {}
+        for k in alg:
+            e = {"alg_bytes_per_launch": alg[k], "events_ms": ms.get(k),
+                 "events_frac": alg[k] / (ms[k] * 1e-3) / 1e9 / HBM_PEAK_GBS if ms.get(k) else None}
+            if k in rp:
+                e.update(kernel=ks["kernels"][k]["kernel"], rocprof_ms=rp[k],
+                         rocprof_frac=alg[k] / (rp[k] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+            if tr and k in tr["kernels"]:
+                e.update(traffic=tr["kernels"][k]["hbm_bytes_per_launch"],
+                         traffic_x_alg=tr["kernels"][k]["hbm_bytes_per_launch"] / alg[k])
+            kernels[k] = e
+        kernels["dominant"] = dom
+        achieved = alg[dom] / (ms[dom] * 1e-3) / 1e9 if dom in ms else None
+        traffic = kernels[dom].get("traffic")
+        kname = kernels[dom].get("kernel", "bqsr_%s" % dom)
         value = args.steps * total_bases / elapsed
         line = {
             "metric": METRIC,
@@ -290,9 +301,11 @@ def main():
                 "traffic_source": tpath if traffic is not None else None,
                 "alg_bytes_per_launch": alg[dom],
                 "kernel_ms": ms,
-                "kernel_ms_method": "HIP events on the launch stream over %d untimed jobs after the timed region "
-                                    "(stage brackets include launch gaps; rocprofv3 kernel averages in profiles/ "
-                                    "are the kernel-only times)" % args.event_steps,
+                "kernel_ms_method": "HIP events on the launch stream around each stage over %d untimed jobs after "
+                                    "the timed region (apply: the kernel alone, its char tables before the "
+                                    "bracket)" % args.event_steps,
+                "kernels": kernels,
+                "kernels_source": {"rocprof": kpath if rp else None, "commit": ks.get("commit") if ks else None},
             },
             "hbm_roofline_frac_step": (total_bases / world) * (4.25 + 32.0 / max(cfg["lens"])) /
                                       (elapsed / args.steps) / (HBM_PEAK_GBS * 1e9),
@@ -306,6 +319,19 @@ def main():
     job.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _profile_json(path, config, reads):
+    """A committed profile summary (profiles/*.json) when it was taken on
+    this config and shard size, else None."""
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != config or d.get("reads_per_gpu") != reads or "kernels" not in d:
+        return None
+    return d
 
 
 def oracle_shard(cfg, batch, sites):

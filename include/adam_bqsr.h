@@ -272,7 +272,12 @@ bqsr_status bqsr_apply_records(bqsr_context* ctx, const bqsr_records* recs, cons
  * The calls above synchronise.  These enqueue on `stream` and return at once,
  * so a driver can keep a whole BQSR job on the device (the benchmark and the
  * multi-GPU path use them; RCCL collectives go between the stages). */
-enum { BQSR_STAGE_RESET = 1, BQSR_STAGE_KERNEL = 2, BQSR_STAGE_FOLD = 4, BQSR_STAGE_PREP = 8 };
+enum { BQSR_STAGE_RESET = 1, BQSR_STAGE_KERNEL = 2, BQSR_STAGE_FOLD = 4, BQSR_STAGE_PREP = 8,
+       BQSR_STAGE_LUT = 16, BQSR_STAGE_NO_LUT = 32 };
+/* apply stages: RESET clears its error words, KERNEL builds the pieces' char
+ * tables (bqsr_apply_chars) and runs the apply kernel; LUT builds the char
+ * tables only, KERNEL | NO_LUT runs the kernel on tables an earlier LUT
+ * stage built for the same LUT (so a caller can time the kernel alone). */
 /* observe stages: RESET clears the error word, PREP is the per-read prep
  * kernel (trimming, CIGAR/MD/known-site masks, validation), KERNEL the
  * observe kernel, FOLD the expectedMismatch fold (result at
