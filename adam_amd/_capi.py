@@ -34,6 +34,7 @@ EXPORTS = [
     "bqsr_batch_create_staged", "bqsr_batch_upload_async", "bqsr_em_fold_async", "bqsr_batch_em_copy_async",
     "bqsr_finalize_device", "bqsr_observe_stage", "bqsr_apply_stage", "bqsr_job_reset_async", "bqsr_job_result", "bqsr_copy_async",
     "bqsr_job_errors_export_async", "bqsr_job_errors_import_async", "bqsr_job_status_async", "bqsr_job_status_get",
+    "bqsr_copy_dyn_async", "bqsr_compact_outputs_async", "bqsr_batch_exception_count_ptr",
 ]
 
 
@@ -152,6 +153,9 @@ def lib():
             "bqsr_job_reset_async": (ctypes.c_int, [vp, vp, vp]),
             "bqsr_job_result": (ctypes.c_int, [vp, vp, ctypes.POINTER(dbl), ctypes.POINTER(i64), vp]),
             "bqsr_copy_async": (ctypes.c_int, [vp, vp, vp, i64, vp]),
+            "bqsr_copy_dyn_async": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i64, vp]),
+            "bqsr_compact_outputs_async": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]),
+            "bqsr_batch_exception_count_ptr": (vp, [vp]),
             "bqsr_job_errors_export_async": (ctypes.c_int, [vp, i64, vp, vp]),
             "bqsr_job_errors_import_async": (ctypes.c_int, [vp, vp, vp]),
             "bqsr_job_status_async": (ctypes.c_int, [vp, vp, i32, vp]),

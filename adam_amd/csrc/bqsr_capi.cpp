@@ -304,6 +304,8 @@ struct bqsr_batch {
   size_t part_words = 0;
   uint8_t* d_chars = nullptr;      // apply: the pieces' char tables (ApplyParams::chars)
   const bqsr_lut* chars_lut = nullptr;  // the LUT they were built from (BQSR_STAGE_LUT)
+  uint64_t* d_off64 = nullptr;     // bqsr_compact_outputs_async scratch (lengths, scan)
+  int64_t off64_n = -1;
   size_t chars_bytes = 0;
   unsigned long long* d_err = nullptr;  // [kErrWords]: observe, apply-prep, apply-kernel errors, exception count
   double* d_em = nullptr;
@@ -326,6 +328,7 @@ struct bqsr_batch {
   uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
   ~bqsr_batch() {
     if (d_part) (void)hipFree(d_part);
+    if (d_off64) (void)hipFree(d_off64);
     if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
     for (void* p : allocs) (void)hipFree(p);
@@ -1889,3 +1892,63 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
 #include "bam_ingest.hip"
 #include "mark_duplicates.cpp"
 #include "adam_out.hip"
+
+// ---- streamed outputs: compaction (uses the SAM code's scans) ----
+extern "C" {
+
+bqsr_status bqsr_compact_outputs_async(bqsr_context* ctx, bqsr_batch* b, const uint8_t* out_qual,
+                                       const uint32_t* out_start, const uint32_t* out_len, uint64_t* exceptions,
+                                       int64_t max_exceptions, uint8_t* chars, uint32_t* offsets, void* stream) {
+  if (!ctx || !b || !out_qual || !out_start || !out_len || !chars || !offsets || max_exceptions < 0 ||
+      (max_exceptions > 0 && !exceptions))
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_compact_outputs_async: bad arguments");
+  if (b->n_slots > (int64_t)UINT32_MAX) return fail(BQSR_ERR_UNSUPPORTED, "compacted chars above 4 GiB");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = S(stream);
+  const int64_t n = b->rd.n_reads;
+  if (!b->d_off64 || b->off64_n < n) {  // scratch: u64 lengths and their scan (kept on the batch)
+    if (b->d_off64) {
+      HIP_TRY(hipStreamSynchronize(s));
+      (void)hipFree(b->d_off64);
+      b->d_off64 = nullptr;
+    }
+    const size_t words = 2 * ((size_t)n + 1) + (size_t)n / samk::kScanChunk + 2;
+    HIP_TRY(hipMalloc((void**)&b->d_off64, words * 8));
+    b->off64_n = n;
+  }
+  uint64_t* len64 = b->d_off64;
+  uint64_t* off64 = len64 + n + 1;
+  uint64_t* part = off64 + n + 1;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 8));
+  if (n > 0) hipLaunchKernelGGL(bqsr_compact_lens, dim3(g), dim3(256), 0, s, out_len, n, len64);
+  bqsr_status st = sam_scan(len64, n, off64, part, s);
+  if (st != BQSR_OK) return st;
+  if (n > 0) {
+    hipLaunchKernelGGL(bqsr_compact_chars, dim3(g), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, out_qual, out_start,
+                       (const uint64_t*)off64, n, chars, offsets);
+    if (max_exceptions > 0)
+      hipLaunchKernelGGL(bqsr_compact_exceptions, dim3(4), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, out_start,
+                         (const uint64_t*)off64, (unsigned long long*)exceptions,
+                         (const unsigned long long*)(b->d_err + kNExc), max_exceptions);
+  } else {
+    HIP_TRY(hipMemsetAsync(offsets, 0, 4, s));
+  }
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+const void* bqsr_batch_exception_count_ptr(const bqsr_batch* b) { return b ? (const void*)(b->d_err + kNExc) : nullptr; }
+
+bqsr_status bqsr_copy_dyn_async(bqsr_context* ctx, void* dst, const void* src, const void* count, int32_t count_bytes,
+                                int64_t scale, int64_t max_bytes, void* stream) {
+  if (!ctx || !dst || !src || !count || (count_bytes != 4 && count_bytes != 8) || scale < 0 || max_bytes < 0)
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_dyn_async: bad arguments");
+  HIP_TRY(hipSetDevice(ctx->device));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_bytes / 16 + 255) / 256, copy_blocks(ctx)));
+  hipLaunchKernelGGL(bqsr_copy_dyn, dim3(g), dim3(256), 0, S(stream), (const uint8_t*)src, (uint8_t*)dst, count,
+                     count_bytes, scale, max_bytes);
+  HIP_TRY(hipGetLastError());
+  return ok();
+}
+
+}  // extern "C"

@@ -2286,6 +2286,69 @@ extern "C" __global__ void bqsr_copy16(const uint4* __restrict__ src, uint4* __r
   for (int64_t i = t0; i < ntail; i += step) tdst[i] = tsrc[i];
 }
 
+// ------------------------------------------- compact outputs (streamed) -----
+// A partition's recalibrated chars leave the device compacted: read r's
+// out_len[r] chars of its slot range [slot + out_start, + out_len) at
+// off[r] (u32 exclusive scan of out_len), so the link carries the chars
+// (Q13: the trimmed ranges) rather than the padded slot array.
+extern "C" __global__ void bqsr_compact_lens(const uint32_t* out_len, int64_t n, uint64_t* len64) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    len64[r] = out_len[r];
+}
+// a wavefront per 64 reads: offsets by lane, then the reads' bytes 64 lanes wide
+extern "C" __global__ void __launch_bounds__(256) bqsr_compact_chars(const ReadMeta* meta, const uint8_t* out_qual,
+                                                                     const uint32_t* out_start, const uint64_t* off64,
+                                                                     int64_t n, uint8_t* chars, uint32_t* off32) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); r0 < n;
+       r0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = r0 + lane;
+    uint64_t src = 0, dst = 0, len = 0;
+    if (r < n) {
+      dst = off64[r];
+      len = off64[r + 1] - dst;
+      src = meta[r].slot + out_start[r];
+      off32[r] = (uint32_t)dst;
+      if (r == n - 1) off32[n] = (uint32_t)off64[n];
+    }
+    for (int j = 0; j < 64; ++j) {
+      const uint64_t l = __shfl(len, j), a = __shfl(src, j), d = __shfl(dst, j);
+      for (uint64_t k = lane; k < l; k += 64) chars[d + k] = out_qual[a + k];
+    }
+  }
+}
+// the exception list's slots -> positions in the compacted chars (the read
+// holding the slot: binary search over the batch's read slots)
+extern "C" __global__ void bqsr_compact_exceptions(const ReadMeta* meta, int64_t n, const uint32_t* out_start,
+                                                   const uint64_t* off64, unsigned long long* exc,
+                                                   const unsigned long long* n_exc, int64_t max_exc) {
+  const int64_t ne = min((int64_t)*n_exc, max_exc);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = exc[i], slot = e >> 16;
+    int64_t lo = 0, hi = n - 1;  // the last read whose slot <= slot
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (meta[mid].slot <= slot) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t pos = off64[lo] + (slot - meta[lo].slot - out_start[lo]);
+    exc[i] = (pos << 16) | (e & 0xFFFFull);
+  }
+}
+// a kernel copy of a byte count the device holds: bytes = min(*count * scale, max)
+extern "C" __global__ void bqsr_copy_dyn(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                         const void* count, int32_t count_bytes, int64_t scale, int64_t max_bytes) {
+  const int64_t c = count_bytes == 4 ? (int64_t)*(const uint32_t*)count : (int64_t)*(const uint64_t*)count;
+  const int64_t bytes = min(c * scale, max_bytes);
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+  if (((uintptr_t)src | (uintptr_t)dst) % 16 == 0) {
+    const int64_t n16 = bytes / 16;
+    for (int64_t i = t0; i < n16; i += step) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (int64_t i = 16 * n16 + t0; i < bytes; i += step) dst[i] = src[i];
+  } else {
+    for (int64_t i = t0; i < bytes; i += step) dst[i] = src[i];
+  }
+}
+
 // --------------------------------------------------------- table merge -----
 extern "C" __global__ void bqsr_table_add(int64_t* acc, const int64_t* part, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

@@ -48,7 +48,7 @@ class StreamedShard:
     def __init__(self, ctx, parts: Sequence, dims, sites_handle=None, device: int = 0, max_exc: int = 1 << 16,
                  site_contigs: Optional[Sequence[str]] = None, read_base: Optional[int] = None,
                  zero_copy: bool = False,
-                 d2h: str = "kernel"):
+                 d2h: str = "kernel", compact: Optional[bool] = None):
         """read_base: global index of the shard's first read (reads of the
         ranks before this one): multi-rank errors are raised in global order;
         required when several ranks run the job."""
@@ -79,6 +79,12 @@ class StreamedShard:
         if d2h not in ("kernel", "dma"):
             raise ValueError("d2h must be 'kernel' or 'dma'")
         self.d2h = d2h
+        # compact: each partition's recalibrated chars go back compacted (chars
+        # at u32 offsets per read, bqsr_compact_outputs_async) instead of the
+        # padded slot array; needs the kernel copies (sizes known on the device only)
+        self.compact = (not self.zero_copy and d2h == "kernel") if compact is None else bool(compact)
+        if self.compact and (self.zero_copy or d2h != "kernel"):
+            raise ValueError("compact outputs need d2h='kernel' and no zero_copy")
         for p in parts:
             self.add_partition(p)
         if parts:
@@ -112,10 +118,19 @@ class StreamedShard:
         self.out_qual = [torch.empty(ms, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.out_start = [torch.empty(max(1, mr), dtype=torch.int32, device=dev) for _ in range(2)]
         self.out_len = [torch.empty(max(1, mr), dtype=torch.int32, device=dev) for _ in range(2)]
-        # host results, pinned: qualities by packed slot, per-read start / length
-        self.host_qual = [torch.empty(n + 64, dtype=torch.uint8, pin_memory=True) for n in self.n_slots]
-        self.host_start = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
-        self.host_len = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
+        if self.compact:
+            # device: the compacted chars and offsets (double-buffered); host, pinned:
+            # per partition the chars and offsets of read r = chars[off[r] : off[r + 1]]
+            self.cchars = [torch.empty(ms, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.coff = [torch.empty(mr + 1, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.host_chars = [torch.empty(n + 64, dtype=torch.uint8, pin_memory=True) for n in self.n_slots]
+            self.host_off = [torch.empty(n + 1, dtype=torch.int32, pin_memory=True) for n in self.n_reads]
+            self.host_qual = self.host_start = self.host_len = None
+        else:
+            # host results, pinned: qualities by packed slot, per-read start / length
+            self.host_qual = [torch.empty(n + 64, dtype=torch.uint8, pin_memory=True) for n in self.n_slots]
+            self.host_start = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
+            self.host_len = [torch.empty(max(1, n), dtype=torch.int32, pin_memory=True) for n in self.n_reads]
         # exception lists (chars above 0xFF, Q14): one slice of max_exc entries
         # per partition, copied back with the partition's qualities
         n = len(self.batches)
@@ -204,10 +219,31 @@ class StreamedShard:
                                      self.max_exc, _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
             if record_apply:
                 self.ev_apply_t[i][1].record(comp)
+            if self.compact:
+                check(L.bqsr_compact_outputs_async(ctx, bh, ctypes.c_void_p(oq.data_ptr()),
+                                                   ctypes.c_void_p(os_.data_ptr()), ctypes.c_void_p(ol.data_ptr()),
+                                                   exc_i, self.max_exc, ctypes.c_void_p(self.cchars[k].data_ptr()),
+                                                   ctypes.c_void_p(self.coff[k].data_ptr()), sp))
             self.ev_ap[i].record(comp)
             dn.wait_event(self.ev_ap[i])
             ns, nr = self.n_slots[i], max(1, self.n_reads[i])
             e0 = i * self.max_exc
+            if self.compact:
+                # sizes on the device: the chars (offset n), the exception count
+                dnp = ctypes.c_void_p(dn.cuda_stream)
+                n_i = self.n_reads[i]
+                cp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+                check(L.bqsr_copy_dyn_async(ctx, cp(self.host_chars[i]), cp(self.cchars[k]),
+                                            ctypes.c_void_p(self.coff[k].data_ptr() + 4 * n_i), 4, 1, ns, dnp))
+                check(L.bqsr_copy_async(ctx, cp(self.host_off[i]), cp(self.coff[k]), 4 * (n_i + 1), dnp))
+                check(L.bqsr_copy_dyn_async(ctx, ctypes.c_void_p(self.host_exc.data_ptr() + 8 * e0),
+                                            ctypes.c_void_p(self.exc.data_ptr() + 8 * e0),
+                                            ctypes.c_void_p(L.bqsr_batch_exception_count_ptr(bh)), 8, 8,
+                                            8 * self.max_exc, dnp))
+                self.ev_dl[k].record(dn)
+                self.ev_exc[i].record(dn)
+                self.dl_used[k] = True
+                continue
             pairs = [] if self.zero_copy else [(self.host_qual[i][:ns], self.out_qual[k][:ns]),
                                                (self.host_start[i][:nr], self.out_start[k][:nr]),
                                                (self.host_len[i][:nr], self.out_len[k][:nr])]
@@ -290,23 +326,49 @@ class StreamedShard:
             raise RuntimeError("a job is pending: its apply and copies overwrite the host results; finish() it first")
 
     def exceptions(self, i: int):
-        """Partition i's chars above 0xFF of the last job: (slot, Java char) pairs."""
+        """Partition i's chars above 0xFF of the last job: (position, Java char)
+        pairs -- the slot in the padded layout, the index into host_chars[i]
+        when compact."""
         self._results_ready()
         a = self.host_exc[i * self.max_exc: i * self.max_exc + self.n_exc[i]].numpy()
         return [(int(v) >> 16, int(v) & 0xFFFF) for v in a]
 
     def qual_chars(self, i: int, slot: int, r: int):
         """Read r's recalibrated quality string of partition i as Java chars
-        (uint16), given its packed slot: the u8 output with the partition's
-        exceptions applied."""
+        (uint16): the u8 output with the partition's exceptions applied (slot:
+        the read's packed slot, used by the padded layout only)."""
         import numpy as np
         self._results_ready()
-        st, ln = int(self.host_start[i][r]), int(self.host_len[i][r])
-        out = self.host_qual[i][slot + st: slot + st + ln].numpy().astype(np.uint16)
+        if self.compact:
+            a, b = int(self.host_off[i][r]) & 0xFFFFFFFF, int(self.host_off[i][r + 1]) & 0xFFFFFFFF
+        else:
+            st, ln = int(self.host_start[i][r]), int(self.host_len[i][r])
+            a, b = slot + st, slot + st + ln
+        out = (self.host_chars[i] if self.compact else self.host_qual[i])[a:b].numpy().astype(np.uint16)
         for s, code in self.exceptions(i):
-            if slot + st <= s < slot + st + ln:
-                out[s - slot - st] = code
+            if a <= s < b:
+                out[s - a] = code
         return out
+
+    def outputs(self, i: int):
+        """Partition i's results of the last job for a checker: ("compact",
+        chars, offsets u32, exceptions) or ("slots", qual by slot, start, len,
+        exceptions); exceptions as the raw (position << 16 | char) words."""
+        self._results_ready()
+        exc = self.host_exc[i * self.max_exc: i * self.max_exc + self.n_exc[i]].numpy()
+        nr = self.n_reads[i]
+        if self.compact:
+            off = self.host_off[i].numpy()[:nr + 1].view("uint32")
+            return "compact", self.host_chars[i].numpy()[:int(off[nr]) if nr else 0], off, exc
+        return ("slots", self.host_qual[i].numpy()[:self.n_slots[i]], self.host_start[i].numpy()[:nr],
+                self.host_len[i].numpy()[:nr], exc)
+
+    def d2h_bytes(self) -> int:
+        """Bytes the last finished job copied back to the host."""
+        if not self.compact:
+            return sum(self.n_slots) + 8 * sum(self.n_reads) + 8 * self.max_exc * len(self.batches)
+        return sum((int(self.host_off[i][self.n_reads[i]]) & 0xFFFFFFFF) + 4 * (self.n_reads[i] + 1) + 8 * self.n_exc[i]
+                   for i in range(len(self.batches)))
 
     def apply_ms(self) -> Optional[float]:
         """Mean apply-kernel time per partition of the last recorded job."""

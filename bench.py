@@ -503,7 +503,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         alg_part = 2.5 * n_bases / parts_n + 16 * R_part
         achieved = alg_part / (am * 1e-3) / 1e9 if am else None
         h2d = sh.staged_bytes
-        d2h = sum(sh.n_slots) + 8 * n_reads + 8 * sh.max_exc * parts_n
+        d2h = sh.d2h_bytes()
         line = {
             "metric": METRIC,
             "value": args.steps * total_bases / elapsed,
@@ -528,6 +528,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
                 "partitions_per_gpu": parts_n,
                 "stream_mode": args.stream_mode,
                 "d2h": args.d2h,
+                "outputs": "compacted chars + u32 offsets" if sh.compact else "padded slots + start/len",
                 "parallelism": "dp%d: read shards per GPU, RCCL int64 table all-reduce" % world,
             },
             "roofline": {
@@ -606,11 +607,7 @@ def parity_stream(cfg, sh, table_t, n_reads, pr, rank, world, dims, dev):
     bad_total, checked, first_bad = 0, 0, np.iinfo(np.int64).max
     for i, part in sorted(keep.items()):
         out, out_len = O.apply_mt(part, d, words, em, n_parts=cores, nthreads=cores)
-        ns, nr = sh.n_slots[i], sh.n_reads[i]
-        exc = sh.host_exc[i * sh.max_exc: i * sh.max_exc + sh.n_exc[i]].numpy()
-        bad, first = O.compare_device_output(part, out, out_len, sh.host_qual[i].numpy()[:ns],
-                                             sh.host_start[i].numpy()[:nr], sh.host_len[i].numpy()[:nr],
-                                             exc if len(exc) else None, nthreads=cores)
+        bad, first = compare_stream_outputs(O, sh, i, part, out, out_len, cores)
         bad_total += bad
         checked += part.n_reads
         if bad:
@@ -629,6 +626,17 @@ def parity_stream(cfg, sh, table_t, n_reads, pr, rank, world, dims, dev):
                        "every rank (tables summed, expectedMismatch folded in global partition order), chars of "
                        "each rank's first and last partitions",
             "check_s": time.perf_counter() - t}
+
+
+def compare_stream_outputs(O, sh, i, part, out, out_len, cores):
+    """(reads differing, first) between the oracle's chars and a streamed
+    partition's results (compacted or by slot)."""
+    res = sh.outputs(i)
+    if res[0] == "compact":
+        _, chars, off, exc = res
+        return O.compare_compact_output(part, out, out_len, chars, off, exc if len(exc) else None, nthreads=cores)
+    _, q, st, ln, exc = res
+    return O.compare_device_output(part, out, out_len, q, st, ln, exc if len(exc) else None, nthreads=cores)
 
 
 def host_cores():

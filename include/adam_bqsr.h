@@ -343,6 +343,22 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin);
  * pieces, unaligned ones byte by byte.  Replaces, for the JNI side, the memcpy of a partition's
  * output buffers back into the executor's direct buffers. */
 bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64_t bytes, void* stream);
+/* The same for a size the device holds: bytes = min(*count * scale, max_bytes)
+ * (count a u32 or u64, count_bytes 4 / 8) -- the compacted outputs below,
+ * whose length the host does not know when it enqueues the copy. */
+bqsr_status bqsr_copy_dyn_async(bqsr_context* ctx, void* dst, const void* src, const void* count, int32_t count_bytes,
+                                int64_t scale, int64_t max_bytes, void* stream);
+/* A partition's apply outputs compacted for the trip to the host (the JNI
+ * side's result buffers hold just the new quality strings, Q13):
+ * chars[offsets[r] .. offsets[r + 1]) = the out_len[r] chars of read r
+ * (device buffers: chars >= the batch's slots, offsets u32 [n + 1]); the
+ * exception list's entries are rewritten to (position in chars) << 16 | char.
+ * Enqueued on `stream` after the apply stage; bqsr_batch_exception_count_ptr
+ * is the device word holding the exception count (for bqsr_copy_dyn_async). */
+bqsr_status bqsr_compact_outputs_async(bqsr_context* ctx, bqsr_batch* b, const uint8_t* out_qual,
+                                       const uint32_t* out_start, const uint32_t* out_len, uint64_t* exceptions,
+                                       int64_t max_exceptions, uint8_t* chars, uint32_t* offsets, void* stream);
+const void* bqsr_batch_exception_count_ptr(const bqsr_batch* b);
 
 /* One job's launches with the fewest host round trips (what bench.py's step
  * runs): the table zeroed and the batch's error words reset in one kernel

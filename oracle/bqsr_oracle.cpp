@@ -718,6 +718,48 @@ int64_t oracle_compare_device_output(const bqsr_records* R, const uint16_t* ref,
   return bad.load();
 }
 
+// The same check against the compacted form (bqsr_compact_outputs_async):
+// read r's chars at got[off[r] .. off[r + 1]), exceptions keyed by position.
+int64_t oracle_compare_compact_output(const bqsr_records* R, const uint16_t* ref, const uint32_t* ref_len,
+                                      const uint8_t* got, const uint32_t* off, const uint64_t* exc, int64_t n_exc,
+                                      int32_t nthreads, int64_t* first_bad) {
+  const int64_t n = R->n_reads;
+  std::vector<std::pair<uint64_t, uint16_t>> ex;
+  for (int64_t i = 0; i < n_exc; ++i) ex.push_back({exc[i] >> 16, (uint16_t)(exc[i] & 0xFFFF)});
+  std::sort(ex.begin(), ex.end());
+  std::atomic<int64_t> bad{0}, first{INT64_MAX};
+  const int nt = std::max(1, nthreads);
+  auto work = [&](int t) {
+    int64_t b = 0, fb = INT64_MAX;
+    for (int64_t r = n * t / nt; r < n * (t + 1) / nt; ++r) {
+      bool ok = off[r + 1] - off[r] == ref_len[r];
+      const uint16_t* rq = ref + R->qual_offset[r];
+      for (uint32_t k = 0; ok && k < ref_len[r]; ++k) {
+        const uint64_t p = (uint64_t)off[r] + k;
+        uint16_t v = got[p];
+        if (rq[k] > 0xFF) {
+          auto it = std::lower_bound(ex.begin(), ex.end(), std::make_pair(p, (uint16_t)0));
+          v = (it != ex.end() && it->first == p) ? it->second : v;
+        }
+        ok = v == rq[k];
+      }
+      if (!ok) {
+        ++b;
+        fb = std::min(fb, r);
+      }
+    }
+    bad += b;
+    int64_t cur = first.load();
+    while (fb < cur && !first.compare_exchange_weak(cur, fb)) {
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+  for (auto& x : th) x.join();
+  *first_bad = bad.load() ? first.load() : -1;
+  return bad.load();
+}
+
 // computeTable over the batch split into n_parts partitions (observe per
 // partition on nthreads threads, RecalTable.++ in partition order,
 // RecalibrateBaseQualities.scala:52-64).  fold1: expectedMismatch folded as if

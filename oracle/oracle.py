@@ -65,6 +65,8 @@ def lib():
         L.oracle_em_fold.argtypes = [vp, i64, i64, vp]
         L.oracle_compare_device_output.restype = i64
         L.oracle_compare_device_output.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp]
+        L.oracle_compare_compact_output.restype = i64
+        L.oracle_compare_compact_output.argtypes = [vp, vp, vp, vp, vp, vp, i64, i32, vp]
         L.oracle_reference_positions.restype = i64
         L.oracle_reference_positions.argtypes = [vp, ctypes.c_uint64, i64, vp, i64]
         L.oracle_reference_end.restype = i64
@@ -277,6 +279,26 @@ def compare_device_output(batch, ref_out: np.ndarray, ref_len: np.ndarray, got_q
     bad = lib().oracle_compare_device_output(ctypes.byref(s), _p(ref_out), _p(ref_len), _p(got_qual), _p(got_start),
                                              _p(got_len), _p(exc), n_exc, int(aligned), nthreads,
                                              ctypes.byref(first))
+    return int(bad), int(first.value)
+
+
+def compare_compact_output(batch, ref_out: np.ndarray, ref_len: np.ndarray, got_chars: np.ndarray,
+                           got_off: np.ndarray, exceptions: Optional[np.ndarray] = None,
+                           nthreads: int = 8) -> Tuple[int, int]:
+    """compare_device_output for the compacted streamed outputs (chars at
+    u32 offsets per read, exceptions keyed by position in the chars)."""
+    s, keep = batch.c_struct()
+    ref_out = np.ascontiguousarray(ref_out, dtype=np.uint16)
+    ref_len = np.ascontiguousarray(ref_len, dtype=np.uint32)
+    got_chars = np.ascontiguousarray(got_chars, dtype=np.uint8)
+    if got_chars.size == 0:
+        got_chars = np.zeros(1, np.uint8)
+    got_off = np.ascontiguousarray(got_off).view(np.uint32)
+    exc = np.ascontiguousarray(exceptions if exceptions is not None else np.zeros(1, np.int64)).view(np.uint64)
+    n_exc = 0 if exceptions is None else len(exceptions)
+    first = ctypes.c_int64(-1)
+    bad = lib().oracle_compare_compact_output(ctypes.byref(s), _p(ref_out), _p(ref_len), _p(got_chars), _p(got_off),
+                                              _p(exc), n_exc, nthreads, ctypes.byref(first))
     return int(bad), int(first.value)
 
 

@@ -146,6 +146,50 @@ def test_crafted_table_chars_above_0xff(seed, em):
     assert ((ref[:n] >= 128) & (ref[:n] <= 0xFF)).sum() > 10  # non-ASCII bytes in the fast path
 
 
+def test_crafted_table_compacted_outputs():
+    """The streamed path's compacted outputs (bqsr_compact_outputs_async):
+    chars at u32 offsets per read, the exception list's entries rewritten to
+    positions in the chars -- on the crafted table whose chars go above 0xFF."""
+    import torch
+    d, w, keys = crafted_table(8)
+    batch = reads_for_keys(keys, 3000, 8)
+    fin = O.Final(d, w, 123.456)
+    ref, ref_len = O.apply(batch, fin)
+    ctx = bqsr.Context.get(0)
+    tab = bqsr.RecalTable(_capi.Dims(2, L10), ctx, expected_mismatch=123.456)
+    tab.set_words(w)
+    gfin = tab.finalize_table()
+    L = _capi.lib()
+    s, keep = batch.c_struct()
+    bh = ctypes.c_void_p()
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _capi.check(L.bqsr_batch_create(ctx.handle, ctypes.byref(s), sp, ctypes.byref(bh)))
+    try:
+        ns, n = int(L.bqsr_batch_slots(bh)), batch.n_reads
+        dev = torch.device("cuda", 0)
+        oq = torch.empty(ns + 64, dtype=torch.uint8, device=dev)
+        ost, oln = (torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2))
+        exc = torch.empty(1 << 16, dtype=torch.int64, device=dev)
+        chars = torch.empty(ns + 64, dtype=torch.uint8, device=dev)
+        off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _capi.check(L.bqsr_apply_stage(ctx.handle, bh, gfin.handle, p(oq), p(ost), p(oln), p(exc), 1 << 16,
+                                       _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
+        _capi.check(L.bqsr_compact_outputs_async(ctx.handle, bh, p(oq), p(ost), p(oln), p(exc), 1 << 16, p(chars),
+                                                 p(off), sp))
+        nexc = ctypes.c_int64()
+        _capi.check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
+        torch.cuda.synchronize()
+        assert nexc.value > 100
+        offs = off.cpu().numpy()
+        assert np.array_equal(np.diff(offs.astype(np.int64)), ref_len[:n].astype(np.int64))
+        bad, first = O.compare_compact_output(batch, ref, ref_len, chars.cpu().numpy()[:int(offs[n])], offs,
+                                              exc.cpu().numpy()[:nexc.value])
+        assert bad == 0, first
+    finally:
+        L.bqsr_batch_destroy(bh)
+
+
 # ---- known sites from the reference's VCF -------------------------------------
 
 def test_sites_from_small_vcf():

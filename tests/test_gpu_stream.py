@@ -46,13 +46,14 @@ def _odd_bases(b):
     return b
 
 
-@pytest.mark.parametrize("sizes,lens,n_rg,with_sites,odd,zero_copy,d2h", [
-    ((7000, 5000, 9000), (150,), 1, True, False, False, "kernel"),
-    ((3000, 1, 4000), (100, 250), 4, False, False, False, "kernel"),
-    ((4000, 6000), (101,), 2, False, True, False, "dma"),
-    ((4000, 6001), (101,), 2, False, True, False, "kernel"),
-    ((5000, 3000), (150,), 1, True, True, True, "kernel")])
-def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy, d2h):
+@pytest.mark.parametrize("sizes,lens,n_rg,with_sites,odd,zero_copy,d2h,compact", [
+    ((7000, 5000, 9000), (150,), 1, True, False, False, "kernel", None),
+    ((3000, 1, 4000), (100, 250), 4, False, False, False, "kernel", None),
+    ((4000, 6000), (101,), 2, False, True, False, "dma", None),
+    ((4000, 6001), (101,), 2, False, True, False, "kernel", None),
+    ((4000, 6001), (101,), 2, False, True, False, "kernel", False),
+    ((5000, 3000), (150,), 1, True, True, True, "kernel", None)])
+def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy, d2h, compact):
     import torch
     from adam_amd.stream import StreamedShard
     dev = torch.device("cuda", 0)
@@ -69,7 +70,8 @@ def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy, d2h)
     th = ctypes.c_void_p()
     _capi.check(L.bqsr_table_create(ctx.handle, d, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
     sh = StreamedShard(ctx, parts, d, snp.handle(ctx) if snp else None, 0,
-                       site_contigs=snp.contigs if snp else None, zero_copy=zero_copy, d2h=d2h)
+                       site_contigs=snp.contigs if snp else None, zero_copy=zero_copy, d2h=d2h, compact=compact)
+    assert sh.compact == (compact is not False and not zero_copy and d2h == "kernel")
     try:
         for _ in range(2):  # the second job re-uploads over the resident partitions
             em_t = sh.run(th)
@@ -80,14 +82,12 @@ def test_streamed_partitions(sizes, lens, n_rg, with_sites, odd, zero_copy, d2h)
         assert float(em_t.cpu()[0]) == o.em
         for i, p in enumerate(parts):
             ref_out, ref_len = o.outs[i]
-            q = sh.host_qual[i].numpy()
-            st, ln = sh.host_start[i].numpy(), sh.host_len[i].numpy()
-            assert np.array_equal(ln[:p.n_reads].astype(np.int64), ref_len.astype(np.int64)[:p.n_reads])
             slots = _slots(p)
             for r in range(p.n_reads):
                 a = int(p.qual_offset[r])
-                got = q[slots[r] + st[r]: slots[r] + st[r] + ln[r]].astype(np.uint16)
-                assert np.array_equal(got, ref_out[a:a + ln[r]]), (i, r)
+                got = sh.qual_chars(i, int(slots[r]), r)
+                assert np.array_equal(got, ref_out[a:a + int(ref_len[r])]), (i, r)
+            assert sh.outputs(i)[0] == ("compact" if sh.compact else "slots")
     finally:
         sh.close()
         L.bqsr_table_destroy(th)
