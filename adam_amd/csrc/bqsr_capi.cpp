@@ -175,9 +175,9 @@ constexpr size_t kLdsMax = 163840;
 // [qw][wcells] x {obs, mm} + masked counts + block histogram, apply's char
 // table [qw][cw][21]
 // (the context table only for the chunk walk, bqsr_observe_chunks)
-size_t observe_lds(int qw, int wcells, bool table) {
+size_t observe_lds(int qw, int wcells, bool table, int hq_span = 0) {
   return (table ? (size_t)kCtxTabBytes : 0) + (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 +
-         (size_t)kMkWords * 4;
+         (size_t)kMkWords * 4 + (size_t)hq_span * qw * 4;
 }
 // a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
 int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
@@ -192,9 +192,9 @@ int lean_orow(int nc, int cw) {
 size_t lean_lds(int qw, int orow, int wcells) { return ((size_t)qw * (orow + wcells) + qw + kQBins) * 4; }
 // copies of the lean window's counters: the most (<= 4) whose rows still hold the batch's qual span
 constexpr int kLeanCopiesMax = 4;
-int observe_rows(int wcells, bool table) {
+int observe_rows(int wcells, bool table, int hq_span = 0) {
   int qw = kQBins;
-  while (qw > 1 && observe_lds(qw, wcells, table) > kLdsMax) --qw;
+  while (qw > 1 && observe_lds(qw, wcells, table, hq_span) > kLdsMax) --qw;
   return qw;
 }
 // the host-packed layout is 16-aligned (ReadsDev::slots_aligned); device batches may be either
@@ -316,6 +316,7 @@ struct bqsr_batch {
   int32_t n_keys = 1;   // n_base * fronts
   int32_t n_base = 1;   // 2 * read group + mate class
   int32_t fronts = 0;   // > 0: front-ordered pieces, a chunk-walk workgroup per key (OrderDev::n_base)
+  bool hq_by_observe = false;  // the last observe kernel built the fold's block histograms (fronts)
   uint32_t* d_perm = nullptr;
   int64_t* d_key_off = nullptr;
   uint32_t* d_key_cnt = nullptr;
@@ -1159,6 +1160,17 @@ int lane_shift(const bqsr_batch* b) {
   while ((1 << s) < c && s < 6) ++s;
   return s;
 }
+// the most fold blocks one front's reads span (wg_begin / wg_of of the kernels)
+int fold_span(const bqsr_batch* b) {
+  const int64_t n = b->rd.n_reads, rpt = b->rd.reads_per_tile, nt = b->rd.n_tiles, G = b->n_blocks;
+  auto blk = [&](int64_t r) { return std::min(G - 1, ((r / rpt + 1) * G - 1) / nt); };
+  int span = 1;
+  for (int64_t f = 0; f < b->fronts; ++f) {
+    const int64_t r0 = (f * n + b->fronts - 1) / b->fronts, r1 = ((f + 1) * n + b->fronts - 1) / b->fronts - 1;
+    if (r1 >= r0) span = std::max<int>(span, (int)(blk(r1) - blk(r0) + 1));
+  }
+  return span;
+}
 bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
   if (b->dims.n_rg > t->dims.n_rg || b->dims.max_len > t->dims.max_len)
     return fail(BQSR_ERR_INVALID_ARG, "table dims smaller than the batch's (n_rg / max_len)");
@@ -1278,7 +1290,11 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       for (int q = 0; q < kQBins && P.rows_all; ++q)
         if (b->qhist[q] && (q < P.w.q_lo || q >= P.w.q_lo + P.w.qw)) P.rows_all = 0;
     } else {
-      P.w = window_rows(b, observe_rows(P.wcells, true));
+      // front-ordered pieces: the fold's block histograms from this kernel
+      // (a piece's reads lie in one front, whose fold blocks it counts in LDS)
+      P.n_fold = b->n_blocks;
+      P.hq_span = b->fronts > 0 ? fold_span(b) : 0;
+      P.w = window_rows(b, observe_rows(P.wcells, true, P.hq_span));
     }
     P.touched = t->touched();
     P.obs = t->obs();
@@ -1299,7 +1315,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = lean ? b->n_blocks : b->pass_blocks();  // (fronts: a chunk-walk workgroup per piece)
-    const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true);
+    const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true, P.hq_span);
+    b->hq_by_observe = P.hq_span > 0;
+    if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
     if (lean)
       hipLaunchKernelGGL(bqsr_observe_lean<true>, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     else
@@ -1312,7 +1330,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-    if (b->bucketed) {  // the observe kernel did not walk the fold's blocks: their histograms
+    if (b->bucketed && !b->hq_by_observe) {  // the observe kernel did not count the fold's blocks: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
                          b->n_blocks, lane_shift(b), b->d_hq);

@@ -946,12 +946,14 @@ struct LaneRead {
   int rg;
   int lq, ls;
   int cell0, dir; // cycle cell of offset o = cell0 + dir * o (DiscreteCycle + L)
+  int aux;        // a pass's own per-read value (set by its fread, carried to the read's chunks)
 };
 
 __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L) {
   LaneRead x;
   x.r = live ? r : rd.n_reads;
   x.ro = x.r;
+  x.aux = 0;
   ReadMeta m{0, 0, 0, 0, 0};
   ReadInfo inf{0, 0, 0, 0};
   if (live) {
@@ -1242,7 +1244,7 @@ constexpr uint32_t kPkRev = 0x8000u;  // packed flags: cycle direction -1
 // (fchunk(x, j, n, on, ld)), so a lane has kU chunks' loads in flight; x
 // holds r, slot, st, en, fl, rg, cell0 and dir of the chunk's read, j = jb +
 // 16k, n = en - st.
-template <uint32_t kAct, int kU, class LD, class FRead, class FLoad, class FChunk>
+template <uint32_t kAct, int kU, class LD, bool kAux, class FRead, class FLoad, class FChunk>
 __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* info, const OrderDev& ord, int64_t q0,
                                            int64_t q1, int64_t qstep, int L, int lane, uint32_t* mk, FRead&& fread,
                                            FLoad&& fload, FChunk&& fchunk) {
@@ -1258,7 +1260,7 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
     const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
     const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
     const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
-    const uint32_t p_rg = (uint32_t)x.rg;
+    const uint32_t p_rg = (uint32_t)x.rg, p_aux = (uint32_t)x.aux;
     for (uint32_t g00 = 0; g00 < total; g00 += 64 * kU) {
       LaneRead c[kU];
       int jj[kU];
@@ -1288,6 +1290,7 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
         c[u].dir = (fl & kPkRev) ? -1 : 1;
         c[u].cell0 = (int)(fl >> 16);
         c[u].rg = (int)bperm(ri, p_rg);
+        c[u].aux = kAux ? (int)bperm(ri, p_aux) : 0;
         const uint32_t ps_c = bperm(ri, ps);
         const int jb_c = rd.slots_aligned ? -(c[u].st & 15) : 0;
         jj[u] = jb_c + 16 * (int)(g0 + lane - ps_c);
@@ -1335,6 +1338,8 @@ struct ObsPiece {
   int rg_w, c_lo, cw, q_lo, qw, wcells;
   bool ident;
   uint32_t tb;  // LDS address of the context table
+  uint32_t* fh;  // front-ordered pieces: the fold blocks' qual histograms [hq_span][qw] (x.aux = block - blk0)
+  int blk0;      // the front's first fold block
 };
 
 __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsPiece& pc, const LaneRead& x, int j,
@@ -1371,6 +1376,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
       if (f) {
         atomicAdd(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k], 1u);
         if (!m) atomicAdd(&pc.w_obs[base + pc.cw + (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)], 1u);
+        if (pc.fh) atomicAdd(&pc.fh[__mul24(x.aux, pc.qw) + row], 1u);  // the fold's block histogram
       }
       fastm |= (uint32_t)f << k;
     }
@@ -1402,6 +1408,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
         const int ccell = cc0 + __mul24(x.dir, k);
         const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
         if (pc.ident) atomicAdd(&pc.blk_hist[q], 1u);
+        if (pc.fh) atomicAdd(&P.hq_block[(int64_t)(pc.blk0 + x.aux) * kQBins + q], 1u);
         const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
         atomicAdd((unsigned long long*)&P.touched[key], 1ull);
         if (!masked) {
@@ -1429,6 +1436,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
   uint32_t* mk_all = blk_hist + kQBins;
+  uint32_t* fh = P.hq_span > 0 ? mk_all + kMkWords : nullptr;  // [hq_span][qw]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* mk = mk_all + wave * 64;
@@ -1444,20 +1452,42 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
     if (p0 >= wb) break;
     if (p0 >= p1) continue;
     const WinGeom gm = win_geom(P.ord, P.g, key);
+    // front-ordered pieces (fronts of read indices, bqsr_capi.cpp fronts()): the
+    // piece's reads lie in its front, whose fold blocks' histograms it keeps in
+    // LDS -- the fold then needs no pass of its own over the quals
+    int blk0 = 0;
+    if (fh) {
+      const int64_t nf = P.ord.n_keys / P.ord.n_base, f = key / P.ord.n_base;
+      blk0 = (int)wg_of(P.rd, (f * P.rd.n_reads + nf - 1) / nf, P.n_fold);
+      for (int i = tid; i < P.hq_span * qw; i += blockDim.x) fh[i] = 0;
+    }
     const ObsPiece pc{w_obs, w_mm, w_masked, blk_hist, key_rg(P.ord, key, P.w.rg_lo), gm.c_lo, gm.cw, P.w.q_lo, qw,
-                      wcells, ident, (uint32_t)(uintptr_t)(LdsHalves)ctab};
+                      wcells, ident, (uint32_t)(uintptr_t)(LdsHalves)ctab, fh, blk0};
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
-    const auto fread = [&](const LaneRead& x, bool live) {
+    const auto fread = [&](LaneRead& x, bool live) {
       if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+      if (fh && live) x.aux = (int)wg_of(P.rd, x.r, P.n_fold) - blk0;  // the read's fold block, in the front
     };
     const auto fload = [&](const LaneRead& x, int j, bool on) { return observe_load(P, x, j, on); };
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) {
       observe_chunk(P, pc, x, j, n, on, ld);
     };
-    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
-                                                                      64 * kWaves, L, lane, mk, fread, fload, fchunk);
+    if (fh)
+      chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, true>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+                                                                           64 * kWaves, L, lane, mk, fread, fload,
+                                                                           fchunk);
+    else
+      chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+                                                                            64 * kWaves, L, lane, mk, fread, fload,
+                                                                            fchunk);
     __syncthreads();
+    if (fh)  // the fold blocks' histograms of this piece: one atomic per non-zero bin
+      for (int i = tid; i < P.hq_span * qw; i += blockDim.x) {
+        const uint32_t v = fh[i];
+        const int b = blk0 + i / qw, q = P.w.q_lo + i % qw;
+        if (v && b < P.n_fold) atomicAdd(&P.hq_block[(int64_t)b * kQBins + q], v);
+      }
     // ---- the piece's window -> its slab; window rows into the block histogram ----
     uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
     for (int i = tid; i < 2 * qw * wcells; i += blockDim.x) pb[i] = w_obs[i];
@@ -2144,7 +2174,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
     __syncthreads();
     const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb, (int)clean_rows[0],
                         (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C};
-    const auto fread = [&](const LaneRead& x, bool live) {
+    const auto fread = [&](LaneRead& x, bool live) {
       if (!live) return;
       if (x.fl & kInfoPass) {  // quality string passed through
         P.out_start[x.ro] = 0;
@@ -2158,7 +2188,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
       apply_chunk(P, &P, pc, x, j, n, on, ld);
     };
-    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
                                                                              64 * kWaves, L, lane, mk, fread, fload,
                                                                              fchunk);
   }  // pieces
