@@ -1311,6 +1311,24 @@ __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
   __hip_atomic_fetch_add((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+#ifdef ADAM_BQSR_WAVE_AGG
+// Wavefront-level aggregation before the LDS atomics (the north_star's form;
+// built only into the A/B library, tools/gpu_r04_agg.sh): the lanes adding 1
+// to one LDS word become one add of their count, by the first of them -- a
+// ballot round per distinct address among the pending lanes.
+__device__ __forceinline__ void lds_add_agg(uint32_t addr, bool on) {
+  const int lane = threadIdx.x & 63;
+  uint64_t todo = __builtin_amdgcn_ballot_w64(on);
+  while (todo) {
+    const int leader = (int)__builtin_ctzll(todo);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)addr, leader);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(((todo >> lane) & 1u) && addr == a);
+    if (lane == leader) lds_add(a, (uint32_t)__builtin_popcountll(m));
+    todo &= ~m;
+  }
+}
+#endif
+
 // Lane per chunk (chunk_walk): the same counts, each lane one 16-offset
 // chunk of the wavefront's reads laid end to end.  LDS: the window as in
 // bqsr_observe_lean's slab layout, then the walk's kMkWords markers.
@@ -1373,11 +1391,22 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
       const bool f = (unsigned)row < (unsigned)pc.qw && ((vmask >> k) & 1u);
       const bool m = (bm >> k) & 1u;
       const int base = __mul24(row, pc.wcells);
+#ifdef ADAM_BQSR_WAVE_AGG
+      {
+        const uint32_t a1 = (uint32_t)(uintptr_t)(LdsWords)(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k]);
+        const uint32_t a2 = (uint32_t)(uintptr_t)(LdsWords)&pc.w_obs[base + pc.cw +
+                                                                   (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)];
+        lds_add_agg(a1, f);
+        lds_add_agg(a2, f && !m);
+        if (pc.fh) lds_add_agg((uint32_t)(uintptr_t)(LdsWords)&pc.fh[__mul24(x.aux, pc.qw) + row], f);
+      }
+#else
       if (f) {
         atomicAdd(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k], 1u);
         if (!m) atomicAdd(&pc.w_obs[base + pc.cw + (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)], 1u);
         if (pc.fh) atomicAdd(&pc.fh[__mul24(x.aux, pc.qw) + row], 1u);  // the fold's block histogram
       }
+#endif
       fastm |= (uint32_t)f << k;
     }
   }
