@@ -600,9 +600,41 @@ __device__ __forceinline__ PrepCols prep_cols(const PrepParams& P, const PrepRec
   return c;
 }
 
+#ifdef ADAM_BQSR_SITES_LDS
+// A/B build (tools/build_variant.sh sites_lds -DADAM_BQSR_SITES_LDS): the
+// north_star's known-site search staged in LDS.  On coordinate-sorted input a
+// prep workgroup's 2048 reads cover a few kb of one contig; its slice of the
+// sorted site list goes to LDS once and each read binary-searches it
+// (SnpTable.isMaskedAtReadOffset, SnpTable.scala:15-23); reads outside the
+// slice (unsorted input, another contig) take the position bitmap.
+constexpr int kSiteLds = 4096;
+struct SiteWin {
+  const int64_t* s;  // LDS: the sites in [lo, hi) of `contig`
+  int n;             // < 0: no window
+  int contig;
+  int64_t lo, hi;
+};
+__device__ __forceinline__ bool sites_lds_acc(const SiteWin& W, int32_t contig, int64_t unclipped, int lq, uint32_t r0,
+                                              uint64_t acc[kAccWords]) {
+  const int64_t a = unclipped, b = unclipped + lq;
+  if (W.n < 0 || contig != W.contig || a < W.lo || b > W.hi) return false;
+  int lo = 0, hi = W.n;  // first site >= a
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (W.s[mid] < a) lo = mid + 1; else hi = mid;
+  }
+  for (int j = lo; j < W.n && W.s[j] < b; ++j) acc_bit(acc, r0 + (uint32_t)(W.s[j] - unclipped), 0);
+  return true;
+}
+#endif
+
 template <bool kStore>
 __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, const PrepCols& cols,
-                          uint64_t acc_out[kAccWords]) {
+                          uint64_t acc_out[kAccWords]
+#ifdef ADAM_BQSR_SITES_LDS
+                          , const SiteWin& W
+#endif
+                          ) {
   const ReadMeta m = x.m;
   const ReadAlign a = x.a;
   const uint16_t f = m.flags;
@@ -705,6 +737,9 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
       }
       bool linear = false;
       if (a.contig >= 0 && a.contig < P.sites.n_contigs) {
+#ifdef ADAM_BQSR_SITES_LDS
+        if (!sites_lds_acc(W, a.contig, unclipped, en, r0, acc))
+#endif
         if (!sites_bitmap_acc(P, a.contig, unclipped, en, r0, acc)) linear = true;
       }
       if (kStore) {
@@ -842,6 +877,52 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
   const int64_t n = P.rd.n_reads;
   const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
   const int lane = threadIdx.x & 63;
+#ifdef ADAM_BQSR_SITES_LDS
+  __shared__ int64_t s_sites[kSiteLds];
+  __shared__ SiteWin s_win;
+  if (threadIdx.x == 0) {
+    SiteWin w{s_sites, -1, -1, 0, 0};
+    const int64_t last = min(n, c0 + kPrepChunk) - 1;
+    if (P.sites.n_contigs > 0 && c0 <= last) {
+      // the window between the first and the last read's starts (+ a read's reach either side)
+      const ReadAlign fa = P.rd.align[c0], la = P.rd.align[last];
+      if (fa.contig == la.contig && fa.contig >= 0 && fa.contig < P.sites.n_contigs && la.start >= fa.start &&
+          la.start - fa.start < (int64_t)1 << 24) {
+        const int64_t lo = fa.start - kMaxReadLen, hi = la.start + 2 * kMaxReadLen;
+        const int64_t* sp = P.sites.pos + P.sites.off[fa.contig];
+        const int64_t ns = (int64_t)(P.sites.off[fa.contig + 1] - P.sites.off[fa.contig]);
+        int64_t a = 0, b = ns;  // first >= lo
+        while (a < b) {
+          const int64_t m = (a + b) >> 1;
+          if (sp[m] < lo) a = m + 1; else b = m;
+        }
+        int64_t e = a, f = ns;  // first >= hi
+        while (e < f) {
+          const int64_t m = (e + f) >> 1;
+          if (sp[m] < hi) e = m + 1; else f = m;
+        }
+        if (e - a <= kSiteLds) w = SiteWin{s_sites, (int)(e - a), fa.contig, lo, hi};
+        s_win = w;
+        s_win.lo = a;  // (the copy's source index, restored below)
+      } else {
+        s_win = w;
+      }
+    } else {
+      s_win = w;
+    }
+  }
+  __syncthreads();
+  if (s_win.n > 0) {
+    const int64_t* sp = P.sites.pos + P.sites.off[s_win.contig] + s_win.lo;
+    for (int i = threadIdx.x; i < s_win.n; i += blockDim.x) s_sites[i] = sp[i];
+  }
+  __syncthreads();
+  SiteWin W = s_win;
+  if (W.n >= 0) {  // the window's bounds again (lo held the copy's source index)
+    const ReadAlign fa = P.rd.align[c0];
+    W.lo = fa.start - kMaxReadLen;
+  }
+#endif
   // software pipeline: the record of the read two iterations ahead and the
   // CIGAR / MD of the next one load while this one is worked
   const int64_t rt = c0 + threadIdx.x;
@@ -852,7 +933,11 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
     const PrepRec x2 = i + 2 * kPrepThreads < kPrepChunk ? prep_rec(P, r + 2 * kPrepThreads) : PrepRec{};
     const PrepCols k1 = i + kPrepThreads < kPrepChunk ? prep_cols(P, x1) : PrepCols{};
     uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
+#ifdef ADAM_BQSR_SITES_LDS
+    const bool todo = r < n && !prep_fast<kStore>(P, r, x0, k0, acc, W);
+#else
     const bool todo = r < n && !prep_fast<kStore>(P, r, x0, k0, acc);
+#endif
     if (kStore) {
       if (todo) {
 #pragma unroll

@@ -64,6 +64,8 @@ struct SynthSpec {
   double p_unmapped, p_duplicate, p_secondary, p_n, p_q2tail, p_indel, p_softclip;
   int64_t first_read;     // index of read 0 in the whole dataset: reads [first, first + n) of one
                           // (seed, ...) dataset, so a rank's shard is a slice of the job's reads
+  int64_t sorted_total;   // > 0: coordinate-sorted (what `transform -sort_reads` leaves): read i of the
+                          // sorted_total-read dataset starts at i / sorted_total of the contig
 };
 
 // flag bits as include/adam_bqsr.h
@@ -177,7 +179,10 @@ void gen_read(const SynthSpec& sp, int64_t r, Read& R) {
   int64_t span = 0;
   for (uint32_t e : R.cigar)
     if ((e & 0xF) == 0 || (e & 0xF) == 2) span += e >> 4;
-  R.start = (int64_t)(g.uni() * (double)std::max<int64_t>(1, sp.contig_len - span - 1));
+  const double u_start = g.uni();
+  R.start = sp.sorted_total > 0
+                ? (int64_t)((double)r / (double)sp.sorted_total * (double)std::max<int64_t>(1, sp.contig_len - 600))
+                : (int64_t)(u_start * (double)std::max<int64_t>(1, sp.contig_len - span - 1));
   // MD over M bases (mismatch = sequencing error) and deletions
   int run = 0;
   int ro = 0;

@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--reads", type=int, default=None, help="reads per GPU (default: the config's)")
+    ap.add_argument("--sorted", action="store_true",
+                    help="coordinate-sorted reads (as after transform -sort_reads; the known-site A/B of cfg3)")
     ap.add_argument("--cpu-reads", type=int, default=10_000_000, help="oracle baseline sample (reads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed job's results")
@@ -183,7 +185,9 @@ def main():
         r0, r1 = rank * n, (rank + 1) * n
     n_reads = r1 - r0
     t_gen = time.time()
-    batch = synth.generate(n_reads, cfg["lens"], cfg["n_rg"], cfg["seed"], first_read=r0)
+    total = (args.reads or cfg["n_reads"]) * (1 if args.config == "cfg3" else world)
+    batch = synth.generate(n_reads, cfg["lens"], cfg["n_rg"], cfg["seed"], first_read=r0,
+                           sorted_total=total if args.sorted else 0)
     sites = synth.known_sites(cfg["sites"]) if cfg["sites"] else None
     snp = bqsr.SnpTable(sites) if sites else None
     t_gen = time.time() - t_gen
@@ -281,7 +285,7 @@ def main():
             "dtype": "u8 in, int64 counts, f64 recalibration",
             "data": "synthetic (deterministic generator, SURVEY.md 8d spec), resident in HBM",
             "config": {
-                "workload": WORKLOADS[args.config],
+                "workload": WORKLOADS[args.config] + (" (coordinate-sorted)" if args.sorted else ""),
                 "reads_per_gpu": R,
                 "bases_per_gpu": n_bases,
                 "reads_total": R * world if args.config != "cfg3" else (args.reads or cfg["n_reads"]),
