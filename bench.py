@@ -432,6 +432,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
     import torch.distributed as dist
 
     from adam_amd import _capi, synth
+    from adam_amd import distributed as D
     from adam_amd._capi import Dims, check
     from adam_amd.stream import StreamedShard
 

@@ -4,7 +4,7 @@ set -e
 TAG=$1; shift || true
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O="$R/gpurun_out/$TAG"; mkdir -p "$O"; cd "$R"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/pytest.log" 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=10 -v --timeout 300 --timeout-method thread > "$O/pytest.log" 2>&1 \
   || { tail -60 "$O/pytest.log"; exit 1; }
 tail -1 "$O/pytest.log"
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
