@@ -247,9 +247,8 @@ def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
         cols[name] = take(hdr.rg_column(key), rgi, pa.string())
     cols["recordGroupRunDateEpoch"] = take(hdr.rg_column("DT", "date"), rgi, pa.int64())
     cols["recordGroupPredictedMedianInsertSize"] = take(hdr.rg_column("PI", "int"), rgi, pa.int32())
-    t = pa.table([cols[name] for name, _ in ADAM_FIELDS], schema=schema())
-    t._adam_keep = keep  # (the host buffers back the arrays)
-    return t
+    # (the arrays hold their host buffers: pa.py_buffer keeps each numpy array alive)
+    return pa.table([cols[name] for name, _ in ADAM_FIELDS], schema=schema())
 
 
 class AdamWriter:
