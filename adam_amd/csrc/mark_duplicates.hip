@@ -399,3 +399,419 @@ bqsr_status mark_duplicates_device(bqsr_sam* s, int64_t* n_duplicates, std::vect
   return ok();
 }
 }  // namespace
+
+// ------------------------------------------------ across partitions ----
+// bqsr_dup_set (include/adam_sam.h): MarkDuplicates' groupBy over every
+// partition of one input.  Each partition's parse leaves a compact record
+// per read -- a 128-bit bucket key (two independent 64-bit hashes of (rg,
+// QNAME)), class, packed 5' position and score of primary reads, library
+// rank -- appended in input order, so a read's global index is its slot.
+// finish() runs the single-parse passes over the records (the bucket keys
+// sorted stably with the slot: a bucket's reads stay in input order) and
+// leaves one duplicate bit per read; apply() sets the bits of a re-parse.
+// Names of reads in different partitions are never compared: two names share
+// a bucket only when both 64-bit hashes agree (no host fallback here).
+
+namespace mdupd {
+
+__device__ __forceinline__ void name_hashes(const DevSam& S, int64_t r, uint64_t* a, uint64_t* b) {
+  const uint8_t* p;
+  const int k = name_len(S, r, &p);
+  uint64_t h = 0xcbf29ce484222325ull, g2 = 0x243F6A8885A308D3ull;
+  const uint32_t f = S.flags[r];
+  const uint32_t g = (f & BQSR_F_HAS_RG) ? (uint32_t)S.rg_id[r] + 1u : 0u;
+  auto step2 = [](uint64_t x, uint32_t c) {
+    x = (x ^ (c + 0x9E3779B97F4A7C15ull)) * 0xBF58476D1CE4E5B9ull;
+    return x ^ (x >> 29);
+  };
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t c = (g >> (8 * i)) & 0xFFu;
+    h = (h ^ c) * 0x100000001b3ull;
+    g2 = step2(g2, c);
+  }
+  for (int i = 0; i < k; ++i) {
+    h = (h ^ p[i]) * 0x100000001b3ull;
+    g2 = step2(g2, p[i]);
+  }
+  g2 = step2(g2, 0x100u + (uint32_t)k);
+  *a = h;
+  *b = g2;
+}
+
+// a thread per read of one partition: its record at slot base + r
+extern "C" __global__ void __launch_bounds__(kThreads) mdup_set_records(DevSam S, int64_t base, uint64_t* k1,
+                                                                       uint64_t* k2, uint64_t* pos, int32_t* score,
+                                                                       uint16_t* lib, uint8_t* cls, int* bad) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < S.n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = base + r;
+    name_hashes(S, r, &k1[o], &k2[o]);
+    const uint32_t f = S.flags[r];
+    const int c = read_class(f);
+    uint64_t p = kNoPos;
+    int32_t sc = 0;
+    if (c == 1) {
+      p = pack_pos(S.sq_id[r], five_prime(S, r), f & BQSR_F_NEG_STRAND, bad);
+      for (uint64_t k = S.qual_off[r]; k < S.qual_off[r + 1]; ++k) {
+        const int v = (int)(int8_t)(uint8_t)(S.qual[k] - 33);
+        if (v >= 15) sc += v;
+      }
+    }
+    int32_t lb = 0;
+    if ((f & BQSR_F_HAS_RG) && S.rg_id[r] >= 0 && S.rg_id[r] < S.n_rg) lb = S.rg_lib[S.rg_id[r]];
+    if (lb >= 4096) atomicOr(bad, 4);
+    pos[o] = p;
+    score[o] = sc;
+    lib[o] = (uint16_t)(lb & 0xFFF);
+    cls[o] = (uint8_t)c;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(kThreads) mdup_iota(int64_t n, uint32_t* idx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    idx[i] = (uint32_t)i;
+}
+
+// heads of the (k1, k2)-sorted slots
+extern "C" __global__ void __launch_bounds__(kThreads) mdup_set_heads(const uint64_t* k1s, const uint64_t* k2,
+                                                                     const uint32_t* idx, int64_t n, uint32_t* head) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    head[i] = (i == 0 || k1s[i] != k1s[i - 1] || k2[idx[i]] != k2[idx[i - 1]]) ? 1u : 0u;
+}
+
+// mdup_buckets over the records
+extern "C" __global__ void __launch_bounds__(kThreads) mdup_set_buckets(
+    const uint64_t* pos, const int32_t* rscore, const uint16_t* lib, const uint8_t* cls, const uint32_t* idx,
+    const uint32_t* head_pos, int64_t nb, int64_t n, uint64_t* kll, uint64_t* kr, uint32_t* first, int32_t* score) {
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nb; b += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = head_pos[b], i1 = b + 1 < nb ? (int64_t)head_pos[b + 1] : n;
+    int64_t p0 = -1, p1 = -1, s0 = -1, u0 = -1;
+    int32_t sc = 0;
+    for (int64_t i = i0; i < i1; ++i) {
+      const int64_t r = idx[i];
+      const int c = cls[r];
+      if (c == 1) {
+        if (p0 < 0) p0 = r; else if (p1 < 0) p1 = r;
+        sc += rscore[r];
+      } else if (c == 2) {
+        if (s0 < 0) s0 = r;
+      } else if (u0 < 0) {
+        u0 = r;
+      }
+    }
+    uint64_t left = kNoPos, right = kNoPos;
+    if (p0 >= 0) {
+      const uint64_t a = pos[p0];
+      if (p1 >= 0) {
+        const uint64_t c = pos[p1];
+        left = a < c ? a : c;
+        right = a < c ? c : a;
+      } else {
+        left = a;
+      }
+    }
+    const int64_t r0 = p0 >= 0 ? p0 : s0 >= 0 ? s0 : u0;
+    kll[b] = (left << 12) | (uint64_t)lib[r0];
+    kr[b] = right;
+    first[b] = idx[i0];
+    score[b] = sc;
+  }
+}
+
+// the duplicate bit of every slot
+extern "C" __global__ void __launch_bounds__(kThreads) mdup_set_mark(const uint32_t* idx, const uint32_t* incl,
+                                                                    int64_t n, const uint8_t* outcome,
+                                                                    const uint8_t* cls, uint32_t* bits,
+                                                                    unsigned long long* n_dup) {
+  uint32_t cnt = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = idx[i];
+    const uint8_t o = outcome[incl[i] - 1];
+    const int c = cls[r];
+    const bool dup = c == 1 ? (o == kFragDup || o == kLose) : c == 2 ? (o != kNone) : false;
+    if (dup) {
+      atomicOr(&bits[r >> 5], 1u << (r & 31));
+      ++cnt;
+    }
+  }
+  if (cnt) atomicAdd(n_dup, (unsigned long long)cnt);
+}
+
+// a re-parse of slots [base, base + n): FLAG 0x400 from the bits
+extern "C" __global__ void __launch_bounds__(kThreads) mdup_set_apply(const uint32_t* bits, int64_t base, int64_t n,
+                                                                     uint32_t* flags, unsigned long long* n_dup) {
+  uint32_t cnt = 0;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t o = (uint64_t)(base + r);
+    const bool dup = (bits[o >> 5] >> (o & 31)) & 1u;
+    const uint32_t f = flags[r];
+    flags[r] = dup ? (f | BQSR_F_DUPLICATE) : (f & ~(uint32_t)BQSR_F_DUPLICATE);
+    cnt += dup;
+  }
+  if (cnt) atomicAdd(n_dup, (unsigned long long)cnt);
+}
+
+}  // namespace mdupd
+
+struct bqsr_dup_set {
+  bqsr_context* ctx = nullptr;
+  int64_t n = 0, cap = 0;
+  uint64_t *k1 = nullptr, *k2 = nullptr, *pos = nullptr;
+  int32_t* score = nullptr;
+  uint16_t* lib = nullptr;
+  uint8_t* cls = nullptr;
+  int* bad = nullptr;
+  unsigned long long* cnt = nullptr;
+  uint32_t* bits = nullptr;
+  std::vector<int64_t> part_base, part_n;
+  std::vector<std::string> libs;  // sorted LB strings of the header (the first partition's)
+  bool have_libs = false, finished = false;
+  int64_t n_dup = 0;
+  void free_records() {
+    for (void* p : {(void*)k1, (void*)k2, (void*)pos, (void*)score, (void*)lib, (void*)cls})
+      if (p) (void)hipFree(p);
+    k1 = k2 = pos = nullptr;
+    score = nullptr;
+    lib = nullptr;
+    cls = nullptr;
+    cap = 0;
+  }
+  ~bqsr_dup_set() {
+    free_records();
+    for (void* p : {(void*)bad, (void*)cnt, (void*)bits})
+      if (p) (void)hipFree(p);
+  }
+};
+
+namespace {
+std::vector<std::string> sam_libraries(const bqsr_sam* s) {
+  std::vector<std::string> libs;
+  for (size_t g = 0; g < s->rg_library.size(); ++g)
+    if (g < s->rg_has_lb.size() && s->rg_has_lb[g]) libs.push_back(s->rg_library[g]);
+  std::sort(libs.begin(), libs.end());
+  libs.erase(std::unique(libs.begin(), libs.end()), libs.end());
+  return libs;
+}
+
+template <class T>
+bqsr_status grow(T** p, int64_t n_old, int64_t cap, hipStream_t st) {
+  T* q = nullptr;
+  HIP_TRY(hipMalloc((void**)&q, (size_t)cap * sizeof(T)));
+  if (*p && n_old) {
+    const hipError_t e = hipMemcpyAsync(q, *p, (size_t)n_old * sizeof(T), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) (void)hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      (void)hipFree(q);
+      return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
+    }
+  }
+  if (*p) (void)hipFree(*p);
+  *p = q;
+  return ok();
+}
+}  // namespace
+
+bqsr_status bqsr_dup_set_create(bqsr_context* ctx, int64_t reads_hint, bqsr_dup_set** out) {
+  if (!ctx || !out) return fail(BQSR_ERR_INVALID_ARG, "null");
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(ctx->device));
+  auto* d = new bqsr_dup_set();
+  d->ctx = ctx;
+  d->cap = std::max<int64_t>(0, reads_hint);
+  hipStream_t st = hipStreamPerThread;
+  bqsr_status e = BQSR_OK;
+  if (d->cap) {
+    const int64_t c = d->cap;
+    d->cap = 0;
+    if ((e = grow(&d->k1, 0, c, st)) || (e = grow(&d->k2, 0, c, st)) || (e = grow(&d->pos, 0, c, st)) ||
+        (e = grow(&d->score, 0, c, st)) || (e = grow(&d->lib, 0, c, st)) || (e = grow(&d->cls, 0, c, st))) {
+      delete d;
+      return e;
+    }
+    d->cap = c;
+  }
+  if (hipMalloc((void**)&d->bad, sizeof(int)) != hipSuccess ||
+      hipMalloc((void**)&d->cnt, sizeof(unsigned long long)) != hipSuccess) {
+    delete d;
+    return fail(BQSR_ERR_DEVICE, "dup set: out of device memory");
+  }
+  HIP_TRY(hipMemset(d->bad, 0, sizeof(int)));
+  *out = d;
+  return ok();
+}
+
+void bqsr_dup_set_destroy(bqsr_dup_set* d) { delete d; }
+
+bqsr_status bqsr_dup_set_add(bqsr_dup_set* d, const bqsr_sam* s) {
+  using namespace mdupd;
+  if (!d || !s) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (d->finished) return fail(BQSR_ERR_INVALID_ARG, "bqsr_dup_set_add after bqsr_dup_set_finish");
+  if (s->ctx != d->ctx) return fail(BQSR_ERR_INVALID_ARG, "parse of another context");
+  HIP_TRY(hipSetDevice(d->ctx->device));
+  const std::vector<std::string> libs = sam_libraries(s);
+  if (!d->have_libs) {
+    d->libs = libs;
+    d->have_libs = true;
+  } else if (libs != d->libs) {
+    return fail(BQSR_ERR_INVALID_ARG, "partitions of one input must share the header's libraries");
+  }
+  const int64_t n = s->n_reads;
+  if (d->n + n >= (1ll << 32) - 1) return fail(BQSR_ERR_UNSUPPORTED, "more than 2^32 - 1 reads in a dup set");
+  hipStream_t st = hipStreamPerThread;
+  if (d->n + n > d->cap) {
+    const int64_t c = std::max<int64_t>(d->n + n, d->cap + d->cap / 2 + 1024);
+    bqsr_status e;
+    if ((e = grow(&d->k1, d->n, c, st)) || (e = grow(&d->k2, d->n, c, st)) || (e = grow(&d->pos, d->n, c, st)) ||
+        (e = grow(&d->score, d->n, c, st)) || (e = grow(&d->lib, d->n, c, st)) || (e = grow(&d->cls, d->n, c, st)))
+      return e;
+    d->cap = c;
+  }
+  d->part_base.push_back(d->n);
+  d->part_n.push_back(n);
+  if (n == 0) return ok();
+  std::vector<int32_t> rg_lib((size_t)std::max(1, s->n_rg), 0);
+  for (int32_t g = 0; g < s->n_rg; ++g)
+    if ((size_t)g < s->rg_has_lb.size() && s->rg_has_lb[(size_t)g])
+      rg_lib[(size_t)g] = 1 + (int32_t)(std::lower_bound(libs.begin(), libs.end(), s->rg_library[(size_t)g]) - libs.begin());
+  int32_t* d_rglib = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_rglib, rg_lib.size() * 4));
+  hipError_t he = hipMemcpyAsync(d_rglib, rg_lib.data(), rg_lib.size() * 4, hipMemcpyHostToDevice, st);
+  if (he == hipSuccess) {
+    DevSam S{s->d_text, s->line_span, s->flags, s->rg_id, s->sq_id, s->start, s->qual_off, s->qual, s->cig_off,
+             s->cig, d_rglib, s->n_rg, n};
+    const unsigned g = (unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)d->ctx->n_cu * 16);
+    hipLaunchKernelGGL(mdup_set_records, dim3(g), dim3(kThreads), 0, st, S, d->n, d->k1, d->k2, d->pos, d->score,
+                       d->lib, d->cls, d->bad);
+    he = hipGetLastError();
+    if (he == hipSuccess) he = hipStreamSynchronize(st);
+  }
+  (void)hipFree(d_rglib);
+  if (he != hipSuccess) return fail(BQSR_ERR_DEVICE, hipGetErrorString(he));
+  d->n += n;
+  return ok();
+}
+
+bqsr_status bqsr_dup_set_finish(bqsr_dup_set* d, int64_t* n_duplicates) {
+  using namespace mdupd;
+  if (!d) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (d->finished) {
+    if (n_duplicates) *n_duplicates = d->n_dup;
+    return ok();
+  }
+  HIP_TRY(hipSetDevice(d->ctx->device));
+  hipStream_t st = hipStreamPerThread;
+  const int64_t n = d->n;
+  const size_t words = (size_t)(n + 31) / 32 + 1;
+  HIP_TRY(hipMalloc((void**)&d->bits, words * 4));
+  HIP_TRY(hipMemsetAsync(d->bits, 0, words * 4, st));
+  HIP_TRY(hipMemsetAsync(d->cnt, 0, sizeof(unsigned long long), st));
+  if (n == 0) {
+    HIP_TRY(hipStreamSynchronize(st));
+    d->finished = true;
+    d->free_records();
+    if (n_duplicates) *n_duplicates = 0;
+    return ok();
+  }
+  int hbad = 0;
+  HIP_TRY(hipMemcpyAsync(&hbad, d->bad, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hbad) return fail(BQSR_ERR_UNSUPPORTED, "MarkDuplicates: a position or library beyond the packed keys");
+  std::vector<void*> tmp;
+  struct Free {
+    std::vector<void*>& v;
+    ~Free() {
+      for (void* p : v) (void)hipFree(p);
+    }
+  } fr{tmp};
+  auto alloc = [&](auto** p, size_t count) -> bqsr_status { return dalloc(tmp, p, std::max<size_t>(count, 1)); };
+  const size_t N = (size_t)n;
+  uint64_t *ka = nullptr, *kb = nullptr, *kll = nullptr, *kr = nullptr;
+  uint32_t *idx = nullptr, *idx2 = nullptr, *head = nullptr, *incl = nullptr, *hpos = nullptr, *first = nullptr;
+  uint32_t *ord = nullptr, *ord2 = nullptr;
+  int32_t* score = nullptr;
+  uint8_t* outcome = nullptr;
+  bqsr_status e = BQSR_OK;
+  if ((e = alloc(&ka, N)) || (e = alloc(&kb, N)) || (e = alloc(&idx, N)) || (e = alloc(&idx2, N)) ||
+      (e = alloc(&head, N)) || (e = alloc(&incl, N)) || (e = alloc(&hpos, N)))
+    return e;
+  size_t tb = 0, tb2 = 0;
+  HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, ka, kb, idx, idx2, N, 0, 64, st));
+  HIP_TRY(rocprim::inclusive_scan(nullptr, tb2, head, incl, N, rocprim::plus<uint32_t>(), st));
+  tb = std::max(tb, tb2);
+  void* temp = nullptr;
+  if ((e = dalloc(tmp, (uint8_t**)&temp, tb))) return e;
+  const unsigned g = (unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)d->ctx->n_cu * 16);
+  // 1. slots sorted by (k1, k2), stable: k2 pass, then k1 pass
+  hipLaunchKernelGGL(mdup_iota, dim3(g), dim3(kThreads), 0, st, n, idx);
+  size_t t = tb;
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t, d->k2, kb, idx, idx2, N, 0, 64, st));
+  hipLaunchKernelGGL(mdup_gather, dim3(g), dim3(kThreads), 0, st, (const uint64_t*)d->k1, (const uint32_t*)idx2, n, ka);
+  t = tb;
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t, ka, kb, idx2, idx, N, 0, 64, st));
+  hipLaunchKernelGGL(mdup_set_heads, dim3(g), dim3(kThreads), 0, st, (const uint64_t*)kb, (const uint64_t*)d->k2,
+                     (const uint32_t*)idx, n, head);
+  t = tb;
+  HIP_TRY(rocprim::inclusive_scan(temp, t, head, incl, N, rocprim::plus<uint32_t>(), st));
+  hipLaunchKernelGGL(mdup_head_pos, dim3(g), dim3(kThreads), 0, st, (const uint32_t*)head, (const uint32_t*)incl, n,
+                     hpos);
+  uint32_t nb32 = 0;
+  HIP_TRY(hipMemcpyAsync(&nb32, incl + (n - 1), 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t nb = nb32;
+  if ((e = alloc(&kll, (size_t)nb)) || (e = alloc(&kr, (size_t)nb)) || (e = alloc(&first, (size_t)nb)) ||
+      (e = alloc(&ord, (size_t)nb)) || (e = alloc(&ord2, (size_t)nb)) || (e = alloc(&score, (size_t)nb)) ||
+      (e = alloc(&outcome, (size_t)nb)))
+    return e;
+  const unsigned gb = (unsigned)std::min<int64_t>((nb + kThreads - 1) / kThreads, (int64_t)d->ctx->n_cu * 16);
+  // 2. per bucket; 3. bucket order; 4. groups (the single-parse passes)
+  hipLaunchKernelGGL(mdup_set_buckets, dim3(gb), dim3(kThreads), 0, st, (const uint64_t*)d->pos,
+                     (const int32_t*)d->score, (const uint16_t*)d->lib, (const uint8_t*)d->cls, (const uint32_t*)idx,
+                     (const uint32_t*)hpos, nb, n, kll, kr, first, score);
+  hipLaunchKernelGGL(mdup_first_keys, dim3(gb), dim3(kThreads), 0, st, (const uint32_t*)first, nb, ka, ord2);
+  t = tb;
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t, ka, kb, ord2, ord, (size_t)nb, 0, 32, st));
+  hipLaunchKernelGGL(mdup_gather, dim3(gb), dim3(kThreads), 0, st, (const uint64_t*)kr, (const uint32_t*)ord, nb, ka);
+  t = tb;
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t, ka, kb, ord, ord2, (size_t)nb, 0, 52, st));
+  hipLaunchKernelGGL(mdup_gather, dim3(gb), dim3(kThreads), 0, st, (const uint64_t*)kll, (const uint32_t*)ord2, nb, ka);
+  t = tb;
+  HIP_TRY(rocprim::radix_sort_pairs(temp, t, ka, kb, ord2, ord, (size_t)nb, 0, 64, st));
+  hipLaunchKernelGGL(mdup_groups, dim3(gb), dim3(kThreads), 0, st, (const uint32_t*)ord, (const uint64_t*)kll,
+                     (const uint64_t*)kr, (const int32_t*)score, nb, outcome);
+  // 5. the bits
+  hipLaunchKernelGGL(mdup_set_mark, dim3(g), dim3(kThreads), 0, st, (const uint32_t*)idx, (const uint32_t*)incl, n,
+                     (const uint8_t*)outcome, (const uint8_t*)d->cls, d->bits, d->cnt);
+  unsigned long long hn = 0;
+  HIP_TRY(hipMemcpyAsync(&hn, d->cnt, sizeof hn, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(hipGetLastError());
+  d->n_dup = (int64_t)hn;
+  d->finished = true;
+  d->free_records();
+  if (n_duplicates) *n_duplicates = d->n_dup;
+  return ok();
+}
+
+bqsr_status bqsr_dup_set_apply(bqsr_dup_set* d, int64_t part, bqsr_sam* s, int64_t* n_duplicates) {
+  using namespace mdupd;
+  if (!d || !s) return fail(BQSR_ERR_INVALID_ARG, "null");
+  if (!d->finished) return fail(BQSR_ERR_INVALID_ARG, "bqsr_dup_set_apply before bqsr_dup_set_finish");
+  if (part < 0 || (size_t)part >= d->part_n.size()) return fail(BQSR_ERR_INVALID_ARG, "no such partition");
+  if (d->part_n[(size_t)part] != s->n_reads)
+    return fail(BQSR_ERR_INVALID_ARG, "the parse's read count differs from the partition added");
+  HIP_TRY(hipSetDevice(d->ctx->device));
+  hipStream_t st = hipStreamPerThread;
+  const int64_t n = s->n_reads;
+  unsigned long long hn = 0;
+  if (n) {
+    HIP_TRY(hipMemsetAsync(d->cnt, 0, sizeof(unsigned long long), st));
+    const unsigned g = (unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)d->ctx->n_cu * 16);
+    hipLaunchKernelGGL(mdup_set_apply, dim3(g), dim3(kThreads), 0, st, (const uint32_t*)d->bits,
+                       d->part_base[(size_t)part], n, s->flags, d->cnt);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&hn, d->cnt, sizeof hn, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  s->dup_marked = true;
+  if (n_duplicates) *n_duplicates = (int64_t)hn;
+  return ok();
+}

@@ -61,6 +61,11 @@ def _lib():
             "bqsr_sam_text_download": (ctypes.c_int, [vp, ctypes.c_char_p]),
             "bqsr_mark_duplicates": (ctypes.c_int, [ctypes.POINTER(DupReads), vp]),
             "bqsr_sam_mark_duplicates": (ctypes.c_int, [vp, ctypes.POINTER(i64)]),
+            "bqsr_dup_set_create": (ctypes.c_int, [vp, i64, pp]),
+            "bqsr_dup_set_add": (ctypes.c_int, [vp, vp]),
+            "bqsr_dup_set_finish": (ctypes.c_int, [vp, ctypes.POINTER(i64)]),
+            "bqsr_dup_set_apply": (ctypes.c_int, [vp, i64, vp, ctypes.POINTER(i64)]),
+            "bqsr_dup_set_destroy": (None, [vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -142,6 +147,45 @@ class SamText:
     def close(self):
         if self.h:
             self.L.bqsr_sam_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DupSet:
+    """MarkDuplicates across the partitions of one input (bqsr_dup_set):
+    add() every partition's parse in input order, finish(), then apply(i,
+    parse) to a re-parse of partition i."""
+
+    def __init__(self, ctx: Optional[bqsr.Context] = None, reads_hint: int = 0):
+        self.L = _lib()
+        self.ctx = ctx or bqsr.Context.get(0)
+        self.h = ctypes.c_void_p()
+        check(self.L.bqsr_dup_set_create(self.ctx.handle, int(reads_hint), ctypes.byref(self.h)))
+        self.parts = 0
+
+    def add(self, sam: SamText) -> int:
+        check(self.L.bqsr_dup_set_add(self.h, sam.h))
+        self.parts += 1
+        return self.parts - 1
+
+    def finish(self) -> int:
+        n = ctypes.c_int64()
+        check(self.L.bqsr_dup_set_finish(self.h, ctypes.byref(n)))
+        return int(n.value)
+
+    def apply(self, part: int, sam: SamText) -> int:
+        n = ctypes.c_int64()
+        check(self.L.bqsr_dup_set_apply(self.h, int(part), sam.h, ctypes.byref(n)))
+        return int(n.value)
+
+    def close(self):
+        if self.h:
+            self.L.bqsr_dup_set_destroy(self.h)
             self.h = ctypes.c_void_p()
 
     def __del__(self):

@@ -32,8 +32,11 @@ stage, cli/Transform.scala:62-97), QUAL rewritten on the device and the
 records appended to the output.  Errors are raised in the reference's order:
 observe errors partition by partition, finalize, then apply errors partition
 by partition; the output file appears only when the job succeeds.
-MarkDuplicates groups reads across the whole input (its groupBy), so it runs
-on one partition: with -mark_duplicate_reads the input is not cut.
+MarkDuplicates groups reads across the whole input (its groupBy): with
+-mark_duplicate_reads every partition is parsed once more up front and its
+reads' compact MarkDuplicates records (sam.DupSet, bqsr_dup_set_*) collected
+on the device; the duplicate bits, found over all partitions, are set on each
+partition's parse before BQSR observes it and before it is written.
 """
 from __future__ import annotations
 
@@ -78,10 +81,12 @@ def sam_partitions(data, partition_bytes: int) -> Tuple[bytes, List[Tuple[int, i
 
 
 def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ctx, device: int, emit,
-                     max_exc: int = 1 << 16) -> Dict[str, float]:
+                     max_exc: int = 1 << 16, dups=None) -> Dict[str, float]:
     """BQSR over several partitions of one SAM input (see the module doc);
     emit(i, sam) gets every partition's parse with its QUAL fields rewritten,
-    in partition order."""
+    in partition order.  dups: a finished sam.DupSet over the same
+    partitions (MarkDuplicates' bits set on every parse before its batch is
+    built and before it is rewritten)."""
     import torch
     L = _capi.lib()
     dev = torch.device("cuda", device)
@@ -100,6 +105,8 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
         for a, b in ranges:
             sam = SamText(header + bytes(data[a:b]), ctx)
             try:
+                if dups is not None:
+                    dups.apply(len(batches), sam)
                 rb = sam.batch()
             finally:
                 sam.close()
@@ -145,6 +152,8 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
                                       "list" % (i, nexc.value))
             sam = SamText(header + bytes(data[a:b]), ctx)
             try:
+                if dups is not None:
+                    dups.apply(i, sam)
                 check(L.bqsr_sam_rewrite_quals(h, sam.h, bh, ptr(out_qual), ptr(out_start), ptr(out_len), ptr(exc),
                                                nexc.value, sp))
                 emit(i, sam)
@@ -161,6 +170,49 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
             if bh:
                 L.bqsr_batch_destroy(bh)
     return {"reads": n_reads, "partitions": len(ranges)}
+
+
+def _partitions(data, header: bytes, ranges, mark_duplicates: bool, recalibrate: bool, dbsnp, ctx, device: int,
+                emit) -> Dict[str, float]:
+    """A SAM input of several partitions: MarkDuplicates over all of them
+    (a DupSet: every partition parsed once for its compact records), then
+    BQSR over the partitions streamed through the device, or (without BQSR)
+    every partition re-parsed, its FLAG fields rewritten and emitted."""
+    from .sam import DupSet
+    dups = None
+    stats: Dict[str, float] = {}
+    try:
+        if mark_duplicates:
+            dups = DupSet(ctx)
+            for a, b in ranges:
+                sam = SamText(header + bytes(data[a:b]), ctx)
+                try:
+                    dups.add(sam)
+                finally:
+                    sam.close()
+            n_dup = dups.finish()
+        if recalibrate:
+            snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
+            stats = _bqsr_partitions(data, header, ranges, snp if snp.table else None, ctx, device, emit,
+                                     dups=dups)
+        else:
+            n_reads = 0
+            for i, (a, b) in enumerate(ranges):
+                sam = SamText(header + bytes(data[a:b]), ctx)
+                try:
+                    n_reads += sam.counts().n_reads
+                    dups.apply(i, sam)
+                    sam.rewrite(None)
+                    emit(i, sam)
+                finally:
+                    sam.close()
+            stats = {"reads": n_reads, "partitions": len(ranges)}
+        if dups is not None:
+            stats["duplicates"] = n_dup
+    finally:
+        if dups is not None:
+            dups.close()
+    return stats
 
 
 def is_parquet(path: str) -> bool:
@@ -299,13 +351,11 @@ def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bo
             try:
                 bam = is_bam(data)
                 ranges = None
-                if recalibrate and not mark_duplicates and not bam and len(data):
+                if (recalibrate or mark_duplicates) and not bam and len(data):
                     header, ranges = sam_partitions(data, partition_bytes)
                 if ranges is not None and len(ranges) > 1:
-                    # BQSR over partitions streamed through the device
-                    snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
-                    stats = _bqsr_partitions(data, header, ranges, snp if snp.table else None, ctx, device,
-                                             sink.emit)
+                    stats = _partitions(data, header, ranges, mark_duplicates, recalibrate, dbsnp, ctx, device,
+                                        sink.emit)
                 else:
                     sam = SamText(bytes(data), ctx, bam=bam)
                     try:
@@ -350,7 +400,7 @@ def main(argv=None) -> int:
         ap.add_argument(flag, action="store_true")
     ap.add_argument("-coalesce", type=int, default=-1)
     ap.add_argument("-partition_bytes", type=int, default=DEFAULT_PARTITION_BYTES,
-                    help="records per streamed partition, in bytes of SAM text (BQSR without MarkDuplicates)")
+                    help="records per streamed partition, in bytes of SAM text")
     ap.add_argument("-parquet_compression", default="gzip", choices=("gzip", "snappy", "zstd", "none"),
                     help="ADAM output: the part files' codec (adamSave's default: GZIP)")
     ap.add_argument("-part_reads", type=int, default=1 << 20, help="ADAM output: records per part file")

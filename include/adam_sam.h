@@ -178,6 +178,28 @@ bqsr_status bqsr_mark_duplicates(const bqsr_dup_reads* reads, uint8_t* dup);
  * `transform -mark_duplicate_reads` does before BQSR. */
 bqsr_status bqsr_sam_mark_duplicates(bqsr_sam* s, int64_t* n_duplicates);
 
+/* MarkDuplicates across the partitions of one input (the reference's
+ * groupBy spans every partition of the RDD, MarkDuplicates.scala:43-58).
+ * add: one partition's parse (partitions in input order, each parsed with
+ * the same header); its reads get global indices after those added before.
+ * Per read the set keeps a compact record on the device (two 64-bit hashes
+ * of (rg, QNAME), class, packed 5' position, score, library rank; 31 bytes),
+ * so partitions need not stay resident.  finish: buckets, groups and the
+ * duplicate bit of every read (the passes of bqsr_sam_mark_duplicates);
+ * records are released.  apply: a parse of partition `part` (the same text
+ * as added) gets its reads' duplicateRead bits, as bqsr_sam_mark_duplicates
+ * leaves them.  Reads of different partitions share a bucket when both
+ * hashes agree (names are not compared across partitions: a 128-bit
+ * collision would merge two buckets).  BQSR_ERR_UNSUPPORTED for more than
+ * 2^32 - 1 reads or positions / libraries beyond the packed keys;
+ * BQSR_ERR_INVALID_ARG for partitions whose headers name other libraries. */
+typedef struct bqsr_dup_set bqsr_dup_set;
+bqsr_status bqsr_dup_set_create(bqsr_context* ctx, int64_t reads_hint, bqsr_dup_set** out);
+bqsr_status bqsr_dup_set_add(bqsr_dup_set* d, const bqsr_sam* s);
+bqsr_status bqsr_dup_set_finish(bqsr_dup_set* d, int64_t* n_duplicates);
+bqsr_status bqsr_dup_set_apply(bqsr_dup_set* d, int64_t part, bqsr_sam* s, int64_t* n_duplicates);
+void bqsr_dup_set_destroy(bqsr_dup_set* d);
+
 #ifdef __cplusplus
 }
 #endif

@@ -295,22 +295,26 @@ def test_rewrite_java_chars_as_utf8():
         sam.close()
 
 
-def test_transform_mark_duplicates(tmp_path):
-    # pairs and fragments stacked on few positions, flags then BQSR's eligibility
-    b = synth.generate(4000, (60,), 2, 11, contig_len=3000, p_duplicate=0.0)
+def _dup_text(n: int, far: bool = False) -> bytes:
+    """pairs and fragments stacked on few positions: mates share a QNAME --
+    read 2k+1 with read 2k, or (far) read k + n/2 with read k, so mates
+    land in different partitions"""
+    b = synth.generate(n, (60,), 2, 11, contig_len=3000, p_duplicate=0.0)
     text = sam_text(b, n_rg=2, qname="p")
     lines = text.split(b"\n")
-    # mates share a QNAME: pair read 2k+1 with read 2k
     body = [l for l in lines if l and not l.startswith(b"@")]
-    for k in range(1, len(body), 2):
+    h = len(body) // 2
+    pairs = [(k + h, k) for k in range(0, h, 3)] if far else [(k, k - 1) for k in range(1, len(body), 2)]
+    for k, m in pairs:
         f = body[k].split(b"\t")
-        f[0] = body[k - 1].split(b"\t")[0]
+        f[0] = body[m].split(b"\t")[0]
         body[k] = b"\t".join(f)
-    text = b"\n".join([l for l in lines if l.startswith(b"@")] + body) + b"\n"
-    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
-    src.write_bytes(text)
-    st = transform(str(src), str(out), mark_duplicates=True)
-    # the restatement over the same records
+    return b"\n".join([l for l in lines if l.startswith(b"@")] + body) + b"\n"
+
+
+def _dup_want(src):
+    """MarkDuplicates' restatement (oracle/markdup.py) over the records of src"""
+    text = open(src, "rb").read()
     batch = read_sam(str(src))
     recs = _records(text)
     rg_lib = {i: "lib%d" % (i % 2) for i in range(2)}
@@ -325,7 +329,16 @@ def test_transform_mark_duplicates(tmp_path):
                           mate_mapped=flag != 0 and bool(flag & 1) and not flag & 8, neg=bool(fl & R.F_NEG_STRAND),
                           ref=0, start=int(batch.start[r]), qual=f[10].decode("latin-1"),
                           cigar=[(int(e) >> 4, "MIDNSHP=X"[int(e) & 15]) for e in cig]))
-    want = M.mark_duplicates(reads)
+    return M.mark_duplicates(reads)
+
+
+def test_transform_mark_duplicates(tmp_path):
+    text = _dup_text(4000)
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    st = transform(str(src), str(out), mark_duplicates=True)
+    recs = _records(text)
+    want = _dup_want(src)
     assert st["duplicates"] == sum(want) > 0
     after = _records(out.read_bytes())
     for r, (a, c) in enumerate(zip(recs, after)):
@@ -481,3 +494,76 @@ def test_bam_ingest_rejects_damaged_bgzf():
         with pytest.raises(_capi.BQSRError) as e:
             SamText(data, bam=True).close()
         assert e.value.status == _capi.SAM_PARSE, (name, e.value)
+
+
+@pytest.mark.parametrize("n_parts,recal", [(3, False), (8, False), (5, True)])
+def test_transform_mark_duplicates_partitions(tmp_path, n_parts, recal):
+    # MarkDuplicates across partitions (bqsr_dup_set): mates in different
+    # partitions still form one bucket; the duplicate bits are the whole
+    # input's, then BQSR streams the partitions with those bits set
+    text = _dup_text(6000, far=True)
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    pb = len(text) // n_parts + 1
+    st = transform(str(src), str(out), mark_duplicates=True, recalibrate=recal, partition_bytes=pb)
+    assert st["partitions"] >= n_parts
+    recs = _records(text)
+    want = _dup_want(src)
+    assert st["duplicates"] == sum(want) > 0
+    after = _records(out.read_bytes())
+    assert len(after) == len(recs)
+    for r, (a, c) in enumerate(zip(recs, after)):
+        flag = int(a[1])
+        assert int(c[1]) == ((flag | 0x400) if want[r] else (flag & ~0x400)), r
+        assert a[2:10] == c[2:10] and a[11:] == c[11:]
+    if not recal:
+        assert [a[10] for a in recs] == [c[10] for c in after]
+        return
+    # BQSR over the same partitions, duplicates flagged, through the oracle
+    parts = _partition_batches(tmp_path, text, pb)
+    base = 0
+    for p in parts:
+        d = np.asarray(want[base:base + p.n_reads], bool)
+        p.flags = np.where(d, p.flags | R.F_DUPLICATE, p.flags & ~np.uint32(R.F_DUPLICATE)).astype(np.uint32)
+        base += p.n_reads
+    o = run_oracle(parts)
+    assert o.error is None, o.error
+    quals = []
+    for p, (chars, out_len) in zip(parts, o.outs):
+        quals += [chars[int(p.qual_offset[r]):int(p.qual_offset[r]) + int(out_len[r])] for r in range(p.n_reads)]
+    flags = np.concatenate([p.flags for p in parts])
+    for r, (a, c) in enumerate(zip(recs, after)):
+        f = int(flags[r])
+        if (f & R.F_MAPPED) and (f & R.F_PRIMARY) and not (f & R.F_DUPLICATE):
+            assert c[10] == "".join(map(chr, quals[r])).encode("utf-8"), r
+        else:
+            assert c[10] == a[10]
+
+
+def test_dup_set_refusals():
+    # apply before finish, a parse of another size, an unknown partition
+    from adam_amd.sam import DupSet
+    text = _dup_text(400)
+    s1 = SamText(text)
+    d = DupSet()
+    try:
+        d.add(s1)
+        with pytest.raises(_capi.BQSRError):
+            d.apply(0, s1)
+        assert d.finish() >= 0
+        with pytest.raises(_capi.BQSRError):
+            d.add(s1)
+        with pytest.raises(_capi.BQSRError):
+            d.apply(1, s1)
+        hdr = b"".join(l + b"\n" for l in text.split(b"\n") if l.startswith(b"@"))
+        body = [l for l in text.split(b"\n") if l and not l.startswith(b"@")]
+        s2 = SamText(hdr + b"\n".join(body[:10]) + b"\n")
+        try:
+            with pytest.raises(_capi.BQSRError):
+                d.apply(0, s2)
+        finally:
+            s2.close()
+        d.apply(0, s1)
+    finally:
+        d.close()
+        s1.close()
