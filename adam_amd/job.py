@@ -36,11 +36,13 @@ from .records import RecordBatch
 class ResidentJob:
     STAGES = ("prep", "observe", "fold", "apply")
 
-    def __init__(self, batch: RecordBatch, dims, snp: Optional["bqsr.SnpTable"] = None, device: int = 0,
-                 max_exc: int = 1 << 16, read_base: Optional[int] = None):
+    def __init__(self, batch: Optional[RecordBatch], dims, snp: Optional["bqsr.SnpTable"] = None, device: int = 0,
+                 max_exc: int = 1 << 16, read_base: Optional[int] = None, sam=None):
         """read_base: global index of the shard's first read (reads of the
         ranks before this one): errors are reported in global read order.
-        Required when several ranks run the job."""
+        Required when several ranks run the job.  sam: a parse (sam.SamText)
+        whose records become the batch on the device (bqsr_sam_batch_create)
+        in place of a host RecordBatch; dims None = the batch's own."""
         import torch
         self.torch = torch
         self.L = L = _capi.lib()
@@ -51,13 +53,21 @@ class ResidentJob:
         self.batch = batch
         self.dims = dims
         self.snp = snp
-        s, keep = batch.c_struct(batch.contig_ids_for(snp.contigs if snp else None))
         self.bh = ctypes.c_void_p()
-        check(L.bqsr_batch_create(self.ctx.handle, ctypes.byref(s), self.sp, ctypes.byref(self.bh)))
-        del keep
+        if sam is not None:
+            self.bh = sam.device_batch(snp.contigs if snp else None, self.sp)
+            self.n_reads = int(L.bqsr_batch_reads(self.bh))
+            self.n_bases = int(L.bqsr_batch_bases(self.bh))
+            if dims is None:
+                dims = L.bqsr_batch_dims(self.bh)
+                self.dims = dims
+        else:
+            s, keep = batch.c_struct(batch.contig_ids_for(snp.contigs if snp else None))
+            check(L.bqsr_batch_create(self.ctx.handle, ctypes.byref(s), self.sp, ctypes.byref(self.bh)))
+            del keep
+            self.n_reads = batch.n_reads
+            self.n_bases = batch.n_bases
         self.n_slots = int(L.bqsr_batch_slots(self.bh))
-        self.n_reads = batch.n_reads
-        self.n_bases = batch.n_bases
         words = int(L.bqsr_table_words(dims))
         self.table = torch.zeros(words, dtype=torch.int64, device=self.dev)
         self.th = ctypes.c_void_p()

@@ -61,6 +61,7 @@ def _lib():
             "bqsr_sam_text_download": (ctypes.c_int, [vp, ctypes.c_char_p]),
             "bqsr_mark_duplicates": (ctypes.c_int, [ctypes.POINTER(DupReads), vp]),
             "bqsr_sam_mark_duplicates": (ctypes.c_int, [vp, ctypes.POINTER(i64)]),
+            "bqsr_sam_batch_create": (ctypes.c_int, [vp, vp, vp, i32, vp, pp]),
             "bqsr_dup_set_create": (ctypes.c_int, [vp, i64, pp]),
             "bqsr_dup_set_add": (ctypes.c_int, [vp, vp]),
             "bqsr_dup_set_finish": (ctypes.c_int, [vp, ctypes.POINTER(i64)]),
@@ -86,7 +87,11 @@ class SamText:
         self.h = ctypes.c_void_p()
         self.bam = bam
         parse = self.L.bqsr_bam_parse if bam else self.L.bqsr_sam_parse
-        check(parse(self.ctx.handle, data, len(data), stream, ctypes.byref(self.h)))
+        # a uint8 numpy array (e.g. a view of an mmap) is passed by address
+        src = ctypes.c_char_p(data.ctypes.data) if isinstance(data, np.ndarray) and data.size else data
+        if isinstance(src, np.ndarray):
+            src = b""
+        check(parse(self.ctx.handle, src, len(data), stream, ctypes.byref(self.h)))
 
     @classmethod
     def read(cls, path: str, ctx: Optional[bqsr.Context] = None) -> "SamText":
@@ -119,6 +124,22 @@ class SamText:
         return RecordBatch(a["flags"], a["rg_id"], a["ref_index"], self.ref_names(), a["start"], a["seq_offset"],
                            a["seq"], a["qual_offset"], a["qual"], a["cigar_offset"], a["cigar"], a["md_offset"],
                            a["md"])
+
+    def device_batch(self, contigs: Optional[Sequence[str]] = None, stream=None) -> ctypes.c_void_p:
+        """The records as a BQSR batch packed on the device
+        (bqsr_sam_batch_create; the caller owns the returned bqsr_batch*).
+        contigs: the SnpTable's contig names (None: no known sites)."""
+        names = self.ref_names()
+        from .records import CONTIG_UNKNOWN
+        lut = np.full(max(1, len(names)), CONTIG_UNKNOWN, np.int32)
+        if contigs:
+            pos = {c: i for i, c in enumerate(contigs)}
+            for i, nm in enumerate(names):
+                lut[i] = pos.get(nm, lut[i])
+        bh = ctypes.c_void_p()
+        check(self.L.bqsr_sam_batch_create(self.ctx.handle, self.h, lut.ctypes.data, len(names), stream,
+                                           ctypes.byref(bh)))
+        return bh
 
     def mark_duplicates(self) -> int:
         """MarkDuplicates over the records (their duplicateRead bits updated); returns the duplicate count."""

@@ -107,17 +107,14 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
             try:
                 if dups is not None:
                     dups.apply(len(batches), sam)
-                rb = sam.batch()
+                bh = sam.device_batch(contigs, sp)  # packed on the device
             finally:
                 sam.close()
-            s, keep = rb.c_struct(rb.contig_ids_for(contigs))
-            bh = ctypes.c_void_p()
-            check(L.bqsr_batch_create(h, ctypes.byref(s), sp, ctypes.byref(bh)))
-            del keep
             batches.append(bh)
-            n_rg, max_len = max(n_rg, rb.n_rg()), max(max_len, rb.max_len())
+            d = L.bqsr_batch_dims(bh)
+            n_rg, max_len = max(n_rg, d.n_rg), max(max_len, d.max_len)
             slots.append(int(L.bqsr_batch_slots(bh)))
-            reads.append(rb.n_reads)
+            reads.append(int(L.bqsr_batch_reads(bh)))
         n_reads = sum(reads)
         # (2) computeTable: every partition observed into the one table, its
         # errors raised partition by partition, expectedMismatch folded in
@@ -325,6 +322,33 @@ class _AdamOut:
         self.w.close(ok)
 
 
+class _Phases:
+    """wall time per named phase (the stats' phase split)"""
+
+    def __init__(self):
+        self.t: Dict[str, float] = {}
+
+    def __call__(self, name: str):
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            t0 = time.perf_counter()
+            try:
+                yield
+            finally:
+                self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - t0
+        return cm()
+
+
+def _host_bytes(data):
+    """the input as a bytes-like object ctypes can pass without a copy: a
+    read-only mmap is passed as a numpy view's address"""
+    if isinstance(data, mmap.mmap):
+        return np.frombuffer(data, np.uint8)
+    return data
+
+
 def is_bam(data) -> bool:
     return bytes(data[:4]) == b"\x1f\x8b\x08\x04"
 
@@ -357,32 +381,41 @@ def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bo
                     stats = _partitions(data, header, ranges, mark_duplicates, recalibrate, dbsnp, ctx, device,
                                         sink.emit)
                 else:
-                    sam = SamText(bytes(data), ctx, bam=bam)
+                    ph = _Phases()
+                    with ph("parse"):
+                        sam = SamText(_host_bytes(data), ctx, bam=bam)
                     try:
                         stats["reads"] = sam.counts().n_reads
                         if mark_duplicates:
-                            stats["duplicates"] = sam.mark_duplicates()
+                            with ph("markdup"):
+                                stats["duplicates"] = sam.mark_duplicates()
                         if recalibrate:
                             from .job import ResidentJob
                             snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
-                            batch = sam.batch()
-                            job = ResidentJob(batch, bqsr.dims_of([batch]), snp if snp.table else None, device)
+                            with ph("batch"):
+                                job = ResidentJob(None, None, snp if snp.table else None, device, sam=sam)
                             try:
-                                job.step()
-                                sam.rewrite(job)
+                                with ph("bqsr"):
+                                    job.step()
+                                with ph("rewrite"):
+                                    sam.rewrite(job)
                             finally:
                                 job.close()
                         elif mark_duplicates:
                             sam.rewrite(None)
-                        sink.emit(0, sam)
+                        with ph("emit"):
+                            sink.emit(0, sam)
                     finally:
                         sam.close()
+                    stats["phases"] = ph.t
             finally:
                 if isinstance(data, mmap.mmap):
                     data.close()
         ok = True
     finally:
+        t1 = time.perf_counter()
         sink.close(ok)
+        stats.setdefault("phases", {})["close"] = time.perf_counter() - t1
     if adam_out:
         stats["parts"] = sink.w.parts
     stats["seconds"] = time.perf_counter() - t0

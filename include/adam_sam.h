@@ -88,6 +88,17 @@ bqsr_status bqsr_sam_device_columns(const bqsr_sam* s, bqsr_sam_columns* out);
 /* copy the columns to caller-allocated host arrays sized by bqsr_sam_get_counts */
 bqsr_status bqsr_sam_download(const bqsr_sam* s, const bqsr_sam_columns* dst);
 
+/* The parse's records as a BQSR batch, packed on the device: the layout,
+ * launch window and read order bqsr_batch_create builds from the same
+ * records' host columns (bqsr_sam_download), without the columns leaving the
+ * device.  ref_contig[i] = the bqsr_sites contig index of referenceName i
+ * (bqsr_sam_ref_name order) or BQSR_CONTIG_UNKNOWN; n_ref may be 0 (no known
+ * sites).  The batch owns its columns (the parse may be destroyed).
+ * BQSR_ERR_UNSUPPORTED as bqsr_batch_create (fields beyond 65535, a
+ * recordGroupId beyond 65535, reads longer than the device path takes). */
+bqsr_status bqsr_sam_batch_create(bqsr_context* ctx, const bqsr_sam* s, const int32_t* ref_contig, int32_t n_ref,
+                                  void* stream, bqsr_batch** out);
+
 /* Output (§8 f2): replace every record's QUAL field by its recalibrated
  * string.  out_qual / out_start / out_len / exceptions are the device
  * buffers bqsr_apply_async wrote for batch `b`, built from this parse's

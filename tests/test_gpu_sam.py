@@ -567,3 +567,58 @@ def test_dup_set_refusals():
     finally:
         d.close()
         s1.close()
+
+
+def _job_outcome(job):
+    """(error name, results) of one step"""
+    try:
+        job.step()
+    except _capi.BQSRError as e:
+        return e.name, None
+    return None, job.results()
+
+
+@pytest.mark.parametrize("name", FIXTURES + ["EDGE", "synthetic", "synthetic-sites"])
+def test_device_batch_matches_host_batch(tmp_path, name):
+    # bqsr_sam_batch_create (the parse packed on the device) against
+    # bqsr_batch_create over the same parse's downloaded columns: the same
+    # slots, dims, and one job step's table, expectedMismatch, outputs and
+    # errors bit for bit
+    from adam_amd.job import ResidentJob
+    snp = None
+    if name == "EDGE":
+        text = EDGE
+    elif name.startswith("synthetic"):
+        b = synth.generate(30000, (76, 100, 151), 3, 5, contig_len=400_000)
+        text = sam_text(b, n_rg=3)
+        if name == "synthetic-sites":
+            sites = synth.known_sites(4000, contig_len=400_000)
+            snp = bqsr.SnpTable({"chr20": sites["chr20"].tolist()})
+    else:
+        text = open(os.path.join(GOLD, name), "rb").read()
+    sam = SamText(text)
+    try:
+        rb = sam.batch()
+        j1 = ResidentJob(rb, bqsr.dims_of([rb]), snp, 0)
+        j2 = ResidentJob(None, None, snp, 0, sam=sam)
+        try:
+            L = _capi.lib()
+            assert int(L.bqsr_batch_slots(j1.bh)) == int(L.bqsr_batch_slots(j2.bh))
+            assert int(L.bqsr_batch_reads(j2.bh)) == rb.n_reads
+            assert int(L.bqsr_batch_bases(j2.bh)) == rb.n_bases
+            d1, d2 = L.bqsr_batch_dims(j1.bh), L.bqsr_batch_dims(j2.bh)
+            assert (d1.n_rg, d1.max_len) == (d2.n_rg, d2.max_len)
+            assert (j2.dims.n_rg, j2.dims.max_len) == (j1.dims.n_rg, j1.dims.max_len)
+            e1, r1 = _job_outcome(j1)
+            e2, r2 = _job_outcome(j2)
+            assert e1 == e2
+            if r1 is not None:
+                assert np.array_equal(r1[0], r2[0])
+                assert np.float64(r1[1]).tobytes() == np.float64(r2[1]).tobytes()
+                for x, y in zip(r1[2:], r2[2:]):
+                    assert np.array_equal(x, y)
+        finally:
+            j1.close()
+            j2.close()
+    finally:
+        sam.close()

@@ -15,7 +15,7 @@ cd "$R"
 COMMIT=$(cat "$R/.commit" 2>/dev/null || echo unknown)
 if [ "$PYTEST" = 1 ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=10 -v --timeout 300 --timeout-method thread > "$O/pytest.log" 2>&1 \
-    || { tail -60 "$O/pytest.log"; exit 1; }
+    || { rc=$?; tail -60 "$O/pytest.log"; exit $rc; }
   tail -1 "$O/pytest.log"
   timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
   tail -1 "$O/smoke.log"
