@@ -1911,6 +1911,7 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
 #include "mark_duplicates.cpp"
 #include "adam_out.hip"
 #include "sam_batch.hip"
+#include "arrow_ingest.hip"
 
 // ---- streamed outputs: compaction (uses the SAM code's scans) ----
 extern "C" {

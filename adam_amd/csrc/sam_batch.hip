@@ -129,13 +129,24 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_pack(
 
 }  // namespace sbk
 
-bqsr_status bqsr_sam_batch_create(bqsr_context* ctx, const bqsr_sam* s, const int32_t* ref_contig, int32_t n_ref,
-                                  void* stream, bqsr_batch** out) {
+namespace {
+// device record columns in the parse layout (bqsr_sam, bqsr_arrow)
+struct PackCols {
+  const uint32_t* flags;
+  const int32_t* rg_id;
+  const int32_t* ref;  // index into the ref_contig map (-1: none)
+  const int64_t* start;
+  const uint64_t *seq_off, *qual_off, *cig_off, *md_off;
+  const uint8_t *seq, *qual, *md;
+  const uint32_t* cig;
+  int64_t n_reads, seq_bytes, md_bytes, cig_ops;
+  int32_t n_rg;  // read-group ids below this are counted for the launch window
+};
+
+bqsr_status pack_batch_device(bqsr_context* ctx, const PackCols& C, const int32_t* ref_contig, int32_t n_ref,
+                              void* stream, bqsr_batch** out) {
   using namespace sbk;
-  if (!ctx || !s || !out || n_ref < 0 || (n_ref && !ref_contig))
-    return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_batch_create: bad arguments");
-  if (s->ctx != ctx) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_batch_create: parse of another context");
-  *out = nullptr;
+  const PackCols* s = &C;
   HIP_TRY(hipSetDevice(ctx->device));
   if ((uint64_t)s->md_bytes > 0xFFFFFFFFull || (uint64_t)s->cig_ops > 0xFFFFFFFFull)
     return fail(BQSR_ERR_UNSUPPORTED, "partition MD / CIGAR columns exceed 4 GiB");
@@ -173,6 +184,7 @@ bqsr_status bqsr_sam_batch_create(bqsr_context* ctx, const bqsr_sam* s, const in
     hipLaunchKernelGGL(sam_batch_spans, dim3(g), dim3(kThreads), 0, st, (const uint32_t*)s->flags,
                        (const int32_t*)s->rg_id, (const uint64_t*)s->seq_off, (const uint64_t*)s->qual_off,
                        (const uint64_t*)s->cig_off, (const uint64_t*)s->md_off, n, span, dl);
+    HIP_TRY(hipGetLastError());
   }
   size_t tb = 0;
   HIP_TRY(rocprim::exclusive_scan(nullptr, tb, span, slot, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), st));
@@ -246,4 +258,16 @@ bqsr_status bqsr_sam_batch_create(bqsr_context* ctx, const bqsr_sam* s, const in
   HIP_TRY(hipStreamSynchronize(st));
   *out = b.release();
   return ok();
+}
+}  // namespace
+
+bqsr_status bqsr_sam_batch_create(bqsr_context* ctx, const bqsr_sam* s, const int32_t* ref_contig, int32_t n_ref,
+                                  void* stream, bqsr_batch** out) {
+  if (!ctx || !s || !out || n_ref < 0 || (n_ref && !ref_contig))
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_batch_create: bad arguments");
+  if (s->ctx != ctx) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_batch_create: parse of another context");
+  *out = nullptr;
+  PackCols C{s->flags, s->rg_id, s->ref, s->start, s->seq_off, s->qual_off, s->cig_off, s->md_off, s->seq, s->qual,
+             s->md, s->cig, s->n_reads, s->seq_bytes, s->md_bytes, s->cig_ops, s->n_rg};
+  return pack_batch_device(ctx, C, ref_contig, n_ref, stream, out);
 }

@@ -37,12 +37,14 @@ class ResidentJob:
     STAGES = ("prep", "observe", "fold", "apply")
 
     def __init__(self, batch: Optional[RecordBatch], dims, snp: Optional["bqsr.SnpTable"] = None, device: int = 0,
-                 max_exc: int = 1 << 16, read_base: Optional[int] = None, sam=None):
+                 max_exc: int = 1 << 16, read_base: Optional[int] = None, sam=None, handle=None):
         """read_base: global index of the shard's first read (reads of the
         ranks before this one): errors are reported in global read order.
         Required when several ranks run the job.  sam: a parse (sam.SamText)
         whose records become the batch on the device (bqsr_sam_batch_create)
-        in place of a host RecordBatch; dims None = the batch's own."""
+        in place of a host RecordBatch; handle: a bqsr_batch* built on the
+        device (parquet.ArrowReads.device_batch), owned by the job from here;
+        dims None = the batch's own."""
         import torch
         self.torch = torch
         self.L = L = _capi.lib()
@@ -54,8 +56,8 @@ class ResidentJob:
         self.dims = dims
         self.snp = snp
         self.bh = ctypes.c_void_p()
-        if sam is not None:
-            self.bh = sam.device_batch(snp.contigs if snp else None, self.sp)
+        if sam is not None or handle is not None:
+            self.bh = handle if handle is not None else sam.device_batch(snp.contigs if snp else None, self.sp)
             self.n_reads = int(L.bqsr_batch_reads(self.bh))
             self.n_bases = int(L.bqsr_batch_bases(self.bh))
             if dims is None:

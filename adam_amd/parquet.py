@@ -18,9 +18,10 @@ goes to the device like a SAM or BAM parse.
 
 Semantics kept: an Avro null is "field absent" (the HAS_* bits, the
 reference's NPEs / NullPointer paths); strings are UTF-8 in Parquet and Java
-strings in the reference, so a qual char c enters as the byte c & 0xFF (BQSR
-uses ``(c - 33).toByte``, which only sees those 8 bits) and a sequence or MD
-char above 0xFF as the byte 0xFF (no base, no MD digit or letter).  A null
+strings in the reference (UTF-16 code units: a char beyond the BMP is a
+surrogate pair), so a qual char c enters as the byte c & 0xFF (BQSR uses
+``(c - 33).toByte``, which only sees those 8 bits) and a sequence or MD char
+above 0xFF as the byte 0xFF (no base, no MD digit or letter).  A null
 boolean is read as false (the reference unboxes it: an NPE -- parity
 unpinned, as is every comparison against files ADAM itself wrote: the
 reference cannot run here, so the reader is checked against its own writer
@@ -28,6 +29,7 @@ and the SAM fixtures' columns).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -72,12 +74,13 @@ def _string_column(col, kind: str) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
     data = data[int(off[0]):int(off[-1])]
     off = (off - off[0]).astype(np.uint64)
-    if data.size and int(data.max()) >= 0x80:  # UTF-8 beyond ASCII: one byte per char, rebuilt per string
-        strs = [bytes(data[int(off[r]):int(off[r + 1])]).decode("utf-8") for r in range(n)]
+    if data.size and int(data.max()) >= 0x80:  # UTF-8 beyond ASCII: one byte per Java char, rebuilt per string
+        units = [np.frombuffer(bytes(data[int(off[r]):int(off[r + 1])]).decode("utf-8").encode("utf-16-le"), "<u2")
+                 for r in range(n)]  # Java chars: UTF-16 code units (surrogate pairs beyond the BMP)
         if kind == "qual":
-            enc = [bytes(ord(c) & 0xFF for c in s) for s in strs]
+            enc = [(u & 0xFF).astype(np.uint8).tobytes() for u in units]
         else:
-            enc = [bytes(min(ord(c), 0xFF) for c in s) for s in strs]
+            enc = [np.minimum(u, 0xFF).astype(np.uint8).tobytes() for u in units]
         lens = np.fromiter((len(b) for b in enc), dtype=np.uint64, count=n)
         off = np.zeros(n + 1, dtype=np.uint64)
         np.cumsum(lens, out=off[1:])
@@ -172,6 +175,165 @@ def table_to_batch(t) -> RecordBatch:
         flags |= np.where(present, np.uint32(bit), np.uint32(0))
     return RecordBatch(flags, rg, ref_index, ref_names, start, s_off, s_data, q_off, q_data, cig_off, cig, m_off,
                        m_data)
+
+
+class _Strings(ctypes.Structure):
+    _fields_ = [("offsets", ctypes.c_void_p), ("data", ctypes.c_void_p), ("validity", ctypes.c_void_p)]
+
+
+class _Chunk(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_int64), ("sequence", _Strings), ("qual", _Strings), ("cigar", _Strings),
+                ("md", _Strings), ("reference", ctypes.c_void_p), ("reference_validity", ctypes.c_void_p),
+                ("start", ctypes.c_void_p), ("start_validity", ctypes.c_void_p), ("record_group", ctypes.c_void_p),
+                ("record_group_validity", ctypes.c_void_p), ("bools", ctypes.c_void_p * 6),
+                ("bools_validity", ctypes.c_void_p * 6)]
+
+
+_arrow_bound = False
+
+
+def _arrow_lib():
+    global _arrow_bound
+    from . import _capi
+    L = _capi.lib()
+    if not _arrow_bound:
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        pp = ctypes.POINTER(ctypes.c_void_p)
+        sig = {
+            "bqsr_arrow_load": (ctypes.c_int, [vp, ctypes.POINTER(_Chunk), i32, vp, pp]),
+            "bqsr_arrow_destroy": (None, [vp]),
+            "bqsr_arrow_reads": (i64, [vp]),
+            "bqsr_arrow_batch_create": (ctypes.c_int, [vp, vp, vp, i32, vp, pp]),
+            "bqsr_arrow_qual_prepare": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, vp, ctypes.POINTER(i64)]),
+            "bqsr_arrow_qual_column": (ctypes.c_int, [vp, vp, vp, vp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _arrow_bound = True
+    return L
+
+
+class ArrowReads:
+    """ADAMRecord columns of an Arrow table on the device (bqsr_arrow,
+    include/adam_sam.h): Arrow's buffers uploaded as they are, the parse
+    layout built on the device; ``device_batch`` packs them into a BQSR batch
+    and ``qual_column`` rebuilds the qual column after apply -- no per-read
+    host work on either side."""
+
+    def __init__(self, table, ctx=None, stream=None):
+        from . import bqsr
+        from ._capi import check
+        pa, pc, _ = _pa()
+        self.L = _arrow_lib()
+        self.ctx = ctx or bqsr.Context.get(0)
+        n = table.num_rows
+        names = set(table.column_names)
+        # referenceName -> indices into one dictionary (its distinct names)
+        if "referenceName" in names:
+            refc = table.column("referenceName")
+            self.ref_names = [v for v in pc.unique(refc).to_pylist() if v is not None]
+        else:
+            self.ref_names = []
+        value_set = pa.array(self.ref_names, pa.string())
+        keep = []
+
+        def flat(a):
+            if a.offset:
+                a = pa.concat_arrays([a])
+            keep.append(a)
+            return a
+
+        def addr(b):
+            return None if b is None else b.address
+
+        chunks = []
+        for rb in table.to_batches():
+            m = rb.num_rows
+            if m == 0:
+                continue
+            C = _Chunk()
+            C.n_reads = m
+            for fld, attr in (("sequence", "sequence"), ("qual", "qual"), ("cigar", "cigar"),
+                              ("mismatchingPositions", "md")):
+                if fld not in names:
+                    continue
+                a = rb.column(rb.schema.get_field_index(fld))
+                if a.type != pa.string():
+                    a = a.cast(pa.string())
+                a = flat(a)
+                b = a.buffers()
+                setattr(C, attr, _Strings(addr(b[1]), addr(b[2]) or addr(b[1]), addr(b[0])))
+            if "referenceName" in names:
+                a = rb.column(rb.schema.get_field_index("referenceName"))
+                idx = flat(pc.index_in(a, value_set=value_set).cast(pa.int32()))
+                b = idx.buffers()
+                C.reference, C.reference_validity = addr(b[1]), addr(b[0])
+            for fld, typ, v, vv in (("start", pa.int64(), "start", "start_validity"),
+                                    ("recordGroupId", pa.int32(), "record_group", "record_group_validity")):
+                if fld in names:
+                    a = rb.column(rb.schema.get_field_index(fld))
+                    a = flat(a if a.type == typ else a.cast(typ))
+                    b = a.buffers()
+                    setattr(C, v, addr(b[1]))
+                    setattr(C, vv, addr(b[0]))
+            for k, (fld, _bit) in enumerate(_BOOL_BITS):
+                if fld in names:
+                    a = flat(rb.column(rb.schema.get_field_index(fld)))
+                    b = a.buffers()
+                    C.bools[k], C.bools_validity[k] = addr(b[1]), addr(b[0])
+            chunks.append(C)
+        arr = (_Chunk * max(1, len(chunks)))(*chunks)
+        self.h = ctypes.c_void_p()
+        check(self.L.bqsr_arrow_load(self.ctx.handle, arr, len(chunks), stream, ctypes.byref(self.h)))
+        del keep
+        self.n_reads = n
+
+    def device_batch(self, contigs: Optional[Sequence[str]] = None, stream=None) -> ctypes.c_void_p:
+        """A BQSR batch of the reads (the caller owns it)."""
+        from ._capi import check
+        from .records import CONTIG_UNKNOWN
+        lut = np.full(max(1, len(self.ref_names)), CONTIG_UNKNOWN, np.int32)
+        if contigs:
+            pos = {c: i for i, c in enumerate(contigs)}
+            for i, nm in enumerate(self.ref_names):
+                lut[i] = pos.get(nm, CONTIG_UNKNOWN)
+        bh = ctypes.c_void_p()
+        check(self.L.bqsr_arrow_batch_create(self.ctx.handle, self.h, lut.ctypes.data, len(self.ref_names), stream,
+                                             ctypes.byref(bh)))
+        return bh
+
+    def qual_column(self, job=None):
+        """The qual column (pa.StringArray) after a ResidentJob's step over
+        this object's batch (job None: the input strings)."""
+        from ._capi import check
+        pa, _, _ = _pa()
+        nb = ctypes.c_int64()
+        if job is None:
+            check(self.L.bqsr_arrow_qual_prepare(self.ctx.handle, self.h, None, None, None, None, None, 0, None,
+                                                 ctypes.byref(nb)))
+        else:
+            p = job._ptr
+            check(self.L.bqsr_arrow_qual_prepare(self.ctx.handle, self.h, job.bh, p(job.out_qual), p(job.out_start),
+                                                 p(job.out_len), p(job.exc), job.n_exc, job.sp, ctypes.byref(nb)))
+        n = self.n_reads
+        off = np.empty(n + 1, np.int32)
+        data = np.empty(max(1, nb.value), np.uint8)
+        valid = np.empty(max(1, (n + 7) // 8), np.uint8)
+        check(self.L.bqsr_arrow_qual_column(self.h, off.ctypes.data, data.ctypes.data, valid.ctypes.data))
+        return pa.StringArray.from_buffers(n, pa.py_buffer(off), pa.py_buffer(data[:nb.value]), pa.py_buffer(valid))
+
+    def close(self):
+        if self.h:
+            self.L.bqsr_arrow_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def read_table(path: str, columns: Optional[Sequence[str]] = None):

@@ -239,16 +239,18 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
     from . import sam as S
     from .records import F_DUPLICATE, RecordBatch, read_sam_records
     t0 = time.perf_counter()
+    batch = None
     if is_parquet(inp):
         table = P.read_table(inp)
-        batch = P.table_to_batch(table.select([c for c in P.BQSR_PROJECTION if c in table.column_names]))
+        if mark_duplicates:  # MarkDuplicates over host columns
+            batch = P.table_to_batch(table.select([c for c in P.BQSR_PROJECTION if c in table.column_names]))
     else:
         if mark_duplicates:  # (the host SAM parse carries no library / mateMapped: use SAM output or ADAM input)
             raise ValueError("-mark_duplicate_reads with SAM input and ADAM output is not supported")
         recs = read_sam_records(inp)
         batch = RecordBatch.from_records(recs)
         table = P.batch_to_table(batch, [r.read_name for r in recs])
-    n = batch.n_reads
+    n = table.num_rows
     stats: Dict[str, float] = {"reads": n}
     if mark_duplicates:
         col = lambda name: table.column(name).to_pylist() if name in table.column_names else [None] * n
@@ -266,8 +268,26 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
         stats["duplicates"] = int(dup.sum())
     if recalibrate:
         snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
-        parts = bqsr.adam_bqsr([batch], snp if snp.table else None, bqsr.Context.get(device))
-        qcol = P.recalibrated_qual_column(parts, n)
+        if is_parquet(inp):
+            # the Arrow columns on the device: batch packed there, the qual
+            # column rebuilt there after apply (parquet.ArrowReads)
+            from .job import ResidentJob
+            cols = [c for c in P.BQSR_PROJECTION if c in table.column_names]
+            tb = table.select(cols)
+            A = P.ArrowReads(tb, bqsr.Context.get(device))
+            try:
+                job = ResidentJob(None, None, snp if snp.table else None, device,
+                                  handle=A.device_batch(snp.contigs if snp.table else None))
+                try:
+                    job.step()
+                    qcol = A.qual_column(job)
+                finally:
+                    job.close()
+            finally:
+                A.close()
+        else:
+            parts = bqsr.adam_bqsr([batch], snp if snp.table else None, bqsr.Context.get(device))
+            qcol = P.recalibrated_qual_column(parts, n)
         table = (table.set_column(table.column_names.index("qual"), "qual", qcol)
                  if "qual" in table.column_names else table.append_column("qual", qcol))
     tmp = out + ".partial"

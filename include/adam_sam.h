@@ -99,6 +99,56 @@ bqsr_status bqsr_sam_download(const bqsr_sam* s, const bqsr_sam_columns* dst);
 bqsr_status bqsr_sam_batch_create(bqsr_context* ctx, const bqsr_sam* s, const int32_t* ref_contig, int32_t n_ref,
                                   void* stream, bqsr_batch** out);
 
+/* ADAMRecord Parquet (§8 f1/f2): adamLoad with the BQSR projection
+ * (core/rdd/AdamContext.scala:139-161, projections/Projection.scala:10-34) as
+ * Arrow decodes it on the host -- the column buffers uploaded as they are and
+ * turned into the parse layout on the device.  One bqsr_arrow_chunk per Arrow
+ * record batch (array offsets 0); a NULL column is all null.  String columns:
+ * int32 offsets [n+1], UTF-8 bytes, validity bitmap (NULL: all valid); chars
+ * are Java chars (a 4-byte UTF-8 sequence is a surrogate pair): a qual char c
+ * enters as the byte c & 0xFF, a sequence / MD char as min(c, 0xFF) (as
+ * adam_amd/parquet.py).  CIGAR strings are parsed by samtools
+ * TextCigarCodec's rules (BQSR_ERR_SAM_PARSE, read index, when malformed).
+ * reference = referenceName dictionary indices (the caller's dictionary; the
+ * ref_contig map of bqsr_arrow_batch_create is indexed by them).  Booleans: a
+ * null reads as false. */
+typedef struct bqsr_arrow_strings {
+  const int32_t* offsets;
+  const uint8_t* data;
+  const uint8_t* validity;
+} bqsr_arrow_strings;
+typedef struct bqsr_arrow_chunk {
+  int64_t n_reads;
+  bqsr_arrow_strings sequence, qual, cigar, md; /* md = mismatchingPositions */
+  const int32_t* reference;
+  const uint8_t* reference_validity;
+  const int64_t* start;
+  const uint8_t* start_validity;
+  const int32_t* record_group; /* recordGroupId */
+  const uint8_t* record_group_validity;
+  /* readPaired, readMapped, readNegativeStrand, secondOfPair, primaryAlignment, duplicateRead */
+  const uint8_t* bools[6];
+  const uint8_t* bools_validity[6];
+} bqsr_arrow_chunk;
+typedef struct bqsr_arrow bqsr_arrow;
+bqsr_status bqsr_arrow_load(bqsr_context* ctx, const bqsr_arrow_chunk* chunks, int32_t n_chunks, void* stream,
+                            bqsr_arrow** out);
+void bqsr_arrow_destroy(bqsr_arrow* a);
+int64_t bqsr_arrow_reads(const bqsr_arrow* a);
+/* the records as a BQSR batch (as bqsr_sam_batch_create) */
+bqsr_status bqsr_arrow_batch_create(bqsr_context* ctx, const bqsr_arrow* a, const int32_t* ref_contig, int32_t n_ref,
+                                    void* stream, bqsr_batch** out);
+/* The qual column after apply (adamSave of the recalibrated records): per
+ * read the recalibrated chars as UTF-8 (pass-through reads keep their input
+ * string; null where the input had none and nothing was written), built on
+ * the device; prepare returns the byte count, column copies the Arrow
+ * buffers (int32 offsets [n+1], bytes, validity bitmap) to the host.  b ==
+ * NULL keeps every input string. */
+bqsr_status bqsr_arrow_qual_prepare(bqsr_context* ctx, bqsr_arrow* a, const bqsr_batch* b, const uint8_t* out_qual,
+                                    const uint32_t* out_start, const uint32_t* out_len, const uint64_t* exceptions,
+                                    int64_t n_exceptions, void* stream, int64_t* n_bytes);
+bqsr_status bqsr_arrow_qual_column(const bqsr_arrow* a, int32_t* offsets, uint8_t* data, uint8_t* validity);
+
 /* Output (§8 f2): replace every record's QUAL field by its recalibrated
  * string.  out_qual / out_start / out_len / exceptions are the device
  * buffers bqsr_apply_async wrote for batch `b`, built from this parse's

@@ -113,3 +113,13 @@ def test_synthetic_round_trip_high_quals(tmp_path):
     path = str(tmp_path / "x.parquet")
     P.write_parquet(b, path)
     same(b, P.read_parquet(path))
+
+
+def test_chars_beyond_the_bmp_are_surrogate_pairs():
+    # a Java String holds U+1F600 as two chars (0xD83D 0xDE00): two quals
+    # (their low bytes), two sequence bytes 0xFF
+    t = pa.table({"sequence": ["A\U0001F600C"], "qual": ["I\U0001F600I"], "cigar": ["4M"],
+                  "start": pa.array([3], pa.int64()), "readMapped": [True], "primaryAlignment": [True]})
+    b = P.table_to_batch(t)
+    assert bytes(b.qual[:4]) == bytes([0x49, 0x3D, 0x00, 0x49])
+    assert bytes(b.seq[:4]) == b"A\xff\xffC"
