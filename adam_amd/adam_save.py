@@ -58,6 +58,11 @@ RG_TAGS = (("recordGroupSequencingCenter", "CN"), ("recordGroupDescription", "DS
            ("recordGroupPlatformUnit", "PU"), ("recordGroupSample", "SM"))
 
 
+PER_READ_STRINGS = ("readName", "sequence", "qual", "attributes", "mismatchingPositions")
+DICT_COLS = [n for n, k in ADAM_FIELDS if n not in PER_READ_STRINGS]
+STATS_COLS = [n for n, k in ADAM_FIELDS if n not in PER_READ_STRINGS]
+
+
 class AdamSizes(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_int64), ("str_bytes", ctypes.c_int64 * 6), ("bitmap_words", ctypes.c_int64)]
 
@@ -178,6 +183,14 @@ def schema():
     return pa.schema([pa.field(n, t[k], nullable=True) for n, k in ADAM_FIELDS])
 
 
+def _pinned(nbytes: int) -> np.ndarray:
+    """a pinned host block (numpy view of a torch pinned tensor; the view
+    keeps the tensor alive)"""
+    import torch
+    t = torch.empty(max(64, int(nbytes)), dtype=torch.uint8, pin_memory=True)
+    return t.numpy()
+
+
 def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
     """The ADAMRecord table of records [r0, r0 + n) of a parse (SamText), from
     its current text (after ``rewrite``: recalibrated qual, MarkDuplicates'
@@ -189,11 +202,19 @@ def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
     sz = AdamSizes()
     check(L.bqsr_sam_adam_prepare(ctx.handle, sam.h, r0, n, stream, ctypes.byref(sz)))
     W = sz.bitmap_words
-    keep = []
+    # every host buffer carved from one pinned block (the D2H copies run at
+    # the link's rate; torch's host allocator recycles the block once the
+    # part file is written and the table dropped)
+    plan = ([(n + 1, np.int32)] * 6 + [(sz.str_bytes[c], np.uint8) for c in range(6)] + [(W, np.uint64)] * 6 +
+            [(n, np.int32)] * 4 + [(n, np.int64)] * 2 + [(W, np.uint64)] * 6 + [(W, np.uint64)] * 11)
+    sizes = [((max(1, cnt) * np.dtype(dt).itemsize + 63) // 64) * 64 for cnt, dt in plan]
+    block = _pinned(sum(sizes))
+    pos = [0]
 
     def buf(count, dtype):
-        a = np.empty(max(1, count), dtype=dtype)
-        keep.append(a)
+        nb = ((max(1, count) * np.dtype(dtype).itemsize + 63) // 64) * 64
+        a = block[pos[0]:pos[0] + nb].view(dtype)[:max(1, count)]
+        pos[0] += nb
         return a
 
     soff = [buf(n + 1, np.int32) for _ in range(6)]
@@ -270,7 +291,11 @@ class AdamWriter:
 
     def _write(self, table, name):
         import pyarrow.parquet as pq
-        pq.write_table(table, os.path.join(self.tmp, name), compression=self.compression, use_dictionary=True)
+        # dictionary pages and statistics where they pay: not for the
+        # per-read strings (names, bases, quals, tags), whose dictionaries
+        # overflow and whose min / max no reader filters on
+        pq.write_table(table, os.path.join(self.tmp, name), compression=self.compression,
+                       use_dictionary=DICT_COLS, write_statistics=STATS_COLS)
 
     def add(self, table):
         name = "part-r-%05d.parquet" % self.parts
