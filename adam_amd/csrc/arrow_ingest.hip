@@ -22,20 +22,20 @@
 namespace arwk {
 
 constexpr int kThreads = 256;
-enum { kSeq = 0, kQual = 1, kCigar = 2, kMd = 3, kStr = 4 };
+enum { kSeq = 0, kQual = 1, kCigar = 2, kMd = 3, kStr = 4, kName = 4, kAll = 5 };  // kStr: the decoded ones
 constexpr int kBools = 6;
 // readPaired, readMapped, readNegativeStrand, secondOfPair, primaryAlignment, duplicateRead
 __constant__ uint32_t kBoolBit[kBools] = {BQSR_F_PAIRED, BQSR_F_MAPPED, BQSR_F_NEG_STRAND, BQSR_F_SECOND_OF_PAIR,
                                           BQSR_F_PRIMARY, BQSR_F_DUPLICATE};
-constexpr uint32_t kStrHas[kStr] = {BQSR_F_HAS_SEQ, BQSR_F_HAS_QUAL, BQSR_F_HAS_CIGAR, BQSR_F_HAS_MD};
+constexpr uint32_t kStrHas[kAll] = {BQSR_F_HAS_SEQ, BQSR_F_HAS_QUAL, BQSR_F_HAS_CIGAR, BQSR_F_HAS_MD, 0};
 
 // one chunk's buffers on the device (copies of Arrow's)
 struct ChunkDev {
   int64_t n, r0;                       // reads; global index of the first
-  const int32_t* off[kStr];            // [n + 1] or null (column absent: all null)
-  const uint8_t* valid[kStr];          // bitmaps or null (all valid)
-  uint64_t dbase[kStr];                // global byte index of the chunk's first data byte
-  int32_t obase[kStr];                 // off[0]
+  const int32_t* off[kAll];            // [n + 1] or null (column absent: all null)
+  const uint8_t* valid[kAll];          // bitmaps or null (all valid)
+  uint64_t dbase[kAll];                // global byte index of the chunk's first data byte
+  int32_t obase[kAll];                 // off[0]
   const int32_t* ref;                  // dictionary indices or null
   const uint8_t* ref_valid;
   const int64_t* start;
@@ -44,14 +44,20 @@ struct ChunkDev {
   const uint8_t* rg_valid;
   const uint8_t* bools[kBools];        // value bitmaps or null (false)
   const uint8_t* bools_valid[kBools];  // null: all valid
+  const int32_t* sq;                   // referenceId (MarkDuplicates) or null
+  const uint8_t* sq_valid;
+  const int32_t* lib;                  // library rank (MarkDuplicates) or null
 };
 
 struct Cols {
-  uint64_t* beg[kStr];  // [n + 1] raw UTF-8 byte range of each read's string (beg[r], beg[r + 1])
+  uint64_t* beg[kAll];  // [n + 1] raw UTF-8 byte range of each read's string (beg[r], beg[r + 1])
   uint32_t* flags;
   int32_t* rg;
   int32_t* ref;
   int64_t* start;
+  uint8_t* name_valid;
+  int32_t* sq;   // referenceId, or the referenceName index without the column (-1: null)
+  int32_t* lib;
 };
 
 __device__ __forceinline__ bool bit(const uint8_t* bm, int64_t i) { return !bm || ((bm[i >> 3] >> (i & 7)) & 1u); }
@@ -60,7 +66,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) arrow_chunk_cols(ChunkDev
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < C.n; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g = C.r0 + r;
     uint32_t f = 0;
-    for (int k = 0; k < kStr; ++k) {
+    for (int k = 0; k < kAll; ++k) {
       if (C.off[k]) {
         O.beg[k][g] = C.dbase[k] + (uint64_t)(int64_t)(C.off[k][r] - C.obase[k]);
         if (last && r == C.n - 1) O.beg[k][g + 1] = C.dbase[k] + (uint64_t)(int64_t)(C.off[k][r + 1] - C.obase[k]);
@@ -91,6 +97,9 @@ extern "C" __global__ void __launch_bounds__(kThreads) arrow_chunk_cols(ChunkDev
     O.ref[g] = ref;
     O.start[g] = st;
     O.rg[g] = rg;
+    O.name_valid[g] = C.off[kName] && bit(C.valid[kName], r);
+    O.sq[g] = C.sq ? (bit(C.sq_valid, r) ? C.sq[r] : -1) : ref;
+    O.lib[g] = C.lib ? C.lib[r] : 0;
   }
 }
 
@@ -283,8 +292,10 @@ struct bqsr_arrow {
   bqsr_context* ctx = nullptr;
   int64_t n = 0;
   int32_t n_rg = 1;
-  uint8_t* raw[arwk::kStr] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t* beg[arwk::kStr] = {nullptr, nullptr, nullptr, nullptr};
+  uint8_t* raw[arwk::kAll] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint64_t* beg[arwk::kAll] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint8_t* name_valid = nullptr;  // readName present (MarkDuplicates)
+  int32_t *sq = nullptr, *lib = nullptr;
   uint32_t* flags = nullptr;
   int32_t *rg = nullptr, *ref = nullptr;
   int64_t* start = nullptr;
@@ -328,12 +339,12 @@ bqsr_status bqsr_arrow_load(bqsr_context* ctx, const bqsr_arrow_chunk* chunks, i
   A->ctx = ctx;
   // totals: reads, raw bytes per string column
   int64_t n = 0;
-  uint64_t tot[kStr] = {0, 0, 0, 0};
+  uint64_t tot[kAll] = {0, 0, 0, 0, 0};
   for (int32_t c = 0; c < n_chunks; ++c) {
     const bqsr_arrow_chunk& C = chunks[c];
     if (C.n_reads < 0) return fail(BQSR_ERR_INVALID_ARG, "bqsr_arrow_load: negative chunk length");
-    const bqsr_arrow_strings* sc[kStr] = {&C.sequence, &C.qual, &C.cigar, &C.md};
-    for (int k = 0; k < kStr; ++k)
+    const bqsr_arrow_strings* sc[kAll] = {&C.sequence, &C.qual, &C.cigar, &C.md, &C.read_name};
+    for (int k = 0; k < kAll; ++k)
       if (sc[k]->offsets) {
         const int32_t a = sc[k]->offsets[0], b = sc[k]->offsets[C.n_reads];
         if (b < a || (b > a && !sc[k]->data)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_arrow_load: bad string offsets");
@@ -344,14 +355,16 @@ bqsr_status bqsr_arrow_load(bqsr_context* ctx, const bqsr_arrow_chunk* chunks, i
   A->n = n;
   std::vector<void*>& K = A->allocs;
   bqsr_status st;
-  for (int k = 0; k < kStr; ++k)
+  for (int k = 0; k < kAll; ++k)
     if ((st = dalloc(K, &A->raw[k], (size_t)tot[k] + 16)) || (st = dalloc(K, &A->beg[k], (size_t)n + 1))) return st;
+  const size_t n1 = (size_t)std::max<int64_t>(n, 1);
+  if ((st = dalloc(K, &A->name_valid, n1)) || (st = dalloc(K, &A->sq, n1)) || (st = dalloc(K, &A->lib, n1))) return st;
   if ((st = dalloc(K, &A->flags, (size_t)std::max<int64_t>(n, 1))) || (st = dalloc(K, &A->rg, (size_t)std::max<int64_t>(n, 1))) ||
       (st = dalloc(K, &A->ref, (size_t)std::max<int64_t>(n, 1))) || (st = dalloc(K, &A->start, (size_t)std::max<int64_t>(n, 1))))
     return st;
-  for (int k = 0; k < kStr; ++k) HIP_TRY(hipMemsetAsync(A->beg[k], 0, 8, s));  // n == 0: beg[0] = 0
+  for (int k = 0; k < kAll; ++k) HIP_TRY(hipMemsetAsync(A->beg[k], 0, 8, s));  // n == 0: beg[0] = 0
   // per chunk: its buffers to the device, then its rows of the global columns
-  uint64_t dpos[kStr] = {0, 0, 0, 0};
+  uint64_t dpos[kAll] = {0, 0, 0, 0, 0};
   int64_t r0 = 0;
   std::vector<void*> tmp;
   struct Free {
@@ -368,8 +381,8 @@ bqsr_status bqsr_arrow_load(bqsr_context* ctx, const bqsr_arrow_chunk* chunks, i
     ChunkDev D{};
     D.n = m;
     D.r0 = r0;
-    const bqsr_arrow_strings* sc[kStr] = {&H.sequence, &H.qual, &H.cigar, &H.md};
-    for (int k = 0; k < kStr; ++k) {
+    const bqsr_arrow_strings* sc[kAll] = {&H.sequence, &H.qual, &H.cigar, &H.md, &H.read_name};
+    for (int k = 0; k < kAll; ++k) {
       D.dbase[k] = dpos[k];
       if (!sc[k]->offsets) continue;
       const int32_t a = sc[k]->offsets[0], b = sc[k]->offsets[m];
@@ -403,7 +416,16 @@ bqsr_status bqsr_arrow_load(bqsr_context* ctx, const bqsr_arrow_chunk* chunks, i
       D.bools[k] = bv;
       D.bools_valid[k] = bvv;
     }
-    Cols O{{A->beg[0], A->beg[1], A->beg[2], A->beg[3]}, A->flags, A->rg, A->ref, A->start};
+    int32_t *sq, *lib;
+    uint8_t* qv;
+    if ((st = arrow_h2d(tmp, &sq, H.reference_id, (size_t)m, s)) ||
+        (st = arrow_h2d(tmp, &qv, H.reference_id_validity, vb, s)) || (st = arrow_h2d(tmp, &lib, H.library, (size_t)m, s)))
+      return st;
+    D.sq = sq;
+    D.sq_valid = H.reference_id ? qv : nullptr;
+    D.lib = lib;
+    Cols O{{A->beg[0], A->beg[1], A->beg[2], A->beg[3], A->beg[4]}, A->flags, A->rg, A->ref, A->start,
+           A->name_valid, A->sq, A->lib};
     hipLaunchKernelGGL(arrow_chunk_cols, dim3(sam_grid(m, kThreads, ctx->n_cu * 16)), dim3(kThreads), 0, s, D, O,
                        (int)(r0 + m == n));
     HIP_TRY(hipGetLastError());
@@ -576,5 +598,73 @@ bqsr_status bqsr_arrow_qual_column(const bqsr_arrow* a, int32_t* offsets, uint8_
   if (offsets) HIP_TRY(hipMemcpy(offsets, a->q_off, (size_t)(a->n + 1) * 4, hipMemcpyDeviceToHost));
   if (data && a->q_bytes) HIP_TRY(hipMemcpy(data, a->q_out, (size_t)a->q_bytes, hipMemcpyDeviceToHost));
   if (validity) HIP_TRY(hipMemcpy(validity, a->q_valid, (size_t)(a->n + 7) / 8, hipMemcpyDeviceToHost));
+  return ok();
+}
+
+bqsr_status bqsr_arrow_mark_duplicates(bqsr_context* ctx, bqsr_arrow* a, int64_t* n_duplicates) {
+  if (!ctx || !a) return fail(BQSR_ERR_INVALID_ARG, "bqsr_arrow_mark_duplicates: bad arguments");
+  if (a->ctx != ctx) return fail(BQSR_ERR_INVALID_ARG, "bqsr_arrow_mark_duplicates: columns of another context");
+  HIP_TRY(hipSetDevice(ctx->device));
+  bqsr_dup_set* d = nullptr;
+  bqsr_status st = bqsr_dup_set_create(ctx, a->n, &d);
+  if (st != BQSR_OK) return st;
+  std::unique_ptr<bqsr_dup_set> own(d);
+  mdupd::DevSam S{};
+  S.text = a->raw[arwk::kName];
+  S.flags = a->flags;
+  S.rg_id = a->rg;
+  S.sq_id = a->sq;
+  S.start = a->start;
+  S.qual_off = a->qual_off;
+  S.qual = a->qual;
+  S.cig_off = a->cig_off;
+  S.cig = a->cig;
+  S.n = a->n;
+  S.name_beg = a->beg[arwk::kName];
+  S.name_valid = a->name_valid;
+  S.read_lib = a->lib;
+  if ((st = dup_set_add_cols(d, S)) != BQSR_OK) return st;
+  int64_t nd = 0;
+  if ((st = bqsr_dup_set_finish(d, &nd)) != BQSR_OK) return st;
+  if (a->n) {
+    hipStream_t s = hipStreamPerThread;
+    const unsigned g = sam_grid(a->n, mdupd::kThreads, ctx->n_cu * 16);
+    HIP_TRY(hipMemsetAsync(d->cnt, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(mdupd::mdup_set_apply, dim3(g), dim3(mdupd::kThreads), 0, s, (const uint32_t*)d->bits,
+                       (int64_t)0, a->n, a->flags, d->cnt);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  if (n_duplicates) *n_duplicates = nd;
+  return ok();
+}
+
+namespace arwk {
+// bit r of the bitmap = (flags[r] & flag) != 0; a wavefront per 64 reads (8 bytes)
+extern "C" __global__ void __launch_bounds__(kThreads) arrow_flag_bits(const uint32_t* flags, int64_t n, uint32_t flag,
+                                                                      uint8_t* bits) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t m = __ballot((flags[r] & flag) != 0);
+    const int lane = threadIdx.x & 63;
+    if (lane < 8 && (r - lane) + 8 * lane < n) bits[((r - lane) >> 3) + lane] = (uint8_t)(m >> (8 * lane));
+  }
+}
+}  // namespace arwk
+
+bqsr_status bqsr_arrow_flag_bitmap(const bqsr_arrow* a, uint32_t flag, uint8_t* bitmap) {
+  if (!a || (!bitmap && a->n)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_arrow_flag_bitmap: bad arguments");
+  if (a->n == 0) return ok();
+  HIP_TRY(hipSetDevice(a->ctx->device));
+  hipStream_t s = hipStreamPerThread;
+  uint8_t* d = nullptr;
+  const size_t nb = (size_t)(a->n + 7) / 8;
+  HIP_TRY(hipMalloc((void**)&d, nb + 8));
+  hipLaunchKernelGGL(arwk::arrow_flag_bits, dim3(sam_grid(a->n, arwk::kThreads, a->ctx->n_cu * 16)),
+                     dim3(arwk::kThreads), 0, s, (const uint32_t*)a->flags, a->n, flag, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(bitmap, d, nb, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(BQSR_ERR_DEVICE, hipGetErrorString(e));
   return ok();
 }

@@ -48,9 +48,18 @@ struct DevSam {
   const int32_t* rg_lib;  // library rank of read group i (0: no LB)
   int32_t n_rg;
   int64_t n;
+  // columns without SAM text (bqsr_arrow): names at [name_beg[r], name_beg[r + 1]) of text,
+  // name_valid[r] = 0 for a null readName, the library rank per read
+  const uint64_t* name_beg;
+  const uint8_t* name_valid;
+  const int32_t* read_lib;
 };
 
 __device__ __forceinline__ int name_len(const DevSam& S, int64_t r, const uint8_t** p) {
+  if (S.name_beg) {
+    *p = S.text + S.name_beg[r];
+    return (int)(S.name_beg[r + 1] - S.name_beg[r]);
+  }
   const uint64_t a = S.line_span[2 * r], b = S.line_span[2 * r + 1];
   const uint8_t* t = S.text + a;
   int k = 0;
@@ -433,7 +442,9 @@ __device__ __forceinline__ void name_hashes(const DevSam& S, int64_t r, uint64_t
     h = (h ^ p[i]) * 0x100000001b3ull;
     g2 = step2(g2, p[i]);
   }
-  g2 = step2(g2, 0x100u + (uint32_t)k);
+  const bool named = !S.name_valid || S.name_valid[r];
+  g2 = step2(g2, named ? 0x100u + (uint32_t)k : 0x3FFu);  // a null readName is its own key
+  if (!named) h ^= 0x9E3779B97F4A7C15ull;
   *a = h;
   *b = g2;
 }
@@ -457,8 +468,9 @@ extern "C" __global__ void __launch_bounds__(kThreads) mdup_set_records(DevSam S
       }
     }
     int32_t lb = 0;
-    if ((f & BQSR_F_HAS_RG) && S.rg_id[r] >= 0 && S.rg_id[r] < S.n_rg) lb = S.rg_lib[S.rg_id[r]];
-    if (lb >= 4096) atomicOr(bad, 4);
+    if (S.read_lib) lb = S.read_lib[r];
+    else if ((f & BQSR_F_HAS_RG) && S.rg_id[r] >= 0 && S.rg_id[r] < S.n_rg) lb = S.rg_lib[S.rg_id[r]];
+    if (lb < 0 || lb >= 4096) atomicOr(bad, 4);
     pos[o] = p;
     score[o] = sc;
     lib[o] = (uint16_t)(lb & 0xFFF);
@@ -641,6 +653,10 @@ bqsr_status bqsr_dup_set_create(bqsr_context* ctx, int64_t reads_hint, bqsr_dup_
 
 void bqsr_dup_set_destroy(bqsr_dup_set* d) { delete d; }
 
+namespace {
+bqsr_status dup_set_add_cols(bqsr_dup_set* d, const mdupd::DevSam& S);
+}
+
 bqsr_status bqsr_dup_set_add(bqsr_dup_set* d, const bqsr_sam* s) {
   using namespace mdupd;
   if (!d || !s) return fail(BQSR_ERR_INVALID_ARG, "null");
@@ -654,7 +670,28 @@ bqsr_status bqsr_dup_set_add(bqsr_dup_set* d, const bqsr_sam* s) {
   } else if (libs != d->libs) {
     return fail(BQSR_ERR_INVALID_ARG, "partitions of one input must share the header's libraries");
   }
-  const int64_t n = s->n_reads;
+  std::vector<int32_t> rg_lib((size_t)std::max(1, s->n_rg), 0);
+  for (int32_t g = 0; g < s->n_rg; ++g)
+    if ((size_t)g < s->rg_has_lb.size() && s->rg_has_lb[(size_t)g])
+      rg_lib[(size_t)g] = 1 + (int32_t)(std::lower_bound(libs.begin(), libs.end(), s->rg_library[(size_t)g]) - libs.begin());
+  int32_t* d_rglib = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_rglib, rg_lib.size() * 4));
+  hipError_t he = hipMemcpy(d_rglib, rg_lib.data(), rg_lib.size() * 4, hipMemcpyHostToDevice);
+  bqsr_status e = he == hipSuccess ? BQSR_OK : fail(BQSR_ERR_DEVICE, hipGetErrorString(he));
+  if (e == BQSR_OK) {
+    mdupd::DevSam S{s->d_text, s->line_span, s->flags, s->rg_id, s->sq_id, s->start, s->qual_off, s->qual,
+                    s->cig_off, s->cig, d_rglib, s->n_rg, s->n_reads};
+    e = dup_set_add_cols(d, S);
+  }
+  (void)hipFree(d_rglib);
+  return e;
+}
+
+namespace {
+// one partition's records appended to the set (slots [d->n, d->n + S.n))
+bqsr_status dup_set_add_cols(bqsr_dup_set* d, const mdupd::DevSam& S) {
+  using namespace mdupd;
+  const int64_t n = S.n;
   if (d->n + n >= (1ll << 32) - 1) return fail(BQSR_ERR_UNSUPPORTED, "more than 2^32 - 1 reads in a dup set");
   hipStream_t st = hipStreamPerThread;
   if (d->n + n > d->cap) {
@@ -668,27 +705,16 @@ bqsr_status bqsr_dup_set_add(bqsr_dup_set* d, const bqsr_sam* s) {
   d->part_base.push_back(d->n);
   d->part_n.push_back(n);
   if (n == 0) return ok();
-  std::vector<int32_t> rg_lib((size_t)std::max(1, s->n_rg), 0);
-  for (int32_t g = 0; g < s->n_rg; ++g)
-    if ((size_t)g < s->rg_has_lb.size() && s->rg_has_lb[(size_t)g])
-      rg_lib[(size_t)g] = 1 + (int32_t)(std::lower_bound(libs.begin(), libs.end(), s->rg_library[(size_t)g]) - libs.begin());
-  int32_t* d_rglib = nullptr;
-  HIP_TRY(hipMalloc((void**)&d_rglib, rg_lib.size() * 4));
-  hipError_t he = hipMemcpyAsync(d_rglib, rg_lib.data(), rg_lib.size() * 4, hipMemcpyHostToDevice, st);
-  if (he == hipSuccess) {
-    DevSam S{s->d_text, s->line_span, s->flags, s->rg_id, s->sq_id, s->start, s->qual_off, s->qual, s->cig_off,
-             s->cig, d_rglib, s->n_rg, n};
-    const unsigned g = (unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)d->ctx->n_cu * 16);
-    hipLaunchKernelGGL(mdup_set_records, dim3(g), dim3(kThreads), 0, st, S, d->n, d->k1, d->k2, d->pos, d->score,
-                       d->lib, d->cls, d->bad);
-    he = hipGetLastError();
-    if (he == hipSuccess) he = hipStreamSynchronize(st);
-  }
-  (void)hipFree(d_rglib);
+  const unsigned g = (unsigned)std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)d->ctx->n_cu * 16);
+  hipLaunchKernelGGL(mdup_set_records, dim3(g), dim3(kThreads), 0, st, S, d->n, d->k1, d->k2, d->pos, d->score,
+                     d->lib, d->cls, d->bad);
+  hipError_t he = hipGetLastError();
+  if (he == hipSuccess) he = hipStreamSynchronize(st);
   if (he != hipSuccess) return fail(BQSR_ERR_DEVICE, hipGetErrorString(he));
   d->n += n;
   return ok();
 }
+}  // namespace
 
 bqsr_status bqsr_dup_set_finish(bqsr_dup_set* d, int64_t* n_duplicates) {
   using namespace mdupd;

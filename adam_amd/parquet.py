@@ -186,7 +186,8 @@ class _Chunk(ctypes.Structure):
                 ("md", _Strings), ("reference", ctypes.c_void_p), ("reference_validity", ctypes.c_void_p),
                 ("start", ctypes.c_void_p), ("start_validity", ctypes.c_void_p), ("record_group", ctypes.c_void_p),
                 ("record_group_validity", ctypes.c_void_p), ("bools", ctypes.c_void_p * 6),
-                ("bools_validity", ctypes.c_void_p * 6)]
+                ("bools_validity", ctypes.c_void_p * 6), ("read_name", _Strings), ("reference_id", ctypes.c_void_p),
+                ("reference_id_validity", ctypes.c_void_p), ("library", ctypes.c_void_p)]
 
 
 _arrow_bound = False
@@ -206,6 +207,8 @@ def _arrow_lib():
             "bqsr_arrow_batch_create": (ctypes.c_int, [vp, vp, vp, i32, vp, pp]),
             "bqsr_arrow_qual_prepare": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, vp, ctypes.POINTER(i64)]),
             "bqsr_arrow_qual_column": (ctypes.c_int, [vp, vp, vp, vp]),
+            "bqsr_arrow_mark_duplicates": (ctypes.c_int, [vp, vp, ctypes.POINTER(i64)]),
+            "bqsr_arrow_flag_bitmap": (ctypes.c_int, [vp, ctypes.c_uint32, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -222,7 +225,9 @@ class ArrowReads:
     and ``qual_column`` rebuilds the qual column after apply -- no per-read
     host work on either side."""
 
-    def __init__(self, table, ctx=None, stream=None):
+    def __init__(self, table, ctx=None, stream=None, markdup: bool = False):
+        """markdup: also load MarkDuplicates' columns (readName, referenceId,
+        recordGroupLibrary) for ``mark_duplicates``."""
         from . import bqsr
         from ._capi import check
         pa, pc, _ = _pa()
@@ -237,6 +242,10 @@ class ArrowReads:
         else:
             self.ref_names = []
         value_set = pa.array(self.ref_names, pa.string())
+        libs = None
+        if markdup and "recordGroupLibrary" in names:
+            libs = pa.array(sorted(v for v in pc.unique(table.column("recordGroupLibrary")).to_pylist()
+                                   if v is not None), pa.string())
         keep = []
 
         def flat(a):
@@ -283,6 +292,22 @@ class ArrowReads:
                     a = flat(rb.column(rb.schema.get_field_index(fld)))
                     b = a.buffers()
                     C.bools[k], C.bools_validity[k] = addr(b[1]), addr(b[0])
+            if markdup:
+                if "readName" in names:
+                    a = rb.column(rb.schema.get_field_index("readName"))
+                    a = flat(a if a.type == pa.string() else a.cast(pa.string()))
+                    b = a.buffers()
+                    C.read_name = _Strings(addr(b[1]), addr(b[2]) or addr(b[1]), addr(b[0]))
+                if "referenceId" in names:
+                    a = rb.column(rb.schema.get_field_index("referenceId"))
+                    a = flat(a if a.type == pa.int32() else a.cast(pa.int32()))
+                    b = a.buffers()
+                    C.reference_id, C.reference_id_validity = addr(b[1]), addr(b[0])
+                if libs is not None:
+                    a = rb.column(rb.schema.get_field_index("recordGroupLibrary"))
+                    rank = pc.add(pc.fill_null(pc.index_in(a, value_set=libs), -1).cast(pa.int32()), 1)
+                    a = flat(rank.cast(pa.int32()))
+                    C.library = addr(a.buffers()[1])
             chunks.append(C)
         arr = (_Chunk * max(1, len(chunks)))(*chunks)
         self.h = ctypes.c_void_p()
@@ -303,6 +328,23 @@ class ArrowReads:
         check(self.L.bqsr_arrow_batch_create(self.ctx.handle, self.h, lut.ctypes.data, len(self.ref_names), stream,
                                              ctypes.byref(bh)))
         return bh
+
+    def mark_duplicates(self) -> int:
+        """MarkDuplicates over the reads (bqsr_arrow_mark_duplicates; load
+        with markdup=True): their duplicateRead bits updated; the count."""
+        from ._capi import check
+        nd = ctypes.c_int64()
+        check(self.L.bqsr_arrow_mark_duplicates(self.ctx.handle, self.h, ctypes.byref(nd)))
+        return int(nd.value)
+
+    def flag_column(self, bit: int):
+        """The reads' flag bit as a pa.BooleanArray (no nulls)."""
+        from ._capi import check
+        pa, _, _ = _pa()
+        n = self.n_reads
+        bm = np.zeros(max(1, (n + 7) // 8), np.uint8)
+        check(self.L.bqsr_arrow_flag_bitmap(self.h, int(bit), bm.ctypes.data))
+        return pa.Array.from_buffers(pa.bool_(), n, [None, pa.py_buffer(bm)])
 
     def qual_column(self, job=None):
         """The qual column (pa.StringArray) after a ResidentJob's step over

@@ -5,11 +5,13 @@
         [-recalibrate_base_qualities] [-dbsnp_sites SITES.vcf]
     python -m adam_amd.transform INPUT.{adam,parquet,sam} OUTPUT.{adam,parquet} [...]
 
-SAM in, SAM out is the device path described below.  ADAMRecord Parquet
-(ADAM's own format) in or out goes through ``transform_parquet``: Arrow
-decodes the Parquet columns on host threads, MarkDuplicates runs over host
-columns, BQSR on the device, and the records are written back as Parquet
-with the qual (and duplicateRead) columns replaced (adamSave).
+SAM or BAM in goes through the device path described below, out as SAM text
+or as ADAMRecord Parquet part files (adamSave, adam_save.py).  ADAMRecord
+Parquet in goes through ``transform_parquet``: Arrow decodes the Parquet
+pages on host threads, the column buffers go to the device as they are
+(parquet.ArrowReads), MarkDuplicates, the BQSR batch and the recalibrated
+qual column are built there, and the records are written back as Parquet
+with the qual (and duplicateRead) columns replaced.
 
 Steps in Transform.run's order (:66-90): load (the SAM text parsed on the
 device, SAMRecordConverter semantics), MarkDuplicates (`adamMarkDuplicates`),
@@ -229,21 +231,16 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
     """`transform` with ADAMRecord Parquet output (adamSave,
     core/rdd/AdamRDDFunctions.scala:37-56): the input -- Parquet (adamLoad,
     AdamContext.scala:318-331, every column kept and written back) or SAM
-    (parsed on the host) -- MarkDuplicates over host columns
-    (bqsr_mark_duplicates), BQSR on the device, the qual (and duplicateRead)
-    columns replaced."""
-    import pyarrow as pa
-    import pyarrow.parquet as pq
-
+    (parsed on the host); for Parquet input the Arrow columns go to the device
+    (parquet.ArrowReads): MarkDuplicates, the BQSR batch and the rebuilt qual
+    column all built there; the qual (and duplicateRead) columns replaced."""
     from . import parquet as P
-    from . import sam as S
-    from .records import F_DUPLICATE, RecordBatch, read_sam_records
+    from .records import RecordBatch, read_sam_records
     t0 = time.perf_counter()
     batch = None
+    A = None
     if is_parquet(inp):
         table = P.read_table(inp)
-        if mark_duplicates:  # MarkDuplicates over host columns
-            batch = P.table_to_batch(table.select([c for c in P.BQSR_PROJECTION if c in table.column_names]))
     else:
         if mark_duplicates:  # (the host SAM parse carries no library / mateMapped: use SAM output or ADAM input)
             raise ValueError("-mark_duplicate_reads with SAM input and ADAM output is not supported")
@@ -252,39 +249,41 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
         table = P.batch_to_table(batch, [r.read_name for r in recs])
     n = table.num_rows
     stats: Dict[str, float] = {"reads": n}
+    if is_parquet(inp) and (mark_duplicates or recalibrate):
+        # the Arrow columns on the device: MarkDuplicates there, the batch
+        # packed there, the qual column rebuilt there after apply
+        cols = [c for c in table.column_names if c in P.BQSR_PROJECTION or c in P.MARKDUP_PROJECTION]
+        A = P.ArrowReads(table.select(cols), bqsr.Context.get(device), markdup=mark_duplicates)
+    try:
+        return _transform_table(A, table, batch, inp, out, mark_duplicates, recalibrate, dbsnp, device, stats, t0)
+    finally:
+        if A is not None:
+            A.close()
+
+
+def _transform_table(A, table, batch, inp, out, mark_duplicates, recalibrate, dbsnp, device, stats, t0):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    from . import parquet as P
+    from .records import F_DUPLICATE
+    n = table.num_rows
     if mark_duplicates:
-        col = lambda name: table.column(name).to_pylist() if name in table.column_names else [None] * n
-        names, libs = col("readName"), col("recordGroupLibrary")
-        mate = np.asarray([bool(v) for v in col("mateMapped")], dtype=np.uint8)
-        ref_id = np.asarray([-1 if v is None else v for v in col("referenceId")], dtype=np.int32)
-        if "referenceId" not in table.column_names:  # the reference index, as the SAM converter sets it
-            ref_id = batch.ref_index.astype(np.int32)
-        dup = S.mark_duplicates(names, libs, batch.flags, mate, batch.rg_id, ref_id, batch.start,
-                                batch.qual_offset, batch.qual, batch.cigar_offset, batch.cigar)
-        batch.flags = np.where(dup, batch.flags | F_DUPLICATE, batch.flags & ~np.uint32(F_DUPLICATE)).astype(np.uint32)
-        dcol = pa.array(dup, pa.bool_())
+        stats["duplicates"] = A.mark_duplicates()
+        dcol = A.flag_column(F_DUPLICATE)
         table = (table.set_column(table.column_names.index("duplicateRead"), "duplicateRead", dcol)
                  if "duplicateRead" in table.column_names else table.append_column("duplicateRead", dcol))
-        stats["duplicates"] = int(dup.sum())
     if recalibrate:
         snp = bqsr.SnpTable.from_vcf(dbsnp) if dbsnp else bqsr.SnpTable()
-        if is_parquet(inp):
-            # the Arrow columns on the device: batch packed there, the qual
-            # column rebuilt there after apply (parquet.ArrowReads)
+        if A is not None:
             from .job import ResidentJob
-            cols = [c for c in P.BQSR_PROJECTION if c in table.column_names]
-            tb = table.select(cols)
-            A = P.ArrowReads(tb, bqsr.Context.get(device))
+            job = ResidentJob(None, None, snp if snp.table else None, device,
+                              handle=A.device_batch(snp.contigs if snp.table else None))
             try:
-                job = ResidentJob(None, None, snp if snp.table else None, device,
-                                  handle=A.device_batch(snp.contigs if snp.table else None))
-                try:
-                    job.step()
-                    qcol = A.qual_column(job)
-                finally:
-                    job.close()
+                job.step()
+                qcol = A.qual_column(job)
             finally:
-                A.close()
+                job.close()
         else:
             parts = bqsr.adam_bqsr([batch], snp if snp.table else None, bqsr.Context.get(device))
             qcol = P.recalibrated_qual_column(parts, n)

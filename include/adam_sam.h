@@ -129,6 +129,13 @@ typedef struct bqsr_arrow_chunk {
   /* readPaired, readMapped, readNegativeStrand, secondOfPair, primaryAlignment, duplicateRead */
   const uint8_t* bools[6];
   const uint8_t* bools_validity[6];
+  /* MarkDuplicates only (NULL otherwise): readName; referenceId (NULL: the
+   * referenceName index); library = 1 + the rank of recordGroupLibrary among
+   * the input's sorted distinct libraries, 0 for null */
+  bqsr_arrow_strings read_name;
+  const int32_t* reference_id;
+  const uint8_t* reference_id_validity;
+  const int32_t* library;
 } bqsr_arrow_chunk;
 typedef struct bqsr_arrow bqsr_arrow;
 bqsr_status bqsr_arrow_load(bqsr_context* ctx, const bqsr_arrow_chunk* chunks, int32_t n_chunks, void* stream,
@@ -148,6 +155,12 @@ bqsr_status bqsr_arrow_qual_prepare(bqsr_context* ctx, bqsr_arrow* a, const bqsr
                                     const uint32_t* out_start, const uint32_t* out_len, const uint64_t* exceptions,
                                     int64_t n_exceptions, void* stream, int64_t* n_bytes);
 bqsr_status bqsr_arrow_qual_column(const bqsr_arrow* a, int32_t* offsets, uint8_t* data, uint8_t* validity);
+/* MarkDuplicates over the reads (bqsr_sam_mark_duplicates' rules; readName
+ * and library from the chunk columns): the duplicateRead bits of the
+ * records (and of the batches built after) set or cleared */
+bqsr_status bqsr_arrow_mark_duplicates(bqsr_context* ctx, bqsr_arrow* a, int64_t* n_duplicates);
+/* the reads' flag bit `flag` (a BQSR_F_* value) as an Arrow boolean bitmap */
+bqsr_status bqsr_arrow_flag_bitmap(const bqsr_arrow* a, uint32_t flag, uint8_t* bitmap);
 
 /* Output (§8 f2): replace every record's QUAL field by its recalibrated
  * string.  out_qual / out_start / out_len / exceptions are the device

@@ -159,3 +159,70 @@ def test_arrow_empty_table():
         assert A.qual_column().to_pylist() == []
     finally:
         A.close()
+
+
+def _dup_table(n=6000, seed=11):
+    """pairs and fragments stacked on few positions (mates share a readName),
+    libraries per read (some null), a few null readNames, referenceId set"""
+    b = synth.generate(n, (60,), 3, seed, contig_len=3000, p_duplicate=0.0)
+    t = P.batch_to_table(b)
+    rng = np.random.default_rng(seed)
+    names = ["r%d" % (r // 2 if r % 4 < 2 else r) for r in range(n)]  # half the reads in pairs
+    for r in rng.choice(n, 20, replace=False):
+        names[r] = None
+    libs = ["lib%d" % (int(b.rg_id[r]) % 2) if r % 13 else None for r in range(n)]
+    t = t.append_column("readName", pa.array(names, pa.string()))
+    t = t.append_column("recordGroupLibrary", pa.array(libs, pa.string()))
+    t = t.append_column("referenceId", pa.array([0 if b.flags[r] & R.F_HAS_REFNAME else None for r in range(n)],
+                                                pa.int32()))
+    t = t.append_column("mateMapped", pa.array([bool(r % 3) for r in range(n)], pa.bool_()))
+    return t
+
+
+def test_arrow_mark_duplicates_matches_host_form():
+    # the device MarkDuplicates over Arrow columns against bqsr_mark_duplicates
+    # (the host form, itself checked against oracle/markdup.py)
+    from adam_amd import sam as S
+    t = _dup_table()
+    batch = P.table_to_batch(t.select([c for c in P.BQSR_PROJECTION if c in t.column_names]))
+    col = lambda name: t.column(name).to_pylist()  # noqa: E731
+    want = S.mark_duplicates(col("readName"), col("recordGroupLibrary"), batch.flags,
+                             np.asarray(col("mateMapped"), np.uint8), batch.rg_id,
+                             np.asarray([-1 if v is None else v for v in col("referenceId")], np.int32), batch.start,
+                             batch.qual_offset, batch.qual, batch.cigar_offset, batch.cigar)
+    assert want.sum() > 0
+    A = P.ArrowReads(t, markdup=True)
+    try:
+        nd = A.mark_duplicates()
+        got = np.asarray(A.flag_column(R.F_DUPLICATE).to_pylist(), bool)
+        assert nd == int(want.sum())
+        assert np.array_equal(got, want)
+        # the batch built after carries the bits
+        bh = A.device_batch()
+        _capi.lib().bqsr_batch_destroy(bh)
+    finally:
+        A.close()
+
+
+def test_transform_adam_markdup_recal_device(tmp_path):
+    # Parquet in -> MarkDuplicates + BQSR on the device -> Parquet out, against
+    # the host form's duplicate bits and the oracle-backed host BQSR path
+    from adam_amd import sam as S
+    from adam_amd.transform import transform
+    t = _dup_table(8000, 5)
+    inp, out = str(tmp_path / "in.parquet"), str(tmp_path / "out.parquet")
+    pq.write_table(t, inp)
+    st = transform(inp, out, mark_duplicates=True, recalibrate=True)
+    o = pq.read_table(out)
+    batch = P.table_to_batch(t.select([c for c in P.BQSR_PROJECTION if c in t.column_names]))
+    col = lambda name: t.column(name).to_pylist()  # noqa: E731
+    want = S.mark_duplicates(col("readName"), col("recordGroupLibrary"), batch.flags,
+                             np.asarray(col("mateMapped"), np.uint8), batch.rg_id,
+                             np.asarray([-1 if v is None else v for v in col("referenceId")], np.int32), batch.start,
+                             batch.qual_offset, batch.qual, batch.cigar_offset, batch.cigar)
+    assert st["duplicates"] == int(want.sum())
+    assert o.column("duplicateRead").to_pylist() == list(want)
+    batch.flags = np.where(want, batch.flags | R.F_DUPLICATE, batch.flags & ~np.uint32(R.F_DUPLICATE)).astype(np.uint32)
+    parts = bqsr.adam_bqsr([batch], None, bqsr.Context.get(0))
+    assert o.column("qual").to_pylist() == P.recalibrated_qual_column(parts, batch.n_reads).to_pylist()
+    assert o.column("readName").to_pylist() == col("readName")
