@@ -196,7 +196,6 @@ def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
     its current text (after ``rewrite``: recalibrated qual, MarkDuplicates'
     flag)."""
     import pyarrow as pa
-    import pyarrow.compute as pc
     L = _lib()
     ctx = sam.ctx
     sz = AdamSizes()
@@ -249,27 +248,46 @@ def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
     cols.update(ints)
     for c, name in enumerate(BOOL_COLS):
         cols[name] = pa.Array.from_buffers(pa.bool_(), n, [None, pb(bools[c])])
-    # by index: the @SQ entry of referenceId / mateReferenceId, the @RG record of recordGroupId
-    ref, mref, rgi = ints["referenceId"], ints["mateReferenceId"], ints["recordGroupId"]
+    # by index: the @SQ entry of referenceId / mateReferenceId, the @RG record
+    # of recordGroupId -- dictionary arrays over the header's values with the
+    # index columns as their indices (no per-record copy; Parquet stores them
+    # as plain string / int columns, dictionary-encoded)
+    src = {"ref": (i32[0], ivalid[0]), "mref": (i32[2], ivalid[2]), "rg": (i32[3], ivalid[3])}
+    masks: Dict[Tuple[str, bytes], object] = {}
 
-    def take(values, idx, typ):
-        return pc.take(pa.array(values if values else [None], typ), idx)
+    def lookup(values, which, typ):
+        idx, valid = src[which]
+        has = np.asarray([v is not None for v in values], bool)
+        if not has.any():
+            return pa.nulls(n, typ)
+        dic = pa.array([v if v is not None else (0 if typ != pa.string() else "") for v in values], typ)
+        if has.all():
+            vbuf = pb(valid)
+        else:  # entries without the value: null
+            key = (which, has.tobytes())
+            if key not in masks:
+                vb = np.unpackbits(valid.view(np.uint8), count=n, bitorder="little").astype(bool)
+                ok = vb & has[np.clip(idx[:n], 0, len(values) - 1)]
+                masks[key] = pa.py_buffer(np.packbits(ok, bitorder="little"))
+            vbuf = masks[key]
+        ind = pa.Array.from_buffers(pa.int32(), n, [vbuf, pb(idx[:n])])
+        return pa.DictionaryArray.from_arrays(ind, dic, safe=False)
 
     sq_name = [r["SN"] for r in hdr.sq]
     sq_len, sq_url = hdr.sq_column("LN", "int"), hdr.sq_column("UR")
-    cols["referenceName"] = take(sq_name, ref, pa.string())
-    cols["referenceLength"] = take(sq_len, ref, pa.int64())
-    cols["referenceUrl"] = take(sq_url, ref, pa.string())
-    cols["mateReference"] = take(sq_name, mref, pa.string())
-    cols["mateReferenceLength"] = take(sq_len, mref, pa.int64())
-    cols["mateReferenceUrl"] = take(sq_url, mref, pa.string())
-    cols["recordGroupName"] = take(hdr.rg_column("ID"), rgi, pa.string())
+    cols["referenceName"] = lookup(sq_name, "ref", pa.string())
+    cols["referenceLength"] = lookup(sq_len, "ref", pa.int64())
+    cols["referenceUrl"] = lookup(sq_url, "ref", pa.string())
+    cols["mateReference"] = lookup(sq_name, "mref", pa.string())
+    cols["mateReferenceLength"] = lookup(sq_len, "mref", pa.int64())
+    cols["mateReferenceUrl"] = lookup(sq_url, "mref", pa.string())
+    cols["recordGroupName"] = lookup(hdr.rg_column("ID"), "rg", pa.string())
     for name, key in RG_TAGS:
-        cols[name] = take(hdr.rg_column(key), rgi, pa.string())
-    cols["recordGroupRunDateEpoch"] = take(hdr.rg_column("DT", "date"), rgi, pa.int64())
-    cols["recordGroupPredictedMedianInsertSize"] = take(hdr.rg_column("PI", "int"), rgi, pa.int32())
+        cols[name] = lookup(hdr.rg_column(key), "rg", pa.string())
+    cols["recordGroupRunDateEpoch"] = lookup(hdr.rg_column("DT", "date"), "rg", pa.int64())
+    cols["recordGroupPredictedMedianInsertSize"] = lookup(hdr.rg_column("PI", "int"), "rg", pa.int32())
     # (the arrays hold their host buffers: pa.py_buffer keeps each numpy array alive)
-    return pa.table([cols[name] for name, _ in ADAM_FIELDS], schema=schema())
+    return pa.table([cols[name] for name, _ in ADAM_FIELDS], names=[name for name, _ in ADAM_FIELDS])
 
 
 class AdamWriter:
@@ -283,6 +301,9 @@ class AdamWriter:
             shutil.rmtree(self.tmp)
         os.makedirs(self.tmp)
         self.compression = None if compression in (None, "none") else compression
+        # gzip at zlib's default level 6 (parquet-mr's GzipCodec through Hadoop;
+        # Arrow's own default is 9)
+        self.level = 6 if self.compression == "gzip" else None
         nth = threads or max(1, min(16, len(os.sched_getaffinity(0))))
         self.pool = ThreadPoolExecutor(max_workers=nth)
         self.futures = []
@@ -295,7 +316,8 @@ class AdamWriter:
         # per-read strings (names, bases, quals, tags), whose dictionaries
         # overflow and whose min / max no reader filters on
         pq.write_table(table, os.path.join(self.tmp, name), compression=self.compression,
-                       use_dictionary=DICT_COLS, write_statistics=STATS_COLS)
+                       compression_level=self.level, use_dictionary=DICT_COLS, write_statistics=STATS_COLS,
+                       store_schema=False)
 
     def add(self, table):
         name = "part-r-%05d.parquet" % self.parts

@@ -374,7 +374,7 @@ def is_bam(data) -> bool:
 
 def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
               dbsnp: Optional[str] = None, device: int = 0, partition_bytes: int = DEFAULT_PARTITION_BYTES,
-              compression: str = "gzip", part_reads: int = 1 << 20) -> Dict[str, float]:
+              compression: str = "gzip", part_reads: int = 1 << 19) -> Dict[str, float]:
     """Transform.run (cli/Transform.scala:62-97) over SAM or BAM input: the
     records parsed on the device (a BAM's records become SAM lines there),
     MarkDuplicates, BQSR, then adamSave (OUT.adam / .parquet / a directory:
@@ -455,7 +455,7 @@ def main(argv=None) -> int:
                     help="records per streamed partition, in bytes of SAM text")
     ap.add_argument("-parquet_compression", default="gzip", choices=("gzip", "snappy", "zstd", "none"),
                     help="ADAM output: the part files' codec (adamSave's default: GZIP)")
-    ap.add_argument("-part_reads", type=int, default=1 << 20, help="ADAM output: records per part file")
+    ap.add_argument("-part_reads", type=int, default=1 << 19, help="ADAM output: records per part file")
     a = ap.parse_args(argv)
     if a.sort_reads or a.realignIndels or a.coalesce != -1:
         ap.error("-sort_reads / -coalesce / -realignIndels are outside this build")

@@ -40,7 +40,12 @@ pytestmark = pytest.mark.gpu
 def _table(data: bytes, bam: bool = False):
     s = SamText(data, bam=bam)
     try:
-        return A.adam_table(s, 0, s.counts().n_reads, A.header_info(s))
+        t = A.adam_table(s, 0, s.counts().n_reads, A.header_info(s))
+        # header-derived columns are dictionary arrays over the header's values
+        for f in t.schema:
+            want = A.schema().field(f.name).type
+            assert f.type == want or (pa.types.is_dictionary(f.type) and f.type.value_type == want), f
+        return t.cast(A.schema())
     finally:
         s.close()
 

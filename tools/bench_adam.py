@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--bam", action="store_true")
     ap.add_argument("--no-markdup", action="store_true")
     ap.add_argument("--compression", default="snappy")
-    ap.add_argument("--part-reads", type=int, default=1 << 20)
+    ap.add_argument("--part-reads", type=int, default=1 << 19)
     ap.add_argument("--partition-bytes", type=int, default=8 << 30)
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--dir", default=None, help="scratch directory (default: a temporary one)")

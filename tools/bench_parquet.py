@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--reads", type=int, default=2_000_000)
     ap.add_argument("--len", type=int, default=100)
     ap.add_argument("--compression", default="snappy")
-    ap.add_argument("--row-group", type=int, default=1 << 20)
+    ap.add_argument("--row-group", type=int, default=0,
+                    help="rows per row group (0: 128 MB of column data, parquet-mr's block size in adamSave)")
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     import pyarrow.parquet as pq
@@ -31,7 +32,8 @@ def main():
     del b
     work = tempfile.mkdtemp(prefix="bench_parquet_")
     path = os.path.join(work, "reads.parquet")
-    pq.write_table(table, path, compression=a.compression, row_group_size=a.row_group)
+    rg = a.row_group or max(1, (128 << 20) * table.num_rows // max(1, table.nbytes))
+    pq.write_table(table, path, compression=a.compression, row_group_size=rg)
     del table
     t_gen = time.perf_counter() - t0
     print("[bench_parquet] wrote %d bytes in %.1f s" % (os.path.getsize(path), t_gen), file=sys.stderr, flush=True)
@@ -65,7 +67,7 @@ def main():
     tot, dec, load, pack = best
     print(json.dumps({"metric": "ADAM Parquet read reads/s (Arrow decode on host threads -> buffers to the device -> "
                                 "parse layout and BQSR batch on the device)",
-                      "reads": a.reads, "read_len": a.len, "compression": a.compression,
+                      "reads": a.reads, "read_len": a.len, "compression": a.compression, "row_group_rows": rg,
                       "seconds": tot, "reads_per_s": a.reads / tot,
                       "split_s": {"arrow_decode": dec, "device_load": load, "batch_pack": pack},
                       "gen_seconds": t_gen}))
