@@ -171,7 +171,7 @@ def _dup_table(n=6000, seed=11):
     for r in rng.choice(n, 20, replace=False):
         names[r] = None
     libs = ["lib%d" % (int(b.rg_id[r]) % 2) if r % 13 else None for r in range(n)]
-    t = t.append_column("readName", pa.array(names, pa.string()))
+    t = t.set_column(t.column_names.index("readName"), "readName", pa.array(names, pa.string()))
     t = t.append_column("recordGroupLibrary", pa.array(libs, pa.string()))
     t = t.append_column("referenceId", pa.array([0 if b.flags[r] & R.F_HAS_REFNAME else None for r in range(n)],
                                                 pa.int32()))
