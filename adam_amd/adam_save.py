@@ -82,6 +82,8 @@ def _lib():
     L = S._lib()
     if not _bound:
         vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.bqsr_sam_adam_set_quals.restype = ctypes.c_int
+        L.bqsr_sam_adam_set_quals.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, vp]
         L.bqsr_sam_adam_prepare.restype = ctypes.c_int
         L.bqsr_sam_adam_prepare.argtypes = [vp, vp, i64, i64, vp, ctypes.POINTER(AdamSizes)]
         L.bqsr_sam_adam_columns.restype = ctypes.c_int
@@ -166,6 +168,13 @@ class HeaderInfo:
                     v = None
             out.append(v)
         return out
+
+
+def set_quals(sam, bh=None, out_qual=None, out_start=None, out_len=None, exc=None, n_exc: int = 0, stream=None):
+    """The ADAM qual column of `sam` from an apply's device outputs for batch
+    bh (bqsr_sam_adam_set_quals: no text rewrite); bh None: the text's."""
+    check(_lib().bqsr_sam_adam_set_quals(sam.ctx.handle, sam.h, bh, out_qual, out_start, out_len, exc, n_exc,
+                                         stream))
 
 
 def header_info(sam) -> HeaderInfo:

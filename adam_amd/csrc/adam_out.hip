@@ -51,7 +51,35 @@ struct AdamParams {
   uint64_t* bools;            // [kBools][W]
   int64_t W;
   unsigned long long* err;
+  // the apply's outputs in place of the text's QUAL (bqsr_sam_adam_set_quals;
+  // out_qual null: the text's), and MarkDuplicates' bits in place of FLAG 0x400
+  const ReadMeta* meta;
+  const ReadInfo* info;
+  const uint8_t* out_qual;
+  const uint32_t* out_start;
+  const uint32_t* out_len;
+  const uint64_t* exc;  // sorted (slot << 16 | char)
+  int64_t n_exc;
+  const uint32_t* dup_flags;
 };
+
+// the recalibrated char at slot (u8 column, exceptions above 0xFF)
+__device__ __forceinline__ uint32_t apply_char(const AdamParams& P, uint64_t slot) {
+  uint32_t c = P.out_qual[slot];
+  int64_t lo = 0, hi = P.n_exc - 1;
+  while (lo <= hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const uint64_t v = P.exc[mid], s = v >> 16;
+    if (s == slot) return (uint32_t)(v & 0xFFFFull);
+    if (s < slot) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return c;
+}
+// record r's QUAL from the apply (not a pass-through read)
+__device__ __forceinline__ bool new_qual(const AdamParams& P, int64_t r) {
+  return P.out_qual && !(P.info[r].fl & kInfoPass);
+}
 
 __device__ __forceinline__ void adam_error(const AdamParams& P, int64_t i, uint32_t code) {
   atomicMin(P.err, (unsigned long long)(((uint64_t)i << 8) | code));
@@ -221,6 +249,8 @@ __device__ void adam_record(const AdamParams& P, int64_t r, AdamRec& x, Tag* tg)
   int64_t flag = 0, pos = 0, mapq = 255, pnext = 0;
   (void)samk::parse_int(t, fa[1], fb[1], &flag);  // (the parse accepted FLAG; POS when the reference is known)
   x.flag = (uint32_t)flag;
+  if (P.dup_flags)  // FLAG 0x400 following duplicateRead, as bqsr_sam_rewrite_quals writes it
+    x.flag = (P.dup_flags[r] & BQSR_F_DUPLICATE) ? (x.flag | 0x400u) : (x.flag & ~0x400u);
   int32_t sq = -1;
   if (!(fb[2] - fa[2] == 1 && t[fa[2]] == '*')) sq = samk::name_lookup(P.sq, t + fa[2], fb[2] - fa[2]);
   // referenceId / referenceName / start / mapq only when the read has a reference (:36-54)
@@ -306,6 +336,13 @@ extern "C" __global__ void __launch_bounds__(256) adam_len(AdamParams P) {
       for (int c = 0; c < kStr; ++c)
         P.len[(int64_t)c * P.n + i] = c == 5 ? (uint64_t)x.attr_n : c == 2 ? (uint64_t)x.cig_n
                                                : x.sv[c] ? (uint64_t)(x.sb[c] - x.sa[c]) : 0ull;
+      const int64_t r = P.r0 + i;
+      if (new_qual(P, r)) {  // the recalibrated chars as UTF-8
+        const uint64_t slot = P.meta[r].slot + P.out_start[r];
+        uint64_t q = 0;
+        for (uint32_t k = 0; k < P.out_len[r]; ++k) q += (uint64_t)samk::utf8_len(apply_char(P, slot + k));
+        P.len[3 * P.n + i] = q;
+      }
     } else {
       x.flag = 0;
       for (int c = 0; c < kStr; ++c) x.sv[c] = false;
@@ -344,6 +381,21 @@ extern "C" __global__ void __launch_bounds__(256) adam_write(AdamParams P) {
         if (x.code == kAdamOk) (void)attributes_text(P.text, tg, x.nt, d, &code);
       } else if (c == 2) {
         (void)cigar_text(P.cig + P.cig_off[r], (int64_t)(P.cig_off[r + 1] - P.cig_off[r]), d);
+      } else if (c == 3 && new_qual(P, r)) {
+        const uint64_t slot = P.meta[r].slot + P.out_start[r];
+        for (uint32_t k = 0; k < P.out_len[r]; ++k) {
+          const uint32_t ch = apply_char(P, slot + k);
+          if (ch < 0x80u) {
+            *d++ = (uint8_t)ch;
+          } else if (ch < 0x800u) {
+            *d++ = (uint8_t)(0xC0u | (ch >> 6));
+            *d++ = (uint8_t)(0x80u | (ch & 0x3Fu));
+          } else {
+            *d++ = (uint8_t)(0xE0u | (ch >> 12));
+            *d++ = (uint8_t)(0x80u | ((ch >> 6) & 0x3Fu));
+            *d++ = (uint8_t)(0x80u | (ch & 0x3Fu));
+          }
+        }
       } else if (x.sv[c]) {
         for (int64_t k = x.sa[c]; k < x.sb[c]; ++k) *d++ = P.text[k];
       }
@@ -367,6 +419,13 @@ struct AdamBufs {
   int64_t tot[adamk::kStr] = {}, cap_bytes[adamk::kStr] = {};
   unsigned long long* err = nullptr;
   bool prepared = false;
+  // bqsr_sam_adam_set_quals: the apply's outputs (caller's device buffers)
+  // and a sorted copy of its exception list
+  const bqsr_batch* qb = nullptr;
+  const uint8_t* out_qual = nullptr;
+  const uint32_t *out_start = nullptr, *out_len = nullptr;
+  uint64_t* exc = nullptr;
+  int64_t n_exc = 0;
   void free_rows() {
     for (void* p : {(void*)len, (void*)off, (void*)part, (void*)svalid, (void*)ivalid, (void*)bools, (void*)soff,
                     (void*)i32, (void*)i64})
@@ -381,6 +440,7 @@ struct AdamBufs {
     for (auto& p : sbytes)
       if (p) (void)hipFree(p);
     if (err) (void)hipFree(err);
+    if (exc) (void)hipFree(exc);
   }
 };
 
@@ -390,7 +450,53 @@ bqsr_sam::~bqsr_sam() {
   if (d_text) (void)hipFree(d_text);
 }
 
+namespace {
+void adam_quals(adamk::AdamParams& P, const AdamBufs& A, const bqsr_sam* s) {
+  if (A.out_qual) {
+    P.meta = A.qb->rd.meta;
+    P.info = (const ReadInfo*)A.qb->d_info;
+    P.out_qual = A.out_qual;
+    P.out_start = A.out_start;
+    P.out_len = A.out_len;
+    P.exc = A.exc;
+    P.n_exc = A.n_exc;
+  }
+  P.dup_flags = s->dup_marked ? s->flags : nullptr;
+}
+}  // namespace
+
 extern "C" {
+
+bqsr_status bqsr_sam_adam_set_quals(bqsr_context* ctx, bqsr_sam* s, const bqsr_batch* b, const uint8_t* out_qual,
+                                    const uint32_t* out_start, const uint32_t* out_len, const uint64_t* exceptions,
+                                    int64_t n_exc, void* stream) {
+  if (!ctx || !s || (b && (!out_qual || !out_start || !out_len)) || n_exc < 0 || (n_exc > 0 && !exceptions))
+    return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_adam_set_quals: bad arguments");
+  if (b && b->rd.n_reads != s->n_reads) return fail(BQSR_ERR_INVALID_ARG, "batch and SAM read counts differ");
+  if (b && !b->prepped) return fail(BQSR_ERR_INVALID_ARG, "the batch has not been through apply");
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (!s->adam) s->adam = new AdamBufs;
+  AdamBufs& A = *(AdamBufs*)s->adam;
+  A.prepared = false;
+  if (A.exc) (void)hipFree(A.exc);
+  A.exc = nullptr;
+  A.n_exc = 0;
+  A.qb = b;
+  A.out_qual = b ? out_qual : nullptr;
+  A.out_start = b ? out_start : nullptr;
+  A.out_len = b ? out_len : nullptr;
+  if (b && n_exc > 0) {  // the exception list in slot order (binary search)
+    hipStream_t st = S(stream);
+    std::vector<uint64_t> h((size_t)n_exc);
+    HIP_TRY(hipMemcpyAsync(h.data(), exceptions, (size_t)n_exc * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::sort(h.begin(), h.end());
+    HIP_TRY(hipMalloc((void**)&A.exc, h.size() * 8));
+    HIP_TRY(hipMemcpy(A.exc, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    A.n_exc = n_exc;
+  }
+  return ok();
+}
 
 bqsr_status bqsr_sam_header_text(const bqsr_sam* s, char* dst, int64_t cap, int64_t* len) {
   if (!s || !len || (cap > 0 && !dst)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_sam_header_text: bad arguments");
@@ -451,6 +557,7 @@ bqsr_status bqsr_sam_adam_prepare(bqsr_context* ctx, bqsr_sam* s, int64_t r0, in
   P.bools = A.bools;
   P.W = W;
   P.err = A.err;
+  adam_quals(P, A, s);
   HIP_TRY(hipMemsetAsync(A.err, 0xFF, 8, st));
   const unsigned g = sam_grid(n, 256, ctx->n_cu * 8);
   if (n > 0) hipLaunchKernelGGL(adamk::adam_len, dim3(g), dim3(256), 0, st, P);
@@ -514,6 +621,7 @@ bqsr_status bqsr_sam_adam_columns(bqsr_context* ctx, bqsr_sam* s, const bqsr_ada
   P.soff = A.soff;
   for (int c = 0; c < adamk::kStr; ++c) P.sbytes[c] = A.sbytes[c];
   P.W = A.W;
+  adam_quals(P, A, s);
   if (n > 0) {
     hipLaunchKernelGGL(adamk::adam_write, dim3(sam_grid(n, 256, ctx->n_cu * 8)), dim3(256), 0, st, P);
   } else {

@@ -86,7 +86,8 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
                      max_exc: int = 1 << 16, dups=None) -> Dict[str, float]:
     """BQSR over several partitions of one SAM input (see the module doc);
     emit(i, sam) gets every partition's parse with its QUAL fields rewritten,
-    in partition order.  dups: a finished sam.DupSet over the same
+    in partition order (emit(i, sam, quals): quals = the apply's outputs for
+    the parse, handed to the sink).  dups: a finished sam.DupSet over the same
     partitions (MarkDuplicates' bits set on every parse before its batch is
     built and before it is rewritten)."""
     import torch
@@ -153,9 +154,7 @@ def _bqsr_partitions(data, header: bytes, ranges: List[Tuple[int, int]], snp, ct
             try:
                 if dups is not None:
                     dups.apply(i, sam)
-                check(L.bqsr_sam_rewrite_quals(h, sam.h, bh, ptr(out_qual), ptr(out_start), ptr(out_len), ptr(exc),
-                                               nexc.value, sp))
-                emit(i, sam)
+                emit(i, sam, (bh, ptr(out_qual), ptr(out_start), ptr(out_len), ptr(exc), nexc.value, sp))
             finally:
                 sam.close()
             L.bqsr_batch_destroy(bh)
@@ -201,8 +200,7 @@ def _partitions(data, header: bytes, ranges, mark_duplicates: bool, recalibrate:
                 try:
                     n_reads += sam.counts().n_reads
                     dups.apply(i, sam)
-                    sam.rewrite(None)
-                    emit(i, sam)
+                    emit(i, sam, None)
                 finally:
                     sam.close()
             stats = {"reads": n_reads, "partitions": len(ranges)}
@@ -306,7 +304,13 @@ class _SamOut:
         self.fh = open(self.tmp, "wb")
         self.first = True
 
-    def emit(self, i, sam):
+    def emit(self, i, sam, quals=None):
+        """quals: (batch, out_qual, out_start, out_len, exceptions, n, stream)
+        of an apply over the parse (None: QUAL kept; FLAG after MarkDuplicates)"""
+        if quals is None:
+            sam.rewrite(None)
+        else:
+            check(_capi.lib().bqsr_sam_rewrite_quals(sam.ctx.handle, sam.h, *quals))
         text = sam.text()
         self.fh.write(text if self.first else text[self._header_len(sam):])
         self.first = False
@@ -334,7 +338,11 @@ class _AdamOut:
         self.w = AdamWriter(path, compression)
         self.part_reads = part_reads
 
-    def emit(self, i, sam):
+    def emit(self, i, sam, quals=None):
+        """the ADAM columns with the apply's quals (no text rewrite)"""
+        from .adam_save import set_quals
+        if quals is not None:
+            set_quals(sam, *quals)
         self.w.emit(sam, self.part_reads)
 
     def close(self, ok: bool = True):
@@ -416,14 +424,15 @@ def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bo
                             try:
                                 with ph("bqsr"):
                                     job.step()
-                                with ph("rewrite"):
-                                    sam.rewrite(job)
+                                p = job._ptr
+                                with ph("emit"):
+                                    sink.emit(0, sam, (job.bh, p(job.out_qual), p(job.out_start), p(job.out_len),
+                                                       p(job.exc), job.n_exc, job.sp))
                             finally:
                                 job.close()
-                        elif mark_duplicates:
-                            sam.rewrite(None)
-                        with ph("emit"):
-                            sink.emit(0, sam)
+                        else:
+                            with ph("emit"):
+                                sink.emit(0, sam, None)
                     finally:
                         sam.close()
                     stats["phases"] = ph.t

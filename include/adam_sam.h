@@ -217,6 +217,15 @@ typedef struct bqsr_adam_host {
 bqsr_status bqsr_sam_adam_prepare(bqsr_context* ctx, bqsr_sam* s, int64_t r0, int64_t n, void* stream,
                                   bqsr_adam_sizes* out);
 bqsr_status bqsr_sam_adam_columns(bqsr_context* ctx, bqsr_sam* s, const bqsr_adam_host* dst, void* stream);
+/* The ADAM columns' qual from an apply's outputs for batch `b` (built from
+ * this parse in read order) instead of the text's QUAL, as
+ * bqsr_sam_rewrite_quals would write them (pass-through reads keep theirs),
+ * without rewriting the text; the device buffers must outlive the following
+ * prepare / columns calls.  b == NULL: the text's QUAL again.  After
+ * MarkDuplicates the duplicateRead column follows its bits either way. */
+bqsr_status bqsr_sam_adam_set_quals(bqsr_context* ctx, bqsr_sam* s, const bqsr_batch* b, const uint8_t* out_qual,
+                                    const uint32_t* out_start, const uint32_t* out_len, const uint64_t* exceptions,
+                                    int64_t n_exceptions, void* stream);
 /* the header lines of the parse (SAM input, or a BAM's header text) */
 bqsr_status bqsr_sam_header_text(const bqsr_sam* s, char* dst, int64_t cap, int64_t* len);
 
