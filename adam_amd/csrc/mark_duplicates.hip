@@ -228,16 +228,16 @@ extern "C" __global__ void __launch_bounds__(kThreads) mdup_groups(const uint32_
                                                                   uint8_t* outcome) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nb; p += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t g = kll[order[p]];
+    if (!has_left(g)) {  // buckets without a primary mapped read: markReads(false), each on its own
+      outcome[order[p]] = kNone;  // (their group -- every such bucket of a library -- can be huge)
+      continue;
+    }
     if (p > 0 && kll[order[p - 1]] == g) continue;  // not a group head
     int64_t q = p;
     bool pairs = false;
     while (q < nb && kll[order[q]] == g) {
       pairs |= kr[order[q]] != kNoPos;
       ++q;
-    }
-    if (!has_left(g)) {  // unmapped buckets: markReads(false)
-      for (int64_t i = p; i < q; ++i) outcome[order[i]] = kNone;
-      continue;
     }
     // scoring runs: each right position when the group has pairs (its
     // fragments are duplicates), else the whole group

@@ -8,7 +8,9 @@
 //   2. rocPRIM exclusive scan of the spans -> each read's first slot;
 //   3. a wavefront per read: ReadMeta / ReadAlign, phred bytes (char - 33) and
 //      4-bit base codes at the read's slots (slots are 16-aligned, so a read's
-//      code bytes are its own), kSeqOther by ballot, the qual histogram in LDS.
+//      code bytes are its own), kSeqOther by ballot;
+//   4. the qual histogram of the packed column (the launch window), per-thread
+//      LDS counters without conflicts (sam_batch_qhist).
 // CIGAR and MD columns are copied whole; a read's offsets are the parse's.
 
 namespace sbk {
@@ -20,6 +22,7 @@ struct Lens {
   uint32_t n_rg;        // max rg id + 1
   uint32_t max_len;     // max sequence length
   unsigned long long bad_read;  // first read whose fields overflow the layout (~0: none)
+  unsigned long long n_qual;    // Σ Lq: qual bytes in the slots (the rest of the column is zero padding)
 };
 
 __device__ __forceinline__ uint32_t field_len(const uint64_t* off, int64_t r) { return (uint32_t)(off[r + 1] - off[r]); }
@@ -28,7 +31,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_spans(const uin
                                                                       const uint64_t* seq_off, const uint64_t* qual_off,
                                                                       const uint64_t* cig_off, const uint64_t* md_off,
                                                                       int64_t n, uint64_t* span, Lens* L) {
-  uint64_t ms = 0;
+  uint64_t ms = 0, nq = 0;
   uint32_t nrg = 1, ml = 1;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t f = flags[r];
@@ -41,6 +44,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_spans(const uin
       atomicMin(&L->bad_read, (unsigned long long)r);
     const uint64_t sl = slot_span(lq, ls);
     span[r] = sl;
+    nq += lq;
     ms = sl > ms ? sl : ms;
     if (has_rg && rg[r] >= 0) nrg = max(nrg, (uint32_t)rg[r] + 1u);
     ml = max(ml, field_len(seq_off, r));  // dims_of: the longest sequence
@@ -49,11 +53,13 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_spans(const uin
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t x = __shfl_xor(ms, o);
     ms = x > ms ? x : ms;
+    nq += __shfl_xor(nq, o);
     nrg = max(nrg, (uint32_t)__shfl_xor((int)nrg, o));
     ml = max(ml, (uint32_t)__shfl_xor((int)ml, o));
   }
   if ((threadIdx.x & 63) == 0) {
     atomicMax((unsigned long long*)&L->max_slot, (unsigned long long)ms);
+    atomicAdd(&L->n_qual, (unsigned long long)nq);
     atomicMax(&L->n_rg, nrg);
     atomicMax(&L->max_len, ml);
   }
@@ -74,10 +80,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_pack(
     const uint32_t* flags, const int32_t* rg, const int32_t* ref, const int64_t* start, const uint64_t* seq_off,
     const uint8_t* seq, const uint64_t* qual_off, const uint8_t* qual_in, const uint64_t* cig_off, const uint64_t* md_off,
     const int32_t* ref_contig, int32_t n_ref, const uint64_t* slot, int64_t n, ReadMeta* meta, ReadAlign* align,
-    uint8_t* qual, uint8_t* bases, unsigned long long* qhist, unsigned long long* rghist, int32_t n_rg_hist) {
-  __shared__ uint32_t h[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) h[i] = 0;
-  __syncthreads();
+    uint8_t* qual, uint8_t* bases, unsigned long long* rghist, int32_t n_rg_hist) {
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -88,9 +91,7 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_pack(
     const uint64_t s0 = slot[r];
     const uint8_t* q = qual_in + qual_off[r];
     for (uint32_t i = lane; i < lq; i += 64) {
-      const uint8_t v = (uint8_t)(q[i] - 33);  // (char - 33).toByte
-      qual[s0 + i] = v;
-      atomicAdd(&h[v], 1u);
+      qual[s0 + i] = (uint8_t)(q[i] - 33);  // (char - 33).toByte
     }
     const uint8_t* sq = seq + seq_off[r];
     bool other = false;
@@ -122,9 +123,39 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_pack(
       if (has_rg && rg[r] >= 0 && rg[r] < n_rg_hist) atomicAdd(&rghist[rg[r]], 1ull);
     }
   }
+}
+
+// The packed qual column's histogram (the batch's launch window): 16-B loads,
+// per-thread counters for quals 0..127 in LDS laid out bin-major (thread t's
+// bin b at word b * kHistThreads + t: the lanes of a wavefront never share a
+// bank or a word, so the adds neither conflict nor need atomics), quals >=
+// 128 in a register; zero padding between reads is counted in bin 0 and
+// taken out on the host (n_slots - Σ Lq).
+constexpr int kHistThreads = 128;
+extern "C" __global__ void __launch_bounds__(kHistThreads) sam_batch_qhist(const uint4* q16, int64_t n16,
+                                                                          unsigned long long* qhist) {
+  __shared__ uint32_t h[kQBins * kHistThreads];
+  const int t = threadIdx.x;
+  for (int b = 0; b < kQBins; ++b) h[b * kHistThreads + t] = 0;
+  uint32_t high = 0;
+  for (int64_t i = blockIdx.x * (int64_t)kHistThreads + t; i < n16; i += (int64_t)gridDim.x * kHistThreads) {
+    const uint4 v = q16[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      if (b < (uint32_t)kQBins) h[b * kHistThreads + t] += 1u;
+      else ++high;
+    }
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < 256; i += blockDim.x)
-    if (h[i]) atomicAdd(&qhist[i], (unsigned long long)h[i]);
+  for (int b = t; b < kQBins; b += kHistThreads) {  // a thread per bin sums the block's counters
+    uint64_t c = 0;
+    for (int j = 0; j < kHistThreads; ++j) c += h[b * kHistThreads + ((j + b) & (kHistThreads - 1))];
+    if (c) atomicAdd(&qhist[b], (unsigned long long)c);
+  }
+  for (int o = 32; o > 0; o >>= 1) high += __shfl_xor(high, o);
+  if ((t & 63) == 0 && high) atomicAdd(&qhist[kQBins], (unsigned long long)high);
 }
 
 }  // namespace sbk
@@ -173,7 +204,7 @@ bqsr_status pack_batch_device(bqsr_context* ctx, const PackCols& C, const int32_
       (e = dalloc(tmp, &d_map, (size_t)std::max(1, n_ref))) || (e = dalloc(tmp, &qh, 256)) ||
       (e = dalloc(tmp, &rgh, (size_t)n_rgh)))
     return e;
-  Lens h0{0, 1, 1, ~0ull};
+  Lens h0{0, 1, 1, ~0ull, 0};
   HIP_TRY(hipMemcpyAsync(dl, &h0, sizeof h0, hipMemcpyHostToDevice, st));
   if (n_ref) HIP_TRY(hipMemcpyAsync(d_map, ref_contig, (size_t)n_ref * 4, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemsetAsync(qh, 0, 256 * 8, st));
@@ -225,8 +256,12 @@ bqsr_status pack_batch_device(bqsr_context* ctx, const PackCols& C, const int32_
                        (const int32_t*)s->rg_id, (const int32_t*)s->ref, (const int64_t*)s->start,
                        (const uint64_t*)s->seq_off, (const uint8_t*)s->seq, (const uint64_t*)s->qual_off,
                        (const uint8_t*)s->qual, (const uint64_t*)s->cig_off, (const uint64_t*)s->md_off,
-                       (const int32_t*)d_map, n_ref, (const uint64_t*)slot, n, meta, align, qual, bases, qh, rgh,
-                       n_rgh);
+                       (const int32_t*)d_map, n_ref, (const uint64_t*)slot, n, meta, align, qual, bases, rgh, n_rgh);
+    HIP_TRY(hipGetLastError());
+    const int64_t n16 = (int64_t)n_slots / 16;  // (16-aligned slots: the column's whole slot range)
+    const unsigned gh = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n16 + kHistThreads - 1) / kHistThreads,
+                                                                          (int64_t)ctx->n_cu * 2));
+    hipLaunchKernelGGL(sam_batch_qhist, dim3(gh), dim3(kHistThreads), 0, st, (const uint4*)qual, n16, qh);
     HIP_TRY(hipGetLastError());
   }
   std::vector<unsigned long long> hq(256), hrg((size_t)n_rgh);
@@ -241,12 +276,13 @@ bqsr_status pack_batch_device(bqsr_context* ctx, const PackCols& C, const int32_
   for (int32_t i = 0; i < n_rgh; ++i)
     if (hrg[(size_t)i] > hrg[(size_t)rg_lo]) rg_lo = i;
   b->rg_lo = rg_lo;
-  int64_t qhist[256];
-  for (int q = 0; q < 256; ++q) qhist[q] = (int64_t)hq[(size_t)q];
+  int64_t qhist[kQBins];
+  for (int q = 0; q < kQBins; ++q) qhist[q] = (int64_t)hq[(size_t)q];
+  qhist[0] -= (int64_t)n_slots - (int64_t)hl.n_qual;  // the slots' zero padding
   b->q_lo = best_q_lo(qhist, 40);
   b->have_qhist = true;
   for (int q = 0; q < kQBins; ++q) b->qhist[q] = qhist[q];
-  for (int q = kQBins; q < 256; ++q) b->qhigh += qhist[q];
+  b->qhigh = (int64_t)hq[kQBins];
   b->rd.meta = meta;
   b->rd.align = align;
   b->rd.qual = qual;
