@@ -81,6 +81,12 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_pack(
     const uint8_t* seq, const uint64_t* qual_off, const uint8_t* qual_in, const uint64_t* cig_off, const uint64_t* md_off,
     const int32_t* ref_contig, int32_t n_ref, const uint64_t* slot, int64_t n, ReadMeta* meta, ReadAlign* align,
     uint8_t* qual, uint8_t* bases, unsigned long long* rghist, int32_t n_rg_hist) {
+  // read-group counts in LDS (one global atomic per group and workgroup at the
+  // end: a global atomic per read on one address serialised at the memory side)
+  constexpr int kRgLds = 1024;
+  __shared__ uint32_t rgh[kRgLds];
+  for (int i = threadIdx.x; i < kRgLds; i += blockDim.x) rgh[i] = 0;
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -120,9 +126,15 @@ extern "C" __global__ void __launch_bounds__(kThreads) sam_batch_pack(
       a.n_cigar = (uint16_t)((f & BQSR_F_HAS_CIGAR) ? field_len(cig_off, r) : 0);
       a.md_len = (uint16_t)((f & BQSR_F_HAS_MD) ? field_len(md_off, r) : 0);
       align[r] = a;
-      if (has_rg && rg[r] >= 0 && rg[r] < n_rg_hist) atomicAdd(&rghist[rg[r]], 1ull);
+      if (has_rg && rg[r] >= 0 && rg[r] < n_rg_hist) {
+        if (rg[r] < kRgLds) atomicAdd(&rgh[rg[r]], 1u);
+        else atomicAdd(&rghist[rg[r]], 1ull);
+      }
     }
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kRgLds && i < n_rg_hist; i += blockDim.x)
+    if (rgh[i]) atomicAdd(&rghist[i], (unsigned long long)rgh[i]);
 }
 
 // The packed qual column's histogram (the batch's launch window): 16-B loads,
