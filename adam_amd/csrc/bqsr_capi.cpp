@@ -25,6 +25,7 @@ using namespace bqsr;
 #include "bqsr_kernels.hip"
 #include "bqsr_observe_lean.hip"
 #include "bqsr_fold.hip"
+#include "bqsr_transport.hip"
 
 // ------------------------------------------------------------- errors -----
 
