@@ -39,3 +39,31 @@ def test_piece_orders(fronts):
     r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=env, capture_output=True, text=True,
                        timeout=280)
     assert r.returncode == 0 and "forms ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_default_fronts_full_parity():
+    # the default front split on a bucketed batch large enough for it
+    # (bqsr_capi.cpp fronts(): 8 read groups -> 16 base keys; 2.4M reads give
+    # min(ceil(8 * 256 / 16), 2.4M / (8192 * 16)) = 18 fronts, 288 pieces >= 256
+    # CUs), no environment override: one job against the oracle over the
+    # whole batch -- table words, expectedMismatch bits, every char
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from adam_amd import bqsr, synth
+    from adam_amd.job import ResidentJob
+    b = synth.generate(2_400_000, (150, 250), 8, seed=71)
+    dims = bqsr.dims_of([b])
+    job = ResidentJob(b, dims, None, 0)
+    try:
+        job.step()
+        words, em, q, st, ln, exc = job.results()
+    finally:
+        job.close()
+    ow, oem, out, out_len = O.bqsr(b, None, O.Dims(dims.n_rg, dims.max_len), n_parts=1, nthreads=16, fold1=True)
+    assert np.array_equal(words, ow)
+    assert np.float64(em).tobytes() == np.float64(oem).tobytes()
+    bad, first = O.compare_device_output(b, out, out_len, q, st, ln, exc)
+    assert bad == 0, first

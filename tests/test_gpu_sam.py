@@ -625,3 +625,17 @@ def test_device_batch_matches_host_batch(tmp_path, name):
             j2.close()
     finally:
         sam.close()
+
+
+def test_transform_mark_duplicates_large_against_restatement(tmp_path):
+    # 60k reads (pairs half the input apart, fragments, two libraries) through
+    # the device MarkDuplicates against oracle/markdup.py directly
+    text = _dup_text(60000, far=True)
+    src, out = tmp_path / "in.sam", tmp_path / "out.sam"
+    src.write_bytes(text)
+    st = transform(str(src), str(out), mark_duplicates=True)
+    want = _dup_want(src)
+    assert st["duplicates"] == sum(want) > 1000
+    after = _records(out.read_bytes())
+    got = [bool(int(c[1]) & 0x400) for c in after]
+    assert got == list(want)
