@@ -154,7 +154,7 @@ def lib():
             "bqsr_job_result": (ctypes.c_int, [vp, vp, ctypes.POINTER(dbl), ctypes.POINTER(i64), vp]),
             "bqsr_copy_async": (ctypes.c_int, [vp, vp, vp, i64, vp]),
             "bqsr_copy_dyn_async": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i64, vp]),
-            "bqsr_compact_outputs_async": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]),
+            "bqsr_compact_outputs_async": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, vp, vp, vp, vp]),
             "bqsr_batch_exception_count_ptr": (vp, [vp]),
             "bqsr_job_errors_export_async": (ctypes.c_int, [vp, i64, vp, vp]),
             "bqsr_job_errors_import_async": (ctypes.c_int, [vp, vp, vp]),

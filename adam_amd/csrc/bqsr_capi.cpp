@@ -200,6 +200,17 @@ int observe_rows(int wcells, bool table, int hq_span = 0) {
 }
 // the host-packed layout is 16-aligned (ReadsDev::slots_aligned); device batches may be either
 constexpr bool align_slots() { return true; }
+// the fold's block histograms of front-ordered bucketed batches counted by the
+// observe kernel in LDS (ADAM_BQSR_FOLD_HIST=observe) instead of bqsr_fold_hist:
+// measured slower on cfg4 (the histograms take LDS rows from the window and add
+// a same-address-heavy atomic per base), kept as the A/B
+bool fold_hist_in_observe() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_FOLD_HIST");
+    return e && strcmp(e, "observe") == 0;
+  }();
+  return v;
+}
 // known sites as sorted lists only (no position bitmaps): ADAM_BQSR_SITES_BITMAP=0 (A/B)
 bool sites_bitmap_off() {
   static const bool v = [] {
@@ -1294,7 +1305,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       // front-ordered pieces: the fold's block histograms from this kernel
       // (a piece's reads lie in one front, whose fold blocks it counts in LDS)
       P.n_fold = b->n_blocks;
-      P.hq_span = b->fronts > 0 ? fold_span(b) : 0;
+      P.hq_span = b->fronts > 0 && fold_hist_in_observe() ? fold_span(b) : 0;
       P.w = window_rows(b, observe_rows(P.wcells, true, P.hq_span));
     }
     P.touched = t->touched();
@@ -1919,7 +1930,8 @@ extern "C" {
 
 bqsr_status bqsr_compact_outputs_async(bqsr_context* ctx, bqsr_batch* b, const uint8_t* out_qual,
                                        const uint32_t* out_start, const uint32_t* out_len, uint64_t* exceptions,
-                                       int64_t max_exceptions, uint8_t* chars, uint32_t* offsets, void* stream) {
+                                       int64_t max_exceptions, uint8_t* chars, uint32_t* offsets, uint16_t* lengths,
+                                       void* stream) {
   if (!ctx || !b || !out_qual || !out_start || !out_len || !chars || !offsets || max_exceptions < 0 ||
       (max_exceptions > 0 && !exceptions))
     return fail(BQSR_ERR_INVALID_ARG, "bqsr_compact_outputs_async: bad arguments");
@@ -1946,7 +1958,7 @@ bqsr_status bqsr_compact_outputs_async(bqsr_context* ctx, bqsr_batch* b, const u
   if (st != BQSR_OK) return st;
   if (n > 0) {
     hipLaunchKernelGGL(bqsr_compact_chars, dim3(g), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, out_qual, out_start,
-                       (const uint64_t*)off64, n, chars, offsets);
+                       (const uint64_t*)off64, n, chars, offsets, lengths);
     if (max_exceptions > 0)
       hipLaunchKernelGGL(bqsr_compact_exceptions, dim3(4), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, out_start,
                          (const uint64_t*)off64, (unsigned long long*)exceptions,

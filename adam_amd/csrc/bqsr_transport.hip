@@ -97,7 +97,8 @@ extern "C" __global__ void bqsr_compact_lens(const uint32_t* out_len, int64_t n,
 // a wavefront per 64 reads: offsets by lane, then the reads' bytes 64 lanes wide
 extern "C" __global__ void __launch_bounds__(256) bqsr_compact_chars(const ReadMeta* meta, const uint8_t* out_qual,
                                                                      const uint32_t* out_start, const uint64_t* off64,
-                                                                     int64_t n, uint8_t* chars, uint32_t* off32) {
+                                                                     int64_t n, uint8_t* chars, uint32_t* off32,
+                                                                     uint16_t* len16) {
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); r0 < n;
        r0 += (int64_t)gridDim.x * blockDim.x) {
@@ -108,6 +109,7 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_compact_chars(const ReadM
       len = off64[r + 1] - dst;
       src = meta[r].slot + out_start[r];
       off32[r] = (uint32_t)dst;
+      if (len16) len16[r] = (uint16_t)len;  // (a read's chars <= kMaxReadLen)
       if (r == n - 1) off32[n] = (uint32_t)off64[n];
     }
     for (int j = 0; j < 64; ++j) {

@@ -119,12 +119,16 @@ class StreamedShard:
         self.out_start = [torch.empty(max(1, mr), dtype=torch.int32, device=dev) for _ in range(2)]
         self.out_len = [torch.empty(max(1, mr), dtype=torch.int32, device=dev) for _ in range(2)]
         if self.compact:
-            # device: the compacted chars and offsets (double-buffered); host, pinned:
-            # per partition the chars and offsets of read r = chars[off[r] : off[r + 1]]
+            # device: the compacted chars, offsets and u16 lengths (double-buffered);
+            # host, pinned: per partition the chars and the lengths (the link
+            # carries 2 B a read; read r = chars[off[r] : off[r + 1]], off their
+            # prefix sum, built on the host when a result is read)
             self.cchars = [torch.empty(ms, dtype=torch.uint8, device=dev) for _ in range(2)]
             self.coff = [torch.empty(mr + 1, dtype=torch.int32, device=dev) for _ in range(2)]
+            self.clen = [torch.empty(max(1, mr), dtype=torch.int16, device=dev) for _ in range(2)]
             self.host_chars = [torch.empty(n + 64, dtype=torch.uint8, pin_memory=True) for n in self.n_slots]
-            self.host_off = [torch.empty(n + 1, dtype=torch.int32, pin_memory=True) for n in self.n_reads]
+            self.host_len16 = [torch.empty(max(1, n), dtype=torch.int16, pin_memory=True) for n in self.n_reads]
+            self._offs = {}
             self.host_qual = self.host_start = self.host_len = None
         else:
             # host results, pinned: qualities by packed slot, per-read start / length
@@ -169,6 +173,8 @@ class StreamedShard:
         once no job is pending (``exceptions`` / ``qual_chars`` refuse to read
         them before), since a pending job's apply and copies overwrite them."""
         torch, L = self.torch, self.L
+        if self.compact:
+            self._offs = {}  # the offsets of the last job's lengths
         if len(self.pending) >= 2:
             raise RuntimeError("two jobs pending: finish() one first")
         comp = torch.cuda.current_stream(self.dev)
@@ -223,7 +229,8 @@ class StreamedShard:
                 check(L.bqsr_compact_outputs_async(ctx, bh, ctypes.c_void_p(oq.data_ptr()),
                                                    ctypes.c_void_p(os_.data_ptr()), ctypes.c_void_p(ol.data_ptr()),
                                                    exc_i, self.max_exc, ctypes.c_void_p(self.cchars[k].data_ptr()),
-                                                   ctypes.c_void_p(self.coff[k].data_ptr()), sp))
+                                                   ctypes.c_void_p(self.coff[k].data_ptr()),
+                                                   ctypes.c_void_p(self.clen[k].data_ptr()), sp))
             self.ev_ap[i].record(comp)
             dn.wait_event(self.ev_ap[i])
             ns, nr = self.n_slots[i], max(1, self.n_reads[i])
@@ -235,7 +242,8 @@ class StreamedShard:
                 cp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
                 check(L.bqsr_copy_dyn_async(ctx, cp(self.host_chars[i]), cp(self.cchars[k]),
                                             ctypes.c_void_p(self.coff[k].data_ptr() + 4 * n_i), 4, 1, ns, dnp))
-                check(L.bqsr_copy_async(ctx, cp(self.host_off[i]), cp(self.coff[k]), 4 * (n_i + 1), dnp))
+                if n_i:
+                    check(L.bqsr_copy_async(ctx, cp(self.host_len16[i]), cp(self.clen[k]), 2 * n_i, dnp))
                 check(L.bqsr_copy_dyn_async(ctx, ctypes.c_void_p(self.host_exc.data_ptr() + 8 * e0),
                                             ctypes.c_void_p(self.exc.data_ptr() + 8 * e0),
                                             ctypes.c_void_p(L.bqsr_batch_exception_count_ptr(bh)), 8, 8,
@@ -340,7 +348,8 @@ class StreamedShard:
         import numpy as np
         self._results_ready()
         if self.compact:
-            a, b = int(self.host_off[i][r]) & 0xFFFFFFFF, int(self.host_off[i][r + 1]) & 0xFFFFFFFF
+            off = self._offsets(i)
+            a, b = int(off[r]), int(off[r + 1])
         else:
             st, ln = int(self.host_start[i][r]), int(self.host_len[i][r])
             a, b = slot + st, slot + st + ln
@@ -358,7 +367,7 @@ class StreamedShard:
         exc = self.host_exc[i * self.max_exc: i * self.max_exc + self.n_exc[i]].numpy()
         nr = self.n_reads[i]
         if self.compact:
-            off = self.host_off[i].numpy()[:nr + 1].view("uint32")
+            off = self._offsets(i)
             return "compact", self.host_chars[i].numpy()[:int(off[nr]) if nr else 0], off, exc
         return ("slots", self.host_qual[i].numpy()[:self.n_slots[i]], self.host_start[i].numpy()[:nr],
                 self.host_len[i].numpy()[:nr], exc)
@@ -367,8 +376,20 @@ class StreamedShard:
         """Bytes the last finished job copied back to the host."""
         if not self.compact:
             return sum(self.n_slots) + 8 * sum(self.n_reads) + 8 * self.max_exc * len(self.batches)
-        return sum((int(self.host_off[i][self.n_reads[i]]) & 0xFFFFFFFF) + 4 * (self.n_reads[i] + 1) + 8 * self.n_exc[i]
+        return sum(int(self._offsets(i)[self.n_reads[i]]) + 2 * self.n_reads[i] + 8 * self.n_exc[i]
                    for i in range(len(self.batches)))
+
+    def _offsets(self, i: int):
+        """u32 offsets [n + 1] of partition i's compacted chars: the prefix
+        sum of the shipped u16 lengths (cached until the next job)"""
+        import numpy as np
+        if i not in self._offs:
+            n = self.n_reads[i]
+            off = np.zeros(n + 1, np.uint32)
+            if n:
+                np.cumsum(self.host_len16[i].numpy()[:n].view(np.uint16), out=off[1:], dtype=np.uint32)
+            self._offs[i] = off
+        return self._offs[i]
 
     def apply_ms(self) -> Optional[float]:
         """Mean apply-kernel time per partition of the last recorded job."""

@@ -351,13 +351,17 @@ bqsr_status bqsr_copy_dyn_async(bqsr_context* ctx, void* dst, const void* src, c
 /* A partition's apply outputs compacted for the trip to the host (the JNI
  * side's result buffers hold just the new quality strings, Q13):
  * chars[offsets[r] .. offsets[r + 1]) = the out_len[r] chars of read r
- * (device buffers: chars >= the batch's slots, offsets u32 [n + 1]); the
- * exception list's entries are rewritten to (position in chars) << 16 | char.
- * Enqueued on `stream` after the apply stage; bqsr_batch_exception_count_ptr
- * is the device word holding the exception count (for bqsr_copy_dyn_async). */
+ * (device buffers: chars >= the batch's slots, offsets u32 [n + 1]); with
+ * `lengths` (u16 [n], may be NULL) also each read's char count -- what a
+ * caller ships instead of the offsets (half the bytes; the offsets are its
+ * prefix sum).  The exception list's entries are rewritten to (position in
+ * chars) << 16 | char.  Enqueued on `stream` after the apply stage;
+ * bqsr_batch_exception_count_ptr is the device word holding the exception
+ * count (for bqsr_copy_dyn_async). */
 bqsr_status bqsr_compact_outputs_async(bqsr_context* ctx, bqsr_batch* b, const uint8_t* out_qual,
                                        const uint32_t* out_start, const uint32_t* out_len, uint64_t* exceptions,
-                                       int64_t max_exceptions, uint8_t* chars, uint32_t* offsets, void* stream);
+                                       int64_t max_exceptions, uint8_t* chars, uint32_t* offsets, uint16_t* lengths,
+                                       void* stream);
 const void* bqsr_batch_exception_count_ptr(const bqsr_batch* b);
 
 /* One job's launches with the fewest host round trips (what bench.py's step

@@ -32,10 +32,12 @@ print("forms ok")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fronts", ["5", "0"])
-def test_piece_orders(fronts):
-    # front-ordered pieces of the bucketed jobs forced on / off (bqsr_capi.cpp fronts())
-    env = dict(os.environ, ADAM_BQSR_FRONTS=fronts)
+@pytest.mark.parametrize("fronts,fold_hist", [("5", "pass"), ("5", "observe"), ("0", "pass")])
+def test_piece_orders(fronts, fold_hist):
+    # front-ordered pieces of the bucketed jobs forced on / off (bqsr_capi.cpp
+    # fronts()); with fronts, the fold's block histograms by bqsr_fold_hist or
+    # counted in the observe kernel (ADAM_BQSR_FOLD_HIST)
+    env = dict(os.environ, ADAM_BQSR_FRONTS=fronts, ADAM_BQSR_FOLD_HIST=fold_hist)
     r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=env, capture_output=True, text=True,
                        timeout=280)
     assert r.returncode == 0 and "forms ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -172,17 +172,19 @@ def test_crafted_table_compacted_outputs():
         exc = torch.empty(1 << 16, dtype=torch.int64, device=dev)
         chars = torch.empty(ns + 64, dtype=torch.uint8, device=dev)
         off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        lens = torch.empty(n, dtype=torch.int16, device=dev)
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         _capi.check(L.bqsr_apply_stage(ctx.handle, bh, gfin.handle, p(oq), p(ost), p(oln), p(exc), 1 << 16,
                                        _capi.STAGE_RESET | _capi.STAGE_KERNEL, sp))
         _capi.check(L.bqsr_compact_outputs_async(ctx.handle, bh, p(oq), p(ost), p(oln), p(exc), 1 << 16, p(chars),
-                                                 p(off), sp))
+                                                 p(off), p(lens), sp))
         nexc = ctypes.c_int64()
         _capi.check(L.bqsr_apply_result(bh, ctypes.byref(nexc), sp))
         torch.cuda.synchronize()
         assert nexc.value > 100
         offs = off.cpu().numpy()
         assert np.array_equal(np.diff(offs.astype(np.int64)), ref_len[:n].astype(np.int64))
+        assert np.array_equal(lens.cpu().numpy().view(np.uint16).astype(np.int64), ref_len[:n].astype(np.int64))
         bad, first = O.compare_compact_output(batch, ref, ref_len, chars.cpu().numpy()[:int(offs[n])], offs,
                                               exc.cpu().numpy()[:nexc.value])
         assert bad == 0, first
