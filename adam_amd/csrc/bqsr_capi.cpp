@@ -17,6 +17,8 @@
 #include <thread>
 #include <vector>
 
+#include <rocprim/rocprim.hpp>
+
 #include "bqsr_internal.h"
 
 using namespace bqsr;
@@ -333,8 +335,23 @@ struct bqsr_batch {
   int64_t* d_key_off = nullptr;
   uint32_t* d_key_cnt = nullptr;
   uint32_t* d_cursor = nullptr;
+  // key-major copy of the quals / base codes (key_major_build): the bucketed
+  // passes' reads of a piece contiguous; the perm it follows is computed once
+  uint8_t *k_qual = nullptr, *k_bases = nullptr;
+  uint64_t* d_kslot = nullptr;
+  bool perm_static = false;  // d_perm / d_key_off built once (key_major_build): prep skips the key sort
   OrderDev order() const {
-    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0} : OrderDev{nullptr, nullptr, 1};
+    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0, k_qual ? d_kslot : nullptr}
+                    : OrderDev{nullptr, nullptr, 1};
+  }
+  // the reads as the per-base passes see them (qual / base columns: the key-major copy when there is one)
+  ReadsDev pass_rd() const {
+    ReadsDev r = rd;
+    if (bucketed && k_qual) {
+      r.qual = k_qual;
+      r.bases = k_bases;
+    }
+    return r;
   }
   // workgroups of the chunk-walk passes: a piece each with fronts, else the fold's blocks
   int32_t pass_blocks() const { return bucketed && fronts > 0 ? n_keys : n_blocks; }
@@ -342,6 +359,8 @@ struct bqsr_batch {
   ~bqsr_batch() {
     if (d_part) (void)hipFree(d_part);
     if (d_off64) (void)hipFree(d_off64);
+    for (void* p : {(void*)k_qual, (void*)k_bases, (void*)d_kslot})
+      if (p) (void)hipFree(p);
     if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
     for (void* p : allocs) (void)hipFree(p);
@@ -607,6 +626,76 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   return BQSR_OK;
 }
 
+// key-major copy of a bucketed batch's quals and base codes (OrderDev::kslot):
+// the reads sorted by their piece key once (the same counting sort prep runs
+// per job, now kept: perm_static), their slot spans scanned in that order, and
+// each read's 16-aligned slot range copied to its key-major slots.  A piece's
+// reads are then contiguous in the copy: the bucketed chunk walks read it
+// sequentially where the read-order layout scattered them over every key's
+// reads (cfg4: 96 read groups).  The batch's data must be on the device
+// (created from records or a parse; a staged batch uploads later and keeps
+// the per-job sort).  1.5 B a slot more HBM.  ADAM_BQSR_KEYMAJOR=0: off (A/B).
+bool key_major_off() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_KEYMAJOR");
+    return e && strcmp(e, "0") == 0;
+  }();
+  return v;
+}
+bqsr_status key_major_build(bqsr_batch* b, hipStream_t s) {
+  if (!b->bucketed || key_major_off() || !b->rd.slots_aligned || b->rd.n_reads == 0) return BQSR_OK;
+  const int64_t n = b->rd.n_reads;
+  bqsr_context* ctx = b->ctx;
+  // the piece order, once
+  HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
+  const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
+  hipLaunchKernelGGL(bqsr_key_count, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys, b->n_base,
+                     std::max(1, b->fronts), b->d_key_cnt);
+  hipLaunchKernelGGL(bqsr_key_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)b->d_key_cnt, b->n_keys, b->d_key_off,
+                     b->d_cursor);
+  const unsigned sb = (unsigned)std::min<int64_t>((n + 4095) / 4096, (int64_t)ctx->n_cu * 8);
+  hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys, b->n_base,
+                     std::max(1, b->fronts), b->d_cursor, b->d_perm);
+  HIP_TRY(hipGetLastError());
+  // key-major slots: spans in perm order, scanned
+  uint64_t* span = nullptr;
+  void* temp = nullptr;
+  size_t tb = 0;
+  HIP_TRY(hipMalloc((void**)&b->d_kslot, (size_t)(n + 1) * 8));
+  HIP_TRY(hipMalloc((void**)&span, (size_t)(n + 1) * 8));
+  hipError_t e = hipMemsetAsync(span + n, 0, 8, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(bqsr_km_spans, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, (const uint32_t*)b->d_perm,
+                       n, span);
+    e = rocprim::exclusive_scan(nullptr, tb, span, b->d_kslot, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s);
+  }
+  if (e == hipSuccess) e = hipMalloc(&temp, std::max<size_t>(tb, 1));
+  if (e == hipSuccess)
+    e = rocprim::exclusive_scan(temp, tb, span, b->d_kslot, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s);
+  if (e == hipSuccess) e = hipMalloc((void**)&b->k_qual, (size_t)b->rd.n_slots + kColumnPad);
+  if (e == hipSuccess) e = hipMalloc((void**)&b->k_bases, (size_t)b->rd.n_slots / 2 + 1 + kColumnPad);
+  if (e == hipSuccess) e = hipMemsetAsync(b->k_qual + b->rd.n_slots, 0, kColumnPad, s);
+  if (e == hipSuccess) e = hipMemsetAsync(b->k_bases + b->rd.n_slots / 2, 0, 1 + kColumnPad, s);
+  if (e == hipSuccess) {
+    const unsigned gw = (unsigned)std::min<int64_t>((n + 3) / 4, (int64_t)ctx->n_cu * 8);
+    hipLaunchKernelGGL(bqsr_km_gather, dim3(gw), dim3(256), 0, s, b->rd, (const uint32_t*)b->d_perm,
+                       (const uint64_t*)b->d_kslot, b->k_qual, b->k_bases);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (span) (void)hipFree(span);
+  if (temp) (void)hipFree(temp);
+  if (e != hipSuccess) {  // without the copy the passes read the batch's own layout
+    for (void* p : {(void*)b->k_qual, (void*)b->k_bases, (void*)b->d_kslot})
+      if (p) (void)hipFree(p);
+    b->k_qual = b->k_bases = nullptr;
+    b->d_kslot = nullptr;
+    return fail(BQSR_ERR_DEVICE, std::string("key-major copy: ") + hipGetErrorString(e));
+  }
+  b->perm_static = true;
+  return BQSR_OK;
+}
+
 // host pack of one record partition (bqsr_records -> device layout)
 struct Packed {
   std::vector<ReadMeta> meta;
@@ -772,7 +861,7 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
   b->rd.md = md;
   b->rd.cigar = cigar;
   b->rd.slots_aligned = align_slots();
-  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK) {
+  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK || (st = key_major_build(b, s)) != BQSR_OK) {
     delete b;
     return st;
   }
@@ -1226,7 +1315,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
       hipLaunchKernelGGL(bqsr_prep_kernel<false>, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, P);
     }
     HIP_TRY(hipGetLastError());
-    if (b->bucketed) {  // counting sort of the reads by read group
+    if (b->bucketed && !b->perm_static) {  // counting sort of the reads by read group
       const int64_t n = b->rd.n_reads;
       HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
       const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
@@ -1265,7 +1354,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     return fail(BQSR_ERR_INVALID_ARG, "observe kernel before the prep stage (or with other known sites)");
   if (stages & BQSR_STAGE_KERNEL) {
     ObserveParams P{};
-    P.rd = b->rd;
+    P.rd = b->pass_rd();
     P.ord = b->order();
     P.info = b->d_info;
     P.sbits = b->d_sbits;
@@ -1656,7 +1745,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   if (b->rd.n_reads == 0 || !(stages & (BQSR_STAGE_KERNEL | BQSR_STAGE_LUT))) return ok();
   ApplyParams P{};
-  P.rd = b->rd;
+  P.rd = b->pass_rd();
   P.ord = b->order();
   P.info = b->d_info;
   P.g = geom(L->dims);

@@ -188,6 +188,12 @@ struct OrderDev {
   // front sweep the same read range together and share its cache lines
   // (bqsr_capi.cpp fronts()).  0: keys are base keys, ranges by wg_begin.
   int32_t n_base = 0;
+  // key-major copy (bqsr_capi.cpp key_major_build): when set, the bucketed
+  // passes read quals / base codes from a copy laid out in perm order -- the
+  // read at sorted position p at kslot[p] -- so a piece's reads are
+  // contiguous; the ReadsDev they get points at that copy, and the slot
+  // bitmap and outputs stay at the read's own slot (LaneRead::oslot)
+  const uint64_t* kslot = nullptr;
 };
 
 struct ObserveParams {

@@ -1034,7 +1034,10 @@ struct LaneRead {
   int aux;        // a pass's own per-read value (set by its fread, carried to the read's chunks)
 };
 
-__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L) {
+// ks: the read's slot in rd's qual / base columns when they are the
+// key-major copy (OrderDev::kslot), ~0 for its own slot
+__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L,
+                                              uint64_t ks = ~0ull) {
   LaneRead x;
   x.r = live ? r : rd.n_reads;
   x.ro = x.r;
@@ -1046,9 +1049,10 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
     inf = info[r];
   }
   x.trimmed = inf.fl & kInfoTrim;
-  inf = resolve_info(rd, inf, m.slot, m.lq);
+  const uint64_t qs = ks == ~0ull ? m.slot : ks;
+  inf = resolve_info(rd, inf, qs, m.lq);
   x.inf = inf;
-  x.slot = m.slot;
+  x.slot = qs;
   x.oslot = m.slot;
   x.fl = inf.fl;
   x.rg = m.rg;
@@ -1335,7 +1339,8 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
                                            FLoad&& fload, FChunk&& fchunk) {
   for (int64_t wb = q0; wb < q1; wb += qstep) {
     const bool live = wb + lane < q1;
-    LaneRead x = lane_read(rd, info, live ? order_read(ord, wb + lane) : 0, live, L);
+    LaneRead x = lane_read(rd, info, live ? order_read(ord, wb + lane) : 0, live, L,
+                           live && ord.kslot ? ord.kslot[wb + lane] : ~0ull);
     fread(x, live);
     const int n = (live && (x.fl & kAct)) ? x.en - x.st : 0;
     const int jb = rd.slots_aligned ? -(x.st & 15) : 0;
@@ -1343,6 +1348,7 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
     const uint32_t pe = wave_incl_add(nch), ps = pe - nch;
     const uint32_t total = __builtin_amdgcn_readlane(pe, 63);
     const uint32_t p_r = (uint32_t)x.r, p_slo = (uint32_t)x.slot, p_shi = (uint32_t)(x.slot >> 32);
+    const uint32_t p_olo = (uint32_t)x.oslot, p_ohi = (uint32_t)(x.oslot >> 32);
     const uint32_t p_se = (uint32_t)x.st | ((uint32_t)x.en << 16);
     const uint32_t p_fl = (uint32_t)x.fl | (x.dir < 0 ? kPkRev : 0u) | ((uint32_t)x.cell0 << 16);
     const uint32_t p_rg = (uint32_t)x.rg, p_aux = (uint32_t)x.aux;
@@ -1367,7 +1373,7 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
         c[u].r = bperm(ri, p_r);
         c[u].slot = ((uint64_t)bperm(ri, p_shi) << 32) | bperm(ri, p_slo);
         c[u].ro = c[u].r;
-        c[u].oslot = c[u].slot;
+        c[u].oslot = ord.kslot ? ((uint64_t)bperm(ri, p_ohi) << 32) | bperm(ri, p_olo) : c[u].slot;
         const uint32_t se = bperm(ri, p_se), fl = bperm(ri, p_fl);
         c[u].st = (int)(se & 0xFFFFu);
         c[u].en = (int)(se >> 16);
@@ -1704,6 +1710,32 @@ __device__ __forceinline__ int sort_key(const ReadMeta& m, int64_t r, int64_t n,
   const int cls = ((m.flags & BQSR_F_PAIRED) && (m.flags & BQSR_F_SECOND_OF_PAIR)) ? 1 : 0;
   const int f = fronts > 1 ? (int)((r * fronts) / n) : 0;
   return f * n_base + 2 * min((int)m.rg, n_base / 2 - 1) + cls;
+}
+
+// ---- key-major copy (OrderDev::kslot; bqsr_capi.cpp key_major_build) ----
+// slot span of the read at each sorted position
+extern "C" __global__ void bqsr_km_spans(const ReadMeta* meta, const uint32_t* perm, int64_t n, uint64_t* span) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const ReadMeta m = meta[perm[p]];
+    span[p] = slot_span(m.lq, m.ls);
+  }
+}
+// a wavefront per read: its qual bytes and base codes to its key-major slots
+// (16-aligned slots: 16-B qual pieces, 8-B code pieces)
+extern "C" __global__ void __launch_bounds__(256) bqsr_km_gather(ReadsDev rd, const uint32_t* perm, const uint64_t* kslot,
+                                                                uint8_t* kqual, uint8_t* kbases) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6, nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t p = w0; p < rd.n_reads; p += nw) {
+    const ReadMeta m = rd.meta[perm[p]];
+    const uint64_t span = slot_span(m.lq, m.ls), d = kslot[p];
+    const uint4* qs = (const uint4*)(rd.qual + m.slot);
+    uint4* qd = (uint4*)(kqual + d);
+    for (uint64_t i = lane; i < span / 16; i += 64) qd[i] = qs[i];
+    const uint64_t* bs = (const uint64_t*)(rd.bases + m.slot / 2);
+    uint64_t* bd = (uint64_t*)(kbases + d / 2);
+    for (uint64_t i = lane; i < span / 16; i += 64) bd[i] = bs[i];
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_count(const ReadMeta* meta, int64_t n,

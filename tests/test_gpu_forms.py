@@ -32,12 +32,14 @@ print("forms ok")
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fronts,fold_hist", [("5", "pass"), ("5", "observe"), ("0", "pass")])
-def test_piece_orders(fronts, fold_hist):
+@pytest.mark.parametrize("fronts,fold_hist,key_major", [("5", "pass", "1"), ("5", "observe", "1"), ("0", "pass", "1"),
+                                                        ("5", "pass", "0"), ("0", "pass", "0")])
+def test_piece_orders(fronts, fold_hist, key_major):
     # front-ordered pieces of the bucketed jobs forced on / off (bqsr_capi.cpp
     # fronts()); with fronts, the fold's block histograms by bqsr_fold_hist or
-    # counted in the observe kernel (ADAM_BQSR_FOLD_HIST)
-    env = dict(os.environ, ADAM_BQSR_FRONTS=fronts, ADAM_BQSR_FOLD_HIST=fold_hist)
+    # counted in the observe kernel (ADAM_BQSR_FOLD_HIST); the bucketed passes
+    # on the key-major copy or the batch's own layout (ADAM_BQSR_KEYMAJOR)
+    env = dict(os.environ, ADAM_BQSR_FRONTS=fronts, ADAM_BQSR_FOLD_HIST=fold_hist, ADAM_BQSR_KEYMAJOR=key_major)
     r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=env, capture_output=True, text=True,
                        timeout=280)
     assert r.returncode == 0 and "forms ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
