@@ -94,6 +94,51 @@ def _bgzf(data: bytes, block: int = 65280) -> bytes:
     return b"".join(out)
 
 
+def _bam_header(head: List[bytes]) -> Tuple[bytes, Dict[bytes, int]]:
+    refs = []
+    for l in head:
+        if l.startswith(b"@SQ"):
+            f = dict(x.split(b":", 1) for x in l.split(b"\t")[1:] if b":" in x)
+            refs.append((f[b"SN"], int(f.get(b"LN", b"0"))))
+    ref_id: Dict[bytes, int] = {}
+    for i, (n, _) in enumerate(refs):
+        ref_id.setdefault(n, i)
+    htext = b"".join(l + b"\n" for l in head)
+    raw = b"BAM\1" + struct.pack("<i", len(htext)) + htext + struct.pack("<i", len(refs))
+    for n, ln in refs:
+        raw += struct.pack("<i", len(n) + 1) + n + b"\0" + struct.pack("<i", ln)
+    return raw, ref_id
+
+
+_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def _chunk_blocks(args) -> bytes:
+    lines, ref_id = args
+    return _bgzf(b"".join(_record(l.split(b"\t"), ref_id) for l in lines))[:-len(_EOF)]
+
+
+def sam_to_bam_parallel(text: bytes, workers: int = 16, progress=None) -> bytes:
+    """sam_to_bam with the records encoded and compressed by a process pool
+    (BGZF blocks are independent: the header's blocks, each slice's blocks,
+    one EOF block).  Fork before the GPU is touched."""
+    from multiprocessing import get_context
+    lines = [l[:-1] if l.endswith(b"\r") else l for l in text.split(b"\n")]
+    head = [l for l in lines if l.startswith(b"@")]
+    body = [l for l in lines if l and not l.startswith(b"@")]
+    raw, ref_id = _bam_header(head)
+    step = max(1, (len(body) + 4 * workers - 1) // (4 * workers))
+    jobs = [(body[i:i + step], ref_id) for i in range(0, len(body), step)]
+    out = [_bgzf(raw)[:-len(_EOF)]]
+    with get_context("fork").Pool(workers) as pool:
+        for i, b in enumerate(pool.imap(_chunk_blocks, jobs)):
+            out.append(b)
+            if progress:
+                progress(i + 1, len(jobs))
+    out.append(_EOF)
+    return b"".join(out)
+
+
 def sam_to_bam(text: bytes) -> bytes:
     """BAM bytes of a SAM text: header text kept, @SQ lines as the reference list."""
     lines = [l[:-1] if l.endswith(b"\r") else l for l in text.split(b"\n")]

@@ -65,8 +65,9 @@ def main():
     t0 = time.perf_counter()
     data = synthetic_sam(a.reads, a.len)
     if a.bam:
-        from adam_amd.bam_writer import sam_to_bam
-        data = sam_to_bam(data)
+        from adam_amd.bam_writer import sam_to_bam_parallel
+        data = sam_to_bam_parallel(data, min(16, os.cpu_count() or 1),
+                                   progress=lambda i, n: log("bam slice %d / %d" % (i, n)) if i % 8 == 0 else None)
     t_gen = time.perf_counter() - t0
     log("generated %d bytes in %.1f s" % (len(data), t_gen))
     import torch

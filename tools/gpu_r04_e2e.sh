@@ -19,6 +19,8 @@ if [ -n "$TESTS" ]; then
 fi
 timeout -k 10 400 python -u tools/bench_adam.py --reads $READS --compression snappy > "$O/e2e_sam_snappy.json" 2> "$O/e2e_sam_snappy.log"
 cat "$O/e2e_sam_snappy.json"
+timeout -k 10 400 python -u tools/bench_adam.py --reads $READS --compression snappy --bam > "$O/e2e_bam_snappy.json" 2> "$O/e2e_bam_snappy.log"
+cat "$O/e2e_bam_snappy.json"
 timeout -k 10 400 python -u tools/bench_adam.py --reads $READS --compression gzip > "$O/e2e_sam_gzip.json" 2> "$O/e2e_sam_gzip.log"
 cat "$O/e2e_sam_gzip.json"
 timeout -k 10 400 python -u tools/bench_parquet.py --reads 2000000 > "$O/parquet_read.json" 2> "$O/parquet_read.log"
