@@ -368,7 +368,7 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   bamk::BamParams P{};
   uint8_t* d_rec;
   if ((st = sam_alloc(tmp, &d_rec, (size_t)(m - body) + 64)) != BQSR_OK) return st;
-  if (m > body) HIP_TRY(hipMemcpyAsync(d_rec, u + body, (size_t)(m - body), hipMemcpyHostToDevice, s));
+  if (m > body && (st = upload_staged(ctx, d_rec, u + body, (size_t)(m - body), s)) != BQSR_OK) return st;
   P.buf = d_rec;
   P.n = nr;
   P.n_ref = (int32_t)n_ref;

@@ -266,7 +266,53 @@ struct bqsr_context {
   double* d_thr = nullptr;    // kThrN doubles
   double* d_qbt = nullptr;    // kQbN bucket thresholds
   int16_t* d_qbq = nullptr;   // kQbN bucket phred values
+  // upload_staged: a pinned ring for large pageable uploads (allocated on first use)
+  std::mutex stage_mu;
+  uint8_t* stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
 };
+
+namespace {
+// H2D of a large pageable host buffer (SAM text, inflated BAM records):
+// chunks copied by host threads into a pinned ring of two buffers while the
+// DMA engine moves the previous chunk -- the runtime's own pageable path
+// stages through one thread's memcpy (~20 GB/s).  Synchronous on return.
+constexpr size_t kStageChunk = 64ull << 20;
+bqsr_status upload_staged(bqsr_context* ctx, void* dst, const void* src, size_t n, hipStream_t s) {
+  hipPointerAttribute_t attr{};
+  const bool pinned = hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // (pageable memory: the query fails)
+  if (pinned || n < 2 * kStageChunk) {
+    HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return BQSR_OK;
+  }
+  std::lock_guard<std::mutex> lock(ctx->stage_mu);
+  for (int i = 0; i < 2; ++i) {
+    if (!ctx->stage[i]) HIP_TRY(hipHostMalloc((void**)&ctx->stage[i], kStageChunk, hipHostMallocDefault));
+    if (!ctx->stage_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming));
+  }
+  const int nth = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const uint8_t* p = (const uint8_t*)src;
+  uint8_t* d = (uint8_t*)dst;
+  int k = 0;
+  for (size_t off = 0; off < n; off += kStageChunk, k ^= 1) {
+    const size_t len = std::min(kStageChunk, n - off);
+    HIP_TRY(hipEventSynchronize(ctx->stage_ev[k]));  // the ring buffer's previous DMA is done
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+      th.emplace_back([&, t] {
+        const size_t a = len * (size_t)t / (size_t)nth, b = len * (size_t)(t + 1) / (size_t)nth;
+        memcpy(ctx->stage[k] + a, p + off + a, b - a);
+      });
+    for (auto& x : th) x.join();
+    HIP_TRY(hipMemcpyAsync(d + off, ctx->stage[k], len, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(ctx->stage_ev[k], s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return BQSR_OK;
+}
+}  // namespace
 
 struct bqsr_sites {
   bqsr_context* ctx = nullptr;
@@ -463,6 +509,10 @@ void bqsr_context_destroy(bqsr_context* c) {
   if (c->d_thr) (void)hipFree(c->d_thr);
   if (c->d_qbt) (void)hipFree(c->d_qbt);
   if (c->d_qbq) (void)hipFree(c->d_qbq);
+  for (int i = 0; i < 2; ++i) {
+    if (c->stage[i]) (void)hipHostFree(c->stage[i]);
+    if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
+  }
   delete c;
 }
 

@@ -1235,7 +1235,13 @@ bqsr_status bqsr_sam_parse(bqsr_context* ctx, const char* text, int64_t n, void*
   uint8_t* d_text = nullptr;
   HIP_TRY(hipMalloc(&d_text, (size_t)n + 64));
   hipError_t e = hipMemsetAsync(d_text + n, 0, 64, s);
-  if (e == hipSuccess && n > 0) e = hipMemcpyAsync(d_text, text, (size_t)n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && n > 0) {
+    const bqsr_status ust = upload_staged(ctx, d_text, text, (size_t)n, s);
+    if (ust != BQSR_OK) {
+      (void)hipFree(d_text);
+      return ust;
+    }
+  }
   if (e != hipSuccess) {
     (void)hipFree(d_text);
     return fail(BQSR_ERR_DEVICE, std::string("bqsr_sam_parse: ") + hipGetErrorString(e));
