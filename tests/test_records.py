@@ -124,6 +124,19 @@ def test_bam_writer_bgzf_structure():
     assert n == sum(1 for l in text.split(b"\n") if l and not l.startswith(b"@"))
 
 
+def test_bam_writer_parallel_same_stream():
+    # the pool form (tools/bench_adam.py --bam): the same decompressed BAM
+    # stream as the serial writer, block boundaries aside
+    import gzip
+    from adam_amd import synth
+    from adam_amd.bam_writer import sam_to_bam, sam_to_bam_parallel
+    from adam_amd.samgen import sam_text
+    text = sam_text(synth.generate(3000, (100,), 2, 5), n_rg=2)
+    par = sam_to_bam_parallel(text, 3)
+    assert gzip.decompress(par) == gzip.decompress(sam_to_bam(text))
+    assert par.endswith(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+
+
 def test_sam_partitions_cut_at_records():
     # transform's streamed partitions: the header once, the records cut after
     # a newline, every record in exactly one range, ranges in file order
