@@ -28,7 +28,6 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
-from . import _capi
 from ._capi import check
 
 # adam.avdl:4-68, in order: (name, arrow type name)

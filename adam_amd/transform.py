@@ -260,7 +260,6 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
 
 
 def _transform_table(A, table, batch, inp, out, mark_duplicates, recalibrate, dbsnp, device, stats, t0):
-    import pyarrow as pa
     import pyarrow.parquet as pq
 
     from . import parquet as P
