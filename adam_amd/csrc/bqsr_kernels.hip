@@ -959,6 +959,11 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
   __syncthreads();
   const uint32_t k = cnt;
   if (!kStore) {
+#ifdef ADAM_BQSR_PREP_PROBE  // timing probe build only (wrong results): the listed reads' share of prep,
+    // each listed read passed through instead (a valid ReadInfo for the later passes)
+    for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads) P.info[list[i]] = ReadInfo{0, 0, kInfoPass, 0};
+    return;
+#endif
     for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads)
       prep_one(P, (int64_t)list[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
     return;
