@@ -104,3 +104,24 @@ def check(parts, sites=None, dims=None, expect_error=None):
         assert o.error == expect_error, "oracle gave %s, expected %s" % (o.error, expect_error)
     assert_same(parts, g, o)
     return g, o
+
+
+def apply_written(batch: RecordBatch, out_qual: np.ndarray, start: np.ndarray, length: np.ndarray) -> np.ndarray:
+    """The apply output bytes a read owns -- [slot + start, + length) in the
+    16-aligned read-order slot layout of bqsr_batch_create -- with every other
+    byte zeroed (the rest of a read's last 16-B chunk is scratch: the apply
+    stores whole chunks, whose tail bytes depend on the neighbouring slots)."""
+    f = batch.flags.astype(np.int64)
+    from adam_amd.records import F_HAS_QUAL, F_HAS_SEQ
+    lq = np.where(f & F_HAS_QUAL, np.diff(batch.qual_offset.astype(np.int64)), 0)
+    ls = np.where(f & F_HAS_SEQ, np.diff(batch.seq_offset.astype(np.int64)), 0)
+    span = (np.maximum(lq, ls) + 15) // 16 * 16
+    slot = np.zeros(batch.n_reads, np.int64)
+    slot[1:] = np.cumsum(span)[:-1]
+    a = slot + start.astype(np.int64)
+    b = a + length.astype(np.int64)
+    d = np.zeros(out_qual.size + 1, np.int64)
+    np.add.at(d, a, 1)
+    np.add.at(d, b, -1)
+    keep = np.cumsum(d[:-1]) > 0
+    return np.where(keep, out_qual, 0).astype(out_qual.dtype)

@@ -616,10 +616,14 @@ def test_device_batch_matches_host_batch(tmp_path, name):
             e2, r2 = _job_outcome(j2)
             assert e1 == e2
             if r1 is not None:
+                from _parity import apply_written
                 assert np.array_equal(r1[0], r2[0])
                 assert np.float64(r1[1]).tobytes() == np.float64(r2[1]).tobytes()
-                for x, y in zip(r1[2:], r2[2:]):
+                for x, y in zip(r1[3:], r2[3:]):
                     assert np.array_equal(x, y)
+                # (a bucketed batch's piece order comes from an atomic counting sort: the scratch
+                # bytes of a read's last chunk may differ between two batches, its chars may not)
+                assert np.array_equal(apply_written(rb, r1[2], r1[3], r1[4]), apply_written(rb, r2[2], r2[3], r2[4]))
         finally:
             j1.close()
             j2.close()
