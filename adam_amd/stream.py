@@ -391,6 +391,39 @@ class StreamedShard:
             self._offs[i] = off
         return self._offs[i]
 
+    def n_bases_of(self, i: int) -> int:
+        """bases of partition i"""
+        return int(self.L.bqsr_batch_bases(self.batches[i]))
+
+    def apply_probe_ms(self, i: int = 0, reps: int = 3) -> Optional[float]:
+        """The apply kernel alone on partition i, no copies in flight (no job
+        pending): its char tables first, then the kernel bracketed by HIP
+        events on the compute stream, `reps` times; the mean in ms.  Writes
+        the device output buffers only (the host results stay)."""
+        torch, L = self.torch, self.L
+        if self.pending or not self.lut or not self.batches:
+            return None
+        torch.cuda.synchronize(self.dev)
+        comp = torch.cuda.current_stream(self.dev)
+        sp = ctypes.c_void_p(comp.cuda_stream)
+        bh = self.batches[i]
+        oq = self.host_qual[i] if self.zero_copy else self.out_qual[0]
+        os_ = self.host_start[i] if self.zero_copy else self.out_start[0]
+        ol = self.host_len[i] if self.zero_copy else self.out_len[0]
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        exc_i = ctypes.c_void_p(self.exc.data_ptr() + 8 * i * self.max_exc)
+        args = (self.ctx.handle, bh, self.lut, p(oq), p(os_), p(ol), exc_i, self.max_exc)
+        check(L.bqsr_apply_stage(*args, _capi.STAGE_LUT, sp))
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        t = []
+        for _ in range(reps):
+            ev[0].record(comp)
+            check(L.bqsr_apply_stage(*args, _capi.STAGE_RESET | _capi.STAGE_KERNEL | _capi.STAGE_NO_LUT, sp))
+            ev[1].record(comp)
+            ev[1].synchronize()
+            t.append(ev[0].elapsed_time(ev[1]))
+        return sum(t) / len(t)
+
     def apply_ms(self) -> Optional[float]:
         """Mean apply-kernel time per partition of the last recorded job."""
         try:

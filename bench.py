@@ -487,6 +487,7 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     apply_ms = [sh.apply_ms()]
+    probe_ms = sh.apply_probe_ms(0)  # the kernel alone (no copies in flight), for the roofline
     n_bases = sh.n_bases
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -505,8 +506,10 @@ def main_stream(args, cfg, world, rank, dev, ctx):
         parts_n = len(sh.batches)
         am = float(np.mean([a for a in apply_ms if a is not None])) if apply_ms else None
         R_part = n_reads / parts_n
-        alg_part = 2.5 * n_bases / parts_n + 16 * R_part
-        achieved = alg_part / (am * 1e-3) / 1e9 if am else None
+        R0 = sh.n_reads[0]
+        B0 = sh.n_bases_of(0)
+        alg_part = 2.5 * B0 + 16 * R0  # partition 0's algorithmic bytes
+        achieved = alg_part / (probe_ms * 1e-3) / 1e9 if probe_ms else None
         h2d = sh.staged_bytes
         d2h = sh.d2h_bytes()
         line = {
@@ -533,19 +536,23 @@ def main_stream(args, cfg, world, rank, dev, ctx):
                 "partitions_per_gpu": parts_n,
                 "stream_mode": args.stream_mode,
                 "d2h": args.d2h,
-                "outputs": "compacted chars + u32 offsets" if sh.compact else "padded slots + start/len",
+                "outputs": "compacted chars + u16 lengths" if sh.compact else "padded slots + start/len",
                 "parallelism": "dp%d: read shards per GPU, RCCL int64 table all-reduce" % world,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "bqsr_apply_kernel (per %d-read partition)" % int(R_part),
+                "kernel": "bqsr_apply_kernel (partition 0: %d reads)" % int(R0),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": None,
                 "alg_bytes_per_launch": alg_part,
-                "kernel_ms": {"apply_per_partition": am},
+                "kernel_ms": {"apply_alone": probe_ms, "apply_in_pipeline_per_partition": am},
+                "kernel_ms_method": "apply_alone: HIP events around the apply kernel on partition 0 after the timed "
+                                    "jobs, no copies in flight (mean of 3); in_pipeline: the recorded timed job's "
+                                    "brackets, sharing the GPU with the copies of the other partitions",
+                "bound_note": "cfg5 is PCIe-bound: see `pcie` (the link, not HBM, sets the job time)",
             },
             "pcie": {"h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
                      "achieved_GBps": (h2d + d2h) / (ms_step * 1e-3) / 1e9},
