@@ -19,7 +19,12 @@ run() {  # name lib sorted env...
       python3 "$R/bench.py" --config cfg3 $sorted --no-cpu-baseline --no-parity --steps 5 --warmup 1 > "$O/$name.log" 2>&1
   )
   echo "== $name"; python3 tools/kstat_summary.py "$O/$name" | grep -E "prep|observe|apply" || true
-  tail -1 "$O/$name.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('ms/job', round(d['ms_per_step'],3))"
+  python3 - "$O/$name.log" <<'PY'
+import json, sys
+for line in open(sys.argv[1]):
+    if line.startswith("{"):
+        print("ms/job", round(json.loads(line)["ms_per_step"], 3))
+PY
 }
 P="$R/adam_amd/libadam_bqsr.so"; V="$R/adam_amd/libadam_bqsr_sites_lds.so"
 run sorted_bitmap "$P" --sorted X=1
@@ -28,5 +33,11 @@ run sorted_lds "$V" --sorted X=1
 run random_bitmap "$P" "" X=1
 run random_lds "$V" "" X=1
 ADAM_BQSR_LIB="$V" timeout -k 10 900 python -u bench.py --config cfg3 --sorted --steps 3 --no-cpu-baseline > "$O/bench_lds_sorted.json" 2> "$O/bench_lds_sorted.err"
-python3 -c "import json; d=json.load(open('$O/bench_lds_sorted.json')); print('lds sorted parity', d['parity']['ok'], d['parity']['reads_checked'])"
+python3 - "$O/bench_lds_sorted.json" <<'PY'
+import json, sys
+for line in open(sys.argv[1]):
+    if line.startswith("{"):
+        d = json.loads(line)
+        print("lds sorted", round(d["ms_per_step"], 3), "parity", d["parity"]["ok"], d["parity"]["reads_checked"])
+PY
 echo done
