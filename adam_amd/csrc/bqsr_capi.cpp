@@ -386,10 +386,6 @@ struct bqsr_batch {
   uint8_t *k_qual = nullptr, *k_bases = nullptr;
   uint64_t* d_kslot = nullptr;
   bool perm_static = false;  // d_perm / d_key_off built once (key_major_build): prep skips the key sort
-  // read order: the chunk -> read map of apply's slot_walk (chunk_owner_build)
-  uint32_t* d_owner = nullptr;
-  uint32_t* d_zero = nullptr;
-  int64_t n_zero = 0;
   OrderDev order() const {
     return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0, k_qual ? d_kslot : nullptr}
                     : OrderDev{nullptr, nullptr, 1};
@@ -409,7 +405,7 @@ struct bqsr_batch {
   ~bqsr_batch() {
     if (d_part) (void)hipFree(d_part);
     if (d_off64) (void)hipFree(d_off64);
-    for (void* p : {(void*)k_qual, (void*)k_bases, (void*)d_kslot, (void*)d_owner, (void*)d_zero})
+    for (void* p : {(void*)k_qual, (void*)k_bases, (void*)d_kslot})
       if (p) (void)hipFree(p);
     if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
@@ -750,46 +746,6 @@ bqsr_status key_major_build(bqsr_batch* b, hipStream_t s) {
   return BQSR_OK;
 }
 
-// Read-order batches: apply's chunk -> read map (ApplyParams::owner,
-// slot_walk), once per batch: 4 B per 16 slots.  ADAM_BQSR_SLOTWALK=0: off
-// (apply keeps the chunk walk's mapping; A/B).
-bool slot_walk_off() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_SLOTWALK");
-    return e && strcmp(e, "0") == 0;
-  }();
-  return v;
-}
-bqsr_status chunk_owner_build(bqsr_batch* b, hipStream_t s) {
-  if (b->bucketed || slot_walk_off() || !b->rd.slots_aligned || b->rd.n_reads == 0 || b->rd.n_reads > UINT32_MAX)
-    return BQSR_OK;
-  const int64_t n = b->rd.n_reads, nc = (b->rd.n_slots + 15) >> 4;
-  unsigned long long* cnt = nullptr;
-  hipError_t e = hipMalloc((void**)&b->d_owner, (size_t)std::max<int64_t>(nc, 1) * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&b->d_zero, (size_t)n * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&cnt, 8);
-  if (e == hipSuccess) e = hipMemsetAsync(b->d_owner, 0xFF, (size_t)std::max<int64_t>(nc, 1) * 4, s);
-  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, 8, s);
-  if (e == hipSuccess) {
-    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)b->ctx->n_cu * 8);
-    hipLaunchKernelGGL(bqsr_chunk_owner, dim3(g), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n,
-                       (uint64_t)b->rd.n_slots, b->d_owner, b->d_zero, cnt);
-    e = hipGetLastError();
-  }
-  unsigned long long nz = 0;
-  if (e == hipSuccess) e = hipMemcpyAsync(&nz, cnt, 8, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (cnt) (void)hipFree(cnt);
-  if (e != hipSuccess) {
-    for (void* p : {(void*)b->d_owner, (void*)b->d_zero})
-      if (p) (void)hipFree(p);
-    b->d_owner = b->d_zero = nullptr;
-    return fail(BQSR_ERR_DEVICE, std::string("chunk map: ") + hipGetErrorString(e));
-  }
-  b->n_zero = (int64_t)nz;
-  return BQSR_OK;
-}
-
 // host pack of one record partition (bqsr_records -> device layout)
 struct Packed {
   std::vector<ReadMeta> meta;
@@ -955,8 +911,7 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
   b->rd.md = md;
   b->rd.cigar = cigar;
   b->rd.slots_aligned = align_slots();
-  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK || (st = key_major_build(b, s)) != BQSR_OK ||
-      (st = chunk_owner_build(b, s)) != BQSR_OK) {
+  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK || (st = key_major_build(b, s)) != BQSR_OK) {
     delete b;
     return st;
   }
@@ -1883,9 +1838,6 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   P.chars = b->d_chars;
   P.rowbad = (uint32_t*)(b->d_chars + (size_t)P.piece_stride * (size_t)b->n_base);
-  P.owner = b->d_owner;
-  P.zero_reads = b->d_zero;
-  P.n_zero = b->n_zero;
   const bool lut_stage = (stages & BQSR_STAGE_LUT) || ((stages & BQSR_STAGE_KERNEL) && !(stages & BQSR_STAGE_NO_LUT));
   if (lut_stage) {
     HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_base * 16, s));

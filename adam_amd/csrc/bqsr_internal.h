@@ -312,12 +312,6 @@ struct ApplyParams {
   const uint8_t* chars;   // [n_keys][piece_stride] the pieces' char tables (bqsr_apply_chars)
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
-  // read order, 16-aligned slots (slot_walk): the read of each 16-slot chunk
-  // of the batch ([n_slots / 16], ~0u past the last read), and the reads
-  // without slots, whose per-read outputs no chunk writes; nullptr: chunk_walk
-  const uint32_t* owner;
-  const uint32_t* zero_reads;
-  int64_t n_zero;
 };
 
 // finalize results read back by the host

@@ -1399,60 +1399,6 @@ __device__ __forceinline__ void chunk_walk(const ReadsDev& rd, const ReadInfo* i
   }
 }
 
-// Read order with 16-aligned slots: the batch's chunks in slot order, chunk
-// c = slots [16c, 16c + 16) of read owner[c] (bqsr_chunk_owner, built once
-// per batch, 0.25 B a slot) -- every lane decodes its own chunk's read from
-// the map instead of the walk's marker / max-scan / ds_bpermute mapping.  A
-// wavefront step takes kU groups of 64 consecutive chunks; fread runs for a
-// read on the lane holding its first chunk (reads without slots: the
-// caller).  Chunks outside the read's visited [st, en) stay off, as the walk
-// never maps them.
-template <uint32_t kAct, int kU, class LD, class FRead, class FLoad, class FChunk>
-__device__ __forceinline__ void slot_walk(const ReadsDev& rd, const ReadInfo* info, const uint32_t* owner, int64_t c0,
-                                          int64_t c1, int64_t cstep, int L, int lane, FRead&& fread, FLoad&& fload,
-                                          FChunk&& fchunk) {
-  for (int64_t cb = c0; cb < c1; cb += cstep) {
-    LaneRead c[kU];
-    int jj[kU];
-    bool on[kU];
-    LD ld[kU];
-    uint32_t rr[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t ci = cb + 64 * u + lane;
-      rr[u] = ci < c1 ? owner[ci] : ~0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t ci = cb + 64 * u + lane;
-      const bool live = rr[u] != ~0u;
-      c[u] = lane_read(rd, info, live ? rr[u] : 0, live, L);
-      const int o0 = (int)(16 * ci - (int64_t)c[u].slot);  // the chunk's first offset in its read
-      if (live && o0 == 0) fread(c[u], true);
-      jj[u] = o0 - c[u].st;
-      on[u] = live && (c[u].fl & kAct) && o0 < c[u].en && o0 + kChunk > c[u].st;
-      ld[u] = fload(c[u], jj[u], on[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) fchunk(c[u], jj[u], c[u].en - c[u].st, on[u], ld[u]);
-  }
-}
-
-// owner[c] of slot_walk: every read's 16-slot chunks (slots up to the next
-// read's, or n_slots), the reads without slots appended to `zero`
-extern "C" __global__ void bqsr_chunk_owner(const ReadMeta* meta, int64_t n, uint64_t n_slots, uint32_t* owner,
-                                            uint32_t* zero, unsigned long long* n_zero) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t s0 = meta[r].slot, s1 = r + 1 < n ? meta[r + 1].slot : n_slots;
-    if (s1 <= s0) {
-      const unsigned long long i = atomicAdd(n_zero, 1ull);
-      zero[i] = (uint32_t)r;
-      continue;
-    }
-    for (uint64_t c = s0 >> 4; c < (s1 + 15) >> 4; ++c) owner[c] = (uint32_t)r;
-  }
-}
-
 // ------------------------------------------------------------ observe ------
 
 typedef __attribute__((address_space(3))) uint32_t* LdsWords;
@@ -2345,22 +2291,6 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
   const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
   ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
-  const auto fread = [&](LaneRead& x, bool live) {
-    if (!live) return;
-    if (x.fl & kInfoPass) {  // quality string passed through
-      P.out_start[x.ro] = 0;
-      P.out_len[x.ro] = (uint32_t)x.en;
-    } else {
-      P.out_start[x.ro] = (uint32_t)x.st;
-      P.out_len[x.ro] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
-    }
-  };
-  if (P.owner) {  // slot_walk: the reads without a chunk
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + tid; i < P.n_zero; i += (int64_t)G * blockDim.x) {
-      LaneRead x = lane_read(P.rd, P.info, P.zero_reads[i], true, L);
-      fread(x, true);
-    }
-  }
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));
@@ -2395,20 +2325,23 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
     __syncthreads();
     const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb, (int)clean_rows[0],
                         (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C};
+    const auto fread = [&](LaneRead& x, bool live) {
+      if (!live) return;
+      if (x.fl & kInfoPass) {  // quality string passed through
+        P.out_start[x.ro] = 0;
+        P.out_len[x.ro] = (uint32_t)x.en;
+      } else {
+        P.out_start[x.ro] = (uint32_t)x.st;
+        P.out_len[x.ro] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
+      }
+    };
     const auto fload = [&](const LaneRead& x, int j, bool on) { return apply_load(P, x, j, on); };
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
       apply_chunk(P, &P, pc, x, j, n, on, ld);
     };
-    constexpr uint32_t kAct = kInfoApp | kInfoAppCheck | kInfoPass;
-    if (P.owner) {  // read order: one piece, the workgroup's reads' chunks
-      const int64_t c0 = (int64_t)(P.rd.meta[p0].slot >> 4);
-      const int64_t c1 = p1 < P.rd.n_reads ? (int64_t)(P.rd.meta[p1].slot >> 4) : (int64_t)((P.rd.n_slots + 15) >> 4);
-      slot_walk<kAct, kApplyU, ChunkLoads>(P.rd, P.info, P.owner, c0 + 64 * kApplyU * wave, c1, 64 * kApplyU * kWaves, L,
-                                           lane, fread, fload, fchunk);
-    } else {
-      chunk_walk<kAct, kApplyU, ChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk,
-                                                   fread, fload, fchunk);
-    }
+    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+                                                                             64 * kWaves, L, lane, mk, fread, fload,
+                                                                             fchunk);
   }  // pieces
 }
 
