@@ -244,17 +244,18 @@ uint32_t le32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// BGZF -> the decompressed BAM (pinned host memory), blocks inflated by threads
-bqsr_status bgzf_inflate(const uint8_t* data, int64_t n, std::vector<uint8_t>& out) {
-  struct Blk {
-    int64_t src, csize, dst, isize;
-  };
-  std::vector<Blk> blks;
-  int64_t p = 0, total = 0;
+struct BgzfBlk {
+  int64_t src, csize, dst, isize;
+};
+
+// The BGZF block list of a file (its headers walked in order; an untrusted
+// file: every field is bounds-checked before it is read) and the inflated size.
+bqsr_status bgzf_blocks(const uint8_t* data, int64_t n, std::vector<BgzfBlk>& blks, int64_t& total) {
+  int64_t p = 0;
+  total = 0;
   while (p < n) {
     if (n - p < 18 || data[p] != 31 || data[p + 1] != 139 || data[p + 2] != 8 || !(data[p + 3] & 4))
       return fail(BQSR_ERR_SAM_PARSE, "BAM: not a BGZF block at byte " + std::to_string(p));
-    // an untrusted file: every field is bounds-checked before it is read
     const int64_t xlen = data[p + 10] | (data[p + 11] << 8);
     const int64_t xend = p + 12 + xlen;
     if (xend > n) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated BGZF header at byte " + std::to_string(p));
@@ -271,42 +272,153 @@ bqsr_status bgzf_inflate(const uint8_t* data, int64_t n, std::vector<uint8_t>& o
     if (blen < hdr + 8) return fail(BQSR_ERR_SAM_PARSE, "BAM: BGZF BSIZE smaller than its header");
     const int64_t isize = le32(data + p + blen - 4);
     if (isize > 65536) return fail(BQSR_ERR_SAM_PARSE, "BAM: BGZF ISIZE above 64 KiB");
-    blks.push_back(Blk{p + hdr, blen - hdr - 8, total, isize});
+    blks.push_back(BgzfBlk{p + hdr, blen - hdr - 8, total, isize});
     total += isize;
     p += blen;
   }
-  out.resize((size_t)total + 64);
-  std::atomic<int64_t> next{0};
-  std::atomic<int> bad{0};
-  auto work = [&]() {
-    for (int64_t i; (i = next.fetch_add(1)) < (int64_t)blks.size();) {
-      const Blk& k = blks[(size_t)i];
-      if (k.isize == 0) continue;
-      z_stream zs{};
-      if (inflateInit2(&zs, -15) != Z_OK) {
-        bad = 1;
-        continue;
-      }
-      zs.next_in = (Bytef*)(data + k.src);
-      zs.avail_in = (uInt)k.csize;
-      zs.next_out = (Bytef*)(out.data() + k.dst);
-      zs.avail_out = (uInt)k.isize;
-      const int rc = inflate(&zs, Z_FINISH);
-      const bool ok_len = rc == Z_STREAM_END && zs.total_out == (uLong)k.isize;
-      inflateEnd(&zs);
-      // the block's CRC32 of its uncompressed bytes (the 4 bytes before ISIZE)
-      if (!ok_len || crc32(0L, out.data() + k.dst, (uInt)k.isize) != le32(data + k.src + k.csize)) bad = 1;
-    }
-  };
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)std::thread::hardware_concurrency(),
-                                                               std::min<int64_t>(16, (int64_t)blks.size())));
-  std::vector<std::thread> th;
-  for (int t = 0; t < nt; ++t) th.emplace_back(work);
-  for (auto& t : th) t.join();
-  if (bad) return fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate or fails its CRC32");
-  out.resize((size_t)total);
   return BQSR_OK;
 }
+
+// Inflate straight to the device: runs of whole blocks (at most kStageChunk
+// bytes inflated) are inflated by host threads into the context's pinned
+// ring and each run is DMA'd to d_out + its offset while the threads inflate
+// the next -- no pageable copy of the inflated stream (its first touch of
+// gigabytes of fresh pages was most of a BAM parse).  `host(buf, off, len)`
+// reads every run, in stream order, before its ring slot is reused.
+template <class Host>
+bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const std::vector<BgzfBlk>& blks,
+                                uint8_t* d_out, hipStream_t s, Host&& host) {
+  std::lock_guard<std::mutex> lock(ctx->stage_mu);
+  bqsr_status st = stage_ring(ctx);
+  if (st != BQSR_OK) return st;
+  const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  size_t i = 0;
+  int k = 0;
+  while (i < blks.size()) {
+    size_t j = i;
+    int64_t len = 0;
+    while (j < blks.size() && len + blks[j].isize <= (int64_t)kStageChunk) len += blks[j++].isize;  // (isize <= 64 KiB)
+    HIP_TRY(hipEventSynchronize(ctx->stage_ev[k]));  // the slot's previous DMA is done
+    uint8_t* buf = ctx->stage[k];
+    const int64_t dst0 = blks[i].dst;
+    std::atomic<size_t> next{i};
+    std::atomic<int> bad{0};
+    auto work = [&]() {
+      for (size_t b; (b = next.fetch_add(1)) < j;) {
+        const BgzfBlk& z = blks[b];
+        if (z.isize == 0) continue;
+        z_stream zs{};
+        if (inflateInit2(&zs, -15) != Z_OK) {
+          bad = 1;
+          continue;
+        }
+        uint8_t* o = buf + (z.dst - dst0);
+        zs.next_in = (Bytef*)(data + z.src);
+        zs.avail_in = (uInt)z.csize;
+        zs.next_out = (Bytef*)o;
+        zs.avail_out = (uInt)z.isize;
+        const int rc = inflate(&zs, Z_FINISH);
+        const bool ok_len = rc == Z_STREAM_END && zs.total_out == (uLong)z.isize;
+        inflateEnd(&zs);
+        // the block's CRC32 of its uncompressed bytes (the 4 bytes before ISIZE)
+        if (!ok_len || crc32(0L, o, (uInt)z.isize) != le32(data + z.src + z.csize)) bad = 1;
+      }
+    };
+    std::vector<std::thread> th;
+    const int nw = (int)std::min<size_t>((size_t)nt, j - i);
+    for (int t = 0; t < nw; ++t) th.emplace_back(work);
+    for (auto& t : th) t.join();
+    if (bad) {
+      (void)hipStreamSynchronize(s);
+      return fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate or fails its CRC32");
+    }
+    if (len > 0) {
+      HIP_TRY(hipMemcpyAsync(d_out + dst0, buf, (size_t)len, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipEventRecord(ctx->stage_ev[k], s));
+    }
+    if ((st = host(buf, dst0, len)) != BQSR_OK) {
+      (void)hipStreamSynchronize(s);
+      return st;
+    }
+    i = j;
+    k ^= 1;
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return BQSR_OK;
+}
+
+// The BAM header (magic, SAM text, binary reference list) from the first m
+// bytes of the inflated stream: 1 parsed (body = the first record's offset),
+// 0 more bytes needed (`all`: there are none -- an error then).
+struct BamHead {
+  int64_t l_text = 0, body = 0;
+  std::vector<uint8_t> ref_blob;
+  std::vector<uint64_t> ref_off{0};
+};
+int bam_head(const uint8_t* u, int64_t m, bool all, BamHead& H, bqsr_status& st) {
+  st = BQSR_OK;
+  const auto need = [&](const char* what) {
+    if (!all) return 0;
+    st = fail(BQSR_ERR_SAM_PARSE, what);
+    return -1;
+  };
+  if (m >= 4 && memcmp(u, "BAM\1", 4) != 0) return (st = fail(BQSR_ERR_SAM_PARSE, "BAM: no BAM magic")), -1;
+  if (m < 12) return need("BAM: no BAM magic");
+  H.l_text = (int32_t)le32(u + 4);
+  if (H.l_text < 0) return (st = fail(BQSR_ERR_SAM_PARSE, "BAM: bad header length")), -1;
+  if (8 + H.l_text + 4 > m) return need("BAM: bad header length");
+  int64_t p = 8 + H.l_text;
+  const int64_t n_ref = (int32_t)le32(u + p);
+  p += 4;
+  // the binary reference list's names: a record's RNAME / RNEXT text
+  // (referenceName then only for a header @SQ name, as for SAM text)
+  H.ref_blob.clear();
+  H.ref_off.assign(1, 0);
+  for (int64_t i = 0; i < n_ref; ++i) {
+    if (p + 4 > m) return need("BAM: truncated reference list");
+    const int64_t l_name = (int32_t)le32(u + p);
+    if (l_name < 1) return (st = fail(BQSR_ERR_SAM_PARSE, "BAM: bad reference name")), -1;
+    if (p + 4 + l_name + 4 > m) return need("BAM: bad reference name");
+    H.ref_blob.insert(H.ref_blob.end(), u + p + 4, u + p + 4 + (l_name - 1));
+    H.ref_off.push_back(H.ref_blob.size());
+    p += 4 + l_name + 4;
+  }
+  H.body = p;
+  return 1;
+}
+
+// Record offsets by their block_size fields, over the stream's runs in order
+// (a field may straddle two runs).
+struct RecScan {
+  int64_t body = 0, p = 0;  // p: the next record's stream offset
+  uint8_t pend[4];
+  int pend_n = 0;
+  std::vector<uint64_t> rec;
+  bool field(uint32_t v) {
+    const int64_t bs = (int32_t)v;
+    if (bs < 32) return false;
+    rec.push_back((uint64_t)(p - body));
+    p += 4 + bs;
+    return true;
+  }
+  bqsr_status consume(const uint8_t* buf, int64_t off, int64_t len) {
+    const int64_t end = off + len;
+    if (pend_n > 0) {
+      int64_t q = off;
+      while (pend_n < 4 && q < end) pend[pend_n++] = buf[q++ - off];
+      if (pend_n < 4) return BQSR_OK;
+      pend_n = 0;
+      if (!field(le32(pend))) return bad();
+    }
+    while (p + 4 <= end) {
+      if (p < off) return bad();  // (cannot happen: p passed a run's end only as a pending field)
+      if (!field(le32(buf + (p - off)))) return bad();
+    }
+    for (int64_t q = std::max(p, off); q < end; ++q) pend[pend_n++] = buf[q - off];
+    return BQSR_OK;
+  }
+  bqsr_status bad() const { return fail(BQSR_ERR_SAM_PARSE, "BAM: bad record size at byte " + std::to_string(p)); }
+};
 
 }  // namespace
 
@@ -314,50 +426,11 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   if (!ctx || !out || n < 0 || (n > 0 && !data)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_bam_parse: bad arguments");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
-  std::vector<uint8_t> raw;
-  bqsr_status st = bgzf_inflate(data, n, raw);
+  std::vector<BgzfBlk> blks;
+  int64_t m = 0;
+  bqsr_status st = bgzf_blocks(data, n, blks, m);
   if (st != BQSR_OK) return st;
-  const int64_t m = (int64_t)raw.size();
-  const uint8_t* u = raw.data();
-  if (m < 12 || memcmp(u, "BAM\1", 4) != 0) return fail(BQSR_ERR_SAM_PARSE, "BAM: no BAM magic");
-  const int64_t l_text = (int32_t)le32(u + 4);
-  if (l_text < 0 || 8 + l_text + 4 > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: bad header length");
-  // the SAM header text (NULs allowed at its end), as bqsr_sam_parse reads it
-  int64_t lt = l_text;
-  while (lt > 0 && u[8 + lt - 1] == 0) --lt;
-  SamHeader H;
-  if ((st = parse_sam_header((const char*)u + 8, lt, &H)) != BQSR_OK) return st;
-  int64_t p = 8 + l_text;
-  const int64_t n_ref = (int32_t)le32(u + p);
-  p += 4;
-  // the binary reference list's names: a record's RNAME / RNEXT text
-  // (referenceName then only for a header @SQ name, as for SAM text)
-  std::vector<uint8_t> ref_blob;
-  std::vector<uint64_t> ref_off(1, 0);
-  for (int64_t i = 0; i < n_ref; ++i) {
-    if (p + 4 > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated reference list");
-    const int64_t l_name = (int32_t)le32(u + p);
-    if (l_name < 1 || p + 4 + l_name + 4 > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: bad reference name");
-    ref_blob.insert(ref_blob.end(), u + p + 4, u + p + 4 + (l_name - 1));
-    ref_off.push_back(ref_blob.size());
-    p += 4 + l_name + 4;
-  }
-  // records: offsets by their block_size fields
-  std::vector<uint64_t> rec;
-  const int64_t body = p;
-  while (p < m) {
-    if (p + 4 > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated record");
-    const int64_t bs = (int32_t)le32(u + p);
-    if (bs < 32 || p + 4 + bs > m) return fail(BQSR_ERR_SAM_PARSE, "BAM: bad record size at byte " + std::to_string(p));
-    rec.push_back((uint64_t)(p - body));
-    p += 4 + bs;
-  }
-  const int64_t nr = (int64_t)rec.size();
-  rec.push_back((uint64_t)(m - body));
-  // the header text, newline-terminated, then the records' SAM lines
-  std::string hdr((const char*)u + 8, (size_t)lt);
-  if (!hdr.empty() && hdr.back() != '\n') hdr.push_back('\n');
-  H.body = (int64_t)hdr.size();
+  if (m < 12) return fail(BQSR_ERR_SAM_PARSE, "BAM: no BAM magic");
   std::vector<void*> tmp;
   struct Free {
     std::vector<void*>& v;
@@ -365,11 +438,53 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
       for (void* q : v) (void)hipFree(q);
     }
   } free_tmp{tmp};
+  uint8_t* d_raw;  // the whole inflated stream; the records start at H.body
+  if ((st = sam_alloc(tmp, &d_raw, (size_t)m + 64)) != BQSR_OK) return st;
+  HIP_TRY(hipMemsetAsync(d_raw + m, 0, 64, s));
+  // on the host, as the runs pass: the header bytes until it parses, then the record offsets
+  BamHead BH;
+  SamHeader H;
+  std::string hdr;
+  std::vector<uint8_t> head;
+  bool have_head = false;
+  RecScan scan;
+  st = bgzf_inflate_device(ctx, data, blks, d_raw, s, [&](const uint8_t* buf, int64_t off, int64_t len) -> bqsr_status {
+    if (have_head) return scan.consume(buf, off, len);
+    head.insert(head.end(), buf, buf + len);
+    bqsr_status e;
+    const int r = bam_head(head.data(), (int64_t)head.size(), off + len == m, BH, e);
+    if (r < 0) return e;
+    if (r == 0) return BQSR_OK;
+    have_head = true;
+    // the SAM header text (NULs allowed at its end), as bqsr_sam_parse reads it
+    int64_t lt = BH.l_text;
+    while (lt > 0 && head[(size_t)(8 + lt - 1)] == 0) --lt;
+    if ((e = parse_sam_header((const char*)head.data() + 8, lt, &H)) != BQSR_OK) return e;
+    hdr.assign((const char*)head.data() + 8, (size_t)lt);
+    scan.body = scan.p = BH.body;
+    e = scan.consume(head.data(), 0, (int64_t)head.size());
+    std::vector<uint8_t>().swap(head);
+    return e;
+  });
+  if (st != BQSR_OK) return st;
+  if (!have_head) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated header");
+  if (scan.pend_n > 0 || scan.p < m) return fail(BQSR_ERR_SAM_PARSE, "BAM: truncated record");
+  if (scan.p > m) {  // the last record overruns the stream
+    scan.p = BH.body + (int64_t)scan.rec.back();
+    return scan.bad();
+  }
+  const int64_t body = BH.body;
+  std::vector<uint64_t>& rec = scan.rec;
+  std::vector<uint8_t>& ref_blob = BH.ref_blob;
+  std::vector<uint64_t>& ref_off = BH.ref_off;
+  const int64_t n_ref = (int64_t)ref_off.size() - 1;
+  const int64_t nr = (int64_t)rec.size();
+  rec.push_back((uint64_t)(m - body));
+  // the header text, newline-terminated, then the records' SAM lines
+  if (!hdr.empty() && hdr.back() != '\n') hdr.push_back('\n');
+  H.body = (int64_t)hdr.size();
   bamk::BamParams P{};
-  uint8_t* d_rec;
-  if ((st = sam_alloc(tmp, &d_rec, (size_t)(m - body) + 64)) != BQSR_OK) return st;
-  if (m > body && (st = upload_staged(ctx, d_rec, u + body, (size_t)(m - body), s)) != BQSR_OK) return st;
-  P.buf = d_rec;
+  P.buf = d_raw + body;
   P.n = nr;
   P.n_ref = (int32_t)n_ref;
   P.hdr = H.body;

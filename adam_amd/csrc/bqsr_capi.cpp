@@ -278,6 +278,14 @@ namespace {
 // DMA engine moves the previous chunk -- the runtime's own pageable path
 // stages through one thread's memcpy (~20 GB/s).  Synchronous on return.
 constexpr size_t kStageChunk = 64ull << 20;
+// the ring's two pinned buffers and events, allocated on first use (caller holds stage_mu)
+bqsr_status stage_ring(bqsr_context* ctx) {
+  for (int i = 0; i < 2; ++i) {
+    if (!ctx->stage[i]) HIP_TRY(hipHostMalloc((void**)&ctx->stage[i], kStageChunk, hipHostMallocDefault));
+    if (!ctx->stage_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming));
+  }
+  return BQSR_OK;
+}
 bqsr_status upload_staged(bqsr_context* ctx, void* dst, const void* src, size_t n, hipStream_t s) {
   hipPointerAttribute_t attr{};
   const bool pinned = hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeHost;
@@ -288,10 +296,8 @@ bqsr_status upload_staged(bqsr_context* ctx, void* dst, const void* src, size_t 
     return BQSR_OK;
   }
   std::lock_guard<std::mutex> lock(ctx->stage_mu);
-  for (int i = 0; i < 2; ++i) {
-    if (!ctx->stage[i]) HIP_TRY(hipHostMalloc((void**)&ctx->stage[i], kStageChunk, hipHostMallocDefault));
-    if (!ctx->stage_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ctx->stage_ev[i], hipEventDisableTiming));
-  }
+  bqsr_status st = stage_ring(ctx);
+  if (st != BQSR_OK) return st;
   const int nth = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   const uint8_t* p = (const uint8_t*)src;
   uint8_t* d = (uint8_t*)dst;
