@@ -1504,7 +1504,8 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
 #pragma unroll
       for (int i = 0; i < 4; ++i) xr[i] = __builtin_amdgcn_alignbyte(u[(i + 1) & 3], u[i], bs);
     }
-    const uint32_t vr = ((vmask | (vmask << 16)) >> rot) & 0xFFFFu, br = ((bm | (bm << 16)) >> rot) & 0xFFFFu;
+    const uint32_t b16 = bm & 0xFFFFu;  // (bits 16.. of bm are the next chunk's)
+    const uint32_t vr = ((vmask | (vmask << 16)) >> rot) & 0xFFFFu, br = ((b16 | (b16 << 16)) >> rot) & 0xFFFFu;
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) {
       const int kk = (k + (int)rot) & 15;  // the offset this lane works at step k
