@@ -1391,15 +1391,6 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
 }
 }  // namespace
 
-// the chunk-walk observe's window row length mod 4 (A/B: ADAM_BQSR_WPAD, default 2)
-static int chunk_wpad() {
-  static const int v = [] {
-    const char* e = getenv("ADAM_BQSR_WPAD");
-    return e && e[0] >= '0' && e[0] <= '3' && !e[1] ? e[0] - '0' : 2;
-  }();
-  return v;
-}
-
 bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
                                int32_t stages, void* stream) {
   if (!ctx || !b || !t) return fail(BQSR_ERR_INVALID_ARG, "null");
@@ -1436,8 +1427,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     // super-chunk and the lane-per-offset rows kernel (SALU-bound, 6.0 ms cfg2).
     const bool lean = !b->bucketed;
     P.wcells = window_cw(b, P.g) + (lean ? kCtxCells : kCtxSlots);
-    const int wpad = lean ? 2 : chunk_wpad();
-    while ((P.wcells & 3) != wpad) ++P.wcells;
+    while ((P.wcells & 3) != 2) ++P.wcells;  // (chunk walk, cfg4: 0 mod 4 5.72 ms, 1 mod 4 4.32, 2 mod 4 4.34)
     if (lean) {
       const int cw = window_cw(b, P.g), span = qual_span(b);
       int best_rows = 0;

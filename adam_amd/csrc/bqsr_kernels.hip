@@ -1479,53 +1479,7 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
                    (unsigned)(wc0 + __mul24((int)nv - 1, x.dir)) < (unsigned)pc.cw;
   const uint32_t vmask = (nv >= 16u ? 0xFFFFu : ((1u << nv) - 1u)) & (0xFFFFu << klo);
   uint32_t fastm = 0;
-#ifdef ADAM_BQSR_ROTATE
-  // A/B build (tools/build_variant.sh rotate -DADAM_BQSR_ROTATE): each lane
-  // walks its chunk's 16 offsets from (lane & 15) round, so at one unrolled
-  // step the lanes add to 16 different cycle cells instead of a few (the
-  // chunks of forward reads start 16-aligned: every lane at one cell mod 16),
-  // spreading the window atomics over the LDS banks.  The chunk's quals,
-  // contexts and bits are rotated in registers once.
   if (cok) {
-    const uint32_t rot = threadIdx.x & 15u, ws = rot >> 2, bs = rot & 3u;
-    uint32_t qr[4], xr[4];
-    {
-      uint32_t t[4], u[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t[i] = (ws & 1u) ? qd[(i + 1) & 3] : qd[i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) u[i] = (ws & 2u) ? t[(i + 2) & 3] : t[i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) qr[i] = __builtin_amdgcn_alignbyte(u[(i + 1) & 3], u[i], bs);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t[i] = (ws & 1u) ? xo[(i + 1) & 3] : xo[i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) u[i] = (ws & 2u) ? t[(i + 2) & 3] : t[i];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) xr[i] = __builtin_amdgcn_alignbyte(u[(i + 1) & 3], u[i], bs);
-    }
-    const uint32_t b16 = bm & 0xFFFFu;  // (bits 16.. of bm are the next chunk's)
-    const uint32_t vr = ((vmask | (vmask << 16)) >> rot) & 0xFFFFu, br = ((b16 | (b16 << 16)) >> rot) & 0xFFFFu;
-#pragma unroll
-    for (int k = 0; k < kChunk; ++k) {
-      const int kk = (k + (int)rot) & 15;  // the offset this lane works at step k
-      const int q = (int)__builtin_amdgcn_ubfe(qr[k >> 2], 8 * (k & 3), 8);
-      const int row = q - pc.q_lo;
-      const bool f = (unsigned)row < (unsigned)pc.qw && ((vr >> k) & 1u);
-      const bool m = (br >> k) & 1u;
-      const int base = __mul24(row, pc.wcells);
-      if (f) {
-        atomicAdd(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + __mul24(x.dir, kk)], 1u);
-        if (!m) atomicAdd(&pc.w_obs[base + pc.cw + (int)__builtin_amdgcn_ubfe(xr[k >> 2], 8 * (k & 3), 8)], 1u);
-        if (pc.fh) atomicAdd(&pc.fh[__mul24(x.aux, pc.qw) + row], 1u);
-      }
-      fastm |= (uint32_t)f << kk;
-    }
-  }
-  if (false) {
-#else
-  if (cok) {
-#endif
 #pragma unroll
     for (int k = 0; k < kChunk; ++k) {
       const int q = (int)__builtin_amdgcn_ubfe(qd[k >> 2], 8 * (k & 3), 8);
