@@ -248,6 +248,19 @@ struct BgzfBlk {
   int64_t src, csize, dst, isize;
 };
 
+// ADAM_BQSR_TIMING=1: a BAM parse prints its host / device phases to stderr
+bool bam_timing() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_TIMING");
+    return e && strcmp(e, "1") == 0;
+  }();
+  return v;
+}
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+struct InflateTimes {
+  double wait = 0, inflate = 0, host = 0, drain = 0;
+};
+
 // The BGZF block list of a file (its headers walked in order; an untrusted
 // file: every field is bounds-checked before it is read) and the inflated size.
 bqsr_status bgzf_blocks(const uint8_t* data, int64_t n, std::vector<BgzfBlk>& blks, int64_t& total) {
@@ -287,7 +300,7 @@ bqsr_status bgzf_blocks(const uint8_t* data, int64_t n, std::vector<BgzfBlk>& bl
 // reads every run, in stream order, before its ring slot is reused.
 template <class Host>
 bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const std::vector<BgzfBlk>& blks,
-                                uint8_t* d_out, hipStream_t s, Host&& host) {
+                                uint8_t* d_out, hipStream_t s, InflateTimes& T, Host&& host) {
   std::lock_guard<std::mutex> lock(ctx->stage_mu);
   bqsr_status st = stage_ring(ctx);
   if (st != BQSR_OK) return st;
@@ -298,7 +311,10 @@ bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const st
     size_t j = i;
     int64_t len = 0;
     while (j < blks.size() && len + blks[j].isize <= (int64_t)kStageChunk) len += blks[j++].isize;  // (isize <= 64 KiB)
+    double t0 = now_s();
     HIP_TRY(hipEventSynchronize(ctx->stage_ev[k]));  // the slot's previous DMA is done
+    double t1 = now_s();
+    T.wait += t1 - t0;
     uint8_t* buf = ctx->stage[k];
     const int64_t dst0 = blks[i].dst;
     std::atomic<size_t> next{i};
@@ -328,6 +344,8 @@ bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const st
     const int nw = (int)std::min<size_t>((size_t)nt, j - i);
     for (int t = 0; t < nw; ++t) th.emplace_back(work);
     for (auto& t : th) t.join();
+    t0 = now_s();
+    T.inflate += t0 - t1;
     if (bad) {
       (void)hipStreamSynchronize(s);
       return fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate or fails its CRC32");
@@ -340,10 +358,13 @@ bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const st
       (void)hipStreamSynchronize(s);
       return st;
     }
+    T.host += now_s() - t0;
     i = j;
     k ^= 1;
   }
+  const double t0 = now_s();
   HIP_TRY(hipStreamSynchronize(s));
+  T.drain += now_s() - t0;
   return BQSR_OK;
 }
 
@@ -426,9 +447,11 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   if (!ctx || !out || n < 0 || (n > 0 && !data)) return fail(BQSR_ERR_INVALID_ARG, "bqsr_bam_parse: bad arguments");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = S(stream);
+  const double t_start = now_s();
   std::vector<BgzfBlk> blks;
   int64_t m = 0;
   bqsr_status st = bgzf_blocks(data, n, blks, m);
+  const double t_blocks = now_s();
   if (st != BQSR_OK) return st;
   if (m < 12) return fail(BQSR_ERR_SAM_PARSE, "BAM: no BAM magic");
   std::vector<void*> tmp;
@@ -448,7 +471,9 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   std::vector<uint8_t> head;
   bool have_head = false;
   RecScan scan;
-  st = bgzf_inflate_device(ctx, data, blks, d_raw, s, [&](const uint8_t* buf, int64_t off, int64_t len) -> bqsr_status {
+  InflateTimes IT;
+  const double t_alloc = now_s();
+  st = bgzf_inflate_device(ctx, data, blks, d_raw, s, IT, [&](const uint8_t* buf, int64_t off, int64_t len) -> bqsr_status {
     if (have_head) return scan.consume(buf, off, len);
     head.insert(head.end(), buf, buf + len);
     bqsr_status e;
@@ -473,6 +498,7 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
     scan.p = BH.body + (int64_t)scan.rec.back();
     return scan.bad();
   }
+  const double t_inflated = now_s();
   const int64_t body = BH.body;
   std::vector<uint64_t>& rec = scan.rec;
   std::vector<uint8_t>& ref_blob = BH.ref_blob;
@@ -531,5 +557,13 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
     (void)hipFree(d_text);
     return fail(BQSR_ERR_DEVICE, std::string("bqsr_bam_parse: ") + hipGetErrorString(e));
   }
-  return sam_parse_device(ctx, H, hdr.data(), d_text, n_text, s, true, out);  // (owns d_text from here)
+  const double t_lines = now_s();
+  st = sam_parse_device(ctx, H, hdr.data(), d_text, n_text, s, true, out);  // (owns d_text from here)
+  if (bam_timing())
+    fprintf(stderr,
+            "[bam_parse] %lld reads, %.2f GB inflated: blocks %.3f, alloc %.3f, runs %.3f (slot waits %.3f, "
+            "inflate %.3f, host scan %.3f, drain %.3f), lines %.3f, SAM parse %.3f s\n",
+            (long long)nr, m / 1e9, t_blocks - t_start, t_alloc - t_blocks, t_inflated - t_alloc, IT.wait, IT.inflate,
+            IT.host, IT.drain, t_lines - t_inflated, now_s() - t_lines);
+  return st;
 }
