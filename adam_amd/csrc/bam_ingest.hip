@@ -248,6 +248,56 @@ struct BgzfBlk {
   int64_t src, csize, dst, isize;
 };
 
+// Raw DEFLATE + CRC32 of one BGZF block.  libdeflate (the system's
+// libdeflate.so.0, loaded at run time: whole-buffer inflate and a folded
+// CRC32, ~3x zlib's per thread) when the image has it, zlib otherwise.
+struct Deflate {
+  typedef void* (*alloc_fn)();
+  typedef int (*inflate_fn)(void*, const void*, size_t, void*, size_t, size_t*);
+  typedef void (*free_fn)(void*);
+  typedef uint32_t (*crc_fn)(uint32_t, const void*, size_t);
+  alloc_fn alloc = nullptr;
+  inflate_fn inflate = nullptr;
+  free_fn free = nullptr;
+  crc_fn crc = nullptr;
+  static const Deflate& get() {
+    static const Deflate d = [] {
+      Deflate x;
+      const char* off = getenv("ADAM_BQSR_LIBDEFLATE");
+      if (off && strcmp(off, "0") == 0) return x;
+      void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+      if (!h) return x;
+      x.alloc = (alloc_fn)dlsym(h, "libdeflate_alloc_decompressor");
+      x.inflate = (inflate_fn)dlsym(h, "libdeflate_deflate_decompress");
+      x.free = (free_fn)dlsym(h, "libdeflate_free_decompressor");
+      x.crc = (crc_fn)dlsym(h, "libdeflate_crc32");
+      if (!x.alloc || !x.inflate || !x.free || !x.crc) x = Deflate{};
+      return x;
+    }();
+    return d;
+  }
+  bool ok() const { return alloc != nullptr; }
+};
+// one block into o (isize bytes); false: it does not inflate to exactly isize or fails its CRC32
+bool inflate_block(const Deflate& D, void* dec, const uint8_t* in, int64_t csize, uint8_t* o, int64_t isize,
+                   uint32_t crc_want) {
+  if (D.ok()) {
+    size_t got = 0;
+    if (D.inflate(dec, in, (size_t)csize, o, (size_t)isize, &got) != 0 || got != (size_t)isize) return false;
+    return D.crc(0, o, (size_t)isize) == crc_want;
+  }
+  z_stream zs{};
+  if (inflateInit2(&zs, -15) != Z_OK) return false;
+  zs.next_in = (Bytef*)in;
+  zs.avail_in = (uInt)csize;
+  zs.next_out = (Bytef*)o;
+  zs.avail_out = (uInt)isize;
+  const int rc = inflate(&zs, Z_FINISH);
+  const bool ok_len = rc == Z_STREAM_END && zs.total_out == (uLong)isize;
+  inflateEnd(&zs);
+  return ok_len && crc32(0L, o, (uInt)isize) == crc_want;
+}
+
 // ADAM_BQSR_TIMING=1: a BAM parse prints its host / device phases to stderr
 bool bam_timing() {
   static const bool v = [] {
@@ -258,7 +308,7 @@ bool bam_timing() {
 }
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 struct InflateTimes {
-  double wait = 0, inflate = 0, host = 0, drain = 0;
+  double wait = 0, inflate = 0, host = 0, drain = 0, read = 0;
 };
 
 // The BGZF block list of a file (its headers walked in order; an untrusted
@@ -293,14 +343,12 @@ bqsr_status bgzf_blocks(const uint8_t* data, int64_t n, std::vector<BgzfBlk>& bl
 }
 
 // Inflate straight to the device: runs of whole blocks (at most kStageChunk
-// bytes inflated) are inflated by host threads into one cacheable run buffer
-// (reused: its pages are touched once), copied by the threads into the
-// context's pinned ring while this thread reads the run (`host(buf, off,
-// len)`, in stream order: the header, the records' block_size chain), and
-// DMA'd to d_out + its offset while the next run inflates.  No pageable copy
-// of the whole inflated stream (first-touching gigabytes of fresh pages was
-// most of a BAM parse), and no host reads of the pinned ring, which is not
-// host-cached (reading the chain from it took 0.6 s at 10M records).
+// bytes inflated) are inflated by host threads into the context's pinned
+// ring and each run is DMA'd to d_out + its offset, while one more thread
+// reads the previous run (`host(buf, off, len)`, in stream order: the
+// header, the records' block_size chain) and the threads inflate the next.
+// No pageable copy of the whole inflated stream: first-touching gigabytes of
+// fresh pages was most of a BAM parse.
 template <class Host>
 bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const std::vector<BgzfBlk>& blks,
                                 uint8_t* d_out, hipStream_t s, InflateTimes& T, Host&& host) {
@@ -308,9 +356,19 @@ bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const st
   bqsr_status st = stage_ring(ctx);
   if (st != BQSR_OK) return st;
   const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  std::unique_ptr<uint8_t[]> run(new (std::nothrow) uint8_t[kStageChunk]);
-  if (!run) return fail(BQSR_ERR_DEVICE, "BAM: no host memory for the inflate buffer");
-  uint8_t* cb = run.get();
+  const Deflate& D = Deflate::get();
+  std::thread reader;  // host() over the previous run
+  struct Join {
+    std::thread& t;
+    ~Join() {
+      if (t.joinable()) t.join();  // (every return path: a running reader is waited for)
+    }
+  } join_guard{reader};
+  bqsr_status rst = BQSR_OK;
+  double t_read = 0;
+  const auto join_reader = [&]() {
+    if (reader.joinable()) reader.join();
+  };
   size_t i = 0;
   int k = 0;
   while (i < blks.size()) {
@@ -319,28 +377,28 @@ bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const st
     while (j < blks.size() && len + blks[j].isize <= (int64_t)kStageChunk) len += blks[j++].isize;  // (isize <= 64 KiB)
     const int64_t dst0 = blks[i].dst;
     double t0 = now_s();
+    // the slot's previous run: DMA done and read (the reader of the run before
+    // this one's predecessor has been joined already, the predecessor's may run on)
+    HIP_TRY(hipEventSynchronize(ctx->stage_ev[k]));
+    double t1 = now_s();
+    T.wait += t1 - t0;
+    uint8_t* buf = ctx->stage[k];
     std::atomic<size_t> next{i};
     std::atomic<int> bad{0};
     auto work = [&]() {
+      void* dec = D.ok() ? D.alloc() : nullptr;
+      if (D.ok() && !dec) {
+        bad = 1;
+        return;
+      }
       for (size_t b; (b = next.fetch_add(1)) < j;) {
         const BgzfBlk& z = blks[b];
         if (z.isize == 0) continue;
-        z_stream zs{};
-        if (inflateInit2(&zs, -15) != Z_OK) {
+        // (the block's CRC32 of its uncompressed bytes: the 4 bytes before ISIZE)
+        if (!inflate_block(D, dec, data + z.src, z.csize, buf + (z.dst - dst0), z.isize, le32(data + z.src + z.csize)))
           bad = 1;
-          continue;
-        }
-        uint8_t* o = cb + (z.dst - dst0);
-        zs.next_in = (Bytef*)(data + z.src);
-        zs.avail_in = (uInt)z.csize;
-        zs.next_out = (Bytef*)o;
-        zs.avail_out = (uInt)z.isize;
-        const int rc = inflate(&zs, Z_FINISH);
-        const bool ok_len = rc == Z_STREAM_END && zs.total_out == (uLong)z.isize;
-        inflateEnd(&zs);
-        // the block's CRC32 of its uncompressed bytes (the 4 bytes before ISIZE)
-        if (!ok_len || crc32(0L, o, (uInt)z.isize) != le32(data + z.src + z.csize)) bad = 1;
       }
+      if (dec) D.free(dec);
     };
     {
       std::vector<std::thread> th;
@@ -348,43 +406,38 @@ bqsr_status bgzf_inflate_device(bqsr_context* ctx, const uint8_t* data, const st
       for (int t = 0; t < nw; ++t) th.emplace_back(work);
       for (auto& t : th) t.join();
     }
-    double t1 = now_s();
-    T.inflate += t1 - t0;
-    if (bad) {
-      (void)hipStreamSynchronize(s);
-      return fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate or fails its CRC32");
-    }
-    HIP_TRY(hipEventSynchronize(ctx->stage_ev[k]));  // the slot's previous DMA is done
     t0 = now_s();
-    T.wait += t0 - t1;
-    uint8_t* slot = ctx->stage[k];
-    {  // the run into the pinned slot (threads) while this thread reads it
-      std::vector<std::thread> th;
-      const int nc = (int)std::min<int64_t>(8, std::max<int64_t>(1, len >> 20));
-      for (int t = 0; t < nc; ++t)
-        th.emplace_back([&, t] {
-          const int64_t a = len * t / nc, e = len * (t + 1) / nc;
-          memcpy(slot + a, cb + a, (size_t)(e - a));
-        });
-      st = host(cb, dst0, len);
-      for (auto& t : th) t.join();
-    }
+    T.inflate += t0 - t1;
+    join_reader();  // the previous run's reader (stream order)
     T.host += now_s() - t0;
-    if (st != BQSR_OK) {
+    if (bad || rst != BQSR_OK) {
       (void)hipStreamSynchronize(s);
-      return st;
+      return rst != BQSR_OK ? rst : fail(BQSR_ERR_SAM_PARSE, "BAM: a BGZF block does not inflate or fails its CRC32");
     }
     if (len > 0) {
-      HIP_TRY(hipMemcpyAsync(d_out + dst0, slot, (size_t)len, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(d_out + dst0, buf, (size_t)len, hipMemcpyHostToDevice, s));
       HIP_TRY(hipEventRecord(ctx->stage_ev[k], s));
     }
+    reader = std::thread([&, buf, dst0, len] {
+      const double r0 = now_s();
+      rst = host(buf, dst0, len);
+      t_read += now_s() - r0;
+    });
     i = j;
     k ^= 1;
+    // the next run reuses slot k: its DMA (event) and its reader -- joined above
+    // before this run's reader started -- are both done once the event is
+  }
+  {
+    const double t0 = now_s();
+    join_reader();
+    T.host += now_s() - t0;
   }
   const double t0 = now_s();
   HIP_TRY(hipStreamSynchronize(s));
   T.drain += now_s() - t0;
-  return BQSR_OK;
+  T.read = t_read;
+  return rst;
 }
 
 // The BAM header (magic, SAM text, binary reference list) from the first m
@@ -452,6 +505,7 @@ struct RecScan {
     }
     while (p + 4 <= end) {
       if (p < off) return bad();  // (cannot happen: p passed a run's end only as a pending field)
+      __builtin_prefetch(buf + (p - off) + 2048);  // the chain's loads depend on each other: fetch ahead
       if (!field(le32(buf + (p - off)))) return bad();
     }
     for (int64_t q = std::max(p, off); q < end; ++q) pend[pend_n++] = buf[q - off];
@@ -580,9 +634,9 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   st = sam_parse_device(ctx, H, hdr.data(), d_text, n_text, s, true, out);  // (owns d_text from here)
   if (bam_timing())
     fprintf(stderr,
-            "[bam_parse] %lld reads, %.2f GB inflated: blocks %.3f, alloc %.3f, runs %.3f (slot waits %.3f, "
-            "inflate %.3f, copy + scan %.3f, drain %.3f), lines %.3f, SAM parse %.3f s\n",
-            (long long)nr, m / 1e9, t_blocks - t_start, t_alloc - t_blocks, t_inflated - t_alloc, IT.wait, IT.inflate,
-            IT.host, IT.drain, t_lines - t_inflated, now_s() - t_lines);
+            "[bam_parse] %lld reads, %.2f GB inflated (%s): blocks %.3f, alloc %.3f, runs %.3f (slot waits %.3f, "
+            "inflate %.3f, reader wait %.3f (reading %.3f), drain %.3f), lines %.3f, SAM parse %.3f s\n",
+            (long long)nr, m / 1e9, Deflate::get().ok() ? "libdeflate" : "zlib", t_blocks - t_start, t_alloc - t_blocks, t_inflated - t_alloc, IT.wait, IT.inflate,
+            IT.host, IT.read, IT.drain, t_lines - t_inflated, now_s() - t_lines);
   return st;
 }

@@ -6,5 +6,5 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 N=$1; shift
 cd "$R"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared "$@" \
-  -x hip adam_amd/csrc/bqsr_capi.cpp -o adam_amd/libadam_bqsr_$N.so -lpthread -lz
+  -x hip adam_amd/csrc/bqsr_capi.cpp -o adam_amd/libadam_bqsr_$N.so -lpthread -lz -ldl
 echo built adam_amd/libadam_bqsr_$N.so
