@@ -16,10 +16,11 @@ with the qual (and duplicateRead) columns replaced.
 Steps in Transform.run's order (:66-90): load (the SAM text parsed on the
 device, SAMRecordConverter semantics), MarkDuplicates (`adamMarkDuplicates`),
 BQSR (`adamBQSR(loadSnpTable)`: an empty SnpTable without -dbsnp_sites,
-:96-105), save.  The output is SAM text -- the input records with their QUAL
-fields replaced by the recalibrated strings (and FLAG 0x400 by MarkDuplicates'
-result) -- where the reference writes ADAM/Parquet (adamSave,
-core/rdd/AdamRDDFunctions.scala:37-56).  -sort_reads, -coalesce and
+:96-105), save.  The output is ADAMRecord Parquet part files, as the
+reference's adamSave writes them (core/rdd/AdamRDDFunctions.scala:37-56;
+OUTPUT.adam / .parquet / a directory), or SAM text -- the input records with
+their QUAL fields replaced by the recalibrated strings (and FLAG 0x400 by
+MarkDuplicates' result).  -sort_reads, -coalesce and
 -realignIndels are outside this build and are refused.
 
 Partitions: an input whose records exceed ``partition_bytes`` is cut at line
