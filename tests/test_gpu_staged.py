@@ -77,3 +77,45 @@ def test_staged_device_job(n_reads, lens, n_rg, seed):
         if th:
             L.bqsr_table_destroy(th)
         L.bqsr_batch_destroy(bh)
+
+
+@pytest.mark.parametrize("lens,with_sites", [((100,), False), ((100,), True), ((150, 250), True)])
+def test_bitmap_consumed_per_job(lens, with_sites):
+    """The observe kernel consumes the prep's slot bitmap (its zeroing for the
+    next atomic-form prep runs on a side stream right after it): every job of
+    a run of three on one batch equals the oracle's table, and a second
+    observe kernel without a prep stage between is refused."""
+    import torch
+    batch = synth.generate(20000, lens, 2, 11)
+    sites = synth.known_sites(2_000_000, seed=5) if with_sites else None
+    snp = bqsr.SnpTable(sites) if sites else None
+    d = bqsr.dims_of([batch])
+    ctx = bqsr.Context.get(0)
+    L = _capi.lib()
+    dev = torch.device("cuda", 0)
+    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    s, keep = batch.c_struct(batch.contig_ids_for(snp.contigs if snp else None))
+    bh, th = ctypes.c_void_p(), ctypes.c_void_p()
+    _capi.check(L.bqsr_batch_create(ctx.handle, ctypes.byref(s), sp, ctypes.byref(bh)))
+    sh = snp.handle(ctx) if snp else None
+    try:
+        words_t = torch.zeros(int(L.bqsr_table_words(d)), dtype=torch.int64, device=dev)
+        _capi.check(L.bqsr_table_create(ctx.handle, d, ctypes.c_void_p(words_t.data_ptr()), ctypes.byref(th)))
+        o = run_oracle([batch], sites)
+        for _ in range(3):
+            _capi.check(L.bqsr_table_zero_async(th, sp))
+            _capi.check(L.bqsr_observe_async(ctx.handle, bh, sh, th, sp))
+            em = ctypes.c_double()
+            _capi.check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
+            assert np.array_equal(words_t.cpu().numpy(), o.words)
+            assert em.value == o.em
+        _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_PREP, sp))
+        _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_KERNEL, sp))
+        with pytest.raises(_capi.BQSRError) as e:
+            _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_KERNEL, sp))
+        assert e.value.status == _capi.INVALID_ARG
+        torch.cuda.synchronize(dev)
+    finally:
+        if th:
+            L.bqsr_table_destroy(th)
+        L.bqsr_batch_destroy(bh)
