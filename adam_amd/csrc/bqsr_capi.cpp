@@ -365,14 +365,6 @@ struct bqsr_batch {
   uint32_t* d_work = nullptr;   // prep worklist (PrepParams::work), count at d_work[n_reads]
   uint64_t* d_bnd = nullptr;    // prep pass 1 wavefront-boundary shares (PrepParams::bnd)
   int64_t sbits_words = 0;
-  // the slot bitmap's zeroing for the next atomic-form prep, issued on a side
-  // stream as soon as the observe kernel has read it (early_zero)
-  hipStream_t zs = nullptr;
-  hipEvent_t ev_obs = nullptr, ev_zero = nullptr;
-  bool zero_pending = false;  // a zeroing is queued on zs: the next prep waits for ev_zero
-  bool sbits_zeroed = false;  // the bitmap is all zero (its zeroing done or waited for)
-  bool sbits_valid = false;   // the bitmap holds the last prep's bits (not yet consumed)
-  bool prep_atomic = false;   // the last prep ORed bits onto a zeroed bitmap
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
   // per-call scratch
@@ -421,12 +413,6 @@ struct bqsr_batch {
   int32_t pass_blocks() const { return bucketed && fronts > 0 ? n_keys : n_blocks; }
   uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
   ~bqsr_batch() {
-    if (zs) {
-      (void)hipStreamSynchronize(zs);
-      (void)hipStreamDestroy(zs);
-    }
-    for (hipEvent_t e : {ev_obs, ev_zero})
-      if (e) (void)hipEventDestroy(e);
     if (d_part) (void)hipFree(d_part);
     if (d_off64) (void)hipFree(d_off64);
     for (void* p : {(void*)k_qual, (void*)k_bases, (void*)d_kslot})
@@ -1373,14 +1359,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     // bitmap cost less (cfg2: 0.25 + 0.03 ms against 0.30)
     P.store_words = b->dims.max_len <= 128 && P.sites.n_contigs > 0;
     P.bnd = b->d_bnd;
-    if (b->zero_pending) {  // the last observe's bitmap zeroing (side stream) lands first
-      HIP_TRY(hipStreamWaitEvent(s, b->ev_zero, 0));
-      b->zero_pending = false;
-      b->sbits_zeroed = true;
-    }
-    if (!P.store_words && !b->sbits_zeroed) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
-    b->sbits_zeroed = false;
-    b->prep_atomic = !P.store_words;
+    if (!P.store_words) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.err = b->d_err;
@@ -1411,34 +1390,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     }
   }
   b->prepped = true;
-  b->sbits_valid = true;
   b->prep_sites = sites;
-  return BQSR_OK;
-}
-
-// After an observe kernel (the bitmap's only reader) of an atomic-form prep:
-// the bitmap's zeroing for the next prep goes on the batch's side stream,
-// where it overlaps the fold / finalize / apply of this job (the fold's chain
-// and finalize's groups are one workgroup each) instead of opening the next
-// job's prep (cfg2: 280 MB, ~40 us).  ADAM_BQSR_EARLY_ZERO=0: the prep zeroes.
-bool early_zero_off() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_EARLY_ZERO");
-    return e && strcmp(e, "0") == 0;
-  }();
-  return v;
-}
-bqsr_status early_zero(bqsr_batch* b, hipStream_t s) {
-  if (!b->prep_atomic || early_zero_off() || b->sbits_words == 0) return BQSR_OK;
-  if (!b->zs) HIP_TRY(hipStreamCreateWithFlags(&b->zs, hipStreamNonBlocking));
-  if (!b->ev_obs) HIP_TRY(hipEventCreateWithFlags(&b->ev_obs, hipEventDisableTiming));
-  if (!b->ev_zero) HIP_TRY(hipEventCreateWithFlags(&b->ev_zero, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(b->ev_obs, s));
-  HIP_TRY(hipStreamWaitEvent(b->zs, b->ev_obs, 0));
-  HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, b->zs));
-  HIP_TRY(hipEventRecord(b->ev_zero, b->zs));
-  b->zero_pending = true;
-  b->sbits_valid = false;  // consumed: another observe kernel needs another prep
   return BQSR_OK;
 }
 }  // namespace
@@ -1460,8 +1412,6 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   }
   if ((stages & BQSR_STAGE_KERNEL) && (!b->prepped || b->prep_sites != sites))
     return fail(BQSR_ERR_INVALID_ARG, "observe kernel before the prep stage (or with other known sites)");
-  if ((stages & BQSR_STAGE_KERNEL) && !b->sbits_valid)
-    return fail(BQSR_ERR_INVALID_ARG, "observe kernel without a prep stage since the last observe kernel");
   if (stages & BQSR_STAGE_KERNEL) {
     ObserveParams P{};
     P.rd = b->pass_rd();
@@ -1534,7 +1484,6 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     else
       hipLaunchKernelGGL(bqsr_observe_chunks, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     HIP_TRY(hipGetLastError());
-    if ((st = early_zero(b, s)) != BQSR_OK) return st;  // (the observe kernel is the bitmap's last reader)
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_base : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb, ry), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,

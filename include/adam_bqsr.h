@@ -281,10 +281,7 @@ enum { BQSR_STAGE_RESET = 1, BQSR_STAGE_KERNEL = 2, BQSR_STAGE_FOLD = 4, BQSR_ST
 /* observe stages: RESET clears the error word, PREP is the per-read prep
  * kernel (trimming, CIGAR/MD/known-site masks, validation), KERNEL the
  * observe kernel, FOLD the expectedMismatch fold (result at
- * bqsr_batch_em_device_ptr).  KERNEL consumes what PREP built (the slot
- * bitmap is cleared for the next job as soon as the kernel has read it):
- * each KERNEL needs a PREP since the last one (BQSR_ERR_INVALID_ARG
- * otherwise); bqsr_observe_async runs both. */
+ * bqsr_batch_em_device_ptr). */
 bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,
                                int32_t stages, void* stream);
 bqsr_status bqsr_observe_async(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, bqsr_table* t,

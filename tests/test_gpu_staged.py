@@ -79,15 +79,11 @@ def test_staged_device_job(n_reads, lens, n_rg, seed):
         L.bqsr_batch_destroy(bh)
 
 
-@pytest.mark.parametrize("lens,with_sites,consumed", [((100,), False, True), ((100,), True, False),
-                                                       ((150, 250), True, True)])
-def test_bitmap_consumed_per_job(lens, with_sites, consumed):
-    """The observe kernel consumes an atomic-form prep's slot bitmap (its
-    zeroing for the next prep runs on a side stream right after it; reads of
-    <= 128 bases with known sites take the word-store form, which needs no
-    zeroing): every job of a run of three on one batch equals the oracle's
-    table, and a second observe kernel without a prep stage between is
-    refused where the bitmap was consumed."""
+@pytest.mark.parametrize("lens,with_sites", [((100,), False), ((100,), True), ((150, 250), True)])
+def test_repeated_jobs_one_batch(lens, with_sites):
+    """Three jobs on one batch (the prep's slot bitmap rebuilt each time, by
+    atomics onto a zeroed bitmap or, reads of <= 128 bases with known sites,
+    by word stores) each equal the oracle's table and expectedMismatch."""
     import torch
     batch = synth.generate(20000, lens, 2, 11)
     sites = synth.known_sites(2_000_000, seed=5) if with_sites else None
@@ -112,15 +108,6 @@ def test_bitmap_consumed_per_job(lens, with_sites, consumed):
             _capi.check(L.bqsr_observe_result(bh, ctypes.byref(em), sp))
             assert np.array_equal(words_t.cpu().numpy(), o.words)
             assert em.value == o.em
-        _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_PREP, sp))
-        _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_KERNEL, sp))
-        if consumed:
-            with pytest.raises(_capi.BQSRError) as e:
-                _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_KERNEL, sp))
-            assert e.value.status == _capi.INVALID_ARG
-        else:
-            _capi.check(L.bqsr_observe_stage(ctx.handle, bh, sh, th, _capi.STAGE_KERNEL, sp))
-        torch.cuda.synchronize(dev)
     finally:
         if th:
             L.bqsr_table_destroy(th)
