@@ -600,18 +600,6 @@ __device__ __forceinline__ PrepCols prep_cols(const PrepParams& P, const PrepRec
   return c;
 }
 
-#ifdef ADAM_BQSR_SITE_PREFETCH
-// one bitmap word at a read's alignment start (0 without a bitmap)
-__device__ __forceinline__ uint32_t site_probe(const PrepParams& P, const PrepRec& x) {
-  const SitesDev& S = P.sites;
-  const int32_t c = x.a.contig;
-  if (c < 0 || c >= S.n_contigs) return 0u;
-  const int64_t nw = (int64_t)(S.bm_off[c + 1] - S.bm_off[c]);
-  const int64_t wi = (x.a.start - S.bm_base[c]) >> 6;
-  return (nw > 0 && wi >= 0 && wi < nw) ? (uint32_t)S.bm[S.bm_off[c] + wi] : 0u;
-}
-#endif
-
 #ifdef ADAM_BQSR_SITES_LDS
 // A/B build (tools/build_variant.sh sites_lds -DADAM_BQSR_SITES_LDS): the
 // north_star's known-site search staged in LDS.  On coordinate-sorted input a
@@ -940,22 +928,10 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
   const int64_t rt = c0 + threadIdx.x;
   PrepRec x0 = prep_rec(P, rt), x1 = prep_rec(P, rt + kPrepThreads);
   PrepCols k0 = prep_cols(P, x0);
-#ifdef ADAM_BQSR_SITE_PREFETCH
-  // A/B build (tools/build_variant.sh siteprefetch -DADAM_BQSR_SITE_PREFETCH):
-  // the known-site bitmap word at the next read's alignment start is loaded
-  // an iteration ahead, so its cache line is in when prep_fast reads the
-  // read's words (on shuffled input every read's words are a miss)
-  uint32_t pf0 = site_probe(P, x0);
-#endif
   for (int i = 0; i < kPrepChunk; i += kPrepThreads) {
     const int64_t r = rt + i;
     const PrepRec x2 = i + 2 * kPrepThreads < kPrepChunk ? prep_rec(P, r + 2 * kPrepThreads) : PrepRec{};
     const PrepCols k1 = i + kPrepThreads < kPrepChunk ? prep_cols(P, x1) : PrepCols{};
-#ifdef ADAM_BQSR_SITE_PREFETCH
-    const uint32_t pf1 = site_probe(P, x1);
-    asm volatile("" ::"v"(pf0));  // this read's probe has landed (issued an iteration ago)
-    pf0 = pf1;
-#endif
     uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
 #ifdef ADAM_BQSR_SITES_LDS
     const bool todo = r < n && !prep_fast<kStore>(P, r, x0, k0, acc, W);
