@@ -1787,6 +1787,16 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin) {
 // stages: BQSR_STAGE_RESET (apply-kernel error word, exception count),
 // BQSR_STAGE_KERNEL (apply kernel).  The prep kernel runs first when observe
 // has not run it on this batch.
+// bucketed batches: the per-read outputs by bqsr_apply_outs in read order
+// instead of the walk's scattered stores (A/B: ADAM_BQSR_APPLY_OUTS=walk|apart)
+static bool apply_outs_apart() {
+  static const bool v = [] {
+    const char* e = getenv("ADAM_BQSR_APPLY_OUTS");
+    return e && strcmp(e, "apart") == 0;
+  }();
+  return v;
+}
+
 bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
                              uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
                              int32_t stages, void* stream) {
@@ -1857,7 +1867,14 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   if (stages & BQSR_STAGE_KERNEL) {
     if (b->chars_lut != L) return fail(BQSR_ERR_INVALID_ARG, "apply kernel before the LUT stage of this LUT");
+    P.outs_apart = b->bucketed && apply_outs_apart();
     hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
+    if (P.outs_apart) {
+      ApplyParams Q = P;
+      Q.rd = b->rd;  // (read order: the batch's own qual column, where a read not yet trimmed is)
+      hipLaunchKernelGGL(bqsr_apply_outs, dim3((unsigned)std::min<int64_t>((b->rd.n_reads + 255) / 256, (int64_t)ctx->n_cu * 8)),
+                         dim3(256), 0, s, Q);
+    }
   }
   HIP_TRY(hipGetLastError());
   return ok();

@@ -309,6 +309,7 @@ struct ApplyParams {
   unsigned long long* n_exc;
   unsigned long long* err;
   int32_t lane_shift;  // lane-per-chunk kernel: log2(lanes per read)
+  int32_t outs_apart;  // the per-read outputs (out_start / out_len) by bqsr_apply_outs in read order, not the walk
   const uint8_t* chars;   // [n_keys][piece_stride] the pieces' char tables (bqsr_apply_chars)
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)

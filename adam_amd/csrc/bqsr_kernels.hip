@@ -2241,6 +2241,23 @@ constexpr int kApplyU = 4;  // chunks in flight per lane
 // A thread per entry; each workgroup of bqsr_apply_kernel then copies its
 // piece's table into LDS (it used to compute it itself: 65 us of a 0.87 ms
 // cfg2 launch with every workgroup repeating the same 156K entries).
+// The per-read outputs in read order (bucketed batches, ApplyParams::
+// outs_apart): the walk visits a piece's reads scattered over the batch, and
+// its two 4-B stores per read each cost a partial line; here a thread per
+// read, the stores coalesced.  Same values as the walk's fread.
+extern "C" __global__ void bqsr_apply_outs(ApplyParams P) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < P.rd.n_reads; r += (int64_t)gridDim.x * blockDim.x) {
+    const LaneRead x = lane_read(P.rd, P.info, r, true, P.g.L);
+    if (x.fl & kInfoPass) {  // quality string passed through
+      P.out_start[r] = 0;
+      P.out_len[r] = (uint32_t)x.en;
+    } else {
+      P.out_start[r] = (uint32_t)x.st;
+      P.out_len[r] = (x.fl & kInfoApp) ? (uint32_t)(x.en - x.st) : 0u;
+    }
+  }
+}
+
 extern "C" __global__ void bqsr_apply_chars(ApplyParams P, uint8_t* chars) {
   const int nk = order_base_keys(P.ord), qw = P.w.qw, q_lo = P.w.q_lo;
   const int64_t total = (int64_t)nk * P.piece_stride;
@@ -2326,7 +2343,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
     const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb, (int)clean_rows[0],
                         (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C};
     const auto fread = [&](LaneRead& x, bool live) {
-      if (!live) return;
+      if (!live || P.outs_apart) return;
       if (x.fl & kInfoPass) {  // quality string passed through
         P.out_start[x.ro] = 0;
         P.out_len[x.ro] = (uint32_t)x.en;
