@@ -1788,11 +1788,12 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin) {
 // BQSR_STAGE_KERNEL (apply kernel).  The prep kernel runs first when observe
 // has not run it on this batch.
 // bucketed batches: the per-read outputs by bqsr_apply_outs in read order
-// instead of the walk's scattered stores (A/B: ADAM_BQSR_APPLY_OUTS=walk|apart)
+// instead of the walk's scattered stores (cfg4: apply 3.95 -> 3.67 ms + 0.13
+// ms for the pass, profiles/r04aa_cfg4_apply_outs_ab.txt; ADAM_BQSR_APPLY_OUTS=walk: the walk's)
 static bool apply_outs_apart() {
   static const bool v = [] {
     const char* e = getenv("ADAM_BQSR_APPLY_OUTS");
-    return e && strcmp(e, "apart") == 0;
+    return !(e && strcmp(e, "walk") == 0);
   }();
   return v;
 }
