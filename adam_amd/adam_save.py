@@ -298,16 +298,41 @@ def adam_table(sam, r0: int, n: int, hdr: HeaderInfo, stream=None):
     return pa.table([cols[name] for name, _ in ADAM_FIELDS], names=[name for name, _ in ADAM_FIELDS])
 
 
+_PART_FILE = re.compile(r"^(part-r-\d{5}\.parquet|_SUCCESS|\.?part-r-\d{5}\.parquet\.crc|\._SUCCESS\.crc)$")
+
+
+def is_adam_output(path: str) -> bool:
+    """A directory holding nothing but adamSave part files (and _SUCCESS):
+    what AdamWriter may replace when asked to overwrite."""
+    if os.path.islink(path) or not os.path.isdir(path):
+        return False
+    for e in os.scandir(path):
+        if not (e.is_file(follow_symlinks=False) and _PART_FILE.match(e.name)):
+            return False
+    return True
+
+
 class AdamWriter:
     """adamSave's output: a directory of part files, written by host threads
     as the tables arrive (``OUT.partial`` renamed to ``OUT`` on ``close``)."""
 
-    def __init__(self, path: str, compression: str = "gzip", threads: Optional[int] = None):
+    def __init__(self, path: str, compression: str = "gzip", threads: Optional[int] = None,
+                 overwrite: bool = False):
         self.path = path
         self.tmp = path + ".partial"
+        # adamSave goes through Hadoop's FileOutputFormat, which refuses an
+        # existing output path (FileAlreadyExistsException).  overwrite=True
+        # replaces only what looks like an earlier adamSave output.
+        for p in (path, self.tmp):
+            if os.path.lexists(p):
+                if not overwrite:
+                    raise FileExistsError("output path %s already exists" % p)
+                if not is_adam_output(p):
+                    raise FileExistsError("refusing to replace %s: not an ADAM part-file directory" % p)
         if os.path.exists(self.tmp):
             shutil.rmtree(self.tmp)
         os.makedirs(self.tmp)
+        self.overwrite = overwrite
         self.compression = None if compression in (None, "none") else compression
         # gzip at zlib's default level 6 (parquet-mr's GzipCodec through Hadoop;
         # Arrow's own default is 9)
@@ -350,10 +375,12 @@ class AdamWriter:
             self.pool.shutdown(wait=True)
         if ok:
             open(os.path.join(self.tmp, "_SUCCESS"), "wb").close()
-            if os.path.isdir(self.path):
+            if os.path.lexists(self.path):
+                # (checked at __init__; checked again: the path may have appeared since)
+                if not (self.overwrite and is_adam_output(self.path)):
+                    shutil.rmtree(self.tmp, ignore_errors=True)
+                    raise FileExistsError("output path %s already exists" % self.path)
                 shutil.rmtree(self.path)
-            elif os.path.exists(self.path):
-                os.remove(self.path)
             os.replace(self.tmp, self.path)
         else:
             shutil.rmtree(self.tmp, ignore_errors=True)

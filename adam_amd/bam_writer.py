@@ -130,11 +130,20 @@ def sam_to_bam_parallel(text: bytes, workers: int = 16, progress=None) -> bytes:
     step = max(1, (len(body) + 4 * workers - 1) // (4 * workers))
     jobs = [(body[i:i + step], ref_id) for i in range(0, len(body), step)]
     out = [_bgzf(raw)[:-len(_EOF)]]
-    with get_context("fork").Pool(workers) as pool:
+    # close() + join() rather than the context manager's terminate(), which
+    # SIGTERMs workers that are still unwinding
+    pool = get_context("fork").Pool(workers)
+    try:
         for i, b in enumerate(pool.imap(_chunk_blocks, jobs)):
             out.append(b)
             if progress:
                 progress(i + 1, len(jobs))
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     out.append(_EOF)
     return b"".join(out)
 

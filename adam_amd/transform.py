@@ -47,6 +47,7 @@ import argparse
 import ctypes
 import mmap
 import os
+import shutil
 import sys
 import time
 from typing import Dict, List, Optional, Tuple
@@ -225,8 +226,22 @@ def is_parquet(path: str) -> bool:
         return False
 
 
+def _check_out(path: str, overwrite: bool, adam: bool) -> None:
+    """The output path must not exist (adamSave's FileOutputFormat refuses an
+    existing one); with overwrite, only a regular file, or (ADAM output) a
+    directory of nothing but part files, may be replaced."""
+    from .adam_save import is_adam_output
+    for p in (path, path + ".partial"):
+        if not os.path.lexists(p):
+            continue
+        if not overwrite:
+            raise FileExistsError("output path %s already exists" % p)
+        if os.path.isdir(p) and not (adam and is_adam_output(p)):
+            raise FileExistsError("refusing to replace directory %s" % p)
+
+
 def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
-                      dbsnp: Optional[str] = None, device: int = 0) -> Dict[str, float]:
+                      dbsnp: Optional[str] = None, device: int = 0, overwrite: bool = False) -> Dict[str, float]:
     """`transform` with ADAMRecord Parquet output (adamSave,
     core/rdd/AdamRDDFunctions.scala:37-56): the input -- Parquet (adamLoad,
     AdamContext.scala:318-331, every column kept and written back) or SAM
@@ -288,6 +303,9 @@ def _transform_table(A, table, batch, inp, out, mark_duplicates, recalibrate, db
         table = (table.set_column(table.column_names.index("qual"), "qual", qcol)
                  if "qual" in table.column_names else table.append_column("qual", qcol))
     tmp = out + ".partial"
+    _check_out(out, overwrite, True)
+    if os.path.isdir(out):
+        shutil.rmtree(out)
     pq.write_table(table, tmp)
     os.replace(tmp, out)
     stats["seconds"] = time.perf_counter() - t0
@@ -298,7 +316,8 @@ class _SamOut:
     """SAM text output (records appended partition by partition; the file
     appears when the job succeeds)."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str, overwrite: bool = False):
+        _check_out(path, overwrite, False)
         self.path = path
         self.tmp = path + ".partial"
         self.fh = open(self.tmp, "wb")
@@ -333,9 +352,9 @@ class _SamOut:
 class _AdamOut:
     """ADAM output (adamSave): part files of `part_reads` records each."""
 
-    def __init__(self, path: str, compression: str, part_reads: int):
+    def __init__(self, path: str, compression: str, part_reads: int, overwrite: bool = False):
         from .adam_save import AdamWriter
-        self.w = AdamWriter(path, compression)
+        self.w = AdamWriter(path, compression, overwrite=overwrite)
         self.part_reads = part_reads
 
     def emit(self, i, sam, quals=None):
@@ -382,18 +401,21 @@ def is_bam(data) -> bool:
 
 def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bool = False,
               dbsnp: Optional[str] = None, device: int = 0, partition_bytes: int = DEFAULT_PARTITION_BYTES,
-              compression: str = "gzip", part_reads: int = 1 << 19) -> Dict[str, float]:
+              compression: str = "gzip", part_reads: int = 1 << 19, overwrite: bool = False) -> Dict[str, float]:
     """Transform.run (cli/Transform.scala:62-97) over SAM or BAM input: the
     records parsed on the device (a BAM's records become SAM lines there),
     MarkDuplicates, BQSR, then adamSave (OUT.adam / .parquet / a directory:
     ADAMRecord Parquet part files, adam_save.py) or SAM text.  ADAM Parquet
     input goes through transform_parquet (Arrow reads it on the host)."""
     if is_parquet(inp):
-        return transform_parquet(inp, out, mark_duplicates, recalibrate, dbsnp, device)
+        return transform_parquet(inp, out, mark_duplicates, recalibrate, dbsnp, device, overwrite)
     t0 = time.perf_counter()
     ctx = bqsr.Context.get(device)
-    adam_out = out.endswith((".adam", ".parquet")) or os.path.isdir(out)
-    sink = _AdamOut(out, compression, part_reads) if adam_out else _SamOut(out)
+    # ADAM output by name, or over an earlier adamSave directory (never just
+    # because `out` is some existing directory: that is refused below)
+    from .adam_save import is_adam_output
+    adam_out = out.endswith((".adam", ".parquet")) or is_adam_output(out)
+    sink = _AdamOut(out, compression, part_reads, overwrite) if adam_out else _SamOut(out, overwrite)
     ok = False
     stats: Dict[str, float] = {}
     try:
@@ -465,11 +487,14 @@ def main(argv=None) -> int:
     ap.add_argument("-parquet_compression", default="gzip", choices=("gzip", "snappy", "zstd", "none"),
                     help="ADAM output: the part files' codec (adamSave's default: GZIP)")
     ap.add_argument("-part_reads", type=int, default=1 << 19, help="ADAM output: records per part file")
+    ap.add_argument("-overwrite", action="store_true",
+                    help="replace an existing output (a file, or a directory of ADAM part files only)")
     a = ap.parse_args(argv)
     if a.sort_reads or a.realignIndels or a.coalesce != -1:
         ap.error("-sort_reads / -coalesce / -realignIndels are outside this build")
     st = transform(a.input, a.output, a.mark_duplicate_reads, a.recalibrate_base_qualities, a.dbsnp_sites,
-                   partition_bytes=a.partition_bytes, compression=a.parquet_compression, part_reads=a.part_reads)
+                   partition_bytes=a.partition_bytes, compression=a.parquet_compression, part_reads=a.part_reads,
+                   overwrite=a.overwrite)
     print(" ".join("%s=%s" % kv for kv in st.items()), file=sys.stderr)
     return 0
 

@@ -42,11 +42,21 @@ def synthetic_sam(n_reads: int, read_len: int) -> bytes:
     (before the GPU is touched); QNAMEs unique per read"""
     from multiprocessing import get_context
     jobs = [(r0, min(CHUNK, n_reads - r0), read_len, n_reads) for r0 in range(0, n_reads, CHUNK)]
-    with get_context("fork").Pool(min(16, max(1, len(jobs)), os.cpu_count() or 1)) as pool:
+    # close() + join(), not the context manager: its terminate() SIGTERMs
+    # workers still unwinding (under rocprofv3 the signal handler prints an
+    # abort trace)
+    pool = get_context("fork").Pool(min(16, max(1, len(jobs)), os.cpu_count() or 1))
+    try:
         parts = []
         for i, t in enumerate(pool.imap(_chunk, jobs)):
             parts.append(t)
             log("slice %d / %d" % (i + 1, len(jobs)))
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     return b"".join(parts)
 
 
@@ -85,13 +95,15 @@ def main():
         # warm: the first call builds the context and loads pyarrow
         log("warm-up transform")
         T.transform(src, out, mark_duplicates=not a.no_markdup, recalibrate=True,
-                    partition_bytes=a.partition_bytes, compression=a.compression, part_reads=a.part_reads)
+                    partition_bytes=a.partition_bytes, compression=a.compression, part_reads=a.part_reads,
+                    overwrite=True)
         best = None
         for _ in range(a.reps):
             log("timed transform")
             t0 = time.perf_counter()
             st = T.transform(src, out, mark_duplicates=not a.no_markdup, recalibrate=True,
-                             partition_bytes=a.partition_bytes, compression=a.compression, part_reads=a.part_reads)
+                             partition_bytes=a.partition_bytes, compression=a.compression, part_reads=a.part_reads,
+                             overwrite=True)
             dt = time.perf_counter() - t0
             if best is None or dt < best[0]:
                 best = (dt, st)
