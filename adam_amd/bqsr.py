@@ -19,6 +19,7 @@ covariates on the CPU.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -47,6 +48,37 @@ class Context:
         if device not in cls._by_device:
             cls._by_device[device] = Context(device)
         return cls._by_device[device]
+
+    # bqsr_context_tune knobs (include/adam_bqsr.h): layout choices of the
+    # batches created afterwards, for tests and A/B runs; None = leave as is
+    _KNOBS = {"order": 1, "fronts": 2, "key_major": 3}
+    _DEFAULTS = {"order": -1, "fronts": -1, "key_major": 1}
+
+    def tune(self, **knobs) -> Dict[str, int]:
+        """Set layout knobs (order: -1 auto / 0 read / 1 read-group buckets;
+        fronts: -1 auto / 0 none / f; key_major: 1 / 0); returns the settings
+        they replace."""
+        cur = getattr(self, "_tuned", dict(self._DEFAULTS))
+        prev = {}
+        for k, v in knobs.items():
+            if v is None:
+                continue
+            if isinstance(v, str):
+                v = {"auto": -1, "read": 0, "group": 1}[v]
+            check(lib().bqsr_context_tune(self.handle, self._KNOBS[k], int(v)))
+            prev[k] = cur[k]
+            cur[k] = int(v)
+        self._tuned = cur
+        return prev
+
+    @contextlib.contextmanager
+    def tuned(self, **knobs):
+        """tune() for a block, the previous settings restored after it"""
+        prev = self.tune(**knobs)
+        try:
+            yield self
+        finally:
+            self.tune(**prev)
 
 
 class SnpTable:

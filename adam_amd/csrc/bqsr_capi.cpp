@@ -182,9 +182,9 @@ constexpr size_t kLdsMax = 163840;
 // [qw][wcells] x {obs, mm} + masked counts + block histogram, apply's char
 // table [qw][cw][21]
 // (the context table only for the chunk walk, bqsr_observe_chunks)
-size_t observe_lds(int qw, int wcells, bool table, int hq_span = 0) {
+size_t observe_lds(int qw, int wcells, bool table) {
   return (table ? (size_t)kCtxTabBytes : 0) + (size_t)qw * wcells * 8 + (size_t)qw * 4 + kQBins * 4 +
-         (size_t)kMkWords * 4 + (size_t)hq_span * qw * 4;
+         (size_t)kMkWords * 4;
 }
 // a piece's char table, rounded up to 16 B (the 16-B copy into LDS)
 int64_t piece_bytes(int qw, int cw) { return ((int64_t)qw * cw * kCtxSlots + 15) & ~(int64_t)15; }
@@ -199,32 +199,13 @@ int lean_orow(int nc, int cw) {
 size_t lean_lds(int qw, int orow, int wcells) { return ((size_t)qw * (orow + wcells) + qw + kQBins) * 4; }
 // copies of the lean window's counters: the most (<= 4) whose rows still hold the batch's qual span
 constexpr int kLeanCopiesMax = 4;
-int observe_rows(int wcells, bool table, int hq_span = 0) {
+int observe_rows(int wcells, bool table) {
   int qw = kQBins;
-  while (qw > 1 && observe_lds(qw, wcells, table, hq_span) > kLdsMax) --qw;
+  while (qw > 1 && observe_lds(qw, wcells, table) > kLdsMax) --qw;
   return qw;
 }
 // the host-packed layout is 16-aligned (ReadsDev::slots_aligned); device batches may be either
 constexpr bool align_slots() { return true; }
-// the fold's block histograms of front-ordered bucketed batches counted by the
-// observe kernel in LDS (ADAM_BQSR_FOLD_HIST=observe) instead of bqsr_fold_hist:
-// measured slower on cfg4 (the histograms take LDS rows from the window and add
-// a same-address-heavy atomic per base), kept as the A/B
-bool fold_hist_in_observe() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_FOLD_HIST");
-    return e && strcmp(e, "observe") == 0;
-  }();
-  return v;
-}
-// known sites as sorted lists only (no position bitmaps): ADAM_BQSR_SITES_BITMAP=0 (A/B)
-bool sites_bitmap_off() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_SITES_BITMAP");
-    return e && strcmp(e, "0") == 0;
-  }();
-  return v;
-}
 // Fronts of a bucketed batch (OrderDev::n_base), for the chunk-walk passes:
 // the sorted order becomes (front, read group, mate class), a front being a
 // contiguous share of the read indices, and each key a workgroup of its own.
@@ -236,12 +217,8 @@ bool sites_bitmap_off() {
 // CU (cfg4, 192 base keys: apply 5.7 -> 4.2 / 3.9 / 3.9 / 4.1 ms at 4 / 8 / 12
 // / 32 fronts, observe 4.4 -> 4.0 ms), pieces of at least 8192 reads; none
 // when that leaves fewer pieces than CUs or there are more base keys than 4
-// per CU.  ADAM_BQSR_FRONTS=f forces f fronts, 0 turns them off (A/B).
-int fronts(int n_base, int n_cu, int64_t n_reads) {
-  static const int forced = [] {
-    const char* e = getenv("ADAM_BQSR_FRONTS");
-    return e ? std::max(0, atoi(e)) : -1;
-  }();
+// per CU.  BQSR_TUNE_FRONTS forces f fronts, 0 turns them off (A/B, tests).
+int fronts(int n_base, int n_cu, int64_t n_reads, int forced) {
   if (forced == 0) return 0;
   int f = forced;
   if (f < 0) {
@@ -274,6 +251,10 @@ struct bqsr_context {
   std::mutex stage_mu;
   uint8_t* stage[2] = {nullptr, nullptr};
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  // bqsr_context_tune
+  int tune_order = -1;
+  int tune_fronts = -1;
+  int tune_keymajor = 1;
 };
 
 namespace {
@@ -386,7 +367,6 @@ struct bqsr_batch {
   int32_t n_keys = 1;   // n_base * fronts
   int32_t n_base = 1;   // 2 * read group + mate class
   int32_t fronts = 0;   // > 0: front-ordered pieces, a chunk-walk workgroup per key (OrderDev::n_base)
-  bool hq_by_observe = false;  // the last observe kernel built the fold's block histograms (fronts)
   uint32_t* d_perm = nullptr;
   int64_t* d_key_off = nullptr;
   uint32_t* d_key_cnt = nullptr;
@@ -481,6 +461,27 @@ const char* bqsr_status_name(bqsr_status s) {
   return kStatusNames[(int)s];
 }
 
+bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value) {
+  if (!ctx) return fail(BQSR_ERR_INVALID_ARG, "bqsr_context_tune: null context");
+  switch (knob) {
+    case BQSR_TUNE_ORDER:
+      if (value < -1 || value > 1) break;
+      ctx->tune_order = (int)value;
+      return BQSR_OK;
+    case BQSR_TUNE_FRONTS:
+      if (value < -1 || value > 4096) break;
+      ctx->tune_fronts = (int)value;
+      return BQSR_OK;
+    case BQSR_TUNE_KEYMAJOR:
+      if (value < 0 || value > 1) break;
+      ctx->tune_keymajor = (int)value;
+      return BQSR_OK;
+    default:
+      return fail(BQSR_ERR_INVALID_ARG, "bqsr_context_tune: unknown knob");
+  }
+  return fail(BQSR_ERR_INVALID_ARG, "bqsr_context_tune: value out of range");
+}
+
 bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (!out) return fail(BQSR_ERR_INVALID_ARG, "null out");
   HIP_TRY(hipSetDevice(device));
@@ -562,7 +563,7 @@ bqsr_status bqsr_sites_create(bqsr_context* ctx, const char* const* contigs, con
     // common path), unless it would hold over 64 words per site
     const int64_t b0 = v.empty() ? 0 : (int64_t)((uint64_t)base & ~(uint64_t)63);  // floor to 64
     const int64_t nw = v.empty() ? 0 : ((v.back() - b0) >> 6) + 1;
-    const bool dense = !sites_bitmap_off() && nw > 0 && nw <= 64 * (int64_t)v.size() + 64 && nw <= (int64_t(1) << 28);
+    const bool dense = nw > 0 && nw <= 64 * (int64_t)v.size() + 64 && nw <= (int64_t(1) << 28);
     if (dense) {
       const size_t w0 = bm.size();
       bm.resize(w0 + (size_t)nw, 0ull);
@@ -657,10 +658,9 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
     return st;
   // read-group buckets (OrderDev): on for several read groups, or when the
   // apply window over all cycle cells would leave more than 0.1% of the bases
-  // outside its qual rows (ADAM_BQSR_ORDER=read / group forces either)
-  const char* ord = getenv("ADAM_BQSR_ORDER");
-  if (ord) {
-    b->bucketed = strcmp(ord, "group") == 0;
+  // outside its qual rows (BQSR_TUNE_ORDER forces either)
+  if (b->ctx->tune_order >= 0) {
+    b->bucketed = b->ctx->tune_order == 1;
   } else {
     b->bucketed = b->dims.n_rg > 1;
     if (!b->bucketed && b->have_qhist) {
@@ -676,7 +676,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   }
   if (b->bucketed) {
     b->n_base = 2 * std::max<int32_t>(1, b->dims.n_rg);  // 2 * read group + mate class
-    b->fronts = fronts(b->n_base, b->ctx->n_cu, n);
+    b->fronts = fronts(b->n_base, b->ctx->n_cu, n, b->ctx->tune_fronts);
     b->n_keys = b->n_base * std::max(1, b->fronts);
     if ((st = dalloc(b->allocs, &b->d_perm, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
     if ((st = dalloc(b->allocs, &b->d_key_off, (size_t)b->n_keys + 1)) != BQSR_OK) return st;
@@ -694,16 +694,9 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
 // sequentially where the read-order layout scattered them over every key's
 // reads (cfg4: 96 read groups).  The batch's data must be on the device
 // (created from records or a parse; a staged batch uploads later and keeps
-// the per-job sort).  1.5 B a slot more HBM.  ADAM_BQSR_KEYMAJOR=0: off (A/B).
-bool key_major_off() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_KEYMAJOR");
-    return e && strcmp(e, "0") == 0;
-  }();
-  return v;
-}
+// the per-job sort).  1.5 B a slot more HBM.  BQSR_TUNE_KEYMAJOR 0: off (A/B).
 bqsr_status key_major_build(bqsr_batch* b, hipStream_t s) {
-  if (!b->bucketed || key_major_off() || !b->rd.slots_aligned || b->rd.n_reads == 0) return BQSR_OK;
+  if (!b->bucketed || !b->ctx->tune_keymajor || !b->rd.slots_aligned || b->rd.n_reads == 0) return BQSR_OK;
   const int64_t n = b->rd.n_reads;
   bqsr_context* ctx = b->ctx;
   // the piece order, once
@@ -1209,6 +1202,28 @@ int64_t bqsr_batch_bases(const bqsr_batch* b) { return b ? b->n_bases : -1; }
 int64_t bqsr_batch_slots(const bqsr_batch* b) { return b ? b->n_slots : -1; }
 bqsr_dims bqsr_batch_dims(const bqsr_batch* b) { return b ? b->dims : bqsr_dims{0, 0}; }
 
+// the per-batch layout work a bucketed batch pays once at creation (the
+// piece-key counting sort and the key-major copy, key_major_build), done
+// again: its wall time is what bench.py reports as layout_ms
+bqsr_status bqsr_batch_relayout(bqsr_batch* b, void* stream, double* ms) {
+  if (!b) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_relayout: null batch");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipStreamSynchronize(s));
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool has = b->perm_static && b->k_qual;
+  if (has) {
+    for (void* p : {(void*)b->k_qual, (void*)b->k_bases, (void*)b->d_kslot}) (void)hipFree(p);
+    b->k_qual = b->k_bases = nullptr;
+    b->d_kslot = nullptr;
+    b->perm_static = false;
+    bqsr_status st = key_major_build(b, s);
+    if (st != BQSR_OK) return st;
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  if (ms) *ms = has ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() : -1.0;
+  return ok();
+}
+
 // window override (exported for device batches whose quals the host never saw)
 bqsr_status bqsr_batch_set_window(bqsr_batch* b, int32_t q_lo, int32_t rg_lo) {
   if (!b || q_lo < 0 || q_lo >= kQBins || rg_lo < 0) return fail(BQSR_ERR_INVALID_ARG, "bad window");
@@ -1320,17 +1335,6 @@ int lane_shift(const bqsr_batch* b) {
   int s = 0;
   while ((1 << s) < c && s < 6) ++s;
   return s;
-}
-// the most fold blocks one front's reads span (wg_begin / wg_of of the kernels)
-int fold_span(const bqsr_batch* b) {
-  const int64_t n = b->rd.n_reads, rpt = b->rd.reads_per_tile, nt = b->rd.n_tiles, G = b->n_blocks;
-  auto blk = [&](int64_t r) { return std::min(G - 1, ((r / rpt + 1) * G - 1) / nt); };
-  int span = 1;
-  for (int64_t f = 0; f < b->fronts; ++f) {
-    const int64_t r0 = (f * n + b->fronts - 1) / b->fronts, r1 = ((f + 1) * n + b->fronts - 1) / b->fronts - 1;
-    if (r1 >= r0) span = std::max<int>(span, (int)(blk(r1) - blk(r0) + 1));
-  }
-  return span;
 }
 bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
   if (b->dims.n_rg > t->dims.n_rg || b->dims.max_len > t->dims.max_len)
@@ -1451,11 +1455,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       for (int q = 0; q < kQBins && P.rows_all; ++q)
         if (b->qhist[q] && (q < P.w.q_lo || q >= P.w.q_lo + P.w.qw)) P.rows_all = 0;
     } else {
-      // front-ordered pieces: the fold's block histograms from this kernel
-      // (a piece's reads lie in one front, whose fold blocks it counts in LDS)
-      P.n_fold = b->n_blocks;
-      P.hq_span = b->fronts > 0 && fold_hist_in_observe() ? fold_span(b) : 0;
-      P.w = window_rows(b, observe_rows(P.wcells, true, P.hq_span));
+      P.w = window_rows(b, observe_rows(P.wcells, true));
     }
     P.touched = t->touched();
     P.obs = t->obs();
@@ -1476,9 +1476,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.hq_block = b->d_hq;
     P.err = b->d_err + kErrObs;
     P.n_blocks = lean ? b->n_blocks : b->pass_blocks();  // (fronts: a chunk-walk workgroup per piece)
-    const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true, P.hq_span);
-    b->hq_by_observe = P.hq_span > 0;
-    if (b->hq_by_observe) HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
+    const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true);
     if (lean)
       hipLaunchKernelGGL(bqsr_observe_lean<true>, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     else
@@ -1491,7 +1489,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-    if (b->bucketed && !b->hq_by_observe) {  // the observe kernel did not count the fold's blocks: their histograms
+    if (b->bucketed) {  // the observe kernel did not walk the fold's blocks in read order: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
                          b->n_blocks, lane_shift(b), b->d_hq);
@@ -1789,14 +1787,7 @@ int32_t bqsr_phred_threshold_table(double* out, int32_t cap, int32_t* qmin) {
 // has not run it on this batch.
 // bucketed batches: the per-read outputs by bqsr_apply_outs in read order
 // instead of the walk's scattered stores (cfg4: apply 3.95 -> 3.67 ms + 0.13
-// ms for the pass, profiles/r04aa_cfg4_apply_outs_ab.txt; ADAM_BQSR_APPLY_OUTS=walk: the walk's)
-static bool apply_outs_apart() {
-  static const bool v = [] {
-    const char* e = getenv("ADAM_BQSR_APPLY_OUTS");
-    return !(e && strcmp(e, "walk") == 0);
-  }();
-  return v;
-}
+// ms for the pass, profiles/r04aa_cfg4_apply_outs_ab.txt)
 
 bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L, uint8_t* out_qual,
                              uint32_t* out_start, uint32_t* out_len, uint64_t* exceptions, int64_t max_exceptions,
@@ -1868,7 +1859,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   if (stages & BQSR_STAGE_KERNEL) {
     if (b->chars_lut != L) return fail(BQSR_ERR_INVALID_ARG, "apply kernel before the LUT stage of this LUT");
-    P.outs_apart = b->bucketed && apply_outs_apart();
+    P.outs_apart = b->bucketed;
     hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
     if (P.outs_apart) {
       ApplyParams Q = P;
@@ -2037,15 +2028,10 @@ bqsr_status bqsr_job_status_get(const bqsr_batch* b, int32_t slot, int32_t part,
 
 // workgroups of a kernel copy: enough stores in flight for the link, few
 // enough CUs that the compute streams' kernels keep running beside it
-// (ADAM_BQSR_COPY_BLOCKS, default 32: cfg5 374.8 / 402.9 / 407.0 ms per job
-// at 32 / 128 / 512 workgroups on one box, profiles/r03n_cfg3_sites_bitmap_ab.txt)
-static int64_t copy_blocks(const bqsr_context* ctx) {
-  static const int64_t v = [] {
-    const char* e = getenv("ADAM_BQSR_COPY_BLOCKS");
-    return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)32;
-  }();
-  return std::min<int64_t>(v, (int64_t)ctx->n_cu * 8);
-}
+// (32: cfg5 374.8 / 402.9 / 407.0 ms per job at 32 / 128 / 512 workgroups on
+// one box, profiles/r03n_cfg3_sites_bitmap_ab.txt; 16-64 within the spread,
+// profiles/r04u_cfg5_copy_blocks_ab.txt)
+static int64_t copy_blocks(const bqsr_context* ctx) { return std::min<int64_t>(32, (int64_t)ctx->n_cu * 8); }
 bqsr_status bqsr_copy_async(bqsr_context* ctx, void* dst, const void* src, int64_t bytes, void* stream) {
   if (!ctx || bytes < 0 || (bytes && (!dst || !src))) return fail(BQSR_ERR_INVALID_ARG, "bqsr_copy_async: bad arguments");
   if (!bytes) return ok();

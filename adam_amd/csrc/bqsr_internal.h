@@ -208,8 +208,8 @@ struct ObserveParams {
   int64_t* mm;       // [K*cells]
   uint32_t* part;      // [n_blocks + n_keys - 1][part_stride] per-piece window counts (obs, mm, touched)
   int32_t part_stride; // 2*qw*wcells + qw, wcells = WinGeom::cw + 21
-  uint32_t* hq_block;  // [n_fold][128] per-block qual histogram of folded bases (identity order; bucketed
-                       // batches: from observe_chunks with hq_span, else bqsr_fold_hist)
+  uint32_t* hq_block;  // [n_blocks][128] per-block qual histogram of folded bases (identity order; bucketed
+                       // batches: bqsr_fold_hist)
   unsigned long long* err;
   int32_t n_blocks;
   int32_t wcells;      // window row length: WinGeom::cw + 21
@@ -217,9 +217,6 @@ struct ObserveParams {
   int32_t orow;        // bqsr_observe_lean: LDS obs row words (nc copies of the cycle and 43 context cells), 2 mod 4
   int32_t nc;          // bqsr_observe_lean: copies of a row's counters (<= 4)
   int32_t rows_all;    // bqsr_observe_lean: every qual of the batch is a window row (host histogram)
-  int32_t n_fold;      // the fold's blocks (hq_block rows)
-  int32_t hq_span;     // > 0: bqsr_observe_chunks on front-ordered pieces builds hq_block itself, with
-                       // LDS histograms of hq_span fold blocks x qw rows per piece (no bqsr_fold_hist)
 };
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----

@@ -600,41 +600,10 @@ __device__ __forceinline__ PrepCols prep_cols(const PrepParams& P, const PrepRec
   return c;
 }
 
-#ifdef ADAM_BQSR_SITES_LDS
-// A/B build (tools/build_variant.sh sites_lds -DADAM_BQSR_SITES_LDS): the
-// north_star's known-site search staged in LDS.  On coordinate-sorted input a
-// prep workgroup's 2048 reads cover a few kb of one contig; its slice of the
-// sorted site list goes to LDS once and each read binary-searches it
-// (SnpTable.isMaskedAtReadOffset, SnpTable.scala:15-23); reads outside the
-// slice (unsorted input, another contig) take the position bitmap.
-constexpr int kSiteLds = 4096;
-struct SiteWin {
-  const int64_t* s;  // LDS: the sites in [lo, hi) of `contig`
-  int n;             // < 0: no window
-  int contig;
-  int64_t lo, hi;
-};
-__device__ __forceinline__ bool sites_lds_acc(const SiteWin& W, int32_t contig, int64_t unclipped, int lq, uint32_t r0,
-                                              uint64_t acc[kAccWords]) {
-  const int64_t a = unclipped, b = unclipped + lq;
-  if (W.n < 0 || contig != W.contig || a < W.lo || b > W.hi) return false;
-  int lo = 0, hi = W.n;  // first site >= a
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (W.s[mid] < a) lo = mid + 1; else hi = mid;
-  }
-  for (int j = lo; j < W.n && W.s[j] < b; ++j) acc_bit(acc, r0 + (uint32_t)(W.s[j] - unclipped), 0);
-  return true;
-}
-#endif
 
 template <bool kStore>
 __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, const PrepCols& cols,
-                          uint64_t acc_out[kAccWords]
-#ifdef ADAM_BQSR_SITES_LDS
-                          , const SiteWin& W
-#endif
-                          ) {
+                          uint64_t acc_out[kAccWords]) {
   const ReadMeta m = x.m;
   const ReadAlign a = x.a;
   const uint16_t f = m.flags;
@@ -737,9 +706,6 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
       }
       bool linear = false;
       if (a.contig >= 0 && a.contig < P.sites.n_contigs) {
-#ifdef ADAM_BQSR_SITES_LDS
-        if (!sites_lds_acc(W, a.contig, unclipped, en, r0, acc))
-#endif
         if (!sites_bitmap_acc(P, a.contig, unclipped, en, r0, acc)) linear = true;
       }
       if (kStore) {
@@ -877,52 +843,6 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
   const int64_t n = P.rd.n_reads;
   const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
   const int lane = threadIdx.x & 63;
-#ifdef ADAM_BQSR_SITES_LDS
-  __shared__ int64_t s_sites[kSiteLds];
-  __shared__ SiteWin s_win;
-  if (threadIdx.x == 0) {
-    SiteWin w{s_sites, -1, -1, 0, 0};
-    const int64_t last = min(n, c0 + kPrepChunk) - 1;
-    if (P.sites.n_contigs > 0 && c0 <= last) {
-      // the window between the first and the last read's starts (+ a read's reach either side)
-      const ReadAlign fa = P.rd.align[c0], la = P.rd.align[last];
-      if (fa.contig == la.contig && fa.contig >= 0 && fa.contig < P.sites.n_contigs && la.start >= fa.start &&
-          la.start - fa.start < (int64_t)1 << 24) {
-        const int64_t lo = fa.start - kMaxReadLen, hi = la.start + 2 * kMaxReadLen;
-        const int64_t* sp = P.sites.pos + P.sites.off[fa.contig];
-        const int64_t ns = (int64_t)(P.sites.off[fa.contig + 1] - P.sites.off[fa.contig]);
-        int64_t a = 0, b = ns;  // first >= lo
-        while (a < b) {
-          const int64_t m = (a + b) >> 1;
-          if (sp[m] < lo) a = m + 1; else b = m;
-        }
-        int64_t e = a, f = ns;  // first >= hi
-        while (e < f) {
-          const int64_t m = (e + f) >> 1;
-          if (sp[m] < hi) e = m + 1; else f = m;
-        }
-        if (e - a <= kSiteLds) w = SiteWin{s_sites, (int)(e - a), fa.contig, lo, hi};
-        s_win = w;
-        s_win.lo = a;  // (the copy's source index, restored below)
-      } else {
-        s_win = w;
-      }
-    } else {
-      s_win = w;
-    }
-  }
-  __syncthreads();
-  if (s_win.n > 0) {
-    const int64_t* sp = P.sites.pos + P.sites.off[s_win.contig] + s_win.lo;
-    for (int i = threadIdx.x; i < s_win.n; i += blockDim.x) s_sites[i] = sp[i];
-  }
-  __syncthreads();
-  SiteWin W = s_win;
-  if (W.n >= 0) {  // the window's bounds again (lo held the copy's source index)
-    const ReadAlign fa = P.rd.align[c0];
-    W.lo = fa.start - kMaxReadLen;
-  }
-#endif
   // software pipeline: the record of the read two iterations ahead and the
   // CIGAR / MD of the next one load while this one is worked
   const int64_t rt = c0 + threadIdx.x;
@@ -933,11 +853,7 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
     const PrepRec x2 = i + 2 * kPrepThreads < kPrepChunk ? prep_rec(P, r + 2 * kPrepThreads) : PrepRec{};
     const PrepCols k1 = i + kPrepThreads < kPrepChunk ? prep_cols(P, x1) : PrepCols{};
     uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
-#ifdef ADAM_BQSR_SITES_LDS
-    const bool todo = r < n && !prep_fast<kStore>(P, r, x0, k0, acc, W);
-#else
     const bool todo = r < n && !prep_fast<kStore>(P, r, x0, k0, acc);
-#endif
     if (kStore) {
       if (todo) {
 #pragma unroll
@@ -959,11 +875,6 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel
   __syncthreads();
   const uint32_t k = cnt;
   if (!kStore) {
-#ifdef ADAM_BQSR_PREP_PROBE  // timing probe build only (wrong results): the listed reads' share of prep,
-    // each listed read passed through instead (a valid ReadInfo for the later passes)
-    for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads) P.info[list[i]] = ReadInfo{0, 0, kInfoPass, 0};
-    return;
-#endif
     for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads)
       prep_one(P, (int64_t)list[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
     return;
@@ -1407,23 +1318,6 @@ __device__ __forceinline__ void lds_add(uint32_t addr, uint32_t v) {
   __hip_atomic_fetch_add((LdsWords)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-#ifdef ADAM_BQSR_WAVE_AGG
-// Wavefront-level aggregation before the LDS atomics (the north_star's form;
-// built only into the A/B library, tools/gpu_r04_agg.sh): the lanes adding 1
-// to one LDS word become one add of their count, by the first of them -- a
-// ballot round per distinct address among the pending lanes.
-__device__ __forceinline__ void lds_add_agg(uint32_t addr, bool on) {
-  const int lane = threadIdx.x & 63;
-  uint64_t todo = __builtin_amdgcn_ballot_w64(on);
-  while (todo) {
-    const int leader = (int)__builtin_ctzll(todo);
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)addr, leader);
-    const uint64_t m = __builtin_amdgcn_ballot_w64(((todo >> lane) & 1u) && addr == a);
-    if (lane == leader) lds_add(a, (uint32_t)__builtin_popcountll(m));
-    todo &= ~m;
-  }
-}
-#endif
 
 // Lane per chunk (chunk_walk): the same counts, each lane one 16-offset
 // chunk of the wavefront's reads laid end to end.  LDS: the window as in
@@ -1452,8 +1346,6 @@ struct ObsPiece {
   int rg_w, c_lo, cw, q_lo, qw, wcells;
   bool ident;
   uint32_t tb;  // LDS address of the context table
-  uint32_t* fh;  // front-ordered pieces: the fold blocks' qual histograms [hq_span][qw] (x.aux = block - blk0)
-  int blk0;      // the front's first fold block
 };
 
 __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsPiece& pc, const LaneRead& x, int j,
@@ -1487,22 +1379,10 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
       const bool f = (unsigned)row < (unsigned)pc.qw && ((vmask >> k) & 1u);
       const bool m = (bm >> k) & 1u;
       const int base = __mul24(row, pc.wcells);
-#ifdef ADAM_BQSR_WAVE_AGG
-      {
-        const uint32_t a1 = (uint32_t)(uintptr_t)(LdsWords)(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k]);
-        const uint32_t a2 = (uint32_t)(uintptr_t)(LdsWords)&pc.w_obs[base + pc.cw +
-                                                                   (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)];
-        lds_add_agg(a1, f);
-        lds_add_agg(a2, f && !m);
-        if (pc.fh) lds_add_agg((uint32_t)(uintptr_t)(LdsWords)&pc.fh[__mul24(x.aux, pc.qw) + row], f);
-      }
-#else
       if (f) {
         atomicAdd(m ? &pc.w_masked[row] : &pc.w_obs[base + wc0 + x.dir * k], 1u);
         if (!m) atomicAdd(&pc.w_obs[base + pc.cw + (int)__builtin_amdgcn_ubfe(xo[k >> 2], 8 * (k & 3), 8)], 1u);
-        if (pc.fh) atomicAdd(&pc.fh[__mul24(x.aux, pc.qw) + row], 1u);  // the fold's block histogram
       }
-#endif
       fastm |= (uint32_t)f << k;
     }
   }
@@ -1533,7 +1413,6 @@ __device__ __forceinline__ void observe_chunk(const ObserveParams& P, const ObsP
         const int ccell = cc0 + __mul24(x.dir, k);
         const int xcell = C + (int)(((k < 8 ? x01 : x23) >> (8 * (k & 7))) & 0xFFu);
         if (pc.ident) atomicAdd(&pc.blk_hist[q], 1u);
-        if (pc.fh) atomicAdd(&P.hq_block[(int64_t)(pc.blk0 + x.aux) * kQBins + q], 1u);
         const int64_t key = (int64_t)q + (int64_t)kMaxQ * x.rg;
         atomicAdd((unsigned long long*)&P.touched[key], 1ull);
         if (!masked) {
@@ -1561,7 +1440,6 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
   uint32_t* mk_all = blk_hist + kQBins;
-  uint32_t* fh = P.hq_span > 0 ? mk_all + kMkWords : nullptr;  // [hq_span][qw]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint32_t* mk = mk_all + wave * 64;
@@ -1577,42 +1455,20 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
     if (p0 >= wb) break;
     if (p0 >= p1) continue;
     const WinGeom gm = win_geom(P.ord, P.g, key);
-    // front-ordered pieces (fronts of read indices, bqsr_capi.cpp fronts()): the
-    // piece's reads lie in its front, whose fold blocks' histograms it keeps in
-    // LDS -- the fold then needs no pass of its own over the quals
-    int blk0 = 0;
-    if (fh) {
-      const int64_t nf = P.ord.n_keys / P.ord.n_base, f = key / P.ord.n_base;
-      blk0 = (int)wg_of(P.rd, (f * P.rd.n_reads + nf - 1) / nf, P.n_fold);
-      for (int i = tid; i < P.hq_span * qw; i += blockDim.x) fh[i] = 0;
-    }
     const ObsPiece pc{w_obs, w_mm, w_masked, blk_hist, key_rg(P.ord, key, P.w.rg_lo), gm.c_lo, gm.cw, P.w.q_lo, qw,
-                      wcells, ident, (uint32_t)(uintptr_t)(LdsHalves)ctab, fh, blk0};
+                      wcells, ident, (uint32_t)(uintptr_t)(LdsHalves)ctab};
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
     const auto fread = [&](LaneRead& x, bool live) {
       if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
-      if (fh && live) x.aux = (int)wg_of(P.rd, x.r, P.n_fold) - blk0;  // the read's fold block, in the front
     };
     const auto fload = [&](const LaneRead& x, int j, bool on) { return observe_load(P, x, j, on); };
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) {
       observe_chunk(P, pc, x, j, n, on, ld);
     };
-    if (fh)
-      chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, true>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
-                                                                           64 * kWaves, L, lane, mk, fread, fload,
-                                                                           fchunk);
-    else
-      chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
-                                                                            64 * kWaves, L, lane, mk, fread, fload,
-                                                                            fchunk);
+    chunk_walk<kInfoObs | kInfoObsCheck, kObserveU, ObsChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
+                                                                          64 * kWaves, L, lane, mk, fread, fload, fchunk);
     __syncthreads();
-    if (fh)  // the fold blocks' histograms of this piece: one atomic per non-zero bin
-      for (int i = tid; i < P.hq_span * qw; i += blockDim.x) {
-        const uint32_t v = fh[i];
-        const int b = blk0 + i / qw, q = P.w.q_lo + i % qw;
-        if (v && b < P.n_fold) atomicAdd(&P.hq_block[(int64_t)b * kQBins + q], v);
-      }
     // ---- the piece's window -> its slab; window rows into the block histogram ----
     uint32_t* pb = P.part + (int64_t)(blockIdx.x + (ident ? 0 : key)) * P.part_stride;
     for (int i = tid; i < 2 * qw * wcells; i += blockDim.x) pb[i] = w_obs[i];

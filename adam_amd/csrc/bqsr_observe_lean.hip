@@ -73,13 +73,8 @@ __device__ __forceinline__ void lean_clean(const uint32_t q[4], const uint32_t x
     const uint32_t qv = __builtin_amdgcn_ubfe(q[p >> 2], 8 * (p & 3), 8);
     const uint32_t xs4 = __builtin_amdgcn_ubfe(xo[p >> 2], 8 * (p & 3), 8);
     const uint32_t rq = __mul24(qv, o4);
-#ifdef ADAM_BQSR_WAVE_AGG
-    lds_add_agg(rq + a_cyc + 4u * (uint32_t)p, true);
-    lds_add_agg(rq + xs4 + a_ctx, true);
-#else
     __hip_atomic_fetch_add((LdsU32)(uintptr_t)(rq + a_cyc) + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_fetch_add((LdsU32)(uintptr_t)(rq + xs4 + a_ctx), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
   }
   uint32_t mk = bm | bx;
   if (__builtin_amdgcn_ballot_w64(mk != 0)) {

@@ -96,6 +96,19 @@ class ResidentJob:
     def _ptr(self, t):
         return ctypes.c_void_p(t.data_ptr())
 
+    def layout_ms(self, reps: int = 3):
+        """Wall time (ms, mean of reps) of the layout a bucketed batch builds
+        once at creation -- piece-key sort, key-major copy -- redone on this
+        batch (bqsr_batch_relayout); None for a batch without one."""
+        ms = []
+        for _ in range(reps):
+            v = ctypes.c_double()
+            check(self.L.bqsr_batch_relayout(self.bh, self.sp, ctypes.byref(v)))
+            if v.value < 0:
+                return None
+            ms.append(v.value)
+        return sum(ms) / len(ms)
+
     def step(self, record: bool = False):
         """One job.  record: bracket the stages with timing events (each event
         record costs the stream ~30 us on this runtime, so callers sample)."""

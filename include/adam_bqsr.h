@@ -135,6 +135,17 @@ const char* bqsr_status_name(bqsr_status s);
 bqsr_status bqsr_context_create(int device, bqsr_context** out);
 void bqsr_context_destroy(bqsr_context* ctx);
 
+/* Layout knobs of a context, for tests and A/B measurements (no reference
+ * counterpart; results are identical under every setting).  They take effect
+ * on batches created afterwards.  The defaults are the measured choices
+ * (DESIGN.md §3).
+ *   BQSR_TUNE_ORDER     -1 auto (read-group buckets for several read groups
+ *                        or quals beyond one window), 0 read order, 1 buckets
+ *   BQSR_TUNE_FRONTS    -1 auto, 0 none, f > 0: f fronts of bucketed batches
+ *   BQSR_TUNE_KEYMAJOR   1 key-major copy of bucketed batches (default), 0 off */
+enum { BQSR_TUNE_ORDER = 1, BQSR_TUNE_FRONTS = 2, BQSR_TUNE_KEYMAJOR = 3 };
+bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value);
+
 /* ---- known sites (SnpTable.apply(File) + broadcast, SnpTable.scala:32-47,
  *      AdamRDDFunctions.scala:105) ------------------------------------------ */
 /* positions are the VCF POS values exactly as stored (no -1: quirk Q7).  Each
@@ -151,6 +162,10 @@ void bqsr_batch_destroy(bqsr_batch* b);
 int64_t bqsr_batch_reads(const bqsr_batch* b);
 int64_t bqsr_batch_bases(const bqsr_batch* b);
 bqsr_dims bqsr_batch_dims(const bqsr_batch* b);
+/* Measurement: redo the layout a bucketed batch builds once at creation
+ * (piece-key sort, key-major copy of quals and codes) and report its wall
+ * time in *ms (-1: the batch has no such layout).  Synchronous on `stream`. */
+bqsr_status bqsr_batch_relayout(bqsr_batch* b, void* stream, double* ms);
 
 /* Caller-owned device buffers already in the packed layout (used by the
  * benchmark, which synthesises reads directly in HBM).  Layout documented in

@@ -77,12 +77,14 @@ def test_synthetic_many_read_groups_mixed_lengths():
 
 
 @pytest.fixture
-def read_order(request, monkeypatch):
-    """ADAM_BQSR_ORDER: 'read' = the per-base passes walk reads in batch order,
-    'group' = bucketed by read group (device counting sort, pieces per read
-    group); the library picks 'group' for several read groups by default."""
-    monkeypatch.setenv("ADAM_BQSR_ORDER", request.param)
-    return request.param
+def read_order(request):
+    """BQSR_TUNE_ORDER (bqsr_context_tune): 'read' = the per-base passes walk
+    reads in batch order, 'group' = bucketed by read group (device counting
+    sort, pieces per read group); the library picks 'group' for several read
+    groups by default."""
+    from adam_amd import bqsr as _b
+    with _b.Context.get(0).tuned(order=request.param):
+        yield request.param
 
 
 @pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
