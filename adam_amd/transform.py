@@ -250,6 +250,7 @@ def transform_parquet(inp: str, out: str, mark_duplicates: bool = False, recalib
     column all built there; the qual (and duplicateRead) columns replaced."""
     from . import parquet as P
     from .records import RecordBatch, read_sam_records
+    _check_out(out, overwrite, True)
     t0 = time.perf_counter()
     batch = None
     A = None
@@ -303,8 +304,7 @@ def _transform_table(A, table, batch, inp, out, mark_duplicates, recalibrate, db
         table = (table.set_column(table.column_names.index("qual"), "qual", qcol)
                  if "qual" in table.column_names else table.append_column("qual", qcol))
     tmp = out + ".partial"
-    _check_out(out, overwrite, True)
-    if os.path.isdir(out):
+    if os.path.isdir(out):  # (transform_parquet checked it: overwrite of a part-file directory)
         shutil.rmtree(out)
     pq.write_table(table, tmp)
     os.replace(tmp, out)
@@ -410,12 +410,16 @@ def transform(inp: str, out: str, mark_duplicates: bool = False, recalibrate: bo
     if is_parquet(inp):
         return transform_parquet(inp, out, mark_duplicates, recalibrate, dbsnp, device, overwrite)
     t0 = time.perf_counter()
-    ctx = bqsr.Context.get(device)
     # ADAM output by name, or over an earlier adamSave directory (never just
-    # because `out` is some existing directory: that is refused below)
+    # because `out` is some existing directory: the sinks refuse that)
     from .adam_save import is_adam_output
     adam_out = out.endswith((".adam", ".parquet")) or is_adam_output(out)
     sink = _AdamOut(out, compression, part_reads, overwrite) if adam_out else _SamOut(out, overwrite)
+    try:
+        ctx = bqsr.Context.get(device)
+    except BaseException:
+        sink.close(False)
+        raise
     ok = False
     stats: Dict[str, float] = {}
     try:

@@ -86,3 +86,20 @@ def test_transform_sinks_refuse_directories(tmp_path):
     s = T._SamOut(str(f), overwrite=True)
     s.close(True)
     assert f.read_bytes() == b""
+
+
+def test_transform_refuses_before_any_work(tmp_path):
+    # the output check comes first: no parse, no device (this runs on CPU)
+    from adam_amd import transform as T
+    d = tmp_path / "results"
+    d.mkdir()
+    (d / "keep").write_text("k")
+    src = tmp_path / "in.sam"
+    src.write_text("@HD\tVN:1.4\n")
+    with pytest.raises(FileExistsError):
+        T.transform(str(src), str(d), recalibrate=True)
+    pq_in = tmp_path / "in.parquet"
+    pq_in.write_bytes(b"PAR1")
+    with pytest.raises(FileExistsError):
+        T.transform(str(pq_in), str(d), recalibrate=True, overwrite=True)
+    assert sorted(os.listdir(d)) == ["keep"]
