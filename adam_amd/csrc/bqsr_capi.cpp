@@ -196,7 +196,7 @@ int lean_orow(int nc, int cw) {
   while ((o & 3) != 2) ++o;
   return o;
 }
-size_t lean_lds(int qw, int orow, int wcells) { return ((size_t)qw * (orow + wcells) + qw + kQBins) * 4; }
+size_t lean_lds(int qw, int orow, int wcells) { return ((size_t)qw * (orow + wcells) + qw + kQBins + 1) * 4; }
 // copies of the lean window's counters: the most (<= 4) whose rows still hold the batch's qual span
 constexpr int kLeanCopiesMax = 4;
 int observe_rows(int wcells, bool table) {
@@ -255,6 +255,7 @@ struct bqsr_context {
   int tune_order = -1;
   int tune_fronts = -1;
   int tune_keymajor = 1;
+  int tune_fused = 0;
 };
 
 namespace {
@@ -348,6 +349,9 @@ struct bqsr_batch {
   int64_t sbits_words = 0;
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
+  // the prep of this job runs inside the observe kernel (bqsr_observe_lean
+  // kLeanFused + kLeanList), which the KERNEL stage launches next
+  bool fused_pending = false;
   // per-call scratch
   uint32_t* d_hq = nullptr;        // [n_blocks][128] fold blocks' qual histograms
   FoldParams fold{};               // the fold's device buffers (FoldParams)
@@ -476,6 +480,10 @@ bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value) {
       if (value < 0 || value > 1) break;
       ctx->tune_keymajor = (int)value;
       return BQSR_OK;
+    case BQSR_TUNE_FUSED_PREP:
+      if (value < 0 || value > 1) break;
+      ctx->tune_fused = (int)value;
+      return BQSR_OK;
     default:
       return fail(BQSR_ERR_INVALID_ARG, "bqsr_context_tune: unknown knob");
   }
@@ -499,7 +507,8 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   for (const void* f : {(const void*)bqsr_apply_kernel, (const void*)bqsr_observe_chunks,
-                        (const void*)bqsr_observe_lean<true>})
+                        (const void*)bqsr_observe_lean<true, kLeanPlain>,
+                        (const void*)bqsr_observe_lean<true, kLeanFused>, (const void*)bqsr_observe_lean<true, kLeanList>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -654,7 +663,8 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_bnd, (size_t)2 * (size_t)(n / 64 + kPrepChunk / 64 + 1))) != BQSR_OK) return st;
-  if ((st = dalloc(b->allocs, &b->d_work, (size_t)(n + kPrepChunk) + (size_t)(n / kPrepChunk + 1))) != BQSR_OK)
+  if ((st = dalloc(b->allocs, &b->d_work,
+                   (size_t)(n + kPrepChunk) + (size_t)std::max<int64_t>(n / kPrepChunk + 1, kMaxFoldBlocks))) != BQSR_OK)
     return st;
   // read-group buckets (OrderDev): on for several read groups, or when the
   // apply window over all cycle cells would leave more than 0.1% of the bases
@@ -1351,9 +1361,18 @@ bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
 //   BQSR_STAGE_FOLD    the expectedMismatch fold kernel
 // Exposed separately so a caller can bracket one kernel with HIP events.
 namespace {
-bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
+// Prep fused into the observe kernel (bqsr_observe_lean kLeanFused): read
+// order, 16-aligned slots, reads of at most 128 bases -- a read's bits then
+// fit one 128-offset step of the lean walk.  No prep launch and no bitmap
+// fill: the lane that observes a common read preps it in registers.
+bool fused_prep_ok(const bqsr_batch* b) {
+  return b->ctx->tune_fused && !b->bucketed && b->rd.slots_aligned && b->dims.max_len <= 128 && b->rd.n_reads > 0;
+}
+bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s,
+                        bool fuse = false) {
   HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
-  if (b->rd.n_reads > 0) {
+  b->fused_pending = fuse && fused_prep_ok(b);
+  if (b->rd.n_reads > 0 && !b->fused_pending) {
     PrepParams P{};
     P.rd = b->rd;
     if (sites) P.sites = sites->dev();
@@ -1408,7 +1427,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   hipStream_t s = S(stream);
   if (stages & BQSR_STAGE_RESET) HIP_TRY(hipMemsetAsync(b->d_err + kErrObs, 0xFF, 8, s));
   if (stages & BQSR_STAGE_PREP) {
-    if ((st = launch_prep(ctx, b, sites, s)) != BQSR_OK) return st;
+    if ((st = launch_prep(ctx, b, sites, s, true)) != BQSR_OK) return st;
   }
   if (b->rd.n_reads == 0) {
     if (stages & BQSR_STAGE_FOLD) HIP_TRY(hipMemsetAsync(b->d_em, 0, 8, s));
@@ -1461,7 +1480,9 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.obs = t->obs();
     P.mm = t->mm();
     P.part_stride = 2 * P.w.qw * P.wcells + P.w.qw;
-    const size_t need = (size_t)P.part_stride * (b->pass_blocks() + b->n_keys - 1);  // slabs w + key
+    const bool fused = lean && b->fused_pending;
+    // slabs w + key; a fused observe's list pass writes a second set
+    const size_t need = (size_t)P.part_stride * (b->pass_blocks() + b->n_keys - 1) * (fused ? 2 : 1);
     if (b->part_words < need) {  // grows with the table geometry; kept across calls
       if (b->d_part) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -1477,18 +1498,34 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.err = b->d_err + kErrObs;
     P.n_blocks = lean ? b->n_blocks : b->pass_blocks();  // (fronts: a chunk-walk workgroup per piece)
     const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true);
-    if (lean)
-      hipLaunchKernelGGL(bqsr_observe_lean<true>, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
-    else
+    if (fused) {
+      // the common reads' prep in their lanes, the rest listed; then the
+      // listed reads (prep_one + the same walk) into a second set of slabs
+      if (sites) P.sites = sites->dev();
+      P.sbits_w = b->d_sbits;
+      P.list = b->d_work;
+      P.n_list = b->d_work + b->rd.n_reads + kPrepChunk;
+      hipLaunchKernelGGL((bqsr_observe_lean<true, kLeanFused>), dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
+      ObserveParams Q = P;
+      Q.part = b->d_part + (size_t)P.part_stride * P.n_blocks;
+      const size_t lds_l = std::max<size_t>(lds, (size_t)kBlockThreads * kListThreadWords * 4);
+      hipLaunchKernelGGL((bqsr_observe_lean<true, kLeanList>), dim3(P.n_blocks), dim3(kBlockThreads), lds_l, s, Q);
+      b->fused_pending = false;
+    } else if (lean) {
+      hipLaunchKernelGGL((bqsr_observe_lean<true, kLeanPlain>), dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
+    } else {
       hipLaunchKernelGGL(bqsr_observe_chunks, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
+    }
     HIP_TRY(hipGetLastError());
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_base : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb, ry), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
-                       P.n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0);
+                       P.n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0,
+                       fused ? 2 : 1);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
+    if (b->fused_pending) return fail(BQSR_ERR_INVALID_ARG, "observe fold before the observe kernel");
     if (b->bucketed) {  // the observe kernel did not walk the fold's blocks in read order: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
@@ -1801,7 +1838,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     HIP_TRY(hipMemsetAsync(b->d_err + kErrAppKern, 0xFF, 8, s));
     HIP_TRY(hipMemsetAsync(b->d_err + kNExc, 0, 8, s));
   }
-  if (!b->prepped || (stages & BQSR_STAGE_PREP)) {
+  if (!b->prepped || b->fused_pending || (stages & BQSR_STAGE_PREP)) {  // (a fused prep whose observe never ran)
     bqsr_status st = launch_prep(ctx, b, nullptr, s);
     if (st != BQSR_OK) return st;
   }

@@ -217,6 +217,15 @@ struct ObserveParams {
   int32_t orow;        // bqsr_observe_lean: LDS obs row words (nc copies of the cycle and 43 context cells), 2 mod 4
   int32_t nc;          // bqsr_observe_lean: copies of a row's counters (<= 4)
   int32_t rows_all;    // bqsr_observe_lean: every qual of the batch is a window row (host histogram)
+  // bqsr_observe_lean fused with prep (kLeanFused: reads of <= 128 bases in
+  // read order, 16-aligned slots): the common read's prep done in registers
+  // by its lane; the rest listed per workgroup (list[wa + i], i < n_list[w],
+  // wa = the workgroup's first read), their bitmap words zeroed, and taken
+  // by the list pass (kLeanList: prep_one, then the same walk)
+  SitesDev sites;
+  uint64_t* sbits_w;   // the slot bitmap (written: zeroed words / prep_one's bits)
+  uint32_t* list;      // [n_reads]
+  uint32_t* n_list;    // [n_blocks]
 };
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----

@@ -500,6 +500,7 @@ __device__ __forceinline__ bool mask_sites_bitmap(const PrepParams& P, int32_t c
   return true;
 }
 
+constexpr int kFastCigOps = 5;  // CIGAR elements of a common read: S? M ((I|D) M)? S?
 struct PrepRec {
   ReadMeta m;
   ReadAlign a;
@@ -507,6 +508,7 @@ struct PrepRec {
 };
 struct PrepCols {
   uint4 c4, md4;
+  uint32_t c5;  // the fifth CIGAR word
 };
 // A read's sbits words in registers (prep_fast, reads whose bits fit in
 // kAccWords words): bit b of the accumulator = slot (rs & ~31) + b; static
@@ -526,9 +528,8 @@ __device__ __forceinline__ void acc_bit(uint64_t acc[kAccWords], uint32_t b, int
   for (int j = 0; j < kAccWords; ++j) acc[j] |= (b >> 5) == (uint32_t)j ? 1ull << ((b & 31) + half) : 0ull;
 }
 // mask_sites_bitmap into the accumulator (offsets 0 .. lq-1 at bits r0 + o)
-__device__ __forceinline__ bool sites_bitmap_acc(const PrepParams& P, int32_t contig, int64_t unclipped, int lq,
+__device__ __forceinline__ bool sites_bitmap_acc(const SitesDev& S, int32_t contig, int64_t unclipped, int lq,
                                                  uint32_t r0, uint64_t acc[kAccWords]) {
-  const SitesDev& S = P.sites;
   const int64_t nw = (int64_t)(S.bm_off[contig + 1] - S.bm_off[contig]);
   if (nw == 0) return false;
   const uint64_t* w = S.bm + S.bm_off[contig];
@@ -590,16 +591,232 @@ __device__ __forceinline__ PrepRec prep_rec(const PrepParams& P, int64_t r) {
   return x;
 }
 // (the columns have 32 B of padding; only reads prep_fast may take load)
-__device__ __forceinline__ PrepCols prep_cols(const PrepParams& P, const PrepRec& x) {
-  PrepCols c{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-  const uint16_t f = x.m.flags;
-  if (eligible_read(f) && x.a.n_cigar > 0 && x.a.n_cigar <= 3) {
-    c.c4 = *(const uint4*)(P.rd.cigar + x.a.cigar_off);
-    if (usable_read(f) && x.a.md_len > 0 && x.a.md_len <= 16) c.md4 = *(const uint4*)(P.rd.md + x.a.md_off);
+__device__ __forceinline__ PrepCols prep_cols(const ReadsDev& rd, const ReadMeta& m, const ReadAlign& a) {
+  PrepCols c{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0u};
+  const uint16_t f = m.flags;
+  if (eligible_read(f) && a.n_cigar > 0 && a.n_cigar <= kFastCigOps) {
+    c.c4 = *(const uint4*)(rd.cigar + a.cigar_off);
+    if (a.n_cigar > 4) c.c5 = rd.cigar[a.cigar_off + 4];
+    if (usable_read(f) && a.md_len > 0 && a.md_len <= 16) c.md4 = *(const uint4*)(rd.md + a.md_off);
   }
   return c;
 }
+__device__ __forceinline__ PrepCols prep_cols(const PrepParams& P, const PrepRec& x) { return prep_cols(P.rd, x.m, x.a); }
 
+
+// The common read's CIGAR: S? M ((I|D) M)? S? -- one insertion or deletion
+// at most -- covering the whole read, no zero-length element (prep_one's
+// CIGAR_INVALID for M / S; a zero I / D is left to prep_one too), the read and
+// sequence no longer than the CIGAR's read span (else CIGAR_SHORT / SEQ_SHORT
+// may arise), positions inside Int (the reference does this arithmetic in
+// Int).  Offsets and reference positions (RichADAMRecord.scala:101-109,
+// 156-187): the leading clip and M1 at unclipped + o; an insertion's offsets
+// have none; M2 (and the trailing clip) continue after the indel.
+struct FastCig {
+  int32_t lead, m1, x, m2;  // leading clip, first M, indel length (0: none), second M
+  bool del;                 // the indel is a deletion
+  int32_t span;             // reference span [start, end): m1 + (del ? x : 0) + m2
+  int32_t o_end;            // first offset past M2: the trailing clip starts here
+  int64_t unclipped;
+};
+__device__ __forceinline__ bool fast_cigar(const uint32_t cw[kFastCigOps], int nc, const ReadMeta& m, int64_t start,
+                                           FastCig& c) {
+  int i = 0;
+  int64_t trail = 0;
+  c.lead = c.m1 = c.x = c.m2 = 0;
+  c.del = false;
+  bool ok = nc >= 1 && nc <= kFastCigOps;
+  // (static indices: a dynamic one would put cw in scratch)
+  auto op = [&](int k) { return cig_op(k == 0 ? cw[0] : k == 1 ? cw[1] : k == 2 ? cw[2] : k == 3 ? cw[3] : cw[4]); };
+  auto len = [&](int k) {
+    return (int64_t)cig_len(k == 0 ? cw[0] : k == 1 ? cw[1] : k == 2 ? cw[2] : k == 3 ? cw[3] : cw[4]);
+  };
+  int64_t lead = 0, m1 = 0, x = 0, m2 = 0;
+  if (ok && op(0) == BQSR_CIGAR_S) {
+    lead = len(0);
+    i = 1;
+  }
+  ok &= i < nc && op(i) == BQSR_CIGAR_M;
+  if (ok) m1 = len(i++);
+  if (ok && i < nc && (op(i) == BQSR_CIGAR_I || op(i) == BQSR_CIGAR_D)) {
+    c.del = op(i) == BQSR_CIGAR_D;
+    x = len(i++);
+    ok &= x > 0 && i < nc && op(i) == BQSR_CIGAR_M;
+    if (ok) m2 = len(i++);
+    ok &= m2 > 0;
+  }
+  if (ok && i < nc && op(i) == BQSR_CIGAR_S) {
+    trail = len(i++);
+    ok &= trail > 0;
+  }
+  ok &= i == nc && m1 > 0 && (lead > 0 || op(0) != BQSR_CIGAR_S);
+  if (!ok) return false;
+  const int64_t rp_len = lead + m1 + (c.del ? 0 : x) + m2 + trail;
+  const int64_t ref_len = m1 + (c.del ? x : 0) + m2;
+  if (rp_len < m.lq || m.ls < m.lq) return false;
+  const int64_t unclipped = start - lead;
+  if (unclipped < 0 || unclipped + rp_len + ref_len > 2147483647LL || rp_len > 65535 || ref_len > 65535) return false;
+  c.lead = (int32_t)lead;
+  c.m1 = (int32_t)m1;
+  c.x = (int32_t)x;
+  c.m2 = (int32_t)m2;
+  c.span = (int32_t)ref_len;
+  c.o_end = (int32_t)(lead + m1 + (c.del ? 0 : x) + m2);
+  c.unclipped = unclipped;
+  return true;
+}
+// read offset of reference position start + rel (0 <= rel < span), -1 in a deletion
+__device__ __forceinline__ int32_t fc_offset(const FastCig& c, int32_t rel) {
+  if (rel < c.m1) return c.lead + rel;
+  if (c.del) return rel < c.m1 + c.x ? -1 : c.lead + rel - c.x;
+  return c.lead + rel + c.x;
+}
+
+// MD (MdTag.scala:38-98, md_scan) of at most 16 bytes: digits ('^'? letters
+// digits)*, the digit runs <= 2^31 - 1 (Integer.parseInt).  One pass:
+// validity, the tag's span, and (reads of < 256 bases) the offsets inside
+// [st, en) of its non-matching positions -- mismatch letters and deleted
+// bases alike (md_scan reports both) -- as a list of bytes o + 1 (at most 8).
+struct FastMd {
+  bool ok, listed;
+  uint64_t lst;
+  int64_t md_total;
+};
+__device__ __forceinline__ FastMd fast_md(const uint4 md4, int n, const FastCig& cg, int st, int en) {
+  // 32-bit arithmetic: `over` marks a digit run past 2^31 - 1 (the tag is
+  // then invalid), and the running position saturates at 2^31 - 1, beyond
+  // any read's reference span, so the comparisons against it keep their outcome
+  const uint32_t w[4] = {md4.x, md4.y, md4.z, md4.w};
+  uint32_t num = 0, pos = 0;
+  bool over = false;
+  int prev = 0;  // class of the previous byte: 0 none, 1 digit, 2 letter, 3 '^'
+  FastMd r{n > 0, en < 256, 0ull, 0};
+  uint32_t lsh = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t c = __builtin_amdgcn_ubfe(w[i >> 2], 8 * (i & 3), 8);
+    if (i < n) {
+      const uint32_t d = c - '0';
+      if (d < 10u) {
+        r.ok &= prev != 3;  // '^' is followed by a letter
+        over |= num > 214748364u;
+        num = num * 10u + d;
+        over |= num > 0x7FFFFFFFu;
+        prev = 1;
+      } else {
+        if (prev == 1) {  // a digit run ends: the matches it counts
+          r.ok &= !over;
+          pos = min(pos + num, 0x7FFFFFFFu);
+          num = 0;
+          over = false;
+        }
+        if (c == '^') {
+          r.ok &= prev == 1;  // after a digit run, before letters
+          prev = 3;
+        } else {
+          r.ok &= md_base((uint8_t)c) && prev != 0;
+          if (pos < (uint32_t)cg.span) {
+            const int32_t o = fc_offset(cg, (int32_t)pos);  // reference position start + pos
+            if (o >= st && o < en) {
+              r.listed &= lsh < 64;  // (more than 8: adjacent letters, e.g. "5AC5")
+              r.lst |= lsh < 64 ? (uint64_t)(o + 1) << lsh : 0ull;
+              lsh += 8;
+            }
+          }
+          pos = min(pos + 1u, 0x7FFFFFFFu);
+          prev = 2;
+        }
+      }
+    }
+  }
+  r.ok &= prev == 1 && !over;  // ends with digits
+  r.md_total = (int64_t)min(pos + num, 0x7FFFFFFFu);
+  return r;
+}
+
+// The bits of a common read over [st, en): emit(lo, hi, half) for each range
+// of offsets -- masked (half 0): the clips and an insertion's offsets
+// (reference positions None or outside [start, end)); mismatch (half 32): the
+// MD's non-matching positions and every position past the tag's span.
+template <class Emit>
+__device__ __forceinline__ void fast_emit(const FastCig& c, const FastMd& md, int st, int en, Emit&& emit) {
+  if (c.lead > st) emit(st, min(c.lead, en), 0);
+  if (!c.del && c.x > 0) {
+    const int lo = max(st, c.lead + c.m1), hi = min(en, c.lead + c.m1 + c.x);
+    if (lo < hi) emit(lo, hi, 0);
+  }
+  if (c.o_end < en) emit(max(st, c.o_end), en, 0);
+  for (uint64_t l = md.lst; l; l >>= 8) {
+    const int o = (int)(l & 0xFFu) - 1;
+    emit(o, o + 1, 32);
+  }
+  if (md.md_total < c.span) {
+    const int32_t t = (int32_t)md.md_total;
+    if (t < c.m1) {  // reference [t, m1) -> offsets lead + t ..
+      const int lo = max(st, c.lead + t), hi = min(en, c.lead + c.m1);
+      if (lo < hi) emit(lo, hi, 32);
+    }
+    const int32_t r2 = max(t, c.m1 + (c.del ? c.x : 0));  // the part after the indel
+    if (c.x > 0 && r2 < c.span) {
+      const int lo = max(st, fc_offset(c, r2)), hi = min(en, c.o_end);
+      if (lo < hi) emit(lo, hi, 32);
+    }
+  }
+}
+
+// OR a 64-bit run of masked bits into the accumulator at bit b (< 32 kAccWords)
+__device__ __forceinline__ void acc_or64(uint64_t acc[kAccWords], uint64_t m, uint32_t b) {
+  const uint32_t wi = b >> 5, sh = b & 31;
+  const uint64_t lo64 = m << sh;
+  const uint32_t w0 = (uint32_t)lo64, w1 = (uint32_t)(lo64 >> 32), w2 = sh ? (uint32_t)(m >> (64 - sh)) : 0u;
+#pragma unroll
+  for (int j = 0; j < kAccWords; ++j)
+    acc[j] |= (uint64_t)(((uint32_t)j == wi ? w0 : 0u) | ((uint32_t)j == wi + 1 ? w1 : 0u) |
+                         ((uint32_t)j == wi + 2 ? w2 : 0u));
+}
+// known sites of offsets [o_lo, o_hi) whose reference position is u + o,
+// from the contig's position bitmap, into the accumulator at bit r0 + o
+__device__ __forceinline__ void sites_seg_acc(const SitesDev& S, int32_t contig, int64_t u, int o_lo, int o_hi,
+                                              uint32_t r0, uint64_t acc[kAccWords]) {
+  const int64_t nw = (int64_t)(S.bm_off[contig + 1] - S.bm_off[contig]);
+  const uint64_t* w = S.bm + S.bm_off[contig];
+  for (int o = o_lo; o < o_hi; o += 64) {
+    const int64_t b0 = u + o - S.bm_base[contig];
+    const int64_t wi = b0 >> 6;
+    const uint32_t sh = (uint32_t)(b0 & 63);
+    const uint64_t lo = (wi >= 0 && wi < nw) ? w[wi] : 0ull, hi = (wi + 1 >= 0 && wi + 1 < nw) ? w[wi + 1] : 0ull;
+    uint64_t m = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    if (o_hi - o < 64) m &= (1ull << (o_hi - o)) - 1ull;
+    if (m) acc_or64(acc, m, r0 + (uint32_t)o);
+  }
+}
+
+// The bits of a common read in registers (offset o at bit r0 + o of acc,
+// r0 + en <= 32 kAccWords), known sites from the contig's position bitmap;
+// *linear when the contig has none (its sorted list must be searched).
+__device__ __forceinline__ void fast_bits(const SitesDev& S, int32_t contig, const FastCig& c, const FastMd& md,
+                                          int st, int en, uint32_t r0, uint64_t acc[kAccWords], bool* linear) {
+  fast_emit(c, md, st, en, [&](int lo, int hi, int half) { acc_range(acc, r0 + (uint32_t)lo, r0 + (uint32_t)hi, half); });
+  *linear = false;
+  if (contig < 0 || contig >= S.n_contigs) return;
+  if (S.bm_off[contig + 1] == S.bm_off[contig]) {
+    *linear = true;
+  } else if (c.x == 0) {
+    sites_bitmap_acc(S, contig, c.unclipped, en, r0, acc);
+  } else {  // the two reference segments either side of the indel
+    sites_seg_acc(S, contig, c.unclipped, 0, min(en, c.lead + c.m1), r0, acc);
+    const int ob = c.lead + c.m1 + (c.del ? 0 : c.x);
+    sites_seg_acc(S, contig, c.unclipped + (c.del ? c.x : -c.x), ob, en, r0, acc);
+  }
+}
+
+// ReadInfo flags of an eligible read that prep finds valid
+__device__ __forceinline__ uint16_t valid_flags(uint16_t f) {
+  return (uint16_t)(kInfoApp | (usable_read(f) ? kInfoObs : 0) | ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
+                    (((f & BQSR_F_PAIRED) && (f & BQSR_F_SECOND_OF_PAIR)) ? kInfoSecond : 0));
+}
+constexpr uint16_t kFastNeed = BQSR_F_HAS_QUAL | BQSR_F_HAS_RG | BQSR_F_HAS_SEQ | BQSR_F_HAS_CIGAR | BQSR_F_HAS_START |
+                               BQSR_F_HAS_REFNAME;
 
 template <bool kStore>
 __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, const PrepCols& cols,
@@ -611,81 +828,19 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
     P.info[r] = ReadInfo{0, 0, kInfoPass, 0};
     return true;
   }
-  constexpr uint16_t need = BQSR_F_HAS_QUAL | BQSR_F_HAS_RG | BQSR_F_HAS_SEQ | BQSR_F_HAS_CIGAR | BQSR_F_HAS_START |
-                            BQSR_F_HAS_REFNAME;
-  if ((f & need) != need || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq == 0 || a.n_cigar == 0 ||
-      a.n_cigar > 3)
+  if ((f & kFastNeed) != kFastNeed || ((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) || m.lq == 0 || a.n_cigar == 0 ||
+      a.n_cigar > kFastCigOps)
     return false;
   const bool usable = usable_read(f);
   if (usable && (a.md_len == 0 || a.md_len > 16)) return false;
-  const uint4 c4 = cols.c4, md4 = cols.md4;
   const int st = 0, en = m.lq;  // bits over the whole read (see above)
-  const uint32_t cw[3] = {c4.x, c4.y, c4.z};
-  const int nc = a.n_cigar;
-  int64_t lead = 0, mlen = 0, trail = 0;
-  {
-    const uint32_t o0 = cig_op(cw[0]), o1 = cig_op(cw[1]), o2 = cig_op(cw[2]);
-    const int64_t l0 = cig_len(cw[0]), l1 = cig_len(cw[1]), l2 = cig_len(cw[2]);
-    if (nc == 1 && o0 == BQSR_CIGAR_M) {
-      mlen = l0;
-    } else if (nc == 2 && o0 == BQSR_CIGAR_S && o1 == BQSR_CIGAR_M) {
-      lead = l0;
-      mlen = l1;
-    } else if (nc == 2 && o0 == BQSR_CIGAR_M && o1 == BQSR_CIGAR_S) {
-      mlen = l0;
-      trail = l1;
-    } else if (nc == 3 && o0 == BQSR_CIGAR_S && o1 == BQSR_CIGAR_M && o2 == BQSR_CIGAR_S) {
-      lead = l0;
-      mlen = l1;
-      trail = l2;
-    } else {
-      return false;
-    }
-    // a zero-length element is prep_one's CIGAR_INVALID
-    if (l0 == 0 || (nc > 1 && l1 == 0) || (nc > 2 && l2 == 0)) return false;
-  }
-  const int64_t rp_len = lead + mlen + trail;
-  if (rp_len < m.lq || m.ls < m.lq) return false;  // else CIGAR_SHORT / SEQ_SHORT may arise: prep_one decides
-  const int64_t start = a.start, unclipped = start - lead;
-  // prep_one's Int-range test (the reference does position arithmetic in Int)
-  if (unclipped < 0 || unclipped + rp_len + mlen > 2147483647LL) return false;
+  const uint32_t cw[kFastCigOps] = {cols.c4.x, cols.c4.y, cols.c4.z, cols.c4.w, cols.c5};
+  FastCig c;
+  if (!fast_cigar(cw, a.n_cigar, m, a.start, c)) return false;
   const uint64_t rs = m.slot;
   if (usable) {
-    // MD (MdTag.scala:38-98): digits (letters digits)*, no deletion; valid iff
-    // every byte is a digit or a base letter and the first and last are digits
-    const uint32_t w[4] = {md4.x, md4.y, md4.z, md4.w};
-    const int n = a.md_len;
-    int64_t num = 0, pos = 0;
-    bool ok = true;
-    // one pass: validity, the tag's span and (reads of < 256 bases) the
-    // mismatch offsets inside [st, en) as a list of bytes o + 1 (at most 7
-    // letters fit 16 bytes), set below -- per letter, not per tag byte
-    bool listed = en < 256;
-    uint64_t lst = 0;
-    uint32_t lsh = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-      if (i < n) {
-        if (c >= '0' && c <= '9') {
-          num = num * 10 + (int64_t)(c - '0');
-          ok &= num <= 2147483647LL;  // Integer.parseInt
-        } else {
-          ok &= md_base((uint8_t)c) && i > 0 && i + 1 < n;
-          pos += num;
-          const int64_t o = lead + pos;  // reference position start + pos
-          if (pos < mlen && o >= st && o < en) {
-            listed &= lsh < 64;  // (more than 8 letters: adjacent ones, e.g. "5AC5")
-            lst |= lsh < 64 ? (uint64_t)(o + 1) << lsh : 0ull;
-            lsh += 8;
-          }
-          pos += 1;
-          num = 0;
-        }
-      }
-    }
-    if (!ok) return false;  // (a letter first or last is invalid: `i > 0 && i + 1 < n`)
-    const int64_t md_total = pos + num;
+    const FastMd md = fast_md(cols.md4, a.md_len, c, st, en);
+    if (!md.ok) return false;  // prep_one raises MD_PARSE at the right offset
     // with known sites (several bits per read, from three sources) the bits
     // are gathered per word first; without, the few bits go straight out
     // (measured: the gathering costs more than it saves on cfg2's reads)
@@ -694,20 +849,11 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
       // the read's sbits words in registers, one atomic OR per word with bits
       // (measured: plain stores of the words a read owns alone, mixed with
       // the neighbours' atomics on the same lines, were 2x slower)
+      if (!md.listed) return false;  // (en <= 160: only a list overflow)
       uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
       const uint32_t r0 = (uint32_t)(rs & 31);  // bit of offset 0 in acc
-      if (lead > st) acc_range(acc, r0 + st, r0 + (uint32_t)min(lead, (int64_t)en), 0);
-      if (lead + mlen < en) acc_range(acc, r0 + (uint32_t)max((int64_t)st, lead + mlen), r0 + en, 0);
-      if (!listed) return false;  // (en <= 160: only a list overflow)
-      for (uint64_t l = lst; l; l >>= 8) acc_bit(acc, r0 + (uint32_t)(l & 0xFFu) - 1u, 32);
-      if (md_total < mlen) {
-        const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
-        if (lo < hi) acc_range(acc, r0 + (uint32_t)lo, r0 + (uint32_t)hi, 32);
-      }
-      bool linear = false;
-      if (a.contig >= 0 && a.contig < P.sites.n_contigs) {
-        if (!sites_bitmap_acc(P, a.contig, unclipped, en, r0, acc)) linear = true;
-      }
+      bool linear;
+      fast_bits(P.sites, a.contig, c, md, st, en, r0, acc, &linear);
       if (kStore) {
         // the words go out with the wavefront's stores (prep_store_words); a
         // contig without a bitmap goes to pass 2, whose atomics land on them
@@ -715,6 +861,7 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
 #pragma unroll
         for (int j = 0; j < kAccWords; ++j) acc_out[j] = acc[j];
       } else {
+        if (linear && c.x > 0) return false;  // (mask_sites_linear maps offsets as unclipped + o)
         const uint64_t wb = rs >> 5;
 #pragma unroll
         for (int j = 0; j < kAccWords; ++j) {
@@ -722,50 +869,39 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
           const uint64_t wi = wb + (uint64_t)j;
           atomicOr((unsigned long long*)&P.sbits[wi], (unsigned long long)acc[j]);
         }
-        if (linear) mask_sites_linear(P, a.contig, unclipped, st, en, rs);
+        if (linear) mask_sites_linear(P, a.contig, c.unclipped, st, en, rs);
       }
     } else {
-      // masked: the clips (reference positions outside [start, start + mlen))
-      if (lead > st) set_sbits(P.sbits, rs + st, rs + min(lead, (int64_t)en), 0);
-      if (lead + mlen < en) set_sbits(P.sbits, rs + max((int64_t)st, lead + mlen), rs + en, 0);
-      // mismatches: each letter's position, then every position past the tag's span
-      if (listed) {
-        for (uint64_t l = lst; l; l >>= 8) {
-          const uint64_t o = (l & 0xFFu) - 1u;
-          set_sbits(P.sbits, rs + o, rs + o + 1, 32);
-        }
-      } else {
-        num = 0;
-        pos = 0;
+      if (a.contig >= 0 && a.contig < P.sites.n_contigs && c.x > 0) return false;  // (sites as unclipped + o)
+      if (!md.listed) {  // more than 8 non-matching positions: the tag's per-byte walk
+        if (c.x > 0) return false;
+        const uint32_t w[4] = {cols.md4.x, cols.md4.y, cols.md4.z, cols.md4.w};
+        int64_t num = 0, pos = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-          if (i < n) {
-            if (c >= '0' && c <= '9') {
-              num = num * 10 + (int64_t)(c - '0');
-            } else {
+          const uint32_t ch = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+          if (i < a.md_len) {
+            if (ch >= '0' && ch <= '9') {
+              num = num * 10 + (int64_t)(ch - '0');
+            } else if (ch != '^') {
               pos += num;
               num = 0;
-              const int64_t o = lead + pos;  // reference position start + pos
-              if (pos < mlen && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
+              const int64_t o = c.lead + pos;  // reference position start + pos
+              if (pos < c.m1 && o >= st && o < en) set_sbits(P.sbits, rs + (uint64_t)o, rs + (uint64_t)o + 1, 32);
               pos += 1;
             }
           }
         }
       }
-      if (md_total < mlen) {
-        const int64_t lo = max((int64_t)st, lead + md_total), hi = min((int64_t)en, lead + mlen);
-        if (lo < hi) set_sbits(P.sbits, rs + (uint64_t)lo, rs + (uint64_t)hi, 32);
-      }
-      if (a.contig >= 0 && a.contig < P.sites.n_contigs && !mask_sites_bitmap(P, a.contig, unclipped, en, rs))
-        mask_sites_linear(P, a.contig, unclipped, st, en, rs);
+      FastMd me = md;
+      if (!md.listed) me.lst = 0;  // (its letters: the walk above)
+      fast_emit(c, me, st, en,
+                [&](int lo, int hi, int half) { set_sbits(P.sbits, rs + (uint64_t)lo, rs + (uint64_t)hi, half); });
+      if (a.contig >= 0 && a.contig < P.sites.n_contigs && !mask_sites_bitmap(P, a.contig, c.unclipped, en, rs))
+        mask_sites_linear(P, a.contig, c.unclipped, st, en, rs);
     }
   }
-  P.info[r] = ReadInfo{0, 0,
-                       (uint16_t)(kInfoTrim | kInfoApp | (usable ? kInfoObs : 0) |
-                                  ((f & BQSR_F_NEG_STRAND) ? kInfoNeg : 0) |
-                                  (((f & BQSR_F_PAIRED) && (f & BQSR_F_SECOND_OF_PAIR)) ? kInfoSecond : 0)),
-                       0};
+  P.info[r] = ReadInfo{0, 0, (uint16_t)(kInfoTrim | valid_flags(f)), 0};
   return true;
 }
 
@@ -950,23 +1086,14 @@ struct LaneRead {
   int aux;        // a pass's own per-read value (set by its fread, carried to the read's chunks)
 };
 
-// ks: the read's slot in rd's qual / base columns when they are the
-// key-major copy (OrderDev::kslot), ~0 for its own slot
-__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L,
-                                              uint64_t ks = ~0ull) {
+// A lane's read from its record and resolved ReadInfo (qs: the read's slot
+// in rd's qual / base columns)
+__device__ __forceinline__ LaneRead lane_decode(int64_t r, const ReadMeta& m, const ReadInfo& inf, uint64_t qs, int L) {
   LaneRead x;
-  x.r = live ? r : rd.n_reads;
-  x.ro = x.r;
+  x.r = r;
+  x.ro = r;
   x.aux = 0;
-  ReadMeta m{0, 0, 0, 0, 0};
-  ReadInfo inf{0, 0, 0, 0};
-  if (live) {
-    m = rd.meta[r];
-    inf = info[r];
-  }
-  x.trimmed = inf.fl & kInfoTrim;
-  const uint64_t qs = ks == ~0ull ? m.slot : ks;
-  inf = resolve_info(rd, inf, qs, m.lq);
+  x.trimmed = false;
   x.inf = inf;
   x.slot = qs;
   x.oslot = m.slot;
@@ -987,6 +1114,24 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
     x.cell0 = sec ? L - (int)m.ls : L + (int)m.ls;
     x.dir = sec ? 1 : -1;
   }
+  return x;
+}
+
+// ks: the read's slot in rd's qual / base columns when they are the
+// key-major copy (OrderDev::kslot), ~0 for its own slot
+__device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo* info, int64_t r, bool live, int L,
+                                              uint64_t ks = ~0ull) {
+  ReadMeta m{0, 0, 0, 0, 0};
+  ReadInfo inf{0, 0, 0, 0};
+  if (live) {
+    m = rd.meta[r];
+    inf = info[r];
+  }
+  const bool trimmed = inf.fl & kInfoTrim;
+  const uint64_t qs = ks == ~0ull ? m.slot : ks;
+  inf = resolve_info(rd, inf, qs, m.lq);
+  LaneRead x = lane_decode(live ? r : rd.n_reads, m, inf, qs, L);
+  x.trimmed = trimmed;
   return x;
 }
 
@@ -1494,7 +1639,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
 // all landed).
 extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd, OrderDev ord, int32_t n_blocks,
                                               int32_t stride, int32_t wcells, Window w, TableGeom g, int64_t* touched,
-                                              int64_t* obs, int64_t* mm, int32_t junk) {
+                                              int64_t* obs, int64_t* mm, int32_t junk, int32_t sets) {
   // fronts: a thread per (base key, word) sums the base key's pieces (slab
   // 2 key of workgroup key), one atomic per table word as without fronts
   const int nk = order_base_keys(ord);
@@ -1523,7 +1668,8 @@ extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd,
         for (int64_t b = w0; b <= w1; ++b) {
           // a workgroup with an empty range in between wrote no slab (its words
           // are read but not added: the loads stay independent)
-          const uint32_t v = part[(b + (ord.perm ? key : 0)) * stride + i];
+          uint32_t v = part[(b + (ord.perm ? key : 0)) * stride + i];
+          if (sets > 1) v += part[(n_blocks + b) * stride + i];  // (read order: a fused observe's list pass)
           if (max(k0, wg_begin(rd, b, n_blocks)) < min(k1, wg_begin(rd, b + 1, n_blocks))) s += v;
         }
       }

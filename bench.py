@@ -58,6 +58,8 @@ def parse(argv=None):
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle check of the timed job's results")
     ap.add_argument("--event-steps", type=int, default=3,
                     help="untimed jobs after the timed region whose stages are timed with HIP events")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=V",
+                    help="bqsr_context_tune layout knob for an A/B run (order, fronts, key_major, fused_prep)")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic json (default profiles/pmc_traffic_<config>.json)")
     ap.add_argument("--part-reads", type=int, default=4_000_000, help="cfg5: reads per streamed partition")
@@ -169,6 +171,8 @@ def main():
             raise SystemExit("bench: process group has %d ranks, expected %d" % (dist.get_world_size(), world))
     L = _capi.lib()
     ctx = bqsr.Context.get(dev_index)
+    if args.tune:
+        ctx.tune(**{k: (v if v in ("auto", "read", "group") else int(v)) for k, v in (t.split("=", 1) for t in args.tune)})
 
     cfg = dict(synth.CONFIGS[args.config])
     if args.config == "cfg5":

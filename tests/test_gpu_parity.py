@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from _parity import check, run_gpu, run_oracle, assert_same
-from adam_amd import synth
+from adam_amd import bqsr, synth
 from adam_amd.records import ADAMRecord, RecordBatch, read_sam
 
 pytestmark = pytest.mark.gpu
@@ -83,11 +83,12 @@ def read_order(request):
     sort, pieces per read group); the library picks 'group' for several read
     groups by default."""
     from adam_amd import bqsr as _b
-    with _b.Context.get(0).tuned(order=request.param):
+    order, _, plain = request.param.partition("-")  # "read-plain": prep in a kernel of its own
+    with _b.Context.get(0).tuned(order=order, fused_prep=0 if plain else 1):
         yield request.param
 
 
-@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
+@pytest.mark.parametrize("read_order", ["read", "read-plain", "group"], indirect=True)
 @pytest.mark.parametrize("n_reads,n_rg,lens,seed", [
     (6000, 96, (150, 250), 21),    # many groups, a few reads per workgroup and group
     (40000, 8, (100,), 22),        # few groups, each spread over many workgroups
@@ -99,7 +100,7 @@ def test_read_orders(read_order, n_reads, n_rg, lens, seed):
     check([b.slice(0, n_reads // 3), b.slice(n_reads // 3, n_reads)], synth.known_sites(2_000_000, seed=5))
 
 
-@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
+@pytest.mark.parametrize("read_order", ["read", "read-plain", "group"], indirect=True)
 def test_read_orders_edge_cases(read_order):
     check([RecordBatch.from_records(EDGE * 3)], sites={"1": [10002, 10005, 40, 44, 10013]})
 
@@ -146,6 +147,17 @@ EDGE = [
     rec(mismatching_positions=None, record_group_id=0),  # not usable, recalibrated in apply
     rec(record_group_id=1, qual="JJJJJJJJJJ"),
     rec(record_group_id=2, qual="5555555555", mismatching_positions="0A0C0G0T6"),
+    # one insertion or deletion: the prep's lock-step form (S? M (I|D) M S?)
+    rec(cigar="1S3M2I3M1S", mismatching_positions="1A1T2"),  # clips both sides, letters either side of the I
+    rec(cigar="3M2D7M", mismatching_positions="1A1^GC2T4"),  # letter before, deletion, letter after
+    rec(cigar="2S4M1D4M", mismatching_positions="4^A0C3"),  # mismatch right after the deletion
+    rec(cigar="10M", mismatching_positions="4^AC6"),  # an MD deletion the CIGAR has not: positions of M
+    rec(cigar="4M2I4M", mismatching_positions="4^A4"),  # MD deletion over an insertion read
+    rec(cigar="5M3D5M", mismatching_positions="5^ACG2"),  # MD shorter than the span past the deletion
+    rec(cigar="2M3I5M", mismatching_positions="7", read_negative_strand=True),
+    rec(cigar="6M1I3M", mismatching_positions="0T8", read_paired=True, second_of_pair=True),
+    rec(cigar="3M0I7M", mismatching_positions="10"),  # zero-length insertion: the per-read path
+    rec(start=10000, cigar="9M1D1M", mismatching_positions="9^T1", sequence="ACGTACGTAC"),
 ]
 
 
@@ -163,6 +175,10 @@ def test_edge_cases_split():
     (rec(mismatching_positions="5Z4"), "MD_PARSE"),
     (rec(mismatching_positions="A5"), "MD_PARSE"),
     (rec(mismatching_positions="5A"), "MD_PARSE"),
+    (rec(mismatching_positions="2147483648"), "MD_PARSE"),  # Integer.parseInt overflow
+    (rec(mismatching_positions="5^4"), "MD_PARSE"),  # '^' without letters
+    (rec(mismatching_positions="5^^A4"), "MD_PARSE"),
+    (rec(cigar="4M2I4M", mismatching_positions="3AZ4"), "MD_PARSE"),
     (rec(cigar="6M"), "CIGAR_SHORT"),
     (rec(cigar="*"), "CIGAR_SHORT"),
     (rec(cigar="0M10M"), "CIGAR_INVALID"),
@@ -172,9 +188,13 @@ def test_edge_cases_split():
     (rec(qual=None), "NULL_FIELD"),
     (rec(sequence="ACGTA", cigar="10M"), "SEQ_SHORT"),
 ])
-def test_errors(bad, err):
+@pytest.mark.parametrize("fused", [1, 0])
+def test_errors(bad, err, fused):
+    # (fused: the common reads' prep inside the observe kernel, the failing
+    # read in its list pass; 0: the prep kernel)
     ok = [rec(), rec(qual="HHHHHHHHHH")]
-    check([RecordBatch.from_records(ok + [bad] + ok)], expect_error=err)
+    with bqsr.Context.get(0).tuned(fused_prep=fused):
+        check([RecordBatch.from_records(ok + [bad] + ok)], expect_error=err)
 
 
 def test_missing_key_in_apply():
