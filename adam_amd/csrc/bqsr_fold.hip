@@ -393,9 +393,6 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
   __shared__ int64_t ev_dst[kSegThreads];
   __shared__ int32_t seg0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef BQSR_FOLD_PROFILE
-  const long long pf_t0 = clock64();
-#endif
   for (int q = tid; q < kQBins; q += kSegThreads) t[q] = P.pow10[q];
   const int b = P.cand_list[c];
   const FoldBlock B = P.blk[b];
@@ -564,9 +561,6 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     if (tid == last) carry_r = Re;
     __syncthreads();
   }
-#ifdef BQSR_FOLD_PROFILE
-  const long long pf_t1 = clock64();
-#endif
   const int ns = min(carry_sid + 1, kFoldMaxSegs);
   if (tid == 0) {
     seg0 = (int32_t)atomicAdd(P.seg_used, (uint32_t)ns);  // this block's place in the compact list
@@ -596,10 +590,6 @@ extern "C" __global__ void __launch_bounds__(kSegThreads) bqsr_fold_segs(FoldPar
     }
     P.seg[seg0 + tid] = g;
   }
-#ifdef BQSR_FOLD_PROFILE
-  if (tid == 0)
-    printf("FOLDSEGS c %d tiles %lld segs %d cycles %lld\n", c, (long long)(c1 - c0), ns, pf_t1 - pf_t0);
-#endif
 }
 
 // --------------------------------------------------------------- chain ----
@@ -643,12 +633,7 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-#ifdef BQSR_FOLD_PROFILE
-__device__ long long g_fold_pf[8];  // seq adds, seq cycles, windows, window cycles, events, event cycles, tables, chunk windows
-#define FPF(i, v) (lane == 0 ? (void)atomicAdd((unsigned long long*)&g_fold_pf[i], (unsigned long long)(v)) : (void)0)
-#else
 #define FPF(i, v) (void)0
-#endif
 #define LDS __attribute__((address_space(3)))
 // one copy (noinline: the chain is a single wavefront whose time goes to
 // latency, and a kernel this size also misses in the instruction cache);
@@ -658,9 +643,6 @@ __device__ __noinline__ double wave_fold(double S, const LDS uint8_t* q, int n, 
   int cur_e = *cur_ep;
   int pos = 0;
   while (pos < n) {
-#ifdef BQSR_FOLD_PROFILE
-    const long long c0 = clock64();
-#endif
     if (S < kFoldSeqLimit) {
       // small S: binades change every few additions and ties are common --
       // add one by one (every lane the same chain), 64 operands per load round
@@ -793,9 +775,6 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   __shared__ double inc[kQBins];
   __shared__ __align__(16) uint8_t scratch[kTileSlots + 64];
   __shared__ int32_t nseg_l[kMaxFoldBlocks], sbase_l[kMaxFoldBlocks];
-#ifdef BQSR_FOLD_PROFILE
-  const long long pf_k0 = clock64();
-#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int nb = P.n_blocks, nc = *P.n_cand;
   // dynamic LDS (chain_lds): streams | per-64 increments | segments | blocks
@@ -832,9 +811,6 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   }
   __syncthreads();
   if (tid >= 64) return;  // one wavefront walks the job
-#ifdef BQSR_FOLD_PROFILE
-  if (lane < 8) g_fold_pf[lane] = 0;
-#endif
   double S = 0.0;
   __shared__ int cur_e_s;
   if (lane == 0) cur_e_s = INT32_MIN;
@@ -846,20 +822,8 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   LDS double* linc = (LDS double*)inc;
   LDS uint8_t* lscratch = (LDS uint8_t*)scratch;
   const int64_t nt = P.rd.n_tiles;
-#ifdef BQSR_FOLD_PROFILE
-  long long pf_blk = 0, pf_blk_fb = 0, pf_run = 0, pf_run_fb = 0, pf_ev = 0, pf_ev_el = 0, pf_glob = 0,
-            pf_glob_tiles = 0, pf_c0 = clock64();
-#define PF(x) x
-#else
 #define PF(x)
-#endif
-#ifdef BQSR_FOLD_PROFILE
-  long long pf_nc = 0, pf_cb = 0;
-#endif
   for (int b = 0; b < nb; ++b) {
-#ifdef BQSR_FOLD_PROFILE
-    const long long bt0 = clock64();
-#endif
     const FoldBlock B = blk[b];
     if (B.cidx < 0) {  // a run of -cidx event-free blocks in binade e: one integer addition
       if (B.e == kFoldNoBase) continue;
@@ -899,9 +863,6 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
         PF(++pf_run_fb);
       } else if (G.kind == kSegEvent) {
         if (G.off + G.inc <= sl) {  // (the LDS copy has 64 B of slack past sl)
-#ifdef BQSR_FOLD_PROFILE
-          const long long w0 = clock64();
-#endif
           S = wave_fold(S, lstreams + G.off, (int)G.inc, lcsum + G.off / 64 * 2, G.e, lt, linc, cur_e, lane);
           PF(pf_glob_tiles += clock64() - w0);
         } else {  // beyond the prefetched bytes: through the scratch buffer, 4 KB at a time
@@ -923,15 +884,6 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
     PF(pf_cb += clock64() - bt0);
   }
   if (lane == 0) P.em_out[0] = S;
-#ifdef BQSR_FOLD_PROFILE
-  if (lane == 0)
-    printf("FOLD2 cand %d stream_used %lld | blocks %lld fallback %lld | runs %lld fallback %lld | events %lld elems %lld | "
-           "global %lld wavefold-cyc %lld noncand-cyc %lld cand-cyc %lld | cycles %lld (prefetch %lld) | seq %lld (%lld cyc) windows %lld (%lld cyc) events %lld (%lld "
-           "cyc) tables %lld chunkwin %lld\n",
-           nc, (long long)used, pf_blk, pf_blk_fb, pf_run, pf_run_fb, pf_ev, pf_ev_el, pf_glob, pf_glob_tiles, pf_nc, pf_cb,
-           clock64() - pf_c0, pf_c0 - pf_k0, g_fold_pf[0], g_fold_pf[1], g_fold_pf[2], g_fold_pf[3], g_fold_pf[4],
-           g_fold_pf[5], g_fold_pf[6], g_fold_pf[7]);
-#endif
 }
 
 }  // namespace bqsr

@@ -21,3 +21,6 @@ rep("        cr[i] = (lv && full && n0 >= 0) ? *(const uint3*)(P.rd.bases + ((n0
 rep(": P.sbits[(s0 >> 5) + w];",
     ": (P.sbits[min(s0 >> 5 & ~(uint64_t)1023, (uint64_t)P.rd.n_slots / 32 - 1024) + lane + 64 * w] & (uint64_t)(P.rows_all - 1));")
 open(p, "w").write(s)
+sys.path.insert(0, __import__("os").path.dirname(__file__))
+import _no_errors
+_no_errors.apply(sys.argv[1])
