@@ -59,6 +59,9 @@ RG_TAGS = (("recordGroupSequencingCenter", "CN"), ("recordGroupDescription", "DS
 
 PER_READ_STRINGS = ("readName", "sequence", "qual", "attributes", "mismatchingPositions")
 DICT_COLS = [n for n, k in ADAM_FIELDS if n not in PER_READ_STRINGS]
+# gzip part files: the per-base strings as literal-only Huffman DEFLATE blocks
+# (parquet_gzip.cpp: their letter frequencies are their redundancy)
+HUFFMAN_COLS = ("sequence", "qual")
 STATS_COLS = [n for n, k in ADAM_FIELDS if n not in PER_READ_STRINGS]
 
 
@@ -89,6 +92,11 @@ def _lib():
         L.bqsr_sam_adam_columns.argtypes = [vp, vp, ctypes.POINTER(AdamHost), vp]
         L.bqsr_sam_header_text.restype = ctypes.c_int
         L.bqsr_sam_header_text.argtypes = [vp, ctypes.c_char_p, i64, ctypes.POINTER(i64)]
+        L.bqsr_parquet_gzip.restype = ctypes.c_int
+        L.bqsr_parquet_gzip.argtypes = [vp, i64, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
+                                        ctypes.POINTER(i64)]
+        L.bqsr_gzip_bytes.restype = ctypes.c_int
+        L.bqsr_gzip_bytes.argtypes = [vp, i64, ctypes.c_int32, ctypes.c_int32, vp, i64, ctypes.POINTER(i64)]
         _bound = True
     return L
 
@@ -317,7 +325,7 @@ class AdamWriter:
     as the tables arrive (``OUT.partial`` renamed to ``OUT`` on ``close``)."""
 
     def __init__(self, path: str, compression: str = "gzip", threads: Optional[int] = None,
-                 overwrite: bool = False):
+                 overwrite: bool = False, native_gzip: bool = True):
         self.path = path
         self.tmp = path + ".partial"
         # adamSave goes through Hadoop's FileOutputFormat, which refuses an
@@ -337,6 +345,9 @@ class AdamWriter:
         # gzip at zlib's default level 6 (parquet-mr's GzipCodec through Hadoop;
         # Arrow's own default is 9)
         self.level = 6 if self.compression == "gzip" else None
+        # (native_gzip False: Arrow's own zlib writer, for comparisons)
+        self.native_gzip = native_gzip
+        self.gzip_threads = 2
         nth = threads or max(1, min(16, len(os.sched_getaffinity(0))))
         self.pool = ThreadPoolExecutor(max_workers=nth)
         self.futures = []
@@ -344,13 +355,27 @@ class AdamWriter:
         self.rows = 0
 
     def _write(self, table, name):
+        import pyarrow as pa
         import pyarrow.parquet as pq
         # dictionary pages and statistics where they pay: not for the
         # per-read strings (names, bases, quals, tags), whose dictionaries
         # overflow and whose min / max no reader filters on
-        pq.write_table(table, os.path.join(self.tmp, name), compression=self.compression,
-                       compression_level=self.level, use_dictionary=DICT_COLS, write_statistics=STATS_COLS,
+        path = os.path.join(self.tmp, name)
+        if self.compression != "gzip" or not self.native_gzip:
+            pq.write_table(table, path, compression=self.compression, compression_level=self.level,
+                           use_dictionary=DICT_COLS, write_statistics=STATS_COLS, store_schema=False)
+            return
+        # gzip: Arrow encodes the pages uncompressed in memory, the library
+        # writes them gzip-compressed (bqsr_parquet_gzip: quals and bases as
+        # literal-only Huffman blocks, the rest at zlib's level 6)
+        buf = pa.BufferOutputStream()
+        pq.write_table(table, buf, compression="none", use_dictionary=DICT_COLS, write_statistics=STATS_COLS,
                        store_schema=False)
+        data = buf.getvalue()
+        n = ctypes.c_int64()
+        check(_lib().bqsr_parquet_gzip(ctypes.c_void_p(data.address), data.size, path.encode(), self.level,
+                                       b",".join(c.encode() for c in HUFFMAN_COLS), self.gzip_threads,
+                                       ctypes.byref(n)))
 
     def add(self, table):
         name = "part-r-%05d.parquet" % self.parts

@@ -2114,6 +2114,7 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
 #include "adam_out.hip"
 #include "sam_batch.hip"
 #include "arrow_ingest.hip"
+#include "parquet_gzip.cpp"
 
 // ---- streamed outputs: compaction (uses the SAM code's scans) ----
 extern "C" {

@@ -283,6 +283,26 @@ bqsr_status bqsr_dup_set_finish(bqsr_dup_set* d, int64_t* n_duplicates);
 bqsr_status bqsr_dup_set_apply(bqsr_dup_set* d, int64_t part, bqsr_sam* s, int64_t* n_duplicates);
 void bqsr_dup_set_destroy(bqsr_dup_set* d);
 
+/* adamSave's GZIP part files (AdamRDDFunctions.scala:37-48 through
+ * parquet-mr; ParquetArgs.scala:27: GZIP by default).  `in` is a Parquet file
+ * written UNCOMPRESSED (Arrow's writer: schema, encodings, dictionary pages,
+ * statistics), here rewritten to `path` with every page a gzip member:
+ * the columns named in `huffman_cols` (comma-separated top-level names, e.g.
+ * "qual,sequence") as one dynamic-Huffman DEFLATE block of literals, the
+ * others by libdeflate (zlib when absent) at `level` (zlib's default 6 is
+ * Hadoop's GzipCodec); page headers, column-chunk metadata and the footer
+ * re-encoded with the new sizes and offsets.  Data page v1 and dictionary
+ * pages; no page index, bloom filter or external column chunks
+ * (BQSR_ERR_INVALID_ARG otherwise).  `threads` compress pages in parallel.
+ * *out_len: bytes written. */
+bqsr_status bqsr_parquet_gzip(const uint8_t* in, int64_t in_len, const char* path, int32_t level,
+                              const char* huffman_cols, int32_t threads, int64_t* out_len);
+/* One gzip member of n bytes into out (cap bytes; *out_len the size, also
+ * when it does not fit): huffman != 0 the literal-only Huffman block, else
+ * libdeflate / zlib at `level` (tests). */
+bqsr_status bqsr_gzip_bytes(const uint8_t* in, int64_t n, int32_t huffman, int32_t level, uint8_t* out, int64_t cap,
+                            int64_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif
