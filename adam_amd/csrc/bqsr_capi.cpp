@@ -354,6 +354,8 @@ struct bqsr_batch {
   bool fused_pending = false;
   // per-call scratch
   uint32_t* d_hq = nullptr;        // [n_blocks][128] fold blocks' qual histograms
+  uint32_t* d_qmask = nullptr;     // [4] their bins holding a base (bqsr_fold_plan)
+  bool hq_valid = false;           // d_qmask written by a fold of this batch (its quals and trims are fixed)
   FoldParams fold{};               // the fold's device buffers (FoldParams)
   uint32_t* d_part = nullptr;      // per-block window counts
   size_t part_words = 0;
@@ -396,7 +398,16 @@ struct bqsr_batch {
   // workgroups of the chunk-walk passes: a piece each with fronts, else the fold's blocks
   int32_t pass_blocks() const { return bucketed && fronts > 0 ? n_keys : n_blocks; }
   uint64_t* h_status = nullptr;  // pinned: bqsr_job_result's one transfer (kJobStatusWords)
+  // bucketed batches: the fold on a stream of its own, beside the observe
+  // kernel and bqsr_window_reduce -- it needs prep's trims, not the table
+  // (ev_obs: recorded after prep, pending until a FOLD stage takes it)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_obs = nullptr, ev_fold = nullptr;
+  bool obs_pending = false;
   ~bqsr_batch() {
+    if (side) (void)hipStreamDestroy(side);
+    for (hipEvent_t e : {ev_obs, ev_fold})
+      if (e) (void)hipEventDestroy(e);
     if (d_part) (void)hipFree(d_part);
     if (d_off64) (void)hipFree(d_off64);
     for (void* p : {(void*)k_qual, (void*)k_bases, (void*)d_kslot})
@@ -641,6 +652,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   b->n_blocks = std::min(b->ctx->n_cu, kMaxFoldBlocks);
   bqsr_status st;
   if ((st = dalloc(b->allocs, &b->d_hq, (size_t)b->n_blocks * kQBins)) != BQSR_OK) return st;
+  if ((st = dalloc(b->allocs, &b->d_qmask, 4)) != BQSR_OK) return st;
   {  // the fold's buffers (bqsr_fold.hip)
     FoldParams& F = b->fold;
     const size_t nt = (size_t)std::max<int64_t>(1, b->rd.n_tiles), nbk = (size_t)b->n_blocks;
@@ -1481,6 +1493,21 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.mm = t->mm();
     P.part_stride = 2 * P.w.qw * P.wcells + P.w.qw;
     const bool fused = lean && b->fused_pending;
+    // bucketed: bqsr_fold_hist makes the fold's histograms from prep's trims,
+    // so the fold runs beside the observe kernel (cfg4: 1.4 ms of fold_hist
+    // and 0.8 ms of fold hidden, the observe kernel 1.6 ms slower beside
+    // them).  In read order the histograms are the observe kernel's, and a
+    // fork after it would only hide bqsr_window_reduce (17 us on cfg2) at
+    // the price of two event records (~15 us each on this runtime)
+    if (!lean) {
+      if (!b->side) {
+        HIP_TRY(hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&b->ev_obs, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&b->ev_fold, hipEventDisableTiming));
+      }
+      HIP_TRY(hipEventRecord(b->ev_obs, s));
+      b->obs_pending = true;
+    }
     // slabs w + key; a fused observe's list pass writes a second set
     const size_t need = (size_t)P.part_stride * (b->pass_blocks() + b->n_keys - 1) * (fused ? 2 : 1);
     if (b->part_words < need) {  // grows with the table geometry; kept across calls
@@ -1526,6 +1553,18 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   }
   if (stages & BQSR_STAGE_FOLD) {
     if (b->fused_pending) return fail(BQSR_ERR_INVALID_ARG, "observe fold before the observe kernel");
+    // bucketed: on the side stream after prep, concurrent with the observe
+    // kernel and bqsr_window_reduce (the fold reads the quals in read order
+    // and resolves deferred trims itself, resolve_info, as observe does; the
+    // observe kernel writes the same trims back) -- the caller's stream
+    // waits at the end
+    const hipStream_t caller = s;
+    const bool fork = b->obs_pending;
+    if (fork) {
+      HIP_TRY(hipStreamWaitEvent(b->side, b->ev_obs, 0));
+      s = b->side;
+      b->obs_pending = false;
+    }
     if (b->bucketed) {  // the observe kernel did not walk the fold's blocks in read order: their histograms
       HIP_TRY(hipMemsetAsync(b->d_hq, 0, (size_t)b->n_blocks * kQBins * 4, s));
       hipLaunchKernelGGL(bqsr_fold_hist, dim3(b->n_blocks * kFhSplit), dim3(kFhWaves * 64), fold_hist_lds(), s, b->rd, (const ReadInfo*)b->d_info,
@@ -1539,12 +1578,18 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     F.pow10 = ctx->d_pow10;
     F.n_blocks = b->n_blocks;
     F.em_out = b->d_em;
+    F.qmask = b->d_qmask;
     hipLaunchKernelGGL(bqsr_fold_plan, dim3(1), dim3(1024), 0, s, F);
     const int64_t max_tpb = (b->rd.n_tiles + b->n_blocks - 1) / b->n_blocks + 1;
     hipLaunchKernelGGL(bqsr_fold_tiles, dim3(ctx->n_cu * 4), dim3(kFtWaves * 64), 0, s, F, max_tpb);
     hipLaunchKernelGGL(bqsr_fold_segs, dim3(b->n_blocks), dim3(kSegThreads), 0, s, F);
     hipLaunchKernelGGL(bqsr_fold_chain, dim3(1), dim3(1024), chain_lds(b->n_blocks), s, F);
     HIP_TRY(hipGetLastError());
+    b->hq_valid = true;
+    if (fork) {
+      HIP_TRY(hipEventRecord(b->ev_fold, s));
+      HIP_TRY(hipStreamWaitEvent(caller, b->ev_fold, 0));
+    }
   }
   return ok();
 }
@@ -1887,6 +1932,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   }
   P.chars = b->d_chars;
   P.rowbad = (uint32_t*)(b->d_chars + (size_t)P.piece_stride * (size_t)b->n_base);
+  P.qmask = b->hq_valid ? b->d_qmask : nullptr;
   const bool lut_stage = (stages & BQSR_STAGE_LUT) || ((stages & BQSR_STAGE_KERNEL) && !(stages & BQSR_STAGE_NO_LUT));
   if (lut_stage) {
     HIP_TRY(hipMemsetAsync(P.rowbad, 0, (size_t)b->n_base * 16, s));

@@ -94,8 +94,10 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
   __shared__ double wsum[16];
   __shared__ int64_t wcnt[16];
   __shared__ int32_t wc[16];
+  __shared__ uint32_t qm[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int q = tid; q < kQBins; q += 1024) t[q] = P.pow10[q];
+  if (tid < 4) qm[tid] = 0;
   __syncthreads();
   const int nb = P.n_blocks;
   // (1) per block: real sum and count
@@ -108,6 +110,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
       uint4 v[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = row[i];
+      uint32_t used = 0;  // bins part * 32 + k holding a base
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t h[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
@@ -115,8 +118,10 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
         for (int j = 0; j < 4; ++j) {
           re += (double)h[j] * t[part * 32 + i * 4 + j];
           n += h[j];
+          used |= (h[j] != 0u ? 1u : 0u) << (i * 4 + j);
         }
       }
+      if (used) atomicOr(&qm[part], used);
     }
     re += __shfl_xor(re, 1);
     re += __shfl_xor(re, 2);
@@ -128,6 +133,7 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_plan(FoldParams P) 
     }
   }
   __syncthreads();
+  if (tid < 4 && P.qmask) P.qmask[tid] = qm[tid];
   // (2) exclusive prefix of the real sums in block order (thread = block)
   {
     const double v0 = tid < nb ? sre[tid] : 0.0;

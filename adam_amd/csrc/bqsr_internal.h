@@ -278,6 +278,8 @@ struct FoldParams {
   int64_t stream_cap;
   unsigned long long* stream_used;
   double* em_out;            // [1]
+  uint32_t* qmask;           // [4] the histograms' bins holding a base (apply skips its
+                             // clean-row test for folded reads when they all lie in clean rows)
 };
 
 // errorProbabilityToPhred by buckets: p's binade (unbiased exponent
@@ -319,6 +321,7 @@ struct ApplyParams {
   const uint8_t* chars;   // [n_keys][piece_stride] the pieces' char tables (bqsr_apply_chars)
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
+  const uint32_t* qmask;  // [4] qual bins of the batch's folded bases (FoldParams::qmask), or null
 };
 
 // finalize results read back by the host

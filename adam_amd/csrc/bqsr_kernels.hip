@@ -964,12 +964,12 @@ __device__ __forceinline__ void prep_store_words(const PrepParams& P, int64_t r,
 // read): no second launch waiting for every workgroup of this one, and the
 // listed reads' latency chains overlap other workgroups' lock-step work.
 // With word stores they wait for bqsr_prep_complex, whose atomics must land
-// on words every workgroup has stored.  The atomic form asks for 6 waves per
-// SIMD (80 VGPRs, a few spills, against 90 and 5: cfg2 prep 0.316 -> 0.308
-// ms, cfg4 0.616 -> 0.593); the store form keeps its 104 (at 6 waves it ran
-// 2.08 -> 3.08 ms on cfg3).
+// on words every workgroup has stored.  The atomic form asks for 5 waves per
+// SIMD (round 5, with the indel fast path's registers: 329.5 -> 317.6 us
+// cfg2 against 6 waves; round 4 had 6 against 5); the store form keeps its
+// 104 VGPRs (at 6 waves it ran 2.08 -> 3.08 ms on cfg3).
 template <bool kStore>
-__global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 6) bqsr_prep_kernel(PrepParams P) {
+__global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 5) bqsr_prep_kernel(PrepParams P) {
   __shared__ uint32_t list[kPrepChunk];
   __shared__ uint32_t cnt;
   __shared__ uint32_t s_cig[kStore ? 1 : kPrepThreads * kPrepCigStride];
@@ -1263,6 +1263,13 @@ __device__ __forceinline__ void ctx_table_fill(uint16_t* t, int tid, int nthread
 }
 typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const uint16_t* LdsHalves;
+// tb + 2 x in one instruction (the compiler's form of the same sum was a
+// shift, a mask and an add: 8 VALU a chunk more)
+__device__ __forceinline__ uint32_t lshl1_add(uint32_t x, uint32_t tb) {
+  uint32_t r;
+  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(tb));
+  return r;
+}
 // raw window (lo: codes 0..15, hi: code 16) of a chunk -> its 16 slots;
 // tb = LDS address of the table half (forward, or reverse for neg reads)
 __device__ __forceinline__ void ctx_lookup(uint64_t lo, uint32_t hi, uint32_t tb, bool neg, uint32_t xo[4]) {
@@ -1275,8 +1282,8 @@ __device__ __forceinline__ void ctx_lookup(uint64_t lo, uint32_t hi, uint32_t tb
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
     u16x2v v;
-    v.x = *(LdsHalves)(uintptr_t)(tb + 2u * ix[2 * w]);
-    v.y = *(LdsHalves)(uintptr_t)(tb + 2u * ix[2 * w + 1]);
+    v.x = *(LdsHalves)(uintptr_t)lshl1_add(ix[2 * w], tb);
+    v.y = *(LdsHalves)(uintptr_t)lshl1_add(ix[2 * w + 1], tb);
     X[w] = __builtin_bit_cast(uint32_t, v);
   }
   const uint32_t sel = neg ? 0x04050607u : 0x03020100u;  // bytes of X[3 - w] reversed, or X[w]
@@ -1331,6 +1338,10 @@ __device__ __forceinline__ void chunk_ctx(const ReadsDev& rd, bool neg, int64_t 
   ctx_lookup(lo, hi, neg ? tb + 2u * kCtxTab : tb, neg, xo);
 }
 
+// the low 16 bits of x mirrored (bit p <- bit 15 - p) when rev
+__device__ __forceinline__ uint32_t mirror_bits16(uint32_t x, bool rev) {
+  return rev ? (__builtin_bitreverse32(x & 0xFFFFu) >> 16) : (x & 0xFFFFu);
+}
 // 16 bytes of x mirrored (byte k <- byte 15 - k) when sel = 0x04050607 (0x03020100: as is)
 __device__ __forceinline__ void mirror16(uint32_t x[4], uint32_t sel) {
   const uint32_t y0 = __builtin_amdgcn_perm(x[3], x[0], sel), y1 = __builtin_amdgcn_perm(x[2], x[1], sel);
@@ -1969,14 +1980,22 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_
     any |= ok;
   }
   for (int k = tid; k < g.K; k += blockDim.x) key_ok[k] = touched[k] != 0;
-  s_go[tid] = go;
-  s_gm[tid] = gm;
-  s_any[tid] = any;
+  // integer sums: the order is immaterial (wavefront sums, then the four)
+  for (int off = 32; off > 0; off >>= 1) {
+    go += __shfl_xor(go, off);
+    gm += __shfl_xor(gm, off);
+    any |= __shfl_xor(any, off);
+  }
+  if ((tid & 63) == 0) {
+    s_go[tid >> 6] = go;
+    s_gm[tid >> 6] = gm;
+    s_any[tid >> 6] = any;
+  }
   __syncthreads();
   if (tid == 0) {
     go = gm = 0;
     any = 0;
-    for (int i = 0; i < (int)blockDim.x; ++i) {  // integer sums: the order is immaterial
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
       go += s_go[i];
       gm += s_gm[i];
       any |= s_any[i];
@@ -2084,6 +2103,8 @@ struct ApplyPiece {
   uint32_t tb;         // LDS address of the context table
   int clean_lo, clean_hi;  // quals whose rows hold no 0 entry
   bool all_cycles;     // the window holds every cycle cell (read order)
+  bool folded_clean;   // every qual of every folded base lies in [clean_lo, clean_hi): a folded
+                       // (kInfoObs) read's chunks skip the clean-row test
 };
 
 struct ChunkLoads {
@@ -2147,6 +2168,11 @@ __device__ __forceinline__ uint4 apply_slow(const ApplyParams* Pp, LaneRead x, i
   return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
+// kTest: the per-chunk clean-row test.  Without it (the piece's folded_clean:
+// every folded base's qual in the clean rows) a folded read's offsets need
+// none, and any other read (eligible without an MD tag: its quals are in no
+// histogram) takes the checked path for every offset.
+template <bool kTest>
 __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyParams* Pp, const ApplyPiece& pc,
                                             const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
   if (!on) return;
@@ -2177,7 +2203,10 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     // cell lies outside the window reads some other entry and is flagged
     // below.  The 16 addresses first (a negative table index wraps far above
     // the table and clamps), then the 16 byte reads into 16-bit halves, two
-    // halves per register, merged by byte permutes.
+    // halves per register, merged by byte permutes.  (Reads in processing
+    // order with the cycle step as the ds_read's immediate offset -- 8 byte
+    // permutes against 16 multiply-adds -- measured equal: cfg2 763 vs 753
+    // us, cfg4 3756 vs 3749, round 5.)
     const uint32_t lbase = (uint32_t)(uintptr_t)(LdsBytes)pc.lut;
     const uint32_t amax = lbase + (uint32_t)(pc.qw * pc.cw21 - 1);
     uint32_t ei[kChunk];
@@ -2201,14 +2230,18 @@ __device__ __forceinline__ void apply_chunk(const ApplyParams& P, const ApplyPar
     // per word: bytes whose qual is outside the clean rows (SWAR, per byte
     // no borrow; q >= 128 never is in them) -- entries 0 (key not in the
     // table, a char above 0xFF: the checked path decides) lie only in other
-    // rows -- gathered to one bit per offset
-    const uint32_t lo4 = (uint32_t)pc.clean_lo * 0x01010101u, hi4 = (uint32_t)pc.clean_hi * 0x01010101u;
-    uint32_t badm = 0;
+    // rows -- gathered to one bit per offset.  Skipped (kTest false) when a
+    // folded read's quals are known to be in the clean rows: cfg2 51 us of
+    // the 0.80 ms launch (profiles/r05p_apply_probes.txt)
+    uint32_t badm = kTest ? 0u : ((x.fl & kInfoObs) ? 0u : 0xFFFFu);
+    if (kTest) {
+      const uint32_t lo4 = (uint32_t)pc.clean_lo * 0x01010101u, hi4 = (uint32_t)pc.clean_hi * 0x01010101u;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t v = qd[w] | 0x80808080u;
-      const uint32_t bad = ((qd[w] | ~(v - lo4) | (v - hi4)) & 0x80808080u) >> 7;  // bit 8i: byte i
-      badm |= (bad | (bad >> 7) | (bad >> 14) | (bad >> 21)) << (4 * w);  // bits 0..3 (higher bits: masked below)
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t v = qd[w] | 0x80808080u;
+        const uint32_t bad = ((qd[w] | ~(v - lo4) | (v - hi4)) & 0x80808080u) >> 7;  // bit 8i: byte i
+        badm |= ((bad | (bad >> 7) | (bad >> 14) | (bad >> 21)) & 0xFu) << (4 * w);  // offsets 4w .. 4w + 3
+      }
     }
     slow = vmask & (cok ? badm : 0xFFFFu);
   }
@@ -2295,7 +2328,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, C = P.g.C, L = P.g.L;
   // LDS: [clean rows 16 B][walk markers][context table][char table]
-  uint32_t* clean_rows = (uint32_t*)smem;  // [lo, hi): quals whose char-table rows hold no 0 entry
+  uint32_t* clean_rows = (uint32_t*)smem;  // [lo, hi): quals whose char-table rows hold no 0 entry; [2] folded_clean
   uint32_t* mk_all = (uint32_t*)(smem + 16);
   uint16_t* ctab = (uint16_t*)(smem + 16 + kMkWords * 4);
   uint8_t* lut = smem + 16 + kMkWords * 4 + kCtxTabBytes;
@@ -2340,10 +2373,20 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
       }
       clean_rows[0] = (uint32_t)(q_lo + best_lo);
       clean_rows[1] = (uint32_t)(q_lo + best_lo + best_n);
+      // the batch's folded quals (bins of the fold histograms) all in the clean rows?
+      uint32_t fc = 0;
+      if (P.qmask) {
+        const uint4 qm = *(const uint4*)P.qmask;
+        const uint32_t qw4[4] = {qm.x, qm.y, qm.z, qm.w};
+        fc = 1;
+        for (int q = 0; q < kQBins; ++q)
+          if (((qw4[q >> 5] >> (q & 31)) & 1u) && (q < q_lo + best_lo || q >= q_lo + best_lo + best_n)) fc = 0;
+      }
+      clean_rows[2] = fc;
     }
     __syncthreads();
     const ApplyPiece pc{lut, rg_lo, gm.c_lo, gm.cw, gm.cw * kCtxSlots, q_lo, qw, tb, (int)clean_rows[0],
-                        (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C};
+                        (int)clean_rows[1], gm.c_lo == 0 && gm.cw == C, clean_rows[2] != 0};
     const auto fread = [&](LaneRead& x, bool live) {
       if (!live || P.outs_apart) return;
       if (x.fl & kInfoPass) {  // quality string passed through
@@ -2355,12 +2398,21 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
       }
     };
     const auto fload = [&](const LaneRead& x, int j, bool on) { return apply_load(P, x, j, on); };
-    const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
-      apply_chunk(P, &P, pc, x, j, n, on, ld);
-    };
-    chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, false>(P.rd, P.info, P.ord, p0 + 64 * wave, p1,
-                                                                             64 * kWaves, L, lane, mk, fread, fload,
-                                                                             fchunk);
+    // two instances of the walk, picked per piece (uniform): with and
+    // without the clean-row test (a per-lane branch around it cost spills)
+    if (pc.folded_clean) {
+      const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
+        apply_chunk<false>(P, &P, pc, x, j, n, on, ld);
+      };
+      chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, false>(
+          P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk, fread, fload, fchunk);
+    } else {
+      const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ChunkLoads& ld) {
+        apply_chunk<true>(P, &P, pc, x, j, n, on, ld);
+      };
+      chunk_walk<kInfoApp | kInfoAppCheck | kInfoPass, kApplyU, ChunkLoads, false>(
+          P.rd, P.info, P.ord, p0 + 64 * wave, p1, 64 * kWaves, L, lane, mk, fread, fload, fchunk);
+    }
   }  // pieces
 }
 

@@ -39,11 +39,6 @@ constexpr uint32_t kT2lo = 0x100C0804u, kT2hi = 0x00000054u;   // (idx(b) + 1) x
 constexpr uint32_t kT1clo = 0x10203040u, kT2clo = 0x04080C10u;  // complemented (A<->T, C<->G)
 constexpr uint32_t kPermId = 0x03020100u, kPermRev = 0x04050607u;
 
-// the 16 bits of x mirrored (bit p <- bit 15 - p) when rev
-__device__ __forceinline__ uint32_t mirror_bits16(uint32_t x, bool rev) {
-  return rev ? (__builtin_bitreverse32(x) >> 16) : (x & 0xFFFFu);
-}
-
 // bytes k of 16 with klo <= k < khi set to 0xFF (k as byte k & 3 of word k >> 2)
 __device__ __forceinline__ uint32_t byte_range(int w, int klo, int khi) {
   const int a = min(max(klo - 4 * w, 0), 4), b = min(max(khi - 4 * w, 0), 4);
