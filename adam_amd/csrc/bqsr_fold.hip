@@ -49,7 +49,7 @@ namespace bqsr {
 constexpr double kFoldSeqLimit = 0.0625;  // below, binades change every few additions: events only
 constexpr double kTwo53 = 9007199254740992.0;
 constexpr int kChainLdsSegs = 384;         // segments prefetched into the chain's LDS
-constexpr int kSegThreads = 512, kSegWaves = kSegThreads / 64;  // bqsr_fold_segs workgroup
+constexpr int kSegThreads = 1024, kSegWaves = kSegThreads / 64;  // bqsr_fold_segs workgroup (1024: cfg2 49 -> 41 us, r05x)
 constexpr int kChainLdsStream = 80 * 1024;  // stream bytes prefetched into the chain's LDS
 constexpr size_t chain_lds(int n_blocks) {
   return kChainLdsStream + 64 + (size_t)kChainLdsStream / 64 * 2 * sizeof(double) + (size_t)kChainLdsSegs * sizeof(FoldSeg) +
@@ -297,13 +297,26 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
       }
     }
     wave_sync();
+    // the tile's quals, 16 slots per lane and step, every step's load issued
+    // before the first is used (one 4-B load per step and lane was 16
+    // dependent round trips a tile: the kernel took 47 us on cfg2)
     const uint8_t* qt = rd.qual + ts0;
-    for (int s0 = lane * 4; s0 < nslots; s0 += 256) {  // 4 slots per lane and step
-      const uint32_t qw4 = *(const uint32_t*)(qt + s0);  // (the qual column has 32 B of padding)
-      const uint32_t bits = (bm[wv][s0 >> 5] >> (s0 & 31)) & 0xFu;
+    constexpr int kSteps = kTileSlots / (64 * 16);
+    uint4 qv[kSteps];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (((bits >> k) & 1u) && s0 + k < nslots) atomicAdd(&hw[(qw4 >> (8 * k)) & 0x7Fu], 1u);
+    for (int i = 0; i < kSteps; ++i) {
+      const int s0 = 16 * (lane + 64 * i);
+      qv[i] = s0 < nslots ? *(const uint4*)(qt + s0) : make_uint4(0, 0, 0, 0);  // (the qual column has 32 B of padding)
+    }
+#pragma unroll
+    for (int i = 0; i < kSteps; ++i) {
+      const int s0 = 16 * (lane + 64 * i);
+      if (s0 >= nslots) continue;
+      const uint32_t bits = (bm[wv][s0 >> 5] >> (s0 & 31)) & 0xFFFFu;
+      const uint32_t w[4] = {qv[i].x, qv[i].y, qv[i].z, qv[i].w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (((bits >> k) & 1u) && s0 + k < nslots) atomicAdd(&hw[(w[k >> 2] >> (8 * (k & 3))) & 0x7Fu], 1u);
     }
     wave_sync();
     double re = 0.0;
@@ -791,29 +804,39 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_fold_chain(FoldParams P)
   const int64_t used = (int64_t)*P.stream_used;
   const int64_t sl = min(used, (int64_t)kChainLdsStream);
   const int nsl = min((int)*P.seg_used, kChainLdsSegs);
-  // prefetch: every thread issues its loads before any is used
-  for (int q = tid; q < kQBins; q += 1024) t[q] = P.pow10[q];
+  // prefetch: every thread issues its loads before any is used -- through
+  // global-typed pointers (the parameter block's pointers are generic: flat
+  // loads, each waited for with every LDS access before it)
+  typedef const __attribute__((address_space(1))) uint64_t* G64;
+  typedef const __attribute__((address_space(1))) double* GF64;
+  typedef const __attribute__((address_space(1))) int32_t* G32;
+  for (int q = tid; q < kQBins; q += 1024) t[q] = ((GF64)P.pow10)[q];
   for (int i = tid; i < nc; i += 1024) {
-    nseg_l[i] = P.nseg[i];
-    sbase_l[i] = P.seg_base[i];
+    nseg_l[i] = ((G32)P.nseg)[i];
+    sbase_l[i] = ((G32)P.seg_base)[i];
   }
   {
-    const uint64_t* src = (const uint64_t*)P.blk;
+    const G64 src = (G64)P.blk;
     uint64_t* dst = (uint64_t*)blk;
     const int nw = nb * (int)(sizeof(FoldBlock) / 8);
     for (int i = tid; i < nw; i += 1024) dst[i] = src[i];
-    const uint64_t* ss = (const uint64_t*)P.seg;
+    const G64 ss = (G64)P.seg;
     uint64_t* sd = (uint64_t*)segs;
     const int sw = nsl * (int)(sizeof(FoldSeg) / 8);
     for (int i = tid; i < sw; i += 1024) sd[i] = ss[i];
-    const uint4* s4 = (const uint4*)P.streams;
-    uint4* d4 = (uint4*)streams;
+    const G64 s8 = (G64)P.streams;
+    uint64_t* d8 = (uint64_t*)streams;
     const int64_t n16 = (sl + 15) / 16;
 #pragma unroll 4
-    for (int64_t i = tid; i < n16; i += 1024) d4[i] = s4[i];
+    for (int64_t i = tid; i < n16; i += 1024) {
+      const uint64_t a = s8[2 * i], b = s8[2 * i + 1];
+      d8[2 * i] = a;
+      d8[2 * i + 1] = b;
+    }
     const int64_t nc2 = sl / 64 * 2;
+    const GF64 cs = (GF64)P.csum;
 #pragma unroll 2
-    for (int64_t i = tid; i < nc2; i += 1024) csum[i] = P.csum[i];
+    for (int64_t i = tid; i < nc2; i += 1024) csum[i] = cs[i];
   }
   __syncthreads();
   if (tid >= 64) return;  // one wavefront walks the job

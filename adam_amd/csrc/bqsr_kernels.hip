@@ -66,8 +66,11 @@ __device__ __forceinline__ bool md_base(uint8_t c) {
 // every mismatch / deleted position p (relative to start) in order; *total =
 // the reference span the tag describes.  isMatch(p) == p in [0,total) && p
 // was not reported.
-template <class F>
-__device__ bool md_scan(const uint8_t* md, int n, int64_t* total, F&& nonmatch) {
+// (MdPtr / CigPtr below: LDS-typed pointers for the staged copies -- a
+// generic pointer made every byte a flat load, each waited for alone: the
+// per-read path took ~60 us a read)
+template <class MdPtr, class F>
+__device__ bool md_scan(MdPtr md, int n, int64_t* total, F&& nonmatch) {
   int off = 0;
   int64_t pos = 0;
   *total = 0;
@@ -101,7 +104,8 @@ __device__ bool md_scan(const uint8_t* md, int n, int64_t* total, F&& nonmatch) 
 }
 
 // read offset holding reference position p, or -1 (position in no M/X/=/S element)
-__device__ int refpos_to_offset(const uint32_t* cig, int ncig, int64_t unclipped, int64_t p) {
+template <class CigPtr>
+__device__ int refpos_to_offset(CigPtr cig, int ncig, int64_t unclipped, int64_t p) {
   int ro = 0;
   int64_t pos = unclipped;
   for (int i = 0; i < ncig; ++i) {
@@ -220,7 +224,11 @@ constexpr int kPrepCig = 4, kPrepCigStride = 5;
 constexpr int kPrepMd = 32, kPrepMdStride = 9;
 constexpr int kPrepChunk = 2048;  // reads per workgroup of bqsr_prep_kernel (8 per thread)
 
-__device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32_t* s_md) {
+template <class CigPtr, class MdPtr>
+__device__ void prep_one_rest(const PrepParams& P, int64_t r, const ReadMeta& m, const ReadAlign& a, ReadInfo inf,
+                              int st, int en, bool usable, CigPtr cig, MdPtr md);
+
+__device__ __forceinline__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32_t* s_md) {  // (inline: see bqsr_prep_kernel)
   const ReadMeta m = P.rd.meta[r];
   const ReadAlign a = P.rd.align[r];  // issued with the meta load: one round trip for both
   ReadInfo inf{0, 0, 0, 0};
@@ -270,35 +278,51 @@ __device__ void prep_one(const PrepParams& P, int64_t r, uint32_t* s_cig, uint32
     P.info[r] = inf;
     return;
   }
-  const uint32_t* cig = P.rd.cigar + a.cigar_off;
-  const uint8_t* md = P.rd.md + a.md_off;
-  {  // short CIGAR / MD (the common case): stage into this thread's LDS slots
-    const bool sc = a.n_cigar <= kPrepCig, sm = (f & BQSR_F_HAS_MD) && a.md_len <= kPrepMd;
-    uint4 c4 = make_uint4(0, 0, 0, 0), m0 = c4, m1 = c4;
-    if (sc) c4 = *(const uint4*)cig;
-    if (sm) {
-      m0 = *(const uint4*)md;
-      m1 = *(const uint4*)(md + 16);
+  const uint32_t* gcig = P.rd.cigar + a.cigar_off;
+  const uint8_t* gmd = P.rd.md + a.md_off;
+  // short CIGAR / MD (the common case): staged into this thread's LDS slots
+  // and read through LDS-typed pointers; otherwise straight from the columns
+  const bool sc = a.n_cigar <= kPrepCig, sm = !(f & BQSR_F_HAS_MD) || a.md_len <= kPrepMd;
+  typedef __attribute__((address_space(3))) uint32_t* LdsW;
+  typedef const __attribute__((address_space(3))) uint32_t* LdsCW;
+  typedef const __attribute__((address_space(3))) uint8_t* LdsCB;
+  if (sc && sm) {
+    const uint4 c4 = *(const uint4*)gcig;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+    if (f & BQSR_F_HAS_MD) {
+      m0 = *(const uint4*)gmd;
+      m1 = *(const uint4*)(gmd + 16);
     }
-    if (sc) {
-      s_cig[0] = c4.x;
-      s_cig[1] = c4.y;
-      s_cig[2] = c4.z;
-      s_cig[3] = c4.w;
-      cig = s_cig;
-    }
-    if (sm) {
-      s_md[0] = m0.x;
-      s_md[1] = m0.y;
-      s_md[2] = m0.z;
-      s_md[3] = m0.w;
-      s_md[4] = m1.x;
-      s_md[5] = m1.y;
-      s_md[6] = m1.z;
-      s_md[7] = m1.w;
-      md = (const uint8_t*)s_md;
-    }
+    LdsW lc = (LdsW)s_cig, lm = (LdsW)s_md;
+    lc[0] = c4.x;
+    lc[1] = c4.y;
+    lc[2] = c4.z;
+    lc[3] = c4.w;
+    lm[0] = m0.x;
+    lm[1] = m0.y;
+    lm[2] = m0.z;
+    lm[3] = m0.w;
+    lm[4] = m1.x;
+    lm[5] = m1.y;
+    lm[6] = m1.z;
+    lm[7] = m1.w;
+    prep_one_rest(P, r, m, a, inf, st, en, usable, (LdsCW)lc, (LdsCB)lm);
+  } else {
+    prep_one_rest(P, r, m, a, inf, st, en, usable, gcig, gmd);
   }
+}
+
+// prep_one after its checks of the record: the CIGAR / MD walks, errors, the
+// ReadInfo and the bits (cig / md: LDS-typed or global pointers)
+template <class CigPtr, class MdPtr>
+__device__ void prep_one_rest(const PrepParams& P, int64_t r, const ReadMeta& m, const ReadAlign& a, ReadInfo inf,
+                              int st, int en, bool usable, CigPtr cig, MdPtr md) {
+  const uint16_t f = m.flags;
+  auto fail = [&](uint64_t key) {
+    if (usable) report(&P.err[kErrObs], key);
+    report(&P.err[kErrAppPrep], key);
+  };
+  const uint16_t check_fl = (usable ? kInfoObsCheck : 0) | kInfoAppCheck;
   // walk the CIGAR once: clip, read-consuming and reference-consuming lengths
   const int ncig = a.n_cigar;
   int64_t lead = 0, rp_len = 0, ref_len = 0;
@@ -682,18 +706,18 @@ struct FastMd {
   uint64_t lst;
   int64_t md_total;
 };
-__device__ __forceinline__ FastMd fast_md(const uint4 md4, int n, const FastCig& cg, int st, int en) {
+template <int kN>
+__device__ __forceinline__ FastMd fast_md_n(const uint32_t (&w)[kN / 4], int n, const FastCig& cg, int st, int en) {
   // 32-bit arithmetic: `over` marks a digit run past 2^31 - 1 (the tag is
   // then invalid), and the running position saturates at 2^31 - 1, beyond
   // any read's reference span, so the comparisons against it keep their outcome
-  const uint32_t w[4] = {md4.x, md4.y, md4.z, md4.w};
   uint32_t num = 0, pos = 0;
   bool over = false;
   int prev = 0;  // class of the previous byte: 0 none, 1 digit, 2 letter, 3 '^'
   FastMd r{n > 0, en < 256, 0ull, 0};
   uint32_t lsh = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < kN; ++i) {
     const uint32_t c = __builtin_amdgcn_ubfe(w[i >> 2], 8 * (i & 3), 8);
     if (i < n) {
       const uint32_t d = c - '0';
@@ -732,6 +756,10 @@ __device__ __forceinline__ FastMd fast_md(const uint4 md4, int n, const FastCig&
   r.ok &= prev == 1 && !over;  // ends with digits
   r.md_total = (int64_t)min(pos + num, 0x7FFFFFFFu);
   return r;
+}
+__device__ __forceinline__ FastMd fast_md(const uint4 md4, int n, const FastCig& cg, int st, int en) {
+  const uint32_t w[4] = {md4.x, md4.y, md4.z, md4.w};
+  return fast_md_n<16>(w, n, cg, st, en);
 }
 
 // The bits of a common read over [st, en): emit(lo, hi, half) for each range
@@ -818,9 +846,14 @@ __device__ __forceinline__ uint16_t valid_flags(uint16_t f) {
 constexpr uint16_t kFastNeed = BQSR_F_HAS_QUAL | BQSR_F_HAS_RG | BQSR_F_HAS_SEQ | BQSR_F_HAS_CIGAR | BQSR_F_HAS_START |
                                BQSR_F_HAS_REFNAME;
 
-template <bool kStore>
-__device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, const PrepCols& cols,
-                          uint64_t acc_out[kAccWords]) {
+// kLong (the listed reads, after pass 1): MD tags up to 32 bytes (md4b: bytes
+// 16..31) and the read's trim resolved here, so only the mismatch letters
+// inside [st, en) are listed -- a read ending in a Q2 run has every trimmed
+// base in its MD as a mismatch (cfg2's listed reads: ~10 of 2048, prep_one
+// 66 us of the launch)
+template <bool kStore, bool kLong = false>
+__device__ __forceinline__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, const PrepCols& cols,
+                          uint64_t acc_out[kAccWords], uint4 md4b = make_uint4(0, 0, 0, 0)) {
   const ReadMeta m = x.m;
   const ReadAlign a = x.a;
   const uint16_t f = m.flags;
@@ -832,14 +865,24 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
       a.n_cigar > kFastCigOps)
     return false;
   const bool usable = usable_read(f);
-  if (usable && (a.md_len == 0 || a.md_len > 16)) return false;
-  const int st = 0, en = m.lq;  // bits over the whole read (see above)
+  if (usable && (a.md_len == 0 || a.md_len > (kLong ? 32 : 16))) return false;
+  int st = 0, en = m.lq;  // bits over the whole read (see above)
+  if (kLong) {
+    trim_quals(P.rd.qual + m.slot, m.lq, st, en);  // isLowQualityBase, minQuality = 2
+    if (st >= en) return false;
+  }
   const uint32_t cw[kFastCigOps] = {cols.c4.x, cols.c4.y, cols.c4.z, cols.c4.w, cols.c5};
   FastCig c;
   if (!fast_cigar(cw, a.n_cigar, m, a.start, c)) return false;
   const uint64_t rs = m.slot;
   if (usable) {
-    const FastMd md = fast_md(cols.md4, a.md_len, c, st, en);
+    FastMd md;
+    if (kLong) {
+      const uint32_t w[8] = {cols.md4.x, cols.md4.y, cols.md4.z, cols.md4.w, md4b.x, md4b.y, md4b.z, md4b.w};
+      md = fast_md_n<32>(w, a.md_len, c, st, en);
+    } else {
+      md = fast_md(cols.md4, a.md_len, c, st, en);
+    }
     if (!md.ok) return false;  // prep_one raises MD_PARSE at the right offset
     // with known sites (several bits per read, from three sources) the bits
     // are gathered per word first; without, the few bits go straight out
@@ -874,7 +917,7 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
     } else {
       if (a.contig >= 0 && a.contig < P.sites.n_contigs && c.x > 0) return false;  // (sites as unclipped + o)
       if (!md.listed) {  // more than 8 non-matching positions: the tag's per-byte walk
-        if (c.x > 0) return false;
+        if (kLong || c.x > 0) return false;
         const uint32_t w[4] = {cols.md4.x, cols.md4.y, cols.md4.z, cols.md4.w};
         int64_t num = 0, pos = 0;
 #pragma unroll
@@ -901,8 +944,27 @@ __device__ bool prep_fast(const PrepParams& P, int64_t r, const PrepRec& x, cons
         mask_sites_linear(P, a.contig, c.unclipped, st, en, rs);
     }
   }
-  P.info[r] = ReadInfo{0, 0, (uint16_t)(kInfoTrim | valid_flags(f)), 0};
+  P.info[r] = kLong ? ReadInfo{(uint16_t)st, (uint16_t)en, valid_flags(f), 0}
+                    : ReadInfo{0, 0, (uint16_t)(kInfoTrim | valid_flags(f)), 0};
   return true;
+}
+
+// a listed read through prep_fast's long form (own loads, no pipeline); false:
+// prep_one decides
+__device__ __forceinline__ bool prep_long(const PrepParams& P, int64_t r) {
+  PrepRec x{};
+  x.m = P.rd.meta[r];
+  x.a = P.rd.align[r];
+  const uint16_t f = x.m.flags;
+  if (!eligible_read(f) || x.a.n_cigar == 0 || x.a.n_cigar > kFastCigOps || x.a.md_len > 32) return false;
+  PrepCols c{*(const uint4*)(P.rd.cigar + x.a.cigar_off), make_uint4(0, 0, 0, 0), P.rd.cigar[x.a.cigar_off + 4]};
+  uint4 md4b = make_uint4(0, 0, 0, 0);
+  if (usable_read(f) && x.a.md_len > 0) {  // (the columns have 32 B of padding)
+    c.md4 = *(const uint4*)(P.rd.md + x.a.md_off);
+    md4b = *(const uint4*)(P.rd.md + x.a.md_off + 16);
+  }
+  uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
+  return prep_fast<false, true>(P, r, x, c, acc, md4b);
 }
 
 // store_words: the wavefront's sbits words as plain stores (no zeroing
@@ -962,7 +1024,15 @@ __device__ __forceinline__ void prep_store_words(const PrepParams& P, int64_t r,
 // Without word stores (kStore false: a zeroed bitmap, bits OR-ed atomically)
 // the workgroup then finishes its listed reads itself (prep_one, a thread a
 // read): no second launch waiting for every workgroup of this one, and the
-// listed reads' latency chains overlap other workgroups' lock-step work.
+// listed reads' latency chains overlap other workgroups' lock-step work
+// (round 5, cfg2: the listed reads -- ~10 of 2048, the reads ending in a Q2
+// run, whose MD lists every trimmed base as a mismatch -- cost 66 us here
+// and 74 us as bqsr_prep_complex after the pass, 251 + 74 against 317 us).
+// Each listed read first tries prep_fast's long form (prep_long: MD up to 32
+// bytes, the trim resolved so only the letters inside it are listed), which
+// takes those reads without prep_one's per-byte walks; prep_one is forced
+// inline (outlined, the call cost more than the long form saved: 308 -> 465
+// us; inline 267 us, profiles/r05ae_prep_long_ab.txt).
 // With word stores they wait for bqsr_prep_complex, whose atomics must land
 // on words every workgroup has stored.  The atomic form asks for 5 waves per
 // SIMD (round 5, with the indel fast path's registers: 329.5 -> 317.6 us
@@ -1012,7 +1082,8 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 5) bqsr_prep_kernel
   const uint32_t k = cnt;
   if (!kStore) {
     for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads)
-      prep_one(P, (int64_t)list[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
+      if (!prep_long(P, (int64_t)list[i]))
+        prep_one(P, (int64_t)list[i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
     return;
   }
   for (uint32_t i = threadIdx.x; i < k; i += kPrepThreads) P.work[c0 + i] = list[i];
@@ -1032,7 +1103,8 @@ extern "C" __global__ void __launch_bounds__(kComplexThreads) bqsr_prep_complex(
       atomicOr((unsigned long long*)&P.sbits[P.bnd[2 * g + 1]], (unsigned long long)P.bnd[2 * g]);
   }
   for (uint32_t i = threadIdx.x; i < k; i += kComplexThreads)
-    prep_one(P, (int64_t)P.work[c0 + i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
+    if (!prep_long(P, (int64_t)P.work[c0 + i]))
+      prep_one(P, (int64_t)P.work[c0 + i], &s_cig[threadIdx.x * kPrepCigStride], &s_md[threadIdx.x * kPrepMdStride]);
 }
 
 // ------------------------------------------------------- lane-per-read ----

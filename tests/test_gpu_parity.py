@@ -158,6 +158,28 @@ EDGE = [
     rec(cigar="6M1I3M", mismatching_positions="0T8", read_paired=True, second_of_pair=True),
     rec(cigar="3M0I7M", mismatching_positions="10"),  # zero-length insertion: the per-read path
     rec(start=10000, cigar="9M1D1M", mismatching_positions="9^T1", sequence="ACGTACGTAC"),
+    # MD tags of 17..32 bytes: the lock-step form's second 16 bytes (fast_md)
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="3A3C3G3T3A3C3G3T6"),  # 8 letters
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="1A1C1G1T1A1C1G1T1A21"),  # 9: per-read path
+    rec(cigar="10M14D10M", sequence="ACGTACGTAC" * 2, qual="I" * 20, mismatching_positions="10^ACGTACGTACGTAC10"),
+    rec(cigar="2S36M2S", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="0A0C0G0T0A0C0G0T4A19",
+        read_negative_strand=True),
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="0" * 29 + "40"),  # 31 digits
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="20A" + "0" * 29 + "19"),  # 33 bytes
+    # Q2 tails: every trimmed base a mismatch, the tag longer than 16 bytes --
+    # listed in pass 1, then prep's long form (only the letters inside the
+    # trimmed window count)
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 30 + "#" * 10,
+        mismatching_positions="30A0C0G0T0A0C0G0T0A0C0"),
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 30 + "#" * 10, read_negative_strand=True,
+        mismatching_positions="5G24A0C0G0T0A0C0G0T0A0C0"),
+    rec(cigar="3S37M", sequence="ACGT" * 10, qual="#" * 4 + "I" * 26 + "#" * 10,
+        mismatching_positions="0T26A0C0G0T0A0C0G0T0A0"),
+    rec(cigar="40M", sequence="ACGT" * 10, qual="#" * 40, mismatching_positions="30A0C0G0T0A0C0G0T0A0C0"),
+    rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 36 + "#" * 4,
+        mismatching_positions="1A1C1G1T1A1C1G1T1A1C16A0C0G0T0"),  # 10 letters in the window
+    rec(cigar="20M2I18M", sequence="ACGT" * 10, qual="I" * 30 + "#" * 10,
+        mismatching_positions="28A0C0G0T0A0C0G0T0A0C0"),
 ]
 
 
@@ -179,6 +201,8 @@ def test_edge_cases_split():
     (rec(mismatching_positions="5^4"), "MD_PARSE"),  # '^' without letters
     (rec(mismatching_positions="5^^A4"), "MD_PARSE"),
     (rec(cigar="4M2I4M", mismatching_positions="3AZ4"), "MD_PARSE"),
+    (rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="3A3C3G3T3A3C3G3Z6"), "MD_PARSE"),
+    (rec(cigar="40M", sequence="ACGT" * 10, qual="I" * 40, mismatching_positions="3A3C3G3T3A3C3G3T6^"), "MD_PARSE"),
     (rec(cigar="6M"), "CIGAR_SHORT"),
     (rec(cigar="*"), "CIGAR_SHORT"),
     (rec(cigar="0M10M"), "CIGAR_INVALID"),
