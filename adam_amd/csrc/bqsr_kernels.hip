@@ -1917,30 +1917,36 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
 // ranges) in read order, for bucketed batches whose observe kernel does not
 // walk the fold's blocks.  kFhSplit workgroups per block, each adding its
 // part into hq_block (zeroed first); lanes as in the lane-per-super-chunk
-// passes (2^ls lanes per read, 64 offsets each, 16-B loads), every folded
-// base one LDS atomic into its wavefront's histogram: kFhCopies copies by
-// lane & 15 against same-bin conflicts (8 copies: 1.70 ms on cfg4, 16: 1.43,
-// 32: 1.46; a copy per lane needs 32 KB per wavefront: 2.57), rows kQBins + 1
-// words apart so one bin's copies sit in different LDS banks; a byte past the
-// read's end adds 0 (no branch per byte).  66 KB of LDS: two workgroups per
-// CU.
+// passes (2^ls lanes per read, 64 offsets each, 16-B loads).  The kernel is
+// bound by its LDS atomics (one per base: 8 / 16 / 32 copies per wavefront
+// against same-bin conflicts ran 1.70 / 1.43 / 1.46 ms on cfg4), so a full
+// chunk counts its bases in PAIRS: one atomic on the cell (q[2k], q[2k+1]) of
+// a 64 x 64 pair table (rows 65 words apart, so a cell's bank is qa + qb mod
+// 32, spread over the banks though the quals crowd a few values; a copy per
+// lane parity), half the atomics; the tables are expanded (row sums plus
+// column sums) once per workgroup.  Partial chunks (a read's last) and pairs
+// with a qual >= 64 add single bases to the wavefront's own 128-bin row.
 constexpr int kFhWaves = 8;
 constexpr int kFhSplit = 4;
-constexpr int kFhCopies = 16;
+constexpr int kFhPairStride = 65;
+constexpr int kFhPairWords = 64 * kFhPairStride;
+constexpr int kFhPairCopies = 2;
 constexpr int kFhStride = kQBins + 1;
-constexpr size_t fold_hist_lds() { return (size_t)kFhWaves * kFhCopies * kFhStride * 4; }
+constexpr size_t fold_hist_lds() { return ((size_t)kFhPairCopies * kFhPairWords + (size_t)kFhWaves * kFhStride) * 4; }
 extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(ReadsDev rd, const ReadInfo* info,
                                                                              int32_t n_blocks, int32_t ls,
                                                                              uint32_t* hq_block) {
   extern __shared__ uint32_t fh_smem[];
-  uint32_t* hist = fh_smem;
+  uint32_t* pairs = fh_smem;
+  uint32_t* singles = fh_smem + kFhPairCopies * kFhPairWords;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < kFhWaves * kFhCopies * kFhStride; i += blockDim.x) hist[i] = 0;
+  for (int i = threadIdx.x; i < kFhPairCopies * kFhPairWords + kFhWaves * kFhStride; i += blockDim.x) fh_smem[i] = 0;
   __syncthreads();
   const int blk = blockIdx.x / kFhSplit, part = blockIdx.x - blk * kFhSplit;
   const int64_t b0 = wg_begin(rd, blk, n_blocks), b1 = wg_begin(rd, blk + 1, n_blocks);
   const int64_t r0 = b0 + (b1 - b0) * part / kFhSplit, r1 = b0 + (b1 - b0) * (part + 1) / kFhSplit;
-  uint32_t* hw = hist + (wv * kFhCopies + (lane & (kFhCopies - 1))) * kFhStride;
+  uint32_t* pw = pairs + (lane & (kFhPairCopies - 1)) * kFhPairWords;
+  uint32_t* sw = singles + wv * kFhStride;
   const int sub = lane & ((1 << ls) - 1), rl = lane >> ls, rpw = 64 >> ls;
   for (int64_t g0 = r0 + (int64_t)rpw * wv; g0 < r1; g0 += (int64_t)rpw * kFhWaves) {
     const int64_t r = g0 + rl;
@@ -1962,18 +1968,37 @@ extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(Reads
 #pragma unroll
       for (int i = 0; i < kSub; ++i) {
         const int m = n - j0 - kChunk * i;  // valid bytes of chunk i (all when >= 16)
-        const uint32_t vm = m >= kChunk ? 0xFFFFu : (m > 0 ? (1u << m) - 1u : 0u);
         const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        if (m >= kChunk) {
+          const bool low = (((w[0] | w[1] | w[2] | w[3]) & 0xC0C0C0C0u) == 0u);  // every qual < 64
+          if (low) {
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k)  // (a byte past the end adds 0: no branch per byte)
-          atomicAdd(&hw[__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 7)], __builtin_amdgcn_ubfe(vm, k, 1));
+            for (int k = 0; k < kChunk; k += 2) {
+              const uint32_t qa = __builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 6);
+              const uint32_t qb = __builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3) + 8, 6);
+              atomicAdd(&pw[__mul24(qa, (uint32_t)kFhPairStride) + qb], 1u);
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < kChunk; ++k) atomicAdd(&sw[__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 7)], 1u);
+          }
+        } else if (m > 0) {
+#pragma unroll
+          for (int k = 0; k < kChunk; ++k)  // (a byte past the end adds 0: no branch per byte)
+            atomicAdd(&sw[__builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 7)], k < m ? 1u : 0u);
+        }
       }
     }
   }
   __syncthreads();
   for (int q = threadIdx.x; q < kQBins; q += blockDim.x) {
     uint32_t s = 0;
-    for (int i = 0; i < kFhWaves * kFhCopies; ++i) s += hist[i * kFhStride + q];
+    for (int i = 0; i < kFhWaves; ++i) s += singles[i * kFhStride + q];
+    if (q < 64)
+      for (int c = 0; c < kFhPairCopies; ++c) {
+        const uint32_t* pc = pairs + c * kFhPairWords;
+        for (int o = 0; o < 64; ++o) s += pc[q * kFhPairStride + o] + pc[o * kFhPairStride + q];  // q first, q second
+      }
     if (s) atomicAdd(&hq_block[(int64_t)blk * kQBins + q], s);
   }
 }
