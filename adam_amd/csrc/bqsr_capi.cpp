@@ -346,7 +346,13 @@ struct bqsr_batch {
   uint64_t* d_sbits = nullptr;  // slot bitmap (PrepParams::sbits)
   uint32_t* d_work = nullptr;   // prep worklist (PrepParams::work), count at d_work[n_reads]
   uint64_t* d_bnd = nullptr;    // prep pass 1 wavefront-boundary shares (PrepParams::bnd)
-  int64_t sbits_words = 0;
+  int64_t sbits_words = 0;      // even: the apply kernel clears it 16 B at a time
+  // the bitmap fill before an atomic-form prep is skipped when the last apply
+  // kernel cleared every word (ApplyParams::zero_bits) after the last
+  // atomic-form prep of this batch: 250 MB, ~35 us a cfg2 job
+  bool sbits_zero = false;
+  bool sbits_atomic = false;  // the last prep OR-ed its bits onto a zeroed bitmap
+  bool err_fresh = false;     // bqsr_job_reset_async reset the error words since the last prep
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
   // the prep of this job runs inside the observe kernel (bqsr_observe_lean
@@ -671,7 +677,7 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   }
   if ((st = dalloc(b->allocs, &b->d_err, kErrWords)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_info, (size_t)std::max<int64_t>(1, n))) != BQSR_OK) return st;
-  b->sbits_words = b->rd.n_slots / 32 + 4;  // the per-base passes read 3 words from any slot's word
+  b->sbits_words = (b->rd.n_slots / 32 + 5) & ~(int64_t)1;  // the per-base passes read 3 words from any slot's word
   if ((st = dalloc(b->allocs, &b->d_sbits, (size_t)b->sbits_words)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_em, 2)) != BQSR_OK) return st;
   if ((st = dalloc(b->allocs, &b->d_bnd, (size_t)2 * (size_t)(n / 64 + kPrepChunk / 64 + 1))) != BQSR_OK) return st;
@@ -1382,8 +1388,10 @@ bool fused_prep_ok(const bqsr_batch* b) {
 }
 bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s,
                         bool fuse = false) {
-  HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));
+  if (!b->err_fresh) HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));  // (else the job reset did)
+  b->err_fresh = false;
   b->fused_pending = fuse && fused_prep_ok(b);
+  b->sbits_atomic = false;  // (a fused prep writes its listed reads' words itself)
   if (b->rd.n_reads > 0 && !b->fused_pending) {
     PrepParams P{};
     P.rd = b->rd;
@@ -1394,7 +1402,8 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     // bitmap cost less (cfg2: 0.25 + 0.03 ms against 0.30)
     P.store_words = b->dims.max_len <= 128 && P.sites.n_contigs > 0;
     P.bnd = b->d_bnd;
-    if (!P.store_words) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
+    if (!P.store_words && !b->sbits_zero) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
+    b->sbits_atomic = !P.store_words;
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.err = b->d_err;
@@ -1425,6 +1434,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     }
   }
   b->prepped = true;
+  b->sbits_zero = false;
   b->prep_sites = sites;
   return BQSR_OK;
 }
@@ -1943,7 +1953,13 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   if (stages & BQSR_STAGE_KERNEL) {
     if (b->chars_lut != L) return fail(BQSR_ERR_INVALID_ARG, "apply kernel before the LUT stage of this LUT");
     P.outs_apart = b->bucketed;
+    const bool zero = b->sbits_atomic && !b->sbits_zero;
+    if (zero) {  // this job's observe is done with the bitmap: the apply kernel clears it for the next prep
+      P.zero_bits = b->d_sbits;
+      P.zero_n16 = b->sbits_words / 2;
+    }
     hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
+    if (zero) b->sbits_zero = true;
     if (P.outs_apart) {
       ApplyParams Q = P;
       Q.rd = b->rd;  // (read order: the batch's own qual column, where a read not yet trimmed is)
@@ -2059,6 +2075,7 @@ bqsr_status bqsr_job_reset_async(bqsr_batch* b, bqsr_table* t, void* stream) {
   const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(1, (n + 255) / 256), (int64_t)b->ctx->n_cu * 8);
   hipLaunchKernelGGL(bqsr_job_reset_kernel, dim3(g), dim3(256), 0, S(stream), t->words, n, b->d_err);
   HIP_TRY(hipGetLastError());
+  b->err_fresh = true;
   return ok();
 }
 

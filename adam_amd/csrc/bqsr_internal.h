@@ -322,6 +322,8 @@ struct ApplyParams {
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
   const uint32_t* qmask;  // [4] qual bins of the batch's folded bases (FoldParams::qmask), or null
+  uint64_t* zero_bits;    // the slot bitmap to clear for the next prep (atomic form), or null
+  int64_t zero_n16;       // its length in 16-B units
 };
 
 // finalize results read back by the host

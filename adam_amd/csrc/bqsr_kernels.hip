@@ -2053,28 +2053,37 @@ extern "C" __global__ void __launch_bounds__(256) bqsr_final_groups(const int64_
   __shared__ int s_any[256];
   // readgroups = keys.sorted.groupBy((t - 1) / 60) (Java division): group r
   // (index r + 1) holds keys 0..60 for r = 0 and 60r+1 .. 60r+60 above; one
-  // thread per group
+  // wavefront per group, a lane per key (a thread walking a group's keys was
+  // a chain of dependent loads: 14 us of cfg2's job)
+  const int lane = tid & 63;
   int64_t go = 0, gm = 0;
   int any = 0;
-  for (int i = tid; i < n_groups; i += blockDim.x) {
+  for (int i = tid >> 6; i < n_groups; i += blockDim.x >> 6) {
     const int r = i - 1;
     int64_t so = 0, sm = 0;
     int ok = 0;
     if (r >= 0) {
-      const int k0 = r == 0 ? 0 : kMaxQ * r + 1, k1 = min(g.K - 1, kMaxQ * r + kMaxQ);
-      for (int k = k0; k <= k1; ++k) {
-        if (!touched[k]) continue;
+      const int k0 = r == 0 ? 0 : kMaxQ * r + 1, k1 = min(g.K - 1, kMaxQ * r + kMaxQ);  // at most 61 keys
+      const int k = k0 + lane;
+      if (k <= k1 && touched[k]) {
         ok = 1;
-        so += qk_obs[k];
-        sm += qk_mm[k];
+        so = qk_obs[k];
+        sm = qk_mm[k];
       }
     }
-    grp_obs[i] = so;
-    grp_mm[i] = sm;
-    grp_ok[i] = (uint8_t)ok;
-    go += so;
-    gm += sm;
-    any |= ok;
+    for (int off = 32; off > 0; off >>= 1) {
+      so += __shfl_xor(so, off);
+      sm += __shfl_xor(sm, off);
+      ok |= __shfl_xor(ok, off);
+    }
+    if (lane == 0) {
+      grp_obs[i] = so;
+      grp_mm[i] = sm;
+      grp_ok[i] = (uint8_t)ok;
+      go += so;
+      gm += sm;
+      any |= ok;
+    }
   }
   for (int k = tid; k < g.K; k += blockDim.x) key_ok[k] = touched[k] != 0;
   // integer sums: the order is immaterial (wavefront sums, then the four)
@@ -2440,6 +2449,11 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
   const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
   ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
+  if (P.zero_bits) {  // the slot bitmap, read by this job's observe only: cleared for the next prep (no fill pass)
+    const int64_t z0 = P.zero_n16 * blockIdx.x / G, z1 = P.zero_n16 * (blockIdx.x + 1) / G;
+    uint4* z = (uint4*)P.zero_bits;
+    for (int64_t i = z0 + tid; i < z1; i += blockDim.x) z[i] = make_uint4(0, 0, 0, 0);
+  }
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));

@@ -59,3 +59,42 @@ def test_default_fronts_full_parity():
     assert np.float64(em).tobytes() == np.float64(oem).tobytes()
     bad, first = O.compare_device_output(b, out, out_len, q, st, ln, exc)
     assert bad == 0, first
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n_rg,lens", [(1, (100,)), (6, (150, 250))])
+def test_repeated_jobs_bitmap_cleared_by_apply(n_rg, lens):
+    # from the second job on, an atomic-form prep finds the slot bitmap cleared
+    # by the last job's apply kernel (ApplyParams::zero_bits) instead of a fill
+    # pass.  One resident batch, jobs with known sites, without, with again:
+    # site bits left from a job would mask bases of the next one.  (100 bp:
+    # the sites job stores whole words, the other needs the fill; 150/250 bp:
+    # every job atomic, the second relies on the clear.)  Each job against
+    # the oracle.
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    from adam_amd import bqsr, synth
+    from adam_amd.job import ResidentJob
+    b = synth.generate(300_000, lens, n_rg, seed=77)
+    sites = synth.known_sites(400_000, seed=78)
+    snp = bqsr.SnpTable(sites)
+    dims = bqsr.dims_of([b])
+    od = O.Dims(dims.n_rg, dims.max_len)
+    want = {True: O.bqsr(b, O.Sites(sites), od, n_parts=1, nthreads=16, fold1=True),
+            False: O.bqsr(b, None, od, n_parts=1, nthreads=16, fold1=True)}
+    job = ResidentJob(b, dims, snp, 0)
+    sites_h = job.sites_h
+    try:
+        for with_sites in (True, False, True, False):
+            job.sites_h = sites_h if with_sites else None
+            job.step()
+            words, em, q, st, ln, exc = job.results()
+            ow, oem, out, out_len = want[with_sites]
+            assert np.array_equal(words, ow), with_sites
+            assert np.float64(em).tobytes() == np.float64(oem).tobytes()
+            bad, first = O.compare_device_output(b, out, out_len, q, st, ln, exc)
+            assert bad == 0, first
+    finally:
+        job.close()
