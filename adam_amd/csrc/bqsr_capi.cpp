@@ -347,11 +347,6 @@ struct bqsr_batch {
   uint32_t* d_work = nullptr;   // prep worklist (PrepParams::work), count at d_work[n_reads]
   uint64_t* d_bnd = nullptr;    // prep pass 1 wavefront-boundary shares (PrepParams::bnd)
   int64_t sbits_words = 0;      // even: the apply kernel clears it 16 B at a time
-  // the bitmap fill before an atomic-form prep is skipped when the last apply
-  // kernel cleared every word (ApplyParams::zero_bits) after the last
-  // atomic-form prep of this batch: 250 MB, ~35 us a cfg2 job
-  bool sbits_zero = false;
-  bool sbits_atomic = false;  // the last prep OR-ed its bits onto a zeroed bitmap
   bool err_fresh = false;     // bqsr_job_reset_async reset the error words since the last prep
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
@@ -1391,7 +1386,6 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
   if (!b->err_fresh) HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));  // (else the job reset did)
   b->err_fresh = false;
   b->fused_pending = fuse && fused_prep_ok(b);
-  b->sbits_atomic = false;  // (a fused prep writes its listed reads' words itself)
   if (b->rd.n_reads > 0 && !b->fused_pending) {
     PrepParams P{};
     P.rd = b->rd;
@@ -1402,8 +1396,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     // bitmap cost less (cfg2: 0.25 + 0.03 ms against 0.30)
     P.store_words = b->dims.max_len <= 128 && P.sites.n_contigs > 0;
     P.bnd = b->d_bnd;
-    if (!P.store_words && !b->sbits_zero) HIP_TRY(hipMemsetAsync(b->d_sbits, 0, (size_t)b->sbits_words * 8, s));
-    b->sbits_atomic = !P.store_words;
+    // (the atomic form's workgroups clear their own slots' words first: no fill)
     P.info = b->d_info;
     P.sbits = b->d_sbits;
     P.err = b->d_err;
@@ -1434,7 +1427,6 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     }
   }
   b->prepped = true;
-  b->sbits_zero = false;
   b->prep_sites = sites;
   return BQSR_OK;
 }
@@ -1953,13 +1945,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
   if (stages & BQSR_STAGE_KERNEL) {
     if (b->chars_lut != L) return fail(BQSR_ERR_INVALID_ARG, "apply kernel before the LUT stage of this LUT");
     P.outs_apart = b->bucketed;
-    const bool zero = b->sbits_atomic && !b->sbits_zero;
-    if (zero) {  // this job's observe is done with the bitmap: the apply kernel clears it for the next prep
-      P.zero_bits = b->d_sbits;
-      P.zero_n16 = b->sbits_words / 2;
-    }
     hipLaunchKernelGGL(bqsr_apply_kernel, dim3(b->pass_blocks()), dim3(kBlockThreads), apply_lds(P.w.qw, cw), s, P);
-    if (zero) b->sbits_zero = true;
     if (P.outs_apart) {
       ApplyParams Q = P;
       Q.rd = b->rd;  // (read order: the batch's own qual column, where a read not yet trimmed is)

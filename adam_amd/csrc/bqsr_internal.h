@@ -158,7 +158,7 @@ struct PrepParams {
   ReadsDev rd;
   SitesDev sites;
   ReadInfo* info;      // [n_reads]
-  uint64_t* sbits;     // [n_slots / 32 + 2]: zeroed before the launch, or (store_words) written whole by pass 1
+  uint64_t* sbits;     // [n_slots / 32 + 4]: each workgroup clears its reads' words first, or (store_words) pass 1 writes them whole
   int32_t store_words; // pass 1 stores every sbits word (reads of <= 128 bases), no zeroing, no atomics
   uint64_t* bnd;       // store_words: per wavefront of pass 1 [bits, word] its first read's share of the word the previous wavefront stored
   unsigned long long* err;  // error words
@@ -322,8 +322,6 @@ struct ApplyParams {
   int64_t piece_stride;   // bytes per piece: qw * cw * 21 rounded up to 16
   uint32_t* rowbad;       // [n_keys][4] rows of a piece's char table holding a 0 entry (bit per row)
   const uint32_t* qmask;  // [4] qual bins of the batch's folded bases (FoldParams::qmask), or null
-  uint64_t* zero_bits;    // the slot bitmap to clear for the next prep (atomic form), or null
-  int64_t zero_n16;       // its length in 16-B units
 };
 
 // finalize results read back by the host

@@ -1044,16 +1044,45 @@ __global__ void __launch_bounds__(kPrepThreads, kStore ? 1 : 5) bqsr_prep_kernel
   __shared__ uint32_t cnt;
   __shared__ uint32_t s_cig[kStore ? 1 : kPrepThreads * kPrepCigStride];
   __shared__ uint32_t s_md[kStore ? 1 : kPrepThreads * kPrepMdStride];
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
+  __shared__ uint64_t s_rng[2];
   const int64_t n = P.rd.n_reads;
   const int64_t c0 = (int64_t)blockIdx.x * kPrepChunk;
+  if (threadIdx.x == 0) {
+    cnt = 0;
+    if (!kStore) {  // the slots of this workgroup's reads: [slot of c0, slot of the next workgroup's first)
+      s_rng[0] = c0 < n ? P.rd.meta[c0].slot : P.rd.n_slots;
+      s_rng[1] = c0 + kPrepChunk < n ? P.rd.meta[c0 + kPrepChunk].slot : P.rd.n_slots;
+    }
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   // software pipeline: the record of the read two iterations ahead and the
   // CIGAR / MD of the next one load while this one is worked
   const int64_t rt = c0 + threadIdx.x;
   PrepRec x0 = prep_rec(P, rt), x1 = prep_rec(P, rt + kPrepThreads);
   PrepCols k0 = prep_cols(P, x0);
+  if (!kStore) {
+    // the bitmap words of this workgroup's slots cleared before its ORs, so
+    // no fill pass precedes the launch: whole words by plain stores, the two
+    // shared with the neighbours' ranges by an AND of this range's bits (a
+    // neighbour's own bits are never cleared, whatever the order).  (The
+    // words' writes cost ~55 us on cfg2 wherever they go -- fill kernel,
+    // apply kernel -- here they overlap the pass's loads.)
+    const uint64_t sa = s_rng[0], sb = s_rng[1];
+    const uint64_t wa = (sa + 31) >> 5, wb = sb >> 5;
+    for (uint64_t w = wa + threadIdx.x; w < wb; w += kPrepThreads) P.sbits[w] = 0ull;
+    if (threadIdx.x < 2 && sa < sb) {
+      const uint64_t w = threadIdx.x == 0 ? sa >> 5 : (sb - 1) >> 5;  // the first / last word
+      const uint64_t lo = max(sa, w << 5) - (w << 5), hi = min(sb, (w << 5) + 32) - (w << 5);
+      const bool part = lo > 0 || hi < 32;  // (a whole word was stored above)
+      const bool mine = threadIdx.x == 0 || (sb - 1) >> 5 != sa >> 5;  // (one word: thread 0's)
+      if (part && mine) {
+        const uint64_t m = (uint64_t)((hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u));
+        atomicAnd((unsigned long long*)&P.sbits[w], (unsigned long long)~(m | (m << 32)));
+      }
+    }
+    __syncthreads();
+  }
   for (int i = 0; i < kPrepChunk; i += kPrepThreads) {
     const int64_t r = rt + i;
     const PrepRec x2 = i + 2 * kPrepThreads < kPrepChunk ? prep_rec(P, r + 2 * kPrepThreads) : PrepRec{};
@@ -2449,11 +2478,6 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_apply_kernel(Ap
   const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
   const int nk = order_keys(P.ord);
   ctx_table_fill(ctab, tid, blockDim.x);  // ready at the piece loop's first barrier
-  if (P.zero_bits) {  // the slot bitmap, read by this job's observe only: cleared for the next prep (no fill pass)
-    const int64_t z0 = P.zero_n16 * blockIdx.x / G, z1 = P.zero_n16 * (blockIdx.x + 1) / G;
-    uint4* z = (uint4*)P.zero_bits;
-    for (int64_t i = z0 + tid; i < z1; i += blockDim.x) z[i] = make_uint4(0, 0, 0, 0);
-  }
 
   for (int key = wa < wb ? key_at(P.ord, wa) : nk; key < nk; ++key) {
     const int64_t p0 = max(wa, key_begin(P.ord, P.rd.n_reads, key));

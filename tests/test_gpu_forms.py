@@ -64,14 +64,13 @@ def test_default_fronts_full_parity():
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("n_rg,lens", [(1, (100,)), (6, (150, 250))])
-def test_repeated_jobs_bitmap_cleared_by_apply(n_rg, lens):
-    # from the second job on, an atomic-form prep finds the slot bitmap cleared
-    # by the last job's apply kernel (ApplyParams::zero_bits) instead of a fill
-    # pass.  One resident batch, jobs with known sites, without, with again:
-    # site bits left from a job would mask bases of the next one.  (100 bp:
-    # the sites job stores whole words, the other needs the fill; 150/250 bp:
-    # every job atomic, the second relies on the clear.)  Each job against
-    # the oracle.
+def test_repeated_jobs_bitmap_cleared(n_rg, lens):
+    # each atomic-form prep workgroup clears its own slots' bitmap words
+    # before its ORs (no fill pass, nothing carried between jobs).  One
+    # resident batch, jobs with known sites, without, with again: site bits
+    # left in a word from one job would mask bases of the next.  (100 bp: the
+    # sites jobs store whole words, the others clear; 150/250 bp: every job
+    # atomic.)  Each job against the oracle.
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
