@@ -51,14 +51,12 @@ class Context:
 
     # bqsr_context_tune knobs (include/adam_bqsr.h): layout choices of the
     # batches created afterwards, for tests and A/B runs; None = leave as is
-    _KNOBS = {"order": 1, "fronts": 2, "key_major": 3, "fused_prep": 4}
-    _DEFAULTS = {"order": -1, "fronts": -1, "key_major": 1, "fused_prep": 0}
+    _KNOBS = {"order": 1, "fronts": 2, "key_major": 3}
+    _DEFAULTS = {"order": -1, "fronts": -1, "key_major": 1}
 
     def tune(self, **knobs) -> Dict[str, int]:
         """Set layout knobs (order: -1 auto / 0 read / 1 read-group buckets;
-        fronts: -1 auto / 0 none / f; key_major: 1 / 0; fused_prep: 1 prep
-        inside the observe kernel where it applies / 0 its own kernel);
-        returns the settings they replace."""
+        fronts: -1 auto / 0 none / f; key_major: 1 / 0); returns the settings they replace."""
         cur = getattr(self, "_tuned", dict(self._DEFAULTS))
         prev = {}
         for k, v in knobs.items():

@@ -255,7 +255,6 @@ struct bqsr_context {
   int tune_order = -1;
   int tune_fronts = -1;
   int tune_keymajor = 1;
-  int tune_fused = 0;
 };
 
 namespace {
@@ -350,9 +349,6 @@ struct bqsr_batch {
   bool err_fresh = false;     // bqsr_job_reset_async reset the error words since the last prep
   bool prepped = false;
   const bqsr_sites* prep_sites = nullptr;
-  // the prep of this job runs inside the observe kernel (bqsr_observe_lean
-  // kLeanFused + kLeanList), which the KERNEL stage launches next
-  bool fused_pending = false;
   // per-call scratch
   uint32_t* d_hq = nullptr;        // [n_blocks][128] fold blocks' qual histograms
   uint32_t* d_qmask = nullptr;     // [4] their bins holding a base (bqsr_fold_plan)
@@ -492,9 +488,8 @@ bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value) {
       if (value < 0 || value > 1) break;
       ctx->tune_keymajor = (int)value;
       return BQSR_OK;
-    case BQSR_TUNE_FUSED_PREP:
-      if (value < 0 || value > 1) break;
-      ctx->tune_fused = (int)value;
+    case BQSR_TUNE_FUSED_PREP:  // (the fused form was removed in round 6: only "off" is accepted)
+      if (value != 0) break;
       return BQSR_OK;
     default:
       return fail(BQSR_ERR_INVALID_ARG, "bqsr_context_tune: unknown knob");
@@ -519,8 +514,7 @@ bqsr_status bqsr_context_create(int device, bqsr_context** out) {
   if (e == hipSuccess) e = hipMemcpy(c->d_qbt, buckets().thr.data(), kQbN * sizeof(double), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(c->d_qbq, buckets().q.data(), kQbN * sizeof(int16_t), hipMemcpyHostToDevice);
   for (const void* f : {(const void*)bqsr_apply_kernel, (const void*)bqsr_observe_chunks,
-                        (const void*)bqsr_observe_lean<true, kLeanPlain>,
-                        (const void*)bqsr_observe_lean<true, kLeanFused>, (const void*)bqsr_observe_lean<true, kLeanList>})
+                        (const void*)bqsr_observe_lean<true>})
     if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)bqsr_fold_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fold_hist_lds());
@@ -1374,19 +1368,13 @@ bqsr_status check_dims(const bqsr_batch* b, const bqsr_table* t) {
 //   BQSR_STAGE_FOLD    the expectedMismatch fold kernel
 // Exposed separately so a caller can bracket one kernel with HIP events.
 namespace {
-// Prep fused into the observe kernel (bqsr_observe_lean kLeanFused): read
-// order, 16-aligned slots, reads of at most 128 bases -- a read's bits then
-// fit one 128-offset step of the lean walk.  No prep launch and no bitmap
-// fill: the lane that observes a common read preps it in registers.
-bool fused_prep_ok(const bqsr_batch* b) {
-  return b->ctx->tune_fused && !b->bucketed && b->rd.slots_aligned && b->dims.max_len <= 128 && b->rd.n_reads > 0;
-}
-bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s,
-                        bool fuse = false) {
+bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* sites, hipStream_t s) {
   if (!b->err_fresh) HIP_TRY(hipMemsetAsync(b->d_err + kErrAppPrep, 0xFF, 8, s));  // (else the job reset did)
   b->err_fresh = false;
-  b->fused_pending = fuse && fused_prep_ok(b);
-  if (b->rd.n_reads > 0 && !b->fused_pending) {
+  // a new prep: the fold's qual mask belongs to the previous job until this
+  // job's fold rewrites it (wrapped device columns may have changed since)
+  b->hq_valid = false;
+  if (b->rd.n_reads > 0) {
     PrepParams P{};
     P.rd = b->rd;
     if (sites) P.sites = sites->dev();
@@ -1441,7 +1429,7 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
   hipStream_t s = S(stream);
   if (stages & BQSR_STAGE_RESET) HIP_TRY(hipMemsetAsync(b->d_err + kErrObs, 0xFF, 8, s));
   if (stages & BQSR_STAGE_PREP) {
-    if ((st = launch_prep(ctx, b, sites, s, true)) != BQSR_OK) return st;
+    if ((st = launch_prep(ctx, b, sites, s)) != BQSR_OK) return st;
   }
   if (b->rd.n_reads == 0) {
     if (stages & BQSR_STAGE_FOLD) HIP_TRY(hipMemsetAsync(b->d_em, 0, 8, s));
@@ -1494,7 +1482,6 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.obs = t->obs();
     P.mm = t->mm();
     P.part_stride = 2 * P.w.qw * P.wcells + P.w.qw;
-    const bool fused = lean && b->fused_pending;
     // bucketed: bqsr_fold_hist makes the fold's histograms from prep's trims,
     // so the fold runs beside the observe kernel (cfg4: 1.4 ms of fold_hist
     // and 0.8 ms of fold hidden, the observe kernel 1.6 ms slower beside
@@ -1510,8 +1497,8 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
       HIP_TRY(hipEventRecord(b->ev_obs, s));
       b->obs_pending = true;
     }
-    // slabs w + key; a fused observe's list pass writes a second set
-    const size_t need = (size_t)P.part_stride * (b->pass_blocks() + b->n_keys - 1) * (fused ? 2 : 1);
+    // slabs w + key
+    const size_t need = (size_t)P.part_stride * (b->pass_blocks() + b->n_keys - 1);
     if (b->part_words < need) {  // grows with the table geometry; kept across calls
       if (b->d_part) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -1527,21 +1514,8 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     P.err = b->d_err + kErrObs;
     P.n_blocks = lean ? b->n_blocks : b->pass_blocks();  // (fronts: a chunk-walk workgroup per piece)
     const size_t lds = lean ? lean_lds(P.w.qw, P.orow, P.wcells) : observe_lds(P.w.qw, P.wcells, true);
-    if (fused) {
-      // the common reads' prep in their lanes, the rest listed; then the
-      // listed reads (prep_one + the same walk) into a second set of slabs
-      if (sites) P.sites = sites->dev();
-      P.sbits_w = b->d_sbits;
-      P.list = b->d_work;
-      P.n_list = b->d_work + b->rd.n_reads + kPrepChunk;
-      hipLaunchKernelGGL((bqsr_observe_lean<true, kLeanFused>), dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
-      ObserveParams Q = P;
-      Q.part = b->d_part + (size_t)P.part_stride * P.n_blocks;
-      const size_t lds_l = std::max<size_t>(lds, (size_t)kBlockThreads * kListThreadWords * 4);
-      hipLaunchKernelGGL((bqsr_observe_lean<true, kLeanList>), dim3(P.n_blocks), dim3(kBlockThreads), lds_l, s, Q);
-      b->fused_pending = false;
-    } else if (lean) {
-      hipLaunchKernelGGL((bqsr_observe_lean<true, kLeanPlain>), dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
+    if (lean) {
+      hipLaunchKernelGGL((bqsr_observe_lean<true>), dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     } else {
       hipLaunchKernelGGL(bqsr_observe_chunks, dim3(P.n_blocks), dim3(kBlockThreads), lds, s, P);
     }
@@ -1549,12 +1523,10 @@ bqsr_status bqsr_observe_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_site
     const int rb = (int)std::min<int64_t>(4096, ((int64_t)P.part_stride * (b->bucketed ? b->n_base : 1) + 255) / 256);
     const unsigned ry = b->bucketed ? 1u : (unsigned)((b->n_blocks + kRedSlabs - 1) / kRedSlabs);
     hipLaunchKernelGGL(bqsr_window_reduce, dim3(rb, ry), dim3(256), 0, s, (const uint32_t*)b->d_part, b->rd, P.ord,
-                       P.n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0,
-                       fused ? 2 : 1);
+                       P.n_blocks, P.part_stride, P.wcells, P.w, P.g, P.touched, P.obs, P.mm, lean ? kCtxJunk : 0);
     HIP_TRY(hipGetLastError());
   }
   if (stages & BQSR_STAGE_FOLD) {
-    if (b->fused_pending) return fail(BQSR_ERR_INVALID_ARG, "observe fold before the observe kernel");
     // bucketed: on the side stream after prep, concurrent with the observe
     // kernel and bqsr_window_reduce (the fold reads the quals in read order
     // and resolves deferred trims itself, resolve_info, as observe does; the
@@ -1885,7 +1857,7 @@ bqsr_status bqsr_apply_stage(bqsr_context* ctx, bqsr_batch* b, const bqsr_lut* L
     HIP_TRY(hipMemsetAsync(b->d_err + kErrAppKern, 0xFF, 8, s));
     HIP_TRY(hipMemsetAsync(b->d_err + kNExc, 0, 8, s));
   }
-  if (!b->prepped || b->fused_pending || (stages & BQSR_STAGE_PREP)) {  // (a fused prep whose observe never ran)
+  if (!b->prepped || (stages & BQSR_STAGE_PREP)) {
     bqsr_status st = launch_prep(ctx, b, nullptr, s);
     if (st != BQSR_OK) return st;
   }

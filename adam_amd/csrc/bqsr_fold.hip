@@ -280,7 +280,7 @@ extern "C" __global__ void __launch_bounds__(kFtWaves * 64) bqsr_fold_tiles(Fold
     ReadInfo inf{0, 0, 0, 0};
     if (lane < nr) {
       m = rd.meta[r0 + lane];
-      inf = resolve_info(rd, P.info[r0 + lane], m.slot, m.lq);
+      inf = resolve_info(rd, info_load(P.info + r0 + lane), m.slot, m.lq);
     }
     const uint64_t ts0 = __shfl(m.slot, 0);
     const int nslots = (int)(__shfl(m.slot + max(m.lq, m.ls), nr - 1) - ts0);
@@ -374,7 +374,7 @@ __device__ void fold_copy_tile(const FoldParams& P, int64_t tl, uint8_t* dst, in
   uint64_t src = 0;
   if (lane < nr) {
     const ReadMeta m = rd.meta[r0 + lane];
-    const ReadInfo inf = resolve_info(rd, P.info[r0 + lane], m.slot, m.lq);
+    const ReadInfo inf = resolve_info(rd, info_load(P.info + r0 + lane), m.slot, m.lq);
     if ((inf.fl & kInfoObs) && inf.en > inf.st) {
       len = inf.en - inf.st;
       src = m.slot + inf.st;
@@ -776,7 +776,7 @@ __device__ __noinline__ double fold_tile_global(const FoldParams& P, double S, i
   int len = 0;
   if (lane < nr) {
     const ReadMeta m = rd.meta[r0 + lane];
-    const ReadInfo inf = resolve_info(rd, P.info[r0 + lane], m.slot, m.lq);
+    const ReadInfo inf = resolve_info(rd, info_load(P.info + r0 + lane), m.slot, m.lq);
     if ((inf.fl & kInfoObs) && inf.en > inf.st) len = inf.en - inf.st;
   }
   int tot = len;

@@ -32,13 +32,28 @@ struct ReadAlign {
 static_assert(sizeof(ReadAlign) == 24, "ReadAlign must be 24 B");
 
 // 8 B per read, written by the prep kernel for the observe / apply passes.
-struct ReadInfo {
+// Invariant: on the device a ReadInfo is read and written as ONE aligned
+// 64-bit access (info_load / info_store).  A bucketed batch's fold runs on a
+// second stream beside bqsr_observe_chunks, which writes deferred trims back
+// (kInfoTrim -> the resolved range) while the fold kernels read the same
+// words: a torn read (new fl without kInfoTrim, old st = en = 0) would drop
+// the read from the fold.  Both sides resolve a kInfoTrim word to the same
+// value, so either whole word is correct.
+struct alignas(8) ReadInfo {
   uint16_t st;  // qualityStartOffset
   uint16_t en;  // qualityEndOffset, or the offset of the read's first error
   uint16_t fl;  // kInfo* bits
   uint16_t pad;
 };
-static_assert(sizeof(ReadInfo) == 8, "ReadInfo must be 8 B");
+static_assert(sizeof(ReadInfo) == 8 && alignof(ReadInfo) == 8, "ReadInfo must be one aligned 8-B word");
+__device__ __forceinline__ ReadInfo info_load(const ReadInfo* p) {
+  const uint64_t v = __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return ReadInfo{(uint16_t)v, (uint16_t)(v >> 16), (uint16_t)(v >> 32), (uint16_t)(v >> 48)};
+}
+__device__ __forceinline__ void info_store(ReadInfo* p, ReadInfo x) {
+  const uint64_t v = (uint64_t)x.st | ((uint64_t)x.en << 16) | ((uint64_t)x.fl << 32) | ((uint64_t)x.pad << 48);
+  __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 constexpr uint16_t kInfoObs = 1;        // usable, valid: its bases go into the table
 constexpr uint16_t kInfoObsCheck = 2;   // usable, fails at `en`: bases before it are only qual-checked
 constexpr uint16_t kInfoApp = 4;        // eligible for recalibration, valid
@@ -217,15 +232,6 @@ struct ObserveParams {
   int32_t orow;        // bqsr_observe_lean: LDS obs row words (nc copies of the cycle and 43 context cells), 2 mod 4
   int32_t nc;          // bqsr_observe_lean: copies of a row's counters (<= 4)
   int32_t rows_all;    // bqsr_observe_lean: every qual of the batch is a window row (host histogram)
-  // bqsr_observe_lean fused with prep (kLeanFused: reads of <= 128 bases in
-  // read order, 16-aligned slots): the common read's prep done in registers
-  // by its lane; the rest listed per workgroup (list[wa + i], i < n_list[w],
-  // wa = the workgroup's first read), their bitmap words zeroed, and taken
-  // by the list pass (kLeanList: prep_one, then the same walk)
-  SitesDev sites;
-  uint64_t* sbits_w;   // the slot bitmap (written: zeroed words / prep_one's bits)
-  uint32_t* list;      // [n_reads]
-  uint32_t* n_list;    // [n_blocks]
 };
 
 // ---- expectedMismatch fold (bqsr_fold.hip) ----

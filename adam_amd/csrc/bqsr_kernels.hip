@@ -1226,7 +1226,7 @@ __device__ __forceinline__ LaneRead lane_read(const ReadsDev& rd, const ReadInfo
   ReadInfo inf{0, 0, 0, 0};
   if (live) {
     m = rd.meta[r];
-    inf = info[r];
+    inf = info_load(info + r);
   }
   const bool trimmed = inf.fl & kInfoTrim;
   const uint64_t qs = ks == ~0ull ? m.slot : ks;
@@ -1717,7 +1717,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
     for (int i = tid; i < 2 * qw * wcells + qw; i += blockDim.x) w_obs[i] = 0;
     __syncthreads();
     const auto fread = [&](LaneRead& x, bool live) {
-      if (live && x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+      if (live && x.trimmed) info_store(P.info + x.r, x.inf);  // fold and apply read the trimmed range
     };
     const auto fload = [&](const LaneRead& x, int j, bool on) { return observe_load(P, x, j, on); };
     const auto fchunk = [&](const LaneRead& x, int j, int n, bool on, const ObsChunkLoads& ld) {
@@ -1751,7 +1751,7 @@ extern "C" __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_chunks(
 // all landed).
 extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd, OrderDev ord, int32_t n_blocks,
                                               int32_t stride, int32_t wcells, Window w, TableGeom g, int64_t* touched,
-                                              int64_t* obs, int64_t* mm, int32_t junk, int32_t sets) {
+                                              int64_t* obs, int64_t* mm, int32_t junk) {
   // fronts: a thread per (base key, word) sums the base key's pieces (slab
   // 2 key of workgroup key), one atomic per table word as without fronts
   const int nk = order_base_keys(ord);
@@ -1781,7 +1781,6 @@ extern "C" __global__ void bqsr_window_reduce(const uint32_t* part, ReadsDev rd,
           // a workgroup with an empty range in between wrote no slab (its words
           // are read but not added: the loads stay independent)
           uint32_t v = part[(b + (ord.perm ? key : 0)) * stride + i];
-          if (sets > 1) v += part[(n_blocks + b) * stride + i];  // (read order: a fused observe's list pass)
           if (max(k0, wg_begin(rd, b, n_blocks)) < min(k1, wg_begin(rd, b + 1, n_blocks))) s += v;
         }
       }
@@ -1983,7 +1982,7 @@ extern "C" __global__ void __launch_bounds__(kFhWaves * 64) bqsr_fold_hist(Reads
     const uint8_t* qp = rd.qual;
     if (r < r1) {
       const ReadMeta m = rd.meta[r];
-      const ReadInfo inf = resolve_info(rd, info[r], m.slot, m.lq);
+      const ReadInfo inf = resolve_info(rd, info_load(info + r), m.slot, m.lq);
       if ((inf.fl & kInfoObs) && inf.en > inf.st) {
         n = inf.en - inf.st;
         qp = rd.qual + m.slot + inf.st;

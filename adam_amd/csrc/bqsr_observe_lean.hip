@@ -90,71 +90,16 @@ __device__ __forceinline__ void lean_clean(const uint32_t q[4], const uint32_t x
   }
 }
 
-// The common read's prep in its lane (kLeanFused): record, CIGAR / MD and
-// the trimmed range (ReadCovariates.scala:30-60, RichADAMRecord.scala:156-187,
-// MdTag.scala:38-98, SnpTable.scala:15-23 -- prep_fast's rules, bits in
-// registers instead of the slot bitmap).  Returns the read's ReadInfo and
-// sets *defer for a read the lane cannot finish (any other CIGAR or MD form,
-// st >= 16, more than 128 bases, a contig without a site bitmap): prep_one
-// takes it in the list pass.  acc: the masked / mismatch bits of offsets 0 ..
-// lq-1 at bit (slot & 31) + o.
-__device__ __forceinline__ ReadInfo fused_prep(const ObserveParams& P, const ReadMeta& m, const ReadAlign& a,
-                                               bool live, uint64_t acc[kAccWords], bool* defer) {
-  const uint16_t f = m.flags;
-  const bool elig = live && eligible_read(f);
-  const bool usable = usable_read(f);
-  const bool cand = elig && (f & kFastNeed) == kFastNeed && !((f & BQSR_F_NEG_STRAND) && (f & kSeqOther)) &&
-                    m.lq > 0 && m.lq <= 128 && a.n_cigar > 0 && a.n_cigar <= kFastCigOps &&
-                    !(usable && (a.md_len == 0 || a.md_len > 16));
-  const PrepCols cols = cand ? prep_cols(P.rd, m, a) : PrepCols{make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), 0u};
-  *defer = false;
-  if (!live) return ReadInfo{0, 0, 0, 0};
-  if (!elig) return ReadInfo{0, 0, kInfoPass, 0};
-  if (!cand) {
-    *defer = true;
-    return ReadInfo{0, 0, 0, 0};
-  }
-  int st, en;
-  trim_quals(P.rd.qual + m.slot, m.lq, st, en);  // isLowQualityBase, minQuality = 2
-  const uint32_t cw[kFastCigOps] = {cols.c4.x, cols.c4.y, cols.c4.z, cols.c4.w, cols.c5};
-  FastCig c;
-  bool ok = fast_cigar(cw, a.n_cigar, m, a.start, c);
-  FastMd md{true, true, 0ull, 0};
-  if (ok && usable) {
-    md = fast_md(cols.md4, a.md_len, c, 0, m.lq);
-    ok = md.ok && md.listed;
-  }
-  if (ok && st < en && st >= 16) ok = false;  // (one 128-offset step from the read's first slot)
-  if (!ok) {
-    *defer = true;
-    return ReadInfo{0, 0, 0, 0};
-  }
-  if (st >= en) return ReadInfo{(uint16_t)st, 0, 0, 0};  // no base is iterated
-  if (usable) {
-    bool linear;
-    fast_bits(P.sites, a.contig, c, md, 0, m.lq, (uint32_t)(m.slot & 31), acc, &linear);
-    if (linear) {
-      *defer = true;
-      return ReadInfo{0, 0, 0, 0};
-    }
-  }
-  return ReadInfo{(uint16_t)st, (uint16_t)en, valid_flags(f), 0};
-}
-
-constexpr int kLeanPlain = 0, kLeanFused = 1, kLeanList = 2;
-constexpr int kListThreadWords = kPrepCigStride + kPrepMdStride;  // kLeanList: prep_one's LDS per thread
-
 // LDS: [obs rows qw][mm rows qw][masked qw][block hist 128][list count]
 // obs rows of P.orow words: nc copies of the C cycle cells, then nc copies of
 // the 43 context cells (21 contexts, 22 junk), padded to 2 mod 4; lane l adds
 // to copy l % nc (same-address adds of a wavefront's lanes -- same qual, same
 // cycle -- split nc ways).  mm rows (rare adds): one copy, wcells = C + 43
 // padded, the slab layout.
-// kMode: kLeanPlain (prep ran before: ReadInfo and the slot bitmap), kLeanFused
-// (the common read's prep in its lane, the rest listed), kLeanList (the listed
-// reads: prep_one, then the walk; its slabs follow the fused pass's, its
-// block histograms are added to the fused pass's)
-template <bool kIdent, int kMode>
+// Prep ran before: ReadInfo and the slot bitmap.  (A form with the common
+// read's prep done in the observing lane -- the "fused prep" -- measured 2.15
+// against 2.06 ms a cfg2 job and was removed in round 6; git history holds it.)
+template <bool kIdent>
 __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams P) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int qw = P.w.qw, cells = P.g.cells, C = P.g.C, L = P.g.L;
@@ -163,7 +108,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   uint32_t* w_mm = w_obs + qw * orow;
   uint32_t* w_masked = w_mm + qw * wcells;
   uint32_t* blk_hist = w_masked + qw;
-  uint32_t& n_def = blk_hist[kQBins];  // kLeanFused: the workgroup's listed reads
   const uint32_t lds_obs = (uint32_t)(uintptr_t)(LdsWords)w_obs, lds_masked = (uint32_t)(uintptr_t)(LdsWords)w_masked;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -182,27 +126,6 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   constexpr bool ident = kIdent;  // P.ord.perm == nullptr
   const int nk = kIdent ? 1 : order_keys(P.ord);
   const int64_t wa = pass_begin(P.rd, P.ord, blockIdx.x, G), wb = pass_begin(P.rd, P.ord, blockIdx.x + 1, G);
-  static_assert(kMode == kLeanPlain || kIdent, "the fused and list passes walk reads in read order");
-  static_assert(NW == kAccWords, "a fused read's bits are one step's bitmap words");
-  int64_t n_list = 0;
-  if (kMode == kLeanList) {
-    // prep_one over the workgroup's listed reads (LDS for its CIGAR / MD
-    // staging, before the window is laid out); their ReadInfo and bitmap bits
-    // then visible to the walk below
-    n_list = P.n_list[blockIdx.x];
-    const PrepParams pp{P.rd, P.sites, P.info, P.sbits_w, 0, nullptr, P.err - kErrObs, nullptr, nullptr};
-    uint32_t* s_cig = (uint32_t*)smem + tid * kPrepCigStride;
-    uint32_t* s_md = (uint32_t*)smem + kBlockThreads * kPrepCigStride + tid * kPrepMdStride;
-    for (int64_t i = tid; i < n_list; i += blockDim.x) prep_one(pp, (int64_t)P.list[wa + i], s_cig, s_md);
-    // workgroup scope: the walk's lanes read what this workgroup's threads
-    // wrote (ReadInfo stores; bitmap ORs, which are device-scope atomics read
-    // back by device-scope loads below).  (An agent-scope __threadfence
-    // writes back the XCD's L2: the pass took 299 us on cfg2 with it.)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  }
-  if (kMode == kLeanFused && tid == 0) n_def = 0;
   for (int i = tid; i < kQBins; i += blockDim.x) blk_hist[i] = 0;
 
   for (int key = kIdent ? 0 : (wa < wb ? key_at(P.ord, wa) : nk); key < nk; ++key) {
@@ -218,41 +141,13 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   for (int i = tid; i < qw * (orow + wcells) + qw; i += blockDim.x) w_obs[i] = 0;
   __syncthreads();
 
-  const int64_t q0 = kMode == kLeanList ? 0 : p0, q1 = kMode == kLeanList ? n_list : p1;
-  for (int64_t g0 = q0 + 64 * wave; g0 < q1; g0 += 64 * kWaves) {
-    const bool live = g0 + lane < q1;
-    uint64_t acc[kAccWords] = {0, 0, 0, 0, 0};
+  for (int64_t g0 = p0 + 64 * wave; g0 < p1; g0 += 64 * kWaves) {
+    const bool live = g0 + lane < p1;
     LaneRead x;
-    if (kMode == kLeanFused) {
-      const int64_t r = g0 + lane;
-      ReadMeta m{0, 0, 0, 0, 0};
-      ReadAlign a{0, 0, 0, 0, 0, 0};
-      if (live) {
-        m = P.rd.meta[r];
-        a = P.rd.align[r];
-      }
-      bool defer;
-      const ReadInfo inf = fused_prep(P, m, a, live, acc, &defer);
-      if (live && !defer) P.info[r] = inf;  // fold and apply read it
-      // a listed read: its bitmap words zeroed here for prep_one's ORs in the
-      // list pass (a neighbour sharing a word reads no bits from it)
-      const uint64_t dm = __builtin_amdgcn_ballot_w64(defer);
-      if (dm) {
-        uint32_t base = 0;
-        if (lane == (int)__builtin_ctzll(dm)) base = atomicAdd(&n_def, (uint32_t)__popcll(dm));
-        base = __shfl(base, (int)__builtin_ctzll(dm));
-        if (defer) {
-          P.list[wa + base + (uint32_t)__popcll(dm & ((1ull << lane) - 1ull))] = (uint32_t)r;
-          const uint64_t w1 = (m.slot + slot_span(m.lq, m.ls) + 31) >> 5;
-          for (uint64_t w = m.slot >> 5; w < w1; ++w) P.sbits_w[w] = 0ull;
-        }
-      }
-      x = lane_decode(live ? r : P.rd.n_reads, m, defer ? ReadInfo{0, 0, 0, 0} : inf, m.slot, L);
-    } else {
-      const int64_t r = !live ? 0 : kMode == kLeanList ? (int64_t)P.list[wa + g0 + lane]
-                                : (kIdent ? g0 + lane : order_read(P.ord, g0 + lane));
+    {
+      const int64_t r = !live ? 0 : (kIdent ? g0 + lane : order_read(P.ord, g0 + lane));
       x = lane_read(P.rd, P.info, r, live, L);
-      if (x.trimmed) P.info[x.r] = x.inf;  // fold and apply read the trimmed range
+      if (x.trimmed) info_store(P.info + x.r, x.inf);  // fold and apply read the trimmed range
     }
     const bool act = x.fl & (kInfoObs | kInfoObsCheck);
     const bool full = x.fl & kInfoObs;
@@ -262,7 +157,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
     const bool rev = x.dir < 0;
     const uint32_t u1lo = neg ? kT2clo : kT1lo, u2lo = neg ? kT1clo : kT2lo;
     const uint32_t sel_q = rev ? kPermRev : kPermId, sel_x = sec ? kPermRev : kPermId;
-    const int jb = (kMode == kLeanFused || P.rd.slots_aligned) ? -(x.st & 15) : 0;
+    const int jb = P.rd.slots_aligned ? -(x.st & 15) : 0;
     const uint8_t* qp = P.rd.qual + x.slot;
     for (int j0 = jb; __builtin_amdgcn_ballot_w64(j0 < n); j0 += kSup) {
       if (j0 >= n) continue;
@@ -280,10 +175,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
       }
 #pragma unroll
       for (int w = 0; w < NW; ++w)
-        bw[w] = kMode == kLeanFused ? (full ? acc[w] : 0ull)  // (the read's first slot is the step's: st < 16)
-                : !(full && (w == 0 || 32 * w - 32 < n - j0)) ? 0ull
-                : kMode == kLeanList ? __hip_atomic_load(&P.sbits[(s0 >> 5) + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : P.sbits[(s0 >> 5) + w];
+        bw[w] = !(full && (w == 0 || 32 * w - 32 < n - j0)) ? 0ull : P.sbits[(s0 >> 5) + w];
 #pragma clang loop unroll(full)
       for (int i = 0; i < kLeanSub; ++i) {
         const int j = j0 + kChunk * i;
@@ -295,7 +187,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
         uint32_t bm = 0, bx = 0;
         uint32_t h[4] = {0x10101010u, 0x10101010u, 0x10101010u, 0x10101010u};  // slot 4
         if (full) {
-          if (kMode == kLeanFused || P.rd.slots_aligned)  // (fused: 16-aligned slots by construction)
+          if (P.rd.slots_aligned)
             sub_bits16<NW>(bw, (uint32_t)(s0 >> 4) & 1u, i, bm, bx);
           else
             sub_bits<NW>(bw, (uint32_t)(s0 & 31), i, bm, bx);
@@ -452,19 +344,10 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
   }
   __syncthreads();
   }  // pieces
-  if (ident) {
-    if (kMode == kLeanList) {  // added to the fused pass's histograms of the same fold block
-      for (int k = tid; k < kQBins; k += blockDim.x)
-        if (blk_hist[k]) atomicAdd(&P.hq_block[(int64_t)blockIdx.x * kQBins + k], blk_hist[k]);
-    } else {
-      for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
-    }
-  }
-  if (kMode == kLeanFused && tid == 0) P.n_list[blockIdx.x] = n_def;
+  if (ident)
+    for (int k = tid; k < kQBins; k += blockDim.x) P.hq_block[(int64_t)blockIdx.x * kQBins + k] = blk_hist[k];
 }
 
-template __global__ void bqsr_observe_lean<true, kLeanPlain>(ObserveParams);
-template __global__ void bqsr_observe_lean<true, kLeanFused>(ObserveParams);
-template __global__ void bqsr_observe_lean<true, kLeanList>(ObserveParams);
+template __global__ void bqsr_observe_lean<true>(ObserveParams);
 
 }  // namespace bqsr

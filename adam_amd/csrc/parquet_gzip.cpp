@@ -631,8 +631,8 @@ bqsr_status rewrite(const uint8_t* in, int64_t n, const char* path, int level, c
     for (auto& p : c.pages) all.push_back(&p);
   std::atomic<size_t> next{0};
   std::atomic<bool> okc{true};
-  auto work = [&]() {
-    for (size_t i; (i = next.fetch_add(1)) < all.size();) {
+  auto work_pages = [&]() {
+    for (size_t i; okc && (i = next.fetch_add(1)) < all.size();) {
       Page& p = *all[i];
       const uint8_t* d = in + p.data_pos;
       if (p.huff) gzip_huffman(d, (size_t)p.data_len, p.body);
@@ -642,6 +642,16 @@ bqsr_status rewrite(const uint8_t* in, int64_t n, const char* path, int level, c
       Writer w;
       w.fields(p.hdr);
       p.hdr_out = std::move(w.out);
+    }
+  };
+  // (a worker's exception -- std::bad_alloc from the page buffers -- must not
+  // escape its thread, which would std::terminate the process: it fails the
+  // call after the join instead)
+  auto work = [&]() {
+    try {
+      work_pages();
+    } catch (...) {
+      okc = false;
     }
   };
   const int nt = std::max(1, std::min<int>(threads, (int)all.size()));

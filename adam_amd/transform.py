@@ -303,10 +303,15 @@ def _transform_table(A, table, batch, inp, out, mark_duplicates, recalibrate, db
             qcol = P.recalibrated_qual_column(parts, n)
         table = (table.set_column(table.column_names.index("qual"), "qual", qcol)
                  if "qual" in table.column_names else table.append_column("qual", qcol))
+    # the new file first, then the old output goes (a failed write leaves the
+    # previous output in place); a leftover part-file directory at the
+    # .partial path (_check_out allowed it under overwrite) is removed first
     tmp = out + ".partial"
+    if os.path.isdir(tmp):
+        shutil.rmtree(tmp)
+    pq.write_table(table, tmp)
     if os.path.isdir(out):  # (transform_parquet checked it: overwrite of a part-file directory)
         shutil.rmtree(out)
-    pq.write_table(table, tmp)
     os.replace(tmp, out)
     stats["seconds"] = time.perf_counter() - t0
     return stats

@@ -59,7 +59,7 @@ def parse(argv=None):
     ap.add_argument("--event-steps", type=int, default=3,
                     help="untimed jobs after the timed region whose stages are timed with HIP events")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=V",
-                    help="bqsr_context_tune layout knob for an A/B run (order, fronts, key_major, fused_prep)")
+                    help="bqsr_context_tune layout knob for an A/B run (order, fronts, key_major)")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic json (default profiles/pmc_traffic_<config>.json)")
     ap.add_argument("--part-reads", type=int, default=4_000_000, help="cfg5: reads per streamed partition")

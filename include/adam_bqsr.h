@@ -143,9 +143,9 @@ void bqsr_context_destroy(bqsr_context* ctx);
  *                        or quals beyond one window), 0 read order, 1 buckets
  *   BQSR_TUNE_FRONTS    -1 auto, 0 none, f > 0: f fronts of bucketed batches
  *   BQSR_TUNE_KEYMAJOR   1 key-major copy of bucketed batches (default), 0 off
- *   BQSR_TUNE_FUSED_PREP 1 prep inside the observe kernel where it applies
- *                        (read order, reads <= 128 bases), 0 a prep kernel
- *                        of its own (default) */
+ *   BQSR_TUNE_FUSED_PREP 0 only: a prep kernel of its own (the form with
+ *                        prep inside the observe kernel was measured slower
+ *                        and removed; 1 is refused) */
 enum { BQSR_TUNE_ORDER = 1, BQSR_TUNE_FRONTS = 2, BQSR_TUNE_KEYMAJOR = 3, BQSR_TUNE_FUSED_PREP = 4 };
 bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value);
 

@@ -83,12 +83,11 @@ def read_order(request):
     sort, pieces per read group); the library picks 'group' for several read
     groups by default."""
     from adam_amd import bqsr as _b
-    order, _, plain = request.param.partition("-")  # "read-plain": prep in a kernel of its own
-    with _b.Context.get(0).tuned(order=order, fused_prep=0 if plain else 1):
+    with _b.Context.get(0).tuned(order=request.param):
         yield request.param
 
 
-@pytest.mark.parametrize("read_order", ["read", "read-plain", "group"], indirect=True)
+@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
 @pytest.mark.parametrize("n_reads,n_rg,lens,seed", [
     (6000, 96, (150, 250), 21),    # many groups, a few reads per workgroup and group
     (40000, 8, (100,), 22),        # few groups, each spread over many workgroups
@@ -100,7 +99,7 @@ def test_read_orders(read_order, n_reads, n_rg, lens, seed):
     check([b.slice(0, n_reads // 3), b.slice(n_reads // 3, n_reads)], synth.known_sites(2_000_000, seed=5))
 
 
-@pytest.mark.parametrize("read_order", ["read", "read-plain", "group"], indirect=True)
+@pytest.mark.parametrize("read_order", ["read", "group"], indirect=True)
 def test_read_orders_edge_cases(read_order):
     check([RecordBatch.from_records(EDGE * 3)], sites={"1": [10002, 10005, 40, 44, 10013]})
 
@@ -212,13 +211,9 @@ def test_edge_cases_split():
     (rec(qual=None), "NULL_FIELD"),
     (rec(sequence="ACGTA", cigar="10M"), "SEQ_SHORT"),
 ])
-@pytest.mark.parametrize("fused", [1, 0])
-def test_errors(bad, err, fused):
-    # (fused: the common reads' prep inside the observe kernel, the failing
-    # read in its list pass; 0: the prep kernel)
+def test_errors(bad, err):
     ok = [rec(), rec(qual="HHHHHHHHHH")]
-    with bqsr.Context.get(0).tuned(fused_prep=fused):
-        check([RecordBatch.from_records(ok + [bad] + ok)], expect_error=err)
+    check([RecordBatch.from_records(ok + [bad] + ok)], expect_error=err)
 
 
 def test_missing_key_in_apply():

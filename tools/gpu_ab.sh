@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-5 A/B of bench variants on one box, kernel stats per variant:
-#   tools/gpu_r05_ab.sh TAG CFG "VARIANT_A" "VARIANT_B" ...
+# A/B of bench variants on one box, kernel stats per variant:
+#   tools/gpu_ab.sh TAG CFG "VARIANT_A" "VARIANT_B" ...
 # VARIANT: extra bench.py flags (e.g. "--tune fused_prep=0"), optionally led by
 # LIB=path (a probe / A/B build of the library, tools/build_probe.sh).
 set -e

@@ -1,5 +1,5 @@
 #!/bin/bash
-# tools/gpu_r05_e2e.sh TAG READS: transform SAM -> ADAM end to end at the
+# tools/gpu_e2e.sh TAG READS: transform SAM -> ADAM end to end at the
 # reference's default gzip codec and at snappy (tools/bench_adam.py), the gzip
 # run under rocprofv3 (kernel trace; its log is checked for signal / abort
 # traces of the generator's process pool)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Measurement pass (run via gpurun): tools/gpu_r05_prof.sh TAG [CONFIGS] [PYTEST]
+# Measurement pass (run via gpurun): tools/gpu_prof.sh TAG [CONFIGS] [PYTEST]
 # Per config: FETCH_SIZE and WRITE_SIZE in separate --pmc passes, a
 # --kernel-trace --stats pass, the summaries bench.py reads
 # (gpurun_out/TAG/CFG/{pmc_traffic,kernel_stats}.json), then the bench line.

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 PMC passes (tools/pmc_profile.sh output): per kernel,
+"""Summarise rocprofv3 PMC passes (tools/gpu_prof.sh output): per kernel,
 mean counter values per dispatch, plus derived HBM bytes (FETCH_SIZE x 2 per
 MI355X_MICROARCH.md's gfx950 correction, + WRITE_SIZE; both in KiB)."""
 import collections
