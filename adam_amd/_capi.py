@@ -26,7 +26,7 @@ STATUS_NAMES = ["OK", "NULL_RG", "MD_PARSE", "CIGAR_SHORT", "BAD_REVCOMP_BASE", 
 EXPORTS = [
     "bqsr_abi_version", "bqsr_last_error", "bqsr_last_error_read", "bqsr_status_name", "bqsr_context_create",
     "bqsr_context_destroy", "bqsr_context_tune", "bqsr_sites_create", "bqsr_sites_destroy", "bqsr_batch_create", "bqsr_batch_destroy",
-    "bqsr_batch_reads", "bqsr_batch_bases", "bqsr_batch_dims", "bqsr_batch_relayout", "bqsr_batch_wrap_device", "bqsr_table_words",
+    "bqsr_batch_reads", "bqsr_batch_bases", "bqsr_batch_dims", "bqsr_batch_relayout", "bqsr_batch_layout_times", "bqsr_batch_wrap_device", "bqsr_table_words",
     "bqsr_table_create", "bqsr_table_destroy", "bqsr_table_dims", "bqsr_table_device_ptr", "bqsr_table_download",
     "bqsr_table_upload", "bqsr_observe", "bqsr_observe_records", "bqsr_table_merge", "bqsr_finalize",
     "bqsr_lut_destroy", "bqsr_lut_stats", "bqsr_lut_shifts", "bqsr_apply", "bqsr_apply_records",
@@ -103,6 +103,7 @@ def lib():
             "bqsr_context_destroy": (None, [vp]),
             "bqsr_context_tune": (ctypes.c_int, [vp, ctypes.c_int, i64]),
             "bqsr_batch_relayout": (ctypes.c_int, [vp, vp, ctypes.POINTER(dbl)]),
+            "bqsr_batch_layout_times": (ctypes.c_int, [vp, ctypes.POINTER(dbl), ctypes.POINTER(dbl)]),
             "bqsr_sites_create": (ctypes.c_int, [vp, vp, vp, vp, i32, pp]),
             "bqsr_sites_destroy": (None, [vp]),
             "bqsr_batch_create": (ctypes.c_int, [vp, vp, vp, pp]),

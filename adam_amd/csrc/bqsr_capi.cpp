@@ -376,17 +376,23 @@ struct bqsr_batch {
   uint32_t* d_cursor = nullptr;
   // key-major copy of the quals / base codes (key_major_build): the bucketed
   // passes' reads of a piece contiguous; the perm it follows is computed once
+  // (allocated once with the batch's other buffers, key_major_alloc; valid once km_ready)
   uint8_t *k_qual = nullptr, *k_bases = nullptr;
   uint64_t* d_kslot = nullptr;
+  uint64_t* d_kspan = nullptr;  // key_major_build scratch: slot spans in perm order, and the scan's temp
+  void* d_ktemp = nullptr;
+  size_t ktemp_bytes = 0;
+  bool km_ready = false;
+  double km_alloc_ms = -1.0, km_build_ms = -1.0;  // wall times of the copy's allocation / kernels (bqsr_batch_layout_times)
   bool perm_static = false;  // d_perm / d_key_off built once (key_major_build): prep skips the key sort
   OrderDev order() const {
-    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0, k_qual ? d_kslot : nullptr}
+    return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0, km_ready ? d_kslot : nullptr}
                     : OrderDev{nullptr, nullptr, 1};
   }
   // the reads as the per-base passes see them (qual / base columns: the key-major copy when there is one)
   ReadsDev pass_rd() const {
     ReadsDev r = rd;
-    if (bucketed && k_qual) {
+    if (bucketed && km_ready) {
       r.qual = k_qual;
       r.bases = k_bases;
     }
@@ -407,8 +413,6 @@ struct bqsr_batch {
       if (e) (void)hipEventDestroy(e);
     if (d_part) (void)hipFree(d_part);
     if (d_off64) (void)hipFree(d_off64);
-    for (void* p : {(void*)k_qual, (void*)k_bases, (void*)d_kslot})
-      if (p) (void)hipFree(p);
     if (d_chars) (void)hipFree(d_chars);
     if (h_status) (void)hipHostFree(h_status);
     for (void* p : allocs) (void)hipFree(p);
@@ -712,10 +716,35 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
 // reads (cfg4: 96 read groups).  The batch's data must be on the device
 // (created from records or a parse; a staged batch uploads later and keeps
 // the per-job sort).  1.5 B a slot more HBM.  BQSR_TUNE_KEYMAJOR 0: off (A/B).
+bool key_major_wanted(const bqsr_batch* b) {
+  return b->bucketed && b->ctx->tune_keymajor && b->rd.slots_aligned && b->rd.n_reads > 0;
+}
+// the copy's buffers and the scan's scratch, once per batch (freed with it)
+bqsr_status key_major_alloc(bqsr_batch* b) {
+  if (b->k_qual) return BQSR_OK;
+  const int64_t n = b->rd.n_reads;
+  bqsr_status st;
+  size_t tb = 0;
+  HIP_TRY(rocprim::exclusive_scan(nullptr, tb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0, (size_t)n + 1,
+                                  rocprim::plus<uint64_t>(), (hipStream_t)0));
+  b->ktemp_bytes = std::max<size_t>(tb, 1);
+  if ((st = dalloc(b->allocs, &b->d_kslot, (size_t)(n + 1))) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->d_kspan, (size_t)(n + 1))) != BQSR_OK ||
+      (st = dalloc(b->allocs, (uint8_t**)&b->d_ktemp, b->ktemp_bytes)) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->k_qual, (size_t)b->rd.n_slots + kColumnPad)) != BQSR_OK ||
+      (st = dalloc(b->allocs, &b->k_bases, (size_t)b->rd.n_slots / 2 + 1 + kColumnPad)) != BQSR_OK)
+    return st;
+  return BQSR_OK;
+}
 bqsr_status key_major_build(bqsr_batch* b, hipStream_t s) {
-  if (!b->bucketed || !b->ctx->tune_keymajor || !b->rd.slots_aligned || b->rd.n_reads == 0) return BQSR_OK;
+  if (!key_major_wanted(b)) return BQSR_OK;
   const int64_t n = b->rd.n_reads;
   bqsr_context* ctx = b->ctx;
+  b->km_ready = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  bqsr_status st = key_major_alloc(b);
+  if (st != BQSR_OK) return st;
+  const auto t1 = std::chrono::steady_clock::now();
   // the piece order, once
   HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
   const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
@@ -728,40 +757,23 @@ bqsr_status key_major_build(bqsr_batch* b, hipStream_t s) {
                      std::max(1, b->fronts), b->d_cursor, b->d_perm);
   HIP_TRY(hipGetLastError());
   // key-major slots: spans in perm order, scanned
-  uint64_t* span = nullptr;
-  void* temp = nullptr;
-  size_t tb = 0;
-  HIP_TRY(hipMalloc((void**)&b->d_kslot, (size_t)(n + 1) * 8));
-  HIP_TRY(hipMalloc((void**)&span, (size_t)(n + 1) * 8));
-  hipError_t e = hipMemsetAsync(span + n, 0, 8, s);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(bqsr_km_spans, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, (const uint32_t*)b->d_perm,
-                       n, span);
-    e = rocprim::exclusive_scan(nullptr, tb, span, b->d_kslot, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s);
-  }
-  if (e == hipSuccess) e = hipMalloc(&temp, std::max<size_t>(tb, 1));
-  if (e == hipSuccess)
-    e = rocprim::exclusive_scan(temp, tb, span, b->d_kslot, (uint64_t)0, (size_t)n + 1, rocprim::plus<uint64_t>(), s);
-  if (e == hipSuccess) e = hipMalloc((void**)&b->k_qual, (size_t)b->rd.n_slots + kColumnPad);
-  if (e == hipSuccess) e = hipMalloc((void**)&b->k_bases, (size_t)b->rd.n_slots / 2 + 1 + kColumnPad);
-  if (e == hipSuccess) e = hipMemsetAsync(b->k_qual + b->rd.n_slots, 0, kColumnPad, s);
-  if (e == hipSuccess) e = hipMemsetAsync(b->k_bases + b->rd.n_slots / 2, 0, 1 + kColumnPad, s);
-  if (e == hipSuccess) {
-    const unsigned gw = (unsigned)std::min<int64_t>((n + 3) / 4, (int64_t)ctx->n_cu * 8);
-    hipLaunchKernelGGL(bqsr_km_gather, dim3(gw), dim3(256), 0, s, b->rd, (const uint32_t*)b->d_perm,
-                       (const uint64_t*)b->d_kslot, b->k_qual, b->k_bases);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (span) (void)hipFree(span);
-  if (temp) (void)hipFree(temp);
-  if (e != hipSuccess) {  // without the copy the passes read the batch's own layout
-    for (void* p : {(void*)b->k_qual, (void*)b->k_bases, (void*)b->d_kslot})
-      if (p) (void)hipFree(p);
-    b->k_qual = b->k_bases = nullptr;
-    b->d_kslot = nullptr;
-    return fail(BQSR_ERR_DEVICE, std::string("key-major copy: ") + hipGetErrorString(e));
-  }
+  HIP_TRY(hipMemsetAsync(b->d_kspan + n, 0, 8, s));
+  hipLaunchKernelGGL(bqsr_km_spans, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, (const uint32_t*)b->d_perm,
+                     n, b->d_kspan);
+  size_t tb = b->ktemp_bytes;
+  HIP_TRY(rocprim::exclusive_scan(b->d_ktemp, tb, b->d_kspan, b->d_kslot, (uint64_t)0, (size_t)n + 1,
+                                  rocprim::plus<uint64_t>(), s));
+  HIP_TRY(hipMemsetAsync(b->k_qual + b->rd.n_slots, 0, kColumnPad, s));
+  HIP_TRY(hipMemsetAsync(b->k_bases + b->rd.n_slots / 2, 0, 1 + kColumnPad, s));
+  const unsigned gw = (unsigned)std::min<int64_t>((n + 3) / 4, (int64_t)ctx->n_cu * 8);
+  hipLaunchKernelGGL(bqsr_km_gather, dim3(gw), dim3(256), 0, s, b->rd, (const uint32_t*)b->d_perm,
+                     (const uint64_t*)b->d_kslot, b->k_qual, b->k_bases);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  const auto t2 = std::chrono::steady_clock::now();
+  b->km_alloc_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  b->km_build_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  b->km_ready = true;
   b->perm_static = true;
   return BQSR_OK;
 }
@@ -1227,17 +1239,22 @@ bqsr_status bqsr_batch_relayout(bqsr_batch* b, void* stream, double* ms) {
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipStreamSynchronize(s));
   const auto t0 = std::chrono::steady_clock::now();
-  const bool has = b->perm_static && b->k_qual;
-  if (has) {
-    for (void* p : {(void*)b->k_qual, (void*)b->k_bases, (void*)b->d_kslot}) (void)hipFree(p);
-    b->k_qual = b->k_bases = nullptr;
-    b->d_kslot = nullptr;
+  const bool has = b->perm_static && b->km_ready;
+  if (has) {  // the sort and the copy again into the batch's buffers (allocated with it)
     b->perm_static = false;
     bqsr_status st = key_major_build(b, s);
     if (st != BQSR_OK) return st;
   }
   HIP_TRY(hipStreamSynchronize(s));
   if (ms) *ms = has ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() : -1.0;
+  return ok();
+}
+
+// the key-major copy's cost when the batch was created: allocation and kernels (wall, each synchronised)
+bqsr_status bqsr_batch_layout_times(const bqsr_batch* b, double* alloc_ms, double* build_ms) {
+  if (!b) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_layout_times: null batch");
+  if (alloc_ms) *alloc_ms = b->km_alloc_ms;
+  if (build_ms) *build_ms = b->km_build_ms;
   return ok();
 }
 

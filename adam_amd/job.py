@@ -109,6 +109,13 @@ class ResidentJob:
             ms.append(v.value)
         return sum(ms) / len(ms)
 
+    def layout_times(self):
+        """(alloc_ms, build_ms) of the layout when the batch was created
+        (bqsr_batch_layout_times); None for a batch without one."""
+        a, b = ctypes.c_double(), ctypes.c_double()
+        check(self.L.bqsr_batch_layout_times(self.bh, ctypes.byref(a), ctypes.byref(b)))
+        return None if b.value < 0 else (a.value, b.value)
+
     def step(self, record: bool = False):
         """One job.  record: bracket the stages with timing events (each event
         record costs the stream ~30 us on this runtime, so callers sample)."""

@@ -166,9 +166,14 @@ int64_t bqsr_batch_reads(const bqsr_batch* b);
 int64_t bqsr_batch_bases(const bqsr_batch* b);
 bqsr_dims bqsr_batch_dims(const bqsr_batch* b);
 /* Measurement: redo the layout a bucketed batch builds once at creation
- * (piece-key sort, key-major copy of quals and codes) and report its wall
- * time in *ms (-1: the batch has no such layout).  Synchronous on `stream`. */
+ * (piece-key sort, key-major copy of quals and codes) into its buffers
+ * (allocated with the batch) and report its wall time in *ms (-1: the batch
+ * has no such layout).  Synchronous on `stream`. */
 bqsr_status bqsr_batch_relayout(bqsr_batch* b, void* stream, double* ms);
+/* The same layout's cost when the batch was created, split into the
+ * allocation of its buffers and its kernels (wall ms, each synchronised;
+ * -1 when the batch built none). */
+bqsr_status bqsr_batch_layout_times(const bqsr_batch* b, double* alloc_ms, double* build_ms);
 
 /* Caller-owned device buffers already in the packed layout (used by the
  * benchmark, which synthesises reads directly in HBM).  Layout documented in
