@@ -254,7 +254,7 @@ struct bqsr_context {
   // bqsr_context_tune
   int tune_order = -1;
   int tune_fronts = -1;
-  int tune_keymajor = 1;
+  int tune_keymajor = 0;
 };
 
 namespace {
@@ -374,17 +374,17 @@ struct bqsr_batch {
   int64_t* d_key_off = nullptr;
   uint32_t* d_key_cnt = nullptr;
   uint32_t* d_cursor = nullptr;
-  // key-major copy of the quals / base codes (key_major_build): the bucketed
+  // key-major copy of the quals / base codes (layout_build): the bucketed
   // passes' reads of a piece contiguous; the perm it follows is computed once
   // (allocated once with the batch's other buffers, key_major_alloc; valid once km_ready)
   uint8_t *k_qual = nullptr, *k_bases = nullptr;
   uint64_t* d_kslot = nullptr;
-  uint64_t* d_kspan = nullptr;  // key_major_build scratch: slot spans in perm order, and the scan's temp
+  uint64_t* d_kspan = nullptr;  // layout_build scratch: slot spans in perm order, and the scan's temp
   void* d_ktemp = nullptr;
   size_t ktemp_bytes = 0;
   bool km_ready = false;
   double km_alloc_ms = -1.0, km_build_ms = -1.0;  // wall times of the copy's allocation / kernels (bqsr_batch_layout_times)
-  bool perm_static = false;  // d_perm / d_key_off built once (key_major_build): prep skips the key sort
+  bool perm_static = false;  // d_perm / d_key_off built once (layout_build): prep skips the key sort
   OrderDev order() const {
     return bucketed ? OrderDev{d_perm, d_key_off, n_keys, fronts > 0 ? n_base : 0, km_ready ? d_kslot : nullptr}
                     : OrderDev{nullptr, nullptr, 1};
@@ -707,18 +707,20 @@ bqsr_status finish_batch(bqsr_batch* b, int64_t max_slot_len) {
   return BQSR_OK;
 }
 
-// key-major copy of a bucketed batch's quals and base codes (OrderDev::kslot):
-// the reads sorted by their piece key once (the same counting sort prep runs
-// per job, now kept: perm_static), their slot spans scanned in that order, and
-// each read's 16-aligned slot range copied to its key-major slots.  A piece's
-// reads are then contiguous in the copy: the bucketed chunk walks read it
-// sequentially where the read-order layout scattered them over every key's
-// reads (cfg4: 96 read groups).  The batch's data must be on the device
-// (created from records or a parse; a staged batch uploads later and keeps
-// the per-job sort).  1.5 B a slot more HBM.  BQSR_TUNE_KEYMAJOR 0: off (A/B).
-bool key_major_wanted(const bqsr_batch* b) {
-  return b->bucketed && b->ctx->tune_keymajor && b->rd.slots_aligned && b->rd.n_reads > 0;
-}
+// Per-batch layout of a bucketed batch whose data is on the device (created
+// from records or a parse; a staged batch uploads later and keeps the per-job
+// sort), built once at creation:
+//  * the piece order: the reads sorted by their piece key (the counting sort
+//    prep otherwise runs per job), kept (perm_static);
+//  * with BQSR_TUNE_KEYMAJOR 1, the key-major copy of the quals and base
+//    codes (OrderDev::kslot): the reads' slot spans (written by the sort's
+//    scatter) scanned in piece order and each read's 16-aligned slot range
+//    copied to its key-major slots.  A piece's reads are then contiguous in
+//    the copy: the bucketed chunk walks read it sequentially where the
+//    read-order layout scattered them over every key's reads (cfg4: 96 read
+//    groups).  1.5 B a slot more HBM.
+bool layout_wanted(const bqsr_batch* b) { return b->bucketed && b->rd.slots_aligned && b->rd.n_reads > 0; }
+bool key_major_wanted(const bqsr_batch* b) { return layout_wanted(b) && b->ctx->tune_keymajor; }
 // the copy's buffers and the scan's scratch, once per batch (freed with it)
 bqsr_status key_major_alloc(bqsr_batch* b) {
   if (b->k_qual) return BQSR_OK;
@@ -736,44 +738,49 @@ bqsr_status key_major_alloc(bqsr_batch* b) {
     return st;
   return BQSR_OK;
 }
-bqsr_status key_major_build(bqsr_batch* b, hipStream_t s) {
-  if (!key_major_wanted(b)) return BQSR_OK;
+// the piece-key counting sort (span: each sorted position's slot span as well, or null)
+void launch_key_sort(bqsr_batch* b, uint64_t* span, hipStream_t s) {
   const int64_t n = b->rd.n_reads;
-  bqsr_context* ctx = b->ctx;
-  b->km_ready = false;
-  const auto t0 = std::chrono::steady_clock::now();
-  bqsr_status st = key_major_alloc(b);
-  if (st != BQSR_OK) return st;
-  const auto t1 = std::chrono::steady_clock::now();
-  // the piece order, once
-  HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
-  const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
+  const int n_cu = b->ctx->n_cu;
+  (void)hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s);
+  const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)n_cu * 4);
   hipLaunchKernelGGL(bqsr_key_count, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys, b->n_base,
                      std::max(1, b->fronts), b->d_key_cnt);
   hipLaunchKernelGGL(bqsr_key_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)b->d_key_cnt, b->n_keys, b->d_key_off,
                      b->d_cursor);
-  const unsigned sb = (unsigned)std::min<int64_t>((n + 4095) / 4096, (int64_t)ctx->n_cu * 8);
+  const unsigned sb = (unsigned)std::min<int64_t>((n + 4095) / 4096, (int64_t)n_cu * 8);
   hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys, b->n_base,
-                     std::max(1, b->fronts), b->d_cursor, b->d_perm);
+                     std::max(1, b->fronts), b->d_cursor, b->d_perm, span);
+}
+bqsr_status layout_build(bqsr_batch* b, hipStream_t s) {
+  if (!layout_wanted(b)) return BQSR_OK;
+  const int64_t n = b->rd.n_reads;
+  bqsr_context* ctx = b->ctx;
+  const bool km = key_major_wanted(b);
+  b->km_ready = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  bqsr_status st = km ? key_major_alloc(b) : BQSR_OK;
+  if (st != BQSR_OK) return st;
+  const auto t1 = std::chrono::steady_clock::now();
+  if (km) HIP_TRY(hipMemsetAsync(b->d_kspan + n, 0, 8, s));
+  launch_key_sort(b, km ? b->d_kspan : nullptr, s);
   HIP_TRY(hipGetLastError());
-  // key-major slots: spans in perm order, scanned
-  HIP_TRY(hipMemsetAsync(b->d_kspan + n, 0, 8, s));
-  hipLaunchKernelGGL(bqsr_km_spans, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, (const uint32_t*)b->d_perm,
-                     n, b->d_kspan);
-  size_t tb = b->ktemp_bytes;
-  HIP_TRY(rocprim::exclusive_scan(b->d_ktemp, tb, b->d_kspan, b->d_kslot, (uint64_t)0, (size_t)n + 1,
-                                  rocprim::plus<uint64_t>(), s));
-  HIP_TRY(hipMemsetAsync(b->k_qual + b->rd.n_slots, 0, kColumnPad, s));
-  HIP_TRY(hipMemsetAsync(b->k_bases + b->rd.n_slots / 2, 0, 1 + kColumnPad, s));
-  const unsigned gw = (unsigned)std::min<int64_t>((n + 3) / 4, (int64_t)ctx->n_cu * 8);
-  hipLaunchKernelGGL(bqsr_km_gather, dim3(gw), dim3(256), 0, s, b->rd, (const uint32_t*)b->d_perm,
-                     (const uint64_t*)b->d_kslot, b->k_qual, b->k_bases);
-  HIP_TRY(hipGetLastError());
+  if (km) {  // key-major slots: the spans in perm order, scanned; then the copy
+    size_t tb = b->ktemp_bytes;
+    HIP_TRY(rocprim::exclusive_scan(b->d_ktemp, tb, b->d_kspan, b->d_kslot, (uint64_t)0, (size_t)n + 1,
+                                    rocprim::plus<uint64_t>(), s));
+    HIP_TRY(hipMemsetAsync(b->k_qual + b->rd.n_slots, 0, kColumnPad, s));
+    HIP_TRY(hipMemsetAsync(b->k_bases + b->rd.n_slots / 2, 0, 1 + kColumnPad, s));
+    const unsigned gw = (unsigned)std::min<int64_t>((n + 16 * kKmPer - 1) / (16 * kKmPer), (int64_t)ctx->n_cu * 64 / kKmPer);
+    hipLaunchKernelGGL(bqsr_km_gather, dim3(gw), dim3(256), 0, s, b->rd, (const uint32_t*)b->d_perm,
+                       (const uint64_t*)b->d_kslot, b->k_qual, b->k_bases);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipStreamSynchronize(s));
   const auto t2 = std::chrono::steady_clock::now();
   b->km_alloc_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   b->km_build_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
-  b->km_ready = true;
+  b->km_ready = km;
   b->perm_static = true;
   return BQSR_OK;
 }
@@ -943,7 +950,7 @@ bqsr_status bqsr_batch_create(bqsr_context* ctx, const bqsr_records* R, void* st
   b->rd.md = md;
   b->rd.cigar = cigar;
   b->rd.slots_aligned = align_slots();
-  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK || (st = key_major_build(b, s)) != BQSR_OK) {
+  if ((st = finish_batch(b, P.max_slot)) != BQSR_OK || (st = layout_build(b, s)) != BQSR_OK) {
     delete b;
     return st;
   }
@@ -1232,17 +1239,17 @@ int64_t bqsr_batch_slots(const bqsr_batch* b) { return b ? b->n_slots : -1; }
 bqsr_dims bqsr_batch_dims(const bqsr_batch* b) { return b ? b->dims : bqsr_dims{0, 0}; }
 
 // the per-batch layout work a bucketed batch pays once at creation (the
-// piece-key counting sort and the key-major copy, key_major_build), done
+// piece-key counting sort and the key-major copy, layout_build), done
 // again: its wall time is what bench.py reports as layout_ms
 bqsr_status bqsr_batch_relayout(bqsr_batch* b, void* stream, double* ms) {
   if (!b) return fail(BQSR_ERR_INVALID_ARG, "bqsr_batch_relayout: null batch");
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipStreamSynchronize(s));
   const auto t0 = std::chrono::steady_clock::now();
-  const bool has = b->perm_static && b->km_ready;
-  if (has) {  // the sort and the copy again into the batch's buffers (allocated with it)
+  const bool has = b->perm_static;
+  if (has) {  // the sort (and the copy) again into the batch's buffers (allocated with it)
     b->perm_static = false;
-    bqsr_status st = key_major_build(b, s);
+    bqsr_status st = layout_build(b, s);
     if (st != BQSR_OK) return st;
   }
   HIP_TRY(hipStreamSynchronize(s));
@@ -1418,16 +1425,7 @@ bqsr_status launch_prep(bqsr_context* ctx, bqsr_batch* b, const bqsr_sites* site
     }
     HIP_TRY(hipGetLastError());
     if (b->bucketed && !b->perm_static) {  // counting sort of the reads by read group
-      const int64_t n = b->rd.n_reads;
-      HIP_TRY(hipMemsetAsync(b->d_key_cnt, 0, (size_t)b->n_keys * 4, s));
-      const unsigned cb = (unsigned)std::min<int64_t>((n + 255) / 256, (int64_t)ctx->n_cu * 4);
-      hipLaunchKernelGGL(bqsr_key_count, dim3(cb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
-                         b->n_base, std::max(1, b->fronts), b->d_key_cnt);
-      hipLaunchKernelGGL(bqsr_key_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)b->d_key_cnt, b->n_keys,
-                         b->d_key_off, b->d_cursor);
-      const unsigned sb = (unsigned)std::min<int64_t>((n + 4095) / 4096, (int64_t)ctx->n_cu * 8);
-      hipLaunchKernelGGL(bqsr_key_scatter, dim3(sb), dim3(256), 0, s, (const ReadMeta*)b->rd.meta, n, b->n_keys,
-                         b->n_base, std::max(1, b->fronts), b->d_cursor, b->d_perm);
+      launch_key_sort(b, nullptr, s);
       HIP_TRY(hipGetLastError());
     }
   }

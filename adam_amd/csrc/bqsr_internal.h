@@ -203,7 +203,7 @@ struct OrderDev {
   // front sweep the same read range together and share its cache lines
   // (bqsr_capi.cpp fronts()).  0: keys are base keys, ranges by wg_begin.
   int32_t n_base = 0;
-  // key-major copy (bqsr_capi.cpp key_major_build): when set, the bucketed
+  // key-major copy (bqsr_capi.cpp layout_build): when set, the bucketed
   // passes read quals / base codes from a copy laid out in perm order -- the
   // read at sorted position p at kslot[p] -- so a piece's reads are
   // contiguous; the ReadsDev they get points at that copy, and the slot

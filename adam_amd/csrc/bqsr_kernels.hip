@@ -1830,29 +1830,52 @@ __device__ __forceinline__ int sort_key(const ReadMeta& m, int64_t r, int64_t n,
   return f * n_base + 2 * min((int)m.rg, n_base / 2 - 1) + cls;
 }
 
-// ---- key-major copy (OrderDev::kslot; bqsr_capi.cpp key_major_build) ----
-// slot span of the read at each sorted position
-extern "C" __global__ void bqsr_km_spans(const ReadMeta* meta, const uint32_t* perm, int64_t n, uint64_t* span) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
-    const ReadMeta m = meta[perm[p]];
-    span[p] = slot_span(m.lq, m.ls);
-  }
-}
-// a wavefront per read: its qual bytes and base codes to its key-major slots
-// (16-aligned slots: 16-B qual pieces, 8-B code pieces)
+// ---- key-major copy (OrderDev::kslot; bqsr_capi.cpp layout_build) ----
+// kKmLanes lanes per sorted position: the read's 16-slot pieces (16-B qual,
+// 8-B code) to its key-major slots, a piece per lane (pieces beyond kKmLanes
+// looped), kKmPer positions per lane group at once with every load of the
+// group issued before the first store.  cfg4 (6.2 GB of quals and codes):
+// a wavefront per read (10-16 of its 64 lanes busy) 8.4 ms a build, a
+// position per lane group 4.1 ms, four 4.4 ms.  Off by default (BQSR_TUNE_KEYMAJOR):
+// it saves 0.27 ms a cfg4 job, so it pays only after ~17 jobs on one batch.
+constexpr int kKmLanes = 16;
+constexpr int kKmPer = 1;
 extern "C" __global__ void __launch_bounds__(256) bqsr_km_gather(ReadsDev rd, const uint32_t* perm, const uint64_t* kslot,
                                                                 uint8_t* kqual, uint8_t* kbases) {
-  const int lane = threadIdx.x & 63;
-  const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6, nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t p = w0; p < rd.n_reads; p += nw) {
-    const ReadMeta m = rd.meta[perm[p]];
-    const uint64_t span = slot_span(m.lq, m.ls), d = kslot[p];
-    const uint4* qs = (const uint4*)(rd.qual + m.slot);
-    uint4* qd = (uint4*)(kqual + d);
-    for (uint64_t i = lane; i < span / 16; i += 64) qd[i] = qs[i];
-    const uint64_t* bs = (const uint64_t*)(rd.bases + m.slot / 2);
-    uint64_t* bd = (uint64_t*)(kbases + d / 2);
-    for (uint64_t i = lane; i < span / 16; i += 64) bd[i] = bs[i];
+  const int sub = threadIdx.x & (kKmLanes - 1);
+  const int64_t g0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kKmLanes;
+  const int64_t ng = ((int64_t)gridDim.x * blockDim.x) / kKmLanes;
+  const int64_t n = rd.n_reads;
+  for (int64_t p0 = g0 * kKmPer; p0 < n; p0 += ng * kKmPer) {
+    uint64_t src[kKmPer], dst[kKmPer];
+    uint32_t pieces[kKmPer];
+#pragma unroll
+    for (int u = 0; u < kKmPer; ++u) {
+      const bool on = p0 + u < n;
+      const ReadMeta m = on ? rd.meta[perm[p0 + u]] : ReadMeta{};
+      src[u] = m.slot;
+      pieces[u] = on ? (uint32_t)(slot_span(m.lq, m.ls) / 16) : 0u;
+      dst[u] = on ? kslot[p0 + u] : 0ull;
+    }
+    for (uint32_t i = sub;; i += kKmLanes) {
+      uint4 q[kKmPer];
+      uint64_t c[kKmPer];
+      bool any = false;
+#pragma unroll
+      for (int u = 0; u < kKmPer; ++u) {
+        const bool on = i < pieces[u];
+        any |= on;
+        q[u] = on ? ((const uint4*)(rd.qual + src[u]))[i] : make_uint4(0, 0, 0, 0);
+        c[u] = on ? ((const uint64_t*)(rd.bases + src[u] / 2))[i] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kKmPer; ++u)
+        if (i < pieces[u]) {
+          ((uint4*)(kqual + dst[u]))[i] = q[u];
+          ((uint64_t*)(kbases + dst[u] / 2))[i] = c[u];
+        }
+      if (!__builtin_amdgcn_ballot_w64(any)) break;
+    }
   }
 }
 
@@ -1906,7 +1929,8 @@ extern "C" __global__ void __launch_bounds__(1024) bqsr_key_scan(const uint32_t*
 extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(const ReadMeta* meta, int64_t n,
                                                                               int32_t n_keys, int32_t n_base,
                                                                               int32_t fronts, uint32_t* cursor,
-                                                                              uint32_t* perm) {
+                                                                              uint32_t* perm, uint64_t* span) {
+  // span (optional): each sorted position's slot span, for the key-major copy's scan
   __shared__ uint32_t h[kSortLdsKeys];
   const bool lds = n_keys <= kSortLdsKeys;
   const int tid = threadIdx.x;
@@ -1915,7 +1939,12 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
     if (!lds) {
       for (int i = 0; i < kSortPer; ++i) {
         const int64_t r = c0 + (int64_t)i * kSortThreads + tid;
-        if (r < n) perm[atomicAdd(&cursor[sort_key(meta[r], r, n, n_base, fronts)], 1u)] = (uint32_t)r;
+        if (r < n) {
+          const ReadMeta m = meta[r];
+          const uint32_t pos = atomicAdd(&cursor[sort_key(m, r, n, n_base, fronts)], 1u);
+          perm[pos] = (uint32_t)r;
+          if (span) span[pos] = slot_span(m.lq, m.ls);
+        }
       }
       continue;
     }
@@ -1923,10 +1952,13 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
     __syncthreads();
     int key[kSortPer];
     uint32_t rank[kSortPer];
+    uint16_t sp[kSortPer];
 #pragma unroll
     for (int i = 0; i < kSortPer; ++i) {
       const int64_t r = c0 + (int64_t)i * kSortThreads + tid;
-      key[i] = r < n ? sort_key(meta[r], r, n, n_base, fronts) : -1;
+      const ReadMeta m = r < n ? meta[r] : ReadMeta{};
+      key[i] = r < n ? sort_key(m, r, n, n_base, fronts) : -1;
+      sp[i] = (uint16_t)(slot_span(m.lq, m.ls) >> 4);
     }
 #pragma unroll
     for (int i = 0; i < kSortPer; ++i) rank[i] = key[i] >= 0 ? atomicAdd(&h[key[i]], 1u) : 0u;
@@ -1936,7 +1968,11 @@ extern "C" __global__ void __launch_bounds__(kSortThreads) bqsr_key_scatter(cons
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kSortPer; ++i)
-      if (key[i] >= 0) perm[h[key[i]] + rank[i]] = (uint32_t)(c0 + (int64_t)i * kSortThreads + tid);
+      if (key[i] >= 0) {
+        const uint32_t pos = h[key[i]] + rank[i];
+        perm[pos] = (uint32_t)(c0 + (int64_t)i * kSortThreads + tid);
+        if (span) span[pos] = (uint64_t)sp[i] << 4;
+      }
     __syncthreads();
   }
 }

@@ -302,7 +302,7 @@ bqsr_status pack_batch_device(bqsr_context* ctx, const PackCols& C, const int32_
   b->rd.md = md;
   b->rd.cigar = cigar;
   b->rd.slots_aligned = align_slots();
-  if ((e = finish_batch(b.get(), (int64_t)hl.max_slot)) != BQSR_OK || (e = key_major_build(b.get(), st)) != BQSR_OK)
+  if ((e = finish_batch(b.get(), (int64_t)hl.max_slot)) != BQSR_OK || (e = layout_build(b.get(), st)) != BQSR_OK)
     return e;
   HIP_TRY(hipStreamSynchronize(st));
   *out = b.release();

@@ -326,10 +326,11 @@ def main():
             "layout_build_ms": layout_created[1] if layout_created else None,
             "job_with_layout_ms": ((elapsed / args.steps * 1e3 + layout_created[0] + layout_created[1])
                                    if layout_created else None),
-            "layout_note": ("bucketed batch with the key-major copy: the piece-key sort and the copy of quals / "
-                            "codes run once when the batch is created (outside the timed jobs); layout_alloc_ms / "
-                            "layout_build_ms are their allocation and kernel wall times at creation, layout_ms the "
-                            "kernels redone on the batch, job_with_layout_ms a single job that pays both")
+            "layout_note": ("bucketed batch: the piece-key sort (and, with key_major=1, the key-major copy of "
+                            "quals / codes) runs once when the batch is created (outside the timed jobs); "
+                            "layout_alloc_ms / layout_build_ms are its allocation and kernel wall times at creation, "
+                            "layout_ms the kernels redone on the batch, job_with_layout_ms a single job that pays "
+                            "both -- the single-pass cost of a partition")
                            if layout_created else None,
             "gen_s": t_gen,
         }

@@ -142,7 +142,8 @@ void bqsr_context_destroy(bqsr_context* ctx);
  *   BQSR_TUNE_ORDER     -1 auto (read-group buckets for several read groups
  *                        or quals beyond one window), 0 read order, 1 buckets
  *   BQSR_TUNE_FRONTS    -1 auto, 0 none, f > 0: f fronts of bucketed batches
- *   BQSR_TUNE_KEYMAJOR   1 key-major copy of bucketed batches (default), 0 off
+ *   BQSR_TUNE_KEYMAJOR   0 off (default: the copy costs ~17 cfg4 jobs of its
+ *                        saving), 1 key-major copy of bucketed batches
  *   BQSR_TUNE_FUSED_PREP 0 only: a prep kernel of its own (the form with
  *                        prep inside the observe kernel was measured slower
  *                        and removed; 1 is refused) */
