@@ -65,6 +65,8 @@ constexpr uint16_t kInfoCycNeg = 128;   // (tile record only) cycle cell decreas
 constexpr uint16_t kInfoTrim = 256;     // st / en not computed yet (prep's lock-step path reads no
                                         // quals): the first pass over the read's quals trims it
                                         // (resolve_info), observe writes the result back
+constexpr uint16_t kInfoNoBits = 512;   // the read has no masked / mismatch bit (prep's common-read
+                                        // path): the per-base passes do not load its slot-bitmap words
 
 // packer-derived flag: the sequence holds a byte outside "ACGTN"
 // (BaseContext.simpleReverseComplement throws on it for reverse reads,

@@ -875,6 +875,7 @@ __device__ __forceinline__ bool prep_fast(const PrepParams& P, int64_t r, const 
   FastCig c;
   if (!fast_cigar(cw, a.n_cigar, m, a.start, c)) return false;
   const uint64_t rs = m.slot;
+  bool nobits = false;  // (kStore false) the read sets no bit: kInfoNoBits, the passes skip its words
   if (usable) {
     FastMd md;
     if (kLong) {
@@ -905,6 +906,7 @@ __device__ __forceinline__ bool prep_fast(const PrepParams& P, int64_t r, const 
         for (int j = 0; j < kAccWords; ++j) acc_out[j] = acc[j];
       } else {
         if (linear && c.x > 0) return false;  // (mask_sites_linear maps offsets as unclipped + o)
+        nobits = !linear && !(acc[0] | acc[1] | acc[2] | acc[3] | acc[4]);
         const uint64_t wb = rs >> 5;
 #pragma unroll
         for (int j = 0; j < kAccWords; ++j) {
@@ -916,6 +918,9 @@ __device__ __forceinline__ bool prep_fast(const PrepParams& P, int64_t r, const 
       }
     } else {
       if (a.contig >= 0 && a.contig < P.sites.n_contigs && c.x > 0) return false;  // (sites as unclipped + o)
+      // bits: clips, an insertion, a tag shorter than the span, MD letters, sites
+      nobits = c.lead <= st && (c.del || c.x == 0) && c.o_end >= en && md.listed && md.lst == 0 &&
+               md.md_total >= c.span && !(a.contig >= 0 && a.contig < P.sites.n_contigs);
       if (!md.listed) {  // more than 8 non-matching positions: the tag's per-byte walk
         if (kLong || c.x > 0) return false;
         const uint32_t w[4] = {cols.md4.x, cols.md4.y, cols.md4.z, cols.md4.w};
@@ -944,8 +949,9 @@ __device__ __forceinline__ bool prep_fast(const PrepParams& P, int64_t r, const 
         mask_sites_linear(P, a.contig, c.unclipped, st, en, rs);
     }
   }
-  P.info[r] = kLong ? ReadInfo{(uint16_t)st, (uint16_t)en, valid_flags(f), 0}
-                    : ReadInfo{0, 0, (uint16_t)(kInfoTrim | valid_flags(f)), 0};
+  const uint16_t nb = nobits ? kInfoNoBits : 0;
+  P.info[r] = kLong ? ReadInfo{(uint16_t)st, (uint16_t)en, (uint16_t)(valid_flags(f) | nb), 0}
+                    : ReadInfo{0, 0, (uint16_t)(kInfoTrim | valid_flags(f) | nb), 0};
   return true;
 }
 
@@ -1592,8 +1598,10 @@ __device__ __forceinline__ ObsChunkLoads observe_load(const ObserveParams& P, co
   if (x.fl & kInfoObs) {
     v.cr = chunk_raw(P.rd, chunk_n0(x, o0));
     const uint64_t s0 = x.oslot + (uint64_t)o0;
-    v.bw0 = P.sbits[s0 >> 5];
-    if ((s0 & 31) > 16) v.bw1 = P.sbits[(s0 >> 5) + 1];  // an unaligned layout's chunk across two words
+    if (!(x.fl & kInfoNoBits)) {  // (a read without bits: nothing to load)
+      v.bw0 = P.sbits[s0 >> 5];
+      if ((s0 & 31) > 16) v.bw1 = P.sbits[(s0 >> 5) + 1];  // an unaligned layout's chunk across two words
+    }
   }
   return v;
 }

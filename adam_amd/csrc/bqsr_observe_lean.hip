@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(kBlockThreads) bqsr_observe_lean(ObserveParams
       }
 #pragma unroll
       for (int w = 0; w < NW; ++w)
-        bw[w] = !(full && (w == 0 || 32 * w - 32 < n - j0)) ? 0ull : P.sbits[(s0 >> 5) + w];
+        bw[w] = !(full && !(x.fl & kInfoNoBits) && (w == 0 || 32 * w - 32 < n - j0)) ? 0ull : P.sbits[(s0 >> 5) + w];
 #pragma clang loop unroll(full)
       for (int i = 0; i < kLeanSub; ++i) {
         const int j = j0 + kChunk * i;
