@@ -514,6 +514,99 @@ struct RecScan {
   bqsr_status bad() const { return fail(BQSR_ERR_SAM_PARSE, "BAM: bad record size at byte " + std::to_string(p)); }
 };
 
+// The device form (bgzf_inflate.hip): the compressed file uploaded once, a
+// thread per BGZF block inflating it into d_raw, the header read back, the
+// records' offsets found and checked on the device (*d_rec, n + 1 entries,
+// from BH.body).  ok = false when it declines -- a block that does not
+// inflate or fails its CRC32, a chain the check rejects, a header it cannot
+// read -- and the caller runs the host form, which reports the file's error
+// as before.
+bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n, const std::vector<BgzfBlk>& blks,
+                               int64_t m, uint8_t* d_raw, hipStream_t s, std::vector<void*>& tmp, BamHead& BH,
+                               SamHeader& H, std::string& hdr, uint64_t** d_rec, int64_t& nr, bool& ok) {
+  ok = false;
+  const int64_t nb = (int64_t)blks.size();
+  std::vector<bgzfk::Blk> hb((size_t)nb);
+  for (int64_t i = 0; i < nb; ++i) {
+    const BgzfBlk& k = blks[(size_t)i];
+    hb[(size_t)i] = bgzfk::Blk{k.src, k.csize, k.dst, (int32_t)k.isize, (uint32_t)le32(data + k.src + k.csize)};
+  }
+  bqsr_status st;
+  uint8_t* d_comp;
+  bgzfk::Blk* d_blk;
+  int32_t* d_status;
+  if ((st = sam_alloc(tmp, &d_comp, (size_t)n + 64)) != BQSR_OK || (st = sam_upload(tmp, &d_blk, hb, s)) != BQSR_OK ||
+      (st = sam_alloc(tmp, &d_status, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK)
+    return st;
+  if ((st = upload_staged(ctx, d_comp, data, (size_t)n, s)) != BQSR_OK) return st;
+  if (nb > 0)
+    hipLaunchKernelGGL(bgzfk::bgzf_inflate_kernel, dim3((unsigned)((nb + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads)),
+                       dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk, nb, d_raw, d_status);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> hs((size_t)std::max<int64_t>(1, nb), 0);
+  if (nb > 0) HIP_TRY(hipMemcpyAsync(hs.data(), d_status, (size_t)nb * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int64_t i = 0; i < nb; ++i)
+    if (hs[(size_t)i] != bgzfk::kInfOk) return BQSR_OK;  // (the host form reports the block)
+  // the header, read back until it parses
+  std::vector<uint8_t> head;
+  for (int64_t want = std::min<int64_t>(m, 1 << 16);; want = std::min<int64_t>(m, want * 4)) {
+    head.resize((size_t)want);
+    HIP_TRY(hipMemcpy(head.data(), d_raw, (size_t)want, hipMemcpyDeviceToHost));
+    bqsr_status e;
+    const int r = bam_head(head.data(), want, want == m, BH, e);
+    if (r < 0) return BQSR_OK;
+    if (r == 1) break;
+  }
+  int64_t lt = BH.l_text;
+  while (lt > 0 && head[(size_t)(8 + lt - 1)] == 0) --lt;
+  if (parse_sam_header((const char*)head.data() + 8, lt, &H) != BQSR_OK) return BQSR_OK;
+  hdr.assign((const char*)head.data() + 8, (size_t)lt);
+  // the records: each block's guess and walk, the chain check, the offsets
+  bgzfk::ChainParams C{};
+  C.u = d_raw;
+  C.m = m;
+  C.body = BH.body;
+  C.blks = d_blk;
+  C.n_blk = nb;
+  C.n_ref = (int32_t)((int64_t)BH.ref_off.size() - 1);
+  uint64_t *part, *base;
+  if ((st = sam_alloc(tmp, &C.guess, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK ||
+      (st = sam_alloc(tmp, &C.exit, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK ||
+      (st = sam_alloc(tmp, &C.count, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK ||
+      (st = sam_alloc(tmp, &base, (size_t)nb + 1)) != BQSR_OK ||
+      (st = sam_alloc(tmp, &part, (size_t)(nb / samk::kScanChunk + 2))) != BQSR_OK ||
+      (st = sam_alloc(tmp, &C.bad, 1)) != BQSR_OK)
+    return st;
+  HIP_TRY(hipMemsetAsync(C.bad, 0, 4, s));
+  const unsigned gb = (unsigned)std::max<int64_t>(1, (nb + 63) / 64);
+  if (nb > 0) {
+    hipLaunchKernelGGL(bgzfk::bam_chain_guess, dim3(gb), dim3(64), 0, s, C);
+    hipLaunchKernelGGL(bgzfk::bam_chain_check, dim3(gb), dim3(64), 0, s, C);
+  }
+  HIP_TRY(hipGetLastError());
+  if ((st = sam_scan(C.count, nb, base, part, s)) != BQSR_OK) return st;
+  int32_t bad = 0;
+  uint64_t total = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, C.bad, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&total, base + nb, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (bad) return BQSR_OK;
+  nr = (int64_t)total;
+  uint64_t* rec;
+  if ((st = sam_alloc(tmp, &rec, (size_t)nr + 1)) != BQSR_OK) return st;
+  C.base = base;
+  C.rec = rec;
+  if (nb > 0) hipLaunchKernelGGL(bgzfk::bam_chain_write, dim3(gb), dim3(64), 0, s, C);
+  HIP_TRY(hipGetLastError());
+  const uint64_t end = (uint64_t)(m - BH.body);
+  HIP_TRY(hipMemcpyAsync(rec + nr, &end, 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *d_rec = rec;
+  ok = true;
+  return BQSR_OK;
+}
+
 }  // namespace
 
 bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, void* stream, bqsr_sam** out) {
@@ -546,6 +639,12 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   RecScan scan;
   InflateTimes IT;
   const double t_alloc = now_s();
+  uint64_t* d_rec = nullptr;  // the records' offsets on the device (the device form), else uploaded from scan.rec
+  int64_t nr_dev = 0;
+  bool dev = false;
+  if (ctx->tune_bgzf && (st = bam_inflate_device(ctx, data, n, blks, m, d_raw, s, tmp, BH, H, hdr, &d_rec, nr_dev, dev)) != BQSR_OK)
+    return st;
+  if (!dev) {
   st = bgzf_inflate_device(ctx, data, blks, d_raw, s, IT, [&](const uint8_t* buf, int64_t off, int64_t len) -> bqsr_status {
     if (have_head) return scan.consume(buf, off, len);
     head.insert(head.end(), buf, buf + len);
@@ -571,14 +670,15 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
     scan.p = BH.body + (int64_t)scan.rec.back();
     return scan.bad();
   }
+  }  // (host form)
   const double t_inflated = now_s();
   const int64_t body = BH.body;
   std::vector<uint64_t>& rec = scan.rec;
   std::vector<uint8_t>& ref_blob = BH.ref_blob;
   std::vector<uint64_t>& ref_off = BH.ref_off;
   const int64_t n_ref = (int64_t)ref_off.size() - 1;
-  const int64_t nr = (int64_t)rec.size();
-  rec.push_back((uint64_t)(m - body));
+  const int64_t nr = dev ? nr_dev : (int64_t)rec.size();
+  if (!dev) rec.push_back((uint64_t)(m - body));
   // the header text, newline-terminated, then the records' SAM lines
   if (!hdr.empty() && hdr.back() != '\n') hdr.push_back('\n');
   H.body = (int64_t)hdr.size();
@@ -587,7 +687,10 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
   P.n = nr;
   P.n_ref = (int32_t)n_ref;
   P.hdr = H.body;
-  if ((st = sam_upload(tmp, (uint64_t**)&P.rec, rec, s)) != BQSR_OK) return st;
+  if (dev)
+    P.rec = d_rec;
+  else if ((st = sam_upload(tmp, (uint64_t**)&P.rec, rec, s)) != BQSR_OK)
+    return st;
   if ((st = sam_upload(tmp, (uint8_t**)&P.ref_blob, ref_blob.empty() ? std::vector<uint8_t>{0} : ref_blob, s)) != BQSR_OK)
     return st;
   if ((st = sam_upload(tmp, (uint64_t**)&P.ref_off, ref_off, s)) != BQSR_OK) return st;
@@ -636,7 +739,7 @@ bqsr_status bqsr_bam_parse(bqsr_context* ctx, const uint8_t* data, int64_t n, vo
     fprintf(stderr,
             "[bam_parse] %lld reads, %.2f GB inflated (%s): blocks %.3f, alloc %.3f, runs %.3f (slot waits %.3f, "
             "inflate %.3f, reader wait %.3f (reading %.3f), drain %.3f), lines %.3f, SAM parse %.3f s\n",
-            (long long)nr, m / 1e9, Deflate::get().ok() ? "libdeflate" : "zlib", t_blocks - t_start, t_alloc - t_blocks, t_inflated - t_alloc, IT.wait, IT.inflate,
+            (long long)nr, m / 1e9, dev ? "device" : Deflate::get().ok() ? "libdeflate" : "zlib", t_blocks - t_start, t_alloc - t_blocks, t_inflated - t_alloc, IT.wait, IT.inflate,
             IT.host, IT.read, IT.drain, t_lines - t_inflated, now_s() - t_lines);
   return st;
 }

@@ -255,6 +255,7 @@ struct bqsr_context {
   int tune_order = -1;
   int tune_fronts = -1;
   int tune_keymajor = 0;
+  int tune_bgzf = 0;  // BAM ingest: BGZF inflated by host threads (BQSR_TUNE_BGZF), 1 on the device
 };
 
 namespace {
@@ -494,6 +495,10 @@ bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value) {
       return BQSR_OK;
     case BQSR_TUNE_FUSED_PREP:  // (the fused form was removed in round 6: only "off" is accepted)
       if (value != 0) break;
+      return BQSR_OK;
+    case BQSR_TUNE_BGZF:
+      if (value < 0 || value > 1) break;
+      ctx->tune_bgzf = (int)value;
       return BQSR_OK;
     default:
       return fail(BQSR_ERR_INVALID_ARG, "bqsr_context_tune: unknown knob");
@@ -2145,6 +2150,7 @@ bqsr_status bqsr_job_result(bqsr_batch* b, bqsr_lut* L, double* em, int64_t* n_e
 
 // ---- SAM ingest / output (include/adam_sam.h) ----
 #include "sam_ingest.hip"
+#include "bgzf_inflate.hip"
 #include "bam_ingest.hip"
 #include "mark_duplicates.cpp"
 #include "adam_out.hip"

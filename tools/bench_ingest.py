@@ -1,7 +1,7 @@
 """SAM / BAM ingest throughput (§8 f1): synthetic SAM text (cfg2-like reads)
 parsed by bqsr_sam_parse, or the same records as BAM (adam_amd/bam_writer.py)
-through bqsr_bam_parse (BGZF inflate on host threads, records decoded on the
-device); prints one JSON line.  Run under rocprofv3 --kernel-trace --stats to
+through bqsr_bam_parse (BGZF inflated on the device or, --bgzf 0, on host
+threads; records decoded on the device); prints one JSON line.  Run under rocprofv3 --kernel-trace --stats to
 split the device kernels from the H2D copy."""
 import argparse
 import ctypes
@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--len", type=int, default=100)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--bam", action="store_true", help="BAM input (BGZF) instead of SAM text")
+    ap.add_argument("--bgzf", type=int, default=0, help="BAM: 0 inflate on host threads (default), 1 on the device")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -36,6 +37,7 @@ def main():
         data = sam_to_bam(data)
     t_gen = time.perf_counter() - t0
     ctx = bqsr.Context.get(0)
+    ctx.tune(bgzf=a.bgzf)
     # pinned host copy: the H2D runs at the link's rate
     pinned = torch.empty(len(data), dtype=torch.uint8, pin_memory=True)
     pinned.numpy()[:] = np.frombuffer(data, np.uint8)
@@ -56,12 +58,12 @@ def main():
     if n_reads != a.reads:
         raise SystemExit("parsed %d records, expected %d" % (n_reads, a.reads))
     t = min(times)
-    fmt = "BAM (BGZF in pinned host memory -> inflate on host threads -> device columns)" if a.bam else \
-        "SAM text in pinned host memory -> device columns"
+    fmt = ("BAM (BGZF in pinned host memory -> inflate on %s -> device columns)" %
+           ("the device" if a.bgzf else "host threads")) if a.bam else "SAM text in pinned host memory -> device columns"
     print(json.dumps({"metric": "%s ingest reads/s (%s)" % ("BAM" if a.bam else "SAM", fmt),
                       "reads": a.reads, "read_len": a.len, "input_bytes": len(data), "seconds": t,
                       "reads_per_s": a.reads / t, "GB_per_s": len(data) / t / 1e9, "gen_seconds": t_gen,
-                      "inflate_threads": min(16, os.cpu_count() or 1) if a.bam else 0}))
+                      "inflate": ("device" if a.bgzf else "host %d threads" % min(16, os.cpu_count() or 1)) if a.bam else None}))
 
 
 if __name__ == "__main__":
