@@ -535,13 +535,17 @@ bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n
   uint8_t* d_comp;
   bgzfk::Blk* d_blk;
   int32_t* d_status;
-  if ((st = sam_alloc(tmp, &d_comp, (size_t)n + 64)) != BQSR_OK || (st = sam_upload(tmp, &d_blk, hb, s)) != BQSR_OK ||
+  if ((st = sam_alloc(tmp, &d_comp, (size_t)n + 256)) != BQSR_OK || (st = sam_upload(tmp, &d_blk, hb, s)) != BQSR_OK ||
       (st = sam_alloc(tmp, &d_status, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK)
     return st;
   if ((st = upload_staged(ctx, d_comp, data, (size_t)n, s)) != BQSR_OK) return st;
   if (nb > 0)
     hipLaunchKernelGGL(bgzfk::bgzf_inflate_kernel, dim3((unsigned)((nb + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads)),
                        dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk, nb, d_raw, d_status);
+  HIP_TRY(hipGetLastError());
+  if (nb > 0)
+    hipLaunchKernelGGL(bgzfk::bgzf_crc_kernel, dim3((unsigned)nb), dim3(bgzfk::kCrcThreads), 0, s,
+                       (const bgzfk::Blk*)d_blk, (const uint8_t*)d_raw, d_status);
   HIP_TRY(hipGetLastError());
   std::vector<int32_t> hs((size_t)std::max<int64_t>(1, nb), 0);
   if (nb > 0) HIP_TRY(hipMemcpyAsync(hs.data(), d_status, (size_t)nb * 4, hipMemcpyDeviceToHost, s));

@@ -5,12 +5,14 @@
 //
 // A BGZF file is a chain of gzip members of at most 64 KiB inflated each; no
 // DEFLATE back-reference crosses a member, so every block inflates on its own:
-// a thread per block (bgzf_inflate_kernel), its Huffman tables in the
+// a thread per block (bgzf_inflate_kernel, kInfThreads blocks a workgroup),
+// its decode tables and a ring its compressed bytes are staged through in the
 // thread's slice of LDS, the output written straight to the block's place in
-// the inflated stream (the host's prefix sum of the blocks' ISIZE), and the
-// CRC32 of the member folded as the bytes are produced (the block is rejected
-// as the host path rejects it: a code that does not decode, an overrun of
-// ISIZE, a short output, a CRC mismatch).
+// the inflated stream (the host's prefix sum of the blocks' ISIZE).  The
+// CRC32 of each member is a second kernel (bgzf_crc_kernel: a workgroup per
+// member, 256-byte chunks combined in GF(2)).  A block is rejected as the
+// host path rejects it: a code that does not decode, an overrun of ISIZE, a
+// short output, a CRC mismatch.
 //
 // The records' offsets (a chain of block_size fields from the first record
 // after the header) are found without walking the chain in order: each block
@@ -23,12 +25,15 @@
 // chain: any implausible, damaged or unusual file fails the check and the
 // caller takes the host path, which reports errors as before.
 //
-// Measured (profiles/r06t_bgzf_device_inflate.txt): correct on every DEFLATE
-// block form, but a thread per block -- 64 blocks a wavefront in lock step,
-// one wavefront a CU (its tables take 99 KB of LDS), each symbol a chain of
-// dependent LDS and global round trips -- inflates 0.43 GB in 189 ms where 16
-// libdeflate threads take 57 ms; the record chain costs 0.5 ms.  So the host
-// form stays the default (BQSR_TUNE_BGZF 0) and this one is selectable.
+// Measured (profiles/r06t_bgzf_device_inflate.txt): a thread per block is
+// serial per member, so the kernel's time is one member's decode latency;
+// what set it, in turn: 64 lanes a wavefront diverging (16 now), the
+// canonical bit-by-bit decode (two-level tables now), a global load per bit
+// refill waiting behind the lane's stores (the LDS ring now), the CRC folded
+// in the same kernel (its LDS table pushed the workgroup past two a CU), and
+// byte-wise match copies (batched now).  0.43 GB: 189 ms -> 44 ms, where 16
+// libdeflate threads take 57 ms (78 ms with the transfer).  Its waves now
+// wait on the match copies' L2 round trips.
 //
 // Included by bqsr_capi.cpp before bam_ingest.hip.
 
@@ -42,23 +47,44 @@ struct Blk {          // one BGZF member
   uint32_t crc;       // CRC32 of those bytes (the member's trailer)
 };
 
-constexpr int kInfThreads = 64;  // a wavefront per workgroup, a thread per block
+constexpr int kInfThreads = 16;  // blocks a workgroup (lanes of one wavefront), a thread per block
+constexpr int kLitRoot = 9;      // the decode tables' root index bits
+constexpr int kLitCap = 512;     // and their second-level entries (zlib's bound for 286 codes, root 9: 852 in all)
+constexpr int kDistRoot = 8;
+constexpr int kDistCap = 256;    // (a code needing more fails the block over to the host form)
 enum : int32_t { kInfOk = 0, kInfBadCode = 1, kInfOverrun = 2, kInfShort = 3, kInfCrc = 4, kInfBadBlock = 5 };
 
 // canonical Huffman code of a DEFLATE block (RFC 1951 §3.2.2): symbols by
 // code, counted per length (decoded bit by bit, the code's bits MSB first)
+template <int kSyms>
 struct Huff {
   uint16_t count[16];
-  uint16_t sym[288];
+  uint16_t sym[kSyms];
 };
-// a thread's LDS: the literal / length and distance codes, the code lengths
-// being read, and the construction's offsets
+// a thread's LDS: the literal / length and distance codes (canonical, and as
+// two-level decode tables, table_build), the code lengths being read, the
+// construction's offsets, and the ring its compressed bytes are staged
+// through; an odd number of dwords, so the lanes' copies of one field fall in
+// different banks
 struct InfLds {
-  Huff lit, dist;
+  Huff<288> lit;
+  Huff<32> dist;
+  uint16_t tlit[(1 << kLitRoot) + kLitCap];
+  uint16_t tdist[(1 << kDistRoot) + kDistCap];
   uint8_t len[320];
   uint16_t offs[16];
+  uint32_t ring[64];
+  uint32_t pad;
 };
+static_assert((sizeof(InfLds) / 4) % 2 == 1, "InfLds: an odd number of dwords");
 
+// the length / distance bases and extra bits (§3.2.5), copied to LDS per workgroup
+struct Codes {
+  uint16_t len_base[29];
+  uint8_t len_extra[29];
+  uint16_t dist_base[30];
+  uint8_t dist_extra[30];
+};
 __constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                       35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
 __constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
@@ -67,24 +93,46 @@ __constant__ uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 
 __constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// LSB-first bit reader over one member's compressed bytes [p, end)
+// LSB-first bit reader over one member's compressed bytes.  The bytes come
+// through a 256-byte ring in the thread's LDS, staged 128 bytes at a time
+// (eight 16-byte loads, one round trip) from the 16-byte-aligned address at
+// or below the member's start: a global load per symbol would wait, in the
+// lane's one counter of outstanding memory operations, for every output
+// byte stored before it.  A half that starts before the member's end may
+// read up to 127 bytes past it (the compressed buffer carries 256 bytes of
+// padding); halves past the end are zeros.  A decode that uses bits past the
+// end fails its checks.
 struct Bits {
-  const uint8_t* p;
-  const uint8_t* end;
+  const uint4* g;    // the member's bytes, aligned down to 16
+  uint32_t* ring;    // 64 words: word w of the stream at [w & 63]
   uint64_t buf;
-  int cnt;
-  bool over;  // read past the data (a damaged block)
+  int cnt;           // bits in buf
+  int q;             // the next word into buf
+  int staged;        // words staged so far
+  int64_t endbits;   // the member's last bit + 1, counted from g
+  __device__ __attribute__((noinline)) void stage() {
+    const uint4* s = g + (staged >> 2);
+    uint4 v[8];
+    const bool in = 32ll * staged < endbits;  // (a decode running on past the end reads zeros)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = in ? s[k] : make_uint4(0u, 0u, 0u, 0u);
+    uint32_t* r = ring + (staged & 63);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      r[4 * k] = v[k].x;
+      r[4 * k + 1] = v[k].y;
+      r[4 * k + 2] = v[k].z;
+      r[4 * k + 3] = v[k].w;
+    }
+    staged += 32;
+  }
+  // to > 32 bits (a ring half is staged only once its predecessor's words are all taken)
   __device__ __forceinline__ void refill() {
-    while (cnt <= 56) {
-      uint64_t b = 0;
-      if (p < end) {
-        b = *p++;
-      } else {
-        over = cnt < 0 || over;  // (zero bits fed past the end; a decode that uses them fails below)
-        p++;
-      }
-      buf |= b << cnt;
-      cnt += 8;
+    while (cnt <= 32) {
+      if (q >= staged) stage();
+      buf |= (uint64_t)ring[q & 63] << cnt;
+      q++;
+      cnt += 32;
     }
   }
   __device__ __forceinline__ uint32_t need(int n) {  // n <= 32 bits
@@ -94,11 +142,12 @@ struct Bits {
     cnt -= n;
     return v;
   }
-  __device__ __forceinline__ bool past() const { return p - (cnt >> 3) > end; }  // bits consumed beyond the data
+  __device__ __forceinline__ bool past() const { return 32ll * q - cnt > endbits; }  // bits consumed beyond the data
 };
 
 // puff-style construction: counts, completeness; 0 complete, > 0 incomplete, < 0 over-subscribed
-__device__ int huff_build(Huff& h, uint16_t* offs, const uint8_t* length, int n) {
+template <int kSyms>
+__device__ __attribute__((noinline)) int huff_build(Huff<kSyms>& h, uint16_t* offs, const uint8_t* length, int n) {
   for (int l = 0; l < 16; ++l) h.count[l] = 0;
   for (int s = 0; s < n; ++s) h.count[length[s]]++;
   if (h.count[0] == n) return 0;
@@ -115,8 +164,59 @@ __device__ int huff_build(Huff& h, uint16_t* offs, const uint8_t* length, int n)
   return left;
 }
 
+// The decode table of a built (not over-subscribed) code, indexed by the
+// next kRoot bits of the stream (the code's first bit lowest): an entry is
+// symbol | code length << 9 for a code of at most kRoot bits (0: no code), or
+// 0x8000 | sub bits << 12 | offset for the root prefix of longer codes, whose
+// second-level table (2^sub entries, indexed by the bits after the root) sits
+// at t[2^kRoot + offset].  The canonical codes are walked in code order
+// (h.sym): the longer codes sharing a root prefix are consecutive there, the
+// last the longest.  false: the second level needs more than kCap entries.
+template <int kRoot, int kCap, int kSyms>
+__device__ __attribute__((noinline)) bool table_build(uint16_t* t, const Huff<kSyms>& h) {
+  constexpr int kN = 1 << kRoot;
+  for (int i = 0; i < kN; ++i) t[i] = 0;
+  int idx = 0, off = 0, gprev = -1, gbits = 0;
+  uint32_t code = 0;
+  for (int l = 1; l < 16; ++l, code <<= 1) {
+    for (int j = 0, c = h.count[l]; j < c; ++j, ++code, ++idx) {
+      const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
+      if (l <= kRoot) {
+        const uint16_t e = (uint16_t)(h.sym[idx] | (l << 9));
+        for (uint32_t i = rev; i < (uint32_t)kN; i += 1u << l) t[i] = e;
+        continue;
+      }
+      const int g = (int)(rev & (kN - 1));
+      if (g != gprev) {
+        if (gprev >= 0) off += 1 << gbits;
+        gprev = g;
+      }
+      gbits = l - kRoot;
+      t[g] = (uint16_t)(0x8000 | (gbits << 12) | off);
+    }
+  }
+  if (gprev >= 0) off += 1 << gbits;
+  if (off > kCap) return false;
+  for (int i = 0; i < off; ++i) t[kN + i] = 0;
+  idx = 0;
+  code = 0;
+  for (int l = 1; l < 16; ++l, code <<= 1) {
+    for (int j = 0, c = h.count[l]; j < c; ++j, ++code, ++idx) {
+      if (l <= kRoot) continue;
+      const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
+      const uint32_t e = t[rev & (kN - 1)];
+      uint16_t* sub = t + kN + (e & 0xFFFu);
+      const uint32_t n = 1u << ((e >> 12) & 7u);
+      const uint16_t leaf = (uint16_t)(h.sym[idx] | (l << 9));
+      for (uint32_t i = rev >> kRoot; i < n; i += 1u << (l - kRoot)) sub[i] = leaf;
+    }
+  }
+  return true;
+}
+
 // one symbol: the code's bits one at a time (MSB of the code first), from a 16-bit peek
-__device__ __forceinline__ int huff_decode(Bits& b, const Huff& h) {
+template <int kSyms>
+__device__ __forceinline__ int huff_decode(Bits& b, const Huff<kSyms>& h) {
   if (b.cnt < 16) b.refill();
   const uint32_t bits = (uint32_t)b.buf;
   int code = 0, first = 0, index = 0;
@@ -136,32 +236,185 @@ __device__ __forceinline__ int huff_decode(Bits& b, const Huff& h) {
   }
   return -1;
 }
-
-__device__ __forceinline__ uint32_t crc_byte(const uint32_t* tab, uint32_t crc, uint32_t v) {
-  return tab[(crc ^ v) & 0xFFu] ^ (crc >> 8);
+// one symbol by a decode table: a root read, a second-level read for a
+// longer code; -1 for bits that start no code
+template <int kRoot>
+__device__ __forceinline__ int table_decode(Bits& b, const uint16_t* t) {
+  if (b.cnt < 16) b.refill();
+  uint32_t e = t[b.buf & ((1u << kRoot) - 1u)];
+  if (e & 0x8000u)
+    e = t[(1u << kRoot) + (e & 0xFFFu) + ((uint32_t)(b.buf >> kRoot) & ((1u << ((e >> 12) & 7u)) - 1u))];
+  const int l = (int)((e >> 9) & 15u);
+  if (l == 0) return -1;
+  b.buf >>= l;
+  b.cnt -= l;
+  return (int)(e & 511u);
 }
 
-// A thread per block.  out: the inflated stream; status[b]: kInf*.
+// A match: len bytes at o + pos repeat the dist bytes before them.  Loads
+// are round trips through L2 (the bytes were stored moments ago by this
+// lane), so the sources of a batch are all loaded before its stores: up to
+// min(dist, 32) bytes a batch for dist >= 8; for dist < 8 the period once
+// (one load of the 8 bytes before), then stores from registers.  Stores are
+// 8 bytes wide; one may run past the match into bytes this lane writes
+// later (never past the block's isize: there the word goes byte by byte).
+__device__ __forceinline__ void store_word(uint8_t* d, uint64_t w, int nb, bool whole) {
+  if (whole) {
+    __builtin_memcpy(d, &w, 8);
+    return;
+  }
+  for (int k = 0; k < nb; ++k) d[k] = (uint8_t)(w >> (8 * k));
+}
+__device__ __forceinline__ void match_copy(uint8_t* o, int pos, int dist, int len, int isize) {
+  uint8_t* d = o + pos;
+  const uint8_t* src = d - dist;
+  const int room = isize - pos;
+  if (dist >= 8) {
+    const int step = dist < 32 ? (dist & ~7) : 32;
+    for (int i = 0; i < len; i += step) {
+      const int nb = min(step, len - i);
+      uint64_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (8 * k < nb) __builtin_memcpy(&w[k], src + i + 8 * k, 8);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (8 * k < nb) store_word(d + i + 8 * k, w[k], min(8, nb - 8 * k), i + 8 * k + 8 <= room);
+    }
+    return;
+  }
+  // the period p (dist bytes), spread over 16 bytes: e0 | e1 << 64 = p p p ...
+  uint64_t v = 0;
+  if (pos >= 8) {
+    uint64_t w;
+    __builtin_memcpy(&w, d - 8, 8);
+    v = w >> (8 * (8 - dist));
+  } else {
+    for (int k = 0; k < dist; ++k) v |= (uint64_t)src[k] << (8 * k);
+  }
+  uint64_t e0 = 0, e1 = 0;
+  for (int k = 0, j = 0; k < 16; ++k) {
+    const uint64_t by = (v >> (8 * j)) & 0xFFull;
+    if (k < 8) e0 |= by << (8 * k); else e1 |= by << (8 * (k - 8));
+    if (++j == dist) j = 0;
+  }
+  const int adv = 8 % dist;  // the phase gained by 8 bytes
+  for (int i = 0, ph = 0; i < len; i += 8) {
+    const uint64_t w = ph == 0 ? e0 : (e0 >> (8 * ph)) | (e1 << (64 - 8 * ph));
+    store_word(d + i, w, min(8, len - i), i + 8 <= room);
+    ph += adv;
+    if (ph >= dist) ph -= dist;
+  }
+}
+
+// ---- the members' CRC32 ----
+// A workgroup per member, a thread per 256-byte chunk of its output: each
+// chunk's CRC32 by slicing-by-8 (tables in LDS), then the chunks' CRCs
+// combined in GF(2)[x] mod the CRC polynomial, as zlib's crc32_combine does:
+// crc(A B) = crc(A) * x^(8 |B|) + crc(B), so crc = sum over chunks t of
+// crc_t * x^(8 * (bytes after chunk t)).
+constexpr int kCrcThreads = 256;
+constexpr int kCrcChunk = 256;  // kCrcThreads * kCrcChunk = 65536, a member's most
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+
+// a * b mod P, bit-reflected (bit 31 is x^0)
+__device__ __forceinline__ uint32_t crc_mult(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) p ^= b;
+    b = (b & 1u) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+// x^(8 n) mod P: squarings of x^8 (x2n[k] = x^(8 * 2^k))
+__device__ __forceinline__ uint32_t crc_x8n(const uint32_t* x2n, uint32_t n) {
+  uint32_t p = 1u << 31;
+  for (int k = 0; n; n >>= 1, ++k)
+    if (n & 1u) p = crc_mult(x2n[k], p);
+  return p;
+}
+
+extern "C" __global__ void __launch_bounds__(kCrcThreads) bgzf_crc_kernel(const Blk* blks, const uint8_t* out,
+                                                                           int32_t* status) {
+  __shared__ uint32_t tab[8 * 256];  // [k][v]: the CRC of v followed by k zero bytes
+  __shared__ uint32_t x2n[20];
+  __shared__ uint32_t part[kCrcThreads / 64];
+  const int64_t bi = blockIdx.x;
+  if (status[bi] != kInfOk) return;  // (uniform over the workgroup)
+  const int t = threadIdx.x;
+  {
+    uint32_t c = (uint32_t)t;
+    for (int k = 0; k < 8; ++k) c = (c & 1u) ? kCrcPoly ^ (c >> 1) : c >> 1;
+    tab[t] = c;
+  }
+  if (t == 0) {
+    x2n[0] = 1u << 23;  // x^8
+    for (int k = 1; k < 20; ++k) x2n[k] = crc_mult(x2n[k - 1], x2n[k - 1]);
+  }
+  __syncthreads();
+  for (int k = 1; k < 8; ++k) {
+    tab[k * 256 + t] = (tab[(k - 1) * 256 + t] >> 8) ^ tab[tab[(k - 1) * 256 + t] & 0xFFu];
+    __syncthreads();
+  }
+  const Blk B = blks[bi];
+  const int lo = t * kCrcChunk, hi = min((int)B.isize, lo + kCrcChunk);
+  uint32_t r = 0;
+  if (lo < hi) {
+    const uint8_t* p = out + B.dst + lo;
+    uint32_t crc = 0xFFFFFFFFu;
+    int i = 0;
+    for (; i + 64 <= hi - lo; i += 64) {  // 8 loads in flight, then their CRC steps
+      uint64_t w[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) __builtin_memcpy(&w[k], p + i + 8 * k, 8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t a = (uint32_t)w[k] ^ crc, b = (uint32_t)(w[k] >> 32);
+        crc = tab[7 * 256 + (a & 0xFFu)] ^ tab[6 * 256 + ((a >> 8) & 0xFFu)] ^ tab[5 * 256 + ((a >> 16) & 0xFFu)] ^
+              tab[4 * 256 + (a >> 24)] ^ tab[3 * 256 + (b & 0xFFu)] ^ tab[2 * 256 + ((b >> 8) & 0xFFu)] ^
+              tab[1 * 256 + ((b >> 16) & 0xFFu)] ^ tab[b >> 24];
+      }
+    }
+    for (; i < hi - lo; ++i) crc = tab[(crc ^ p[i]) & 0xFFu] ^ (crc >> 8);
+    r = crc_mult(crc ^ 0xFFFFFFFFu, crc_x8n(x2n, (uint32_t)(B.isize - hi)));
+  }
+  for (int o = 32; o > 0; o >>= 1) r ^= __shfl_xor(r, o);
+  if ((t & 63) == 0) part[t >> 6] = r;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kCrcThreads / 64; ++w) c ^= part[w];
+    if (c != B.crc) status[bi] = kInfCrc;
+  }
+}
+
+// A thread per block.  out: the inflated stream; status[b]: kInf* (the CRC
+// is bgzf_crc_kernel's).
 extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(const uint8_t* comp, const Blk* blks,
                                                                               int64_t n_blk, uint8_t* out,
                                                                               int32_t* status) {
-  __shared__ uint32_t crc_tab[256];
   __shared__ InfLds lds[kInfThreads];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-    uint32_t c = (uint32_t)i;
-    for (int k = 0; k < 8; ++k) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-    crc_tab[i] = c;
+  __shared__ Codes C;
+  for (int i = threadIdx.x; i < 30; i += blockDim.x) {
+    if (i < 29) {
+      C.len_base[i] = kLenBase[i];
+      C.len_extra[i] = kLenExtra[i];
+    }
+    C.dist_base[i] = kDistBase[i];
+    C.dist_extra[i] = kDistExtra[i];
   }
   __syncthreads();
   const int64_t bi = (int64_t)blockIdx.x * kInfThreads + threadIdx.x;
   if (bi >= n_blk) return;
   const Blk B = blks[bi];
   InfLds& L = lds[threadIdx.x];
-  Bits b{comp + B.src, comp + B.src + B.csize, 0ull, 0, false};
+  const uintptr_t a0 = (uintptr_t)(comp + B.src), skip = a0 & 15u;
+  Bits b{(const uint4*)(a0 - skip), L.ring, 0ull, 0, (int)(skip >> 2), 0, 8 * ((int64_t)skip + B.csize)};
+  b.refill();
+  b.need((int)(skip & 3u) * 8);
   uint8_t* o = out + B.dst;
   const int32_t isize = B.isize;
   int32_t pos = 0;
-  uint32_t crc = 0xFFFFFFFFu;
   int32_t st = kInfOk;
   bool last = false;
   while (!last && st == kInfOk) {
@@ -175,7 +428,6 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
       for (uint32_t i = 0; i < len; ++i) {
         const uint32_t v = b.need(8);
         o[pos++] = (uint8_t)v;
-        crc = crc_byte(crc_tab, crc, v);
       }
       if (b.past()) { st = kInfBadBlock; break; }
       continue;
@@ -184,8 +436,10 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
     if (type == 1) {  // fixed codes (RFC 1951 §3.2.6)
       for (int s = 0; s < 288; ++s) L.len[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
       huff_build(L.lit, L.offs, L.len, 288);
+      table_build<kLitRoot, kLitCap>(L.tlit, L.lit);
       for (int s = 0; s < 30; ++s) L.len[s] = 5;
       huff_build(L.dist, L.offs, L.len, 30);
+      table_build<kDistRoot, kDistCap>(L.tdist, L.dist);
     } else {  // dynamic codes (§3.2.7)
       const int nlen = (int)b.need(5) + 257, ndist = (int)b.need(5) + 1, ncode = (int)b.need(4) + 4;
       if (nlen > 286 || ndist > 30) { st = kInfBadBlock; break; }
@@ -217,42 +471,51 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
       if (L.len[256] == 0) { st = kInfBadBlock; break; }  // no end-of-block code
       const int el = huff_build(L.lit, L.offs, L.len, nlen);
       if (el < 0 || (el > 0 && nlen - L.lit.count[0] != 1)) { st = kInfBadBlock; break; }
+      if (!table_build<kLitRoot, kLitCap>(L.tlit, L.lit)) { st = kInfBadBlock; break; }
       // (the distance lengths start at len[nlen]: copied down for the build)
       for (int i = 0; i < ndist; ++i) L.len[i] = L.len[nlen + i];
       const int ed = huff_build(L.dist, L.offs, L.len, ndist);
       if (ed < 0 || (ed > 0 && ndist - L.dist.count[0] != 1)) { st = kInfBadBlock; break; }
+      if (!table_build<kDistRoot, kDistCap>(L.tdist, L.dist)) { st = kInfBadBlock; break; }
     }
-    // the block's codes
+    // the block's codes; literals gather in a register word (up to 8, stored
+    // as one; flushed before a match, which may read them, and at the block's end)
+    uint64_t lit = 0;
+    int nlit = 0;
     while (true) {
-      const int sym = huff_decode(b, L.lit);
+      const int sym = table_decode<kLitRoot>(b, L.tlit);
       if (sym < 0) { st = kInfBadCode; break; }
       if (sym < 256) {
         if (pos >= isize) { st = kInfOverrun; break; }
-        o[pos++] = (uint8_t)sym;
-        crc = crc_byte(crc_tab, crc, (uint32_t)sym);
+        lit |= (uint64_t)sym << (8 * nlit);
+        pos++;
+        if (++nlit == 8) {
+          __builtin_memcpy(o + pos - 8, &lit, 8);
+          lit = 0;
+          nlit = 0;
+        }
         continue;
+      }
+      if (nlit) {
+        store_word(o + pos - nlit, lit, nlit, pos - nlit + 8 <= isize);
+        lit = 0;
+        nlit = 0;
       }
       if (sym == 256) break;
       const int ls = sym - 257;
       if (ls >= 29) { st = kInfBadCode; break; }
-      const int len = kLenBase[ls] + (int)b.need(kLenExtra[ls]);
-      const int ds = huff_decode(b, L.dist);
+      const int len = C.len_base[ls] + (int)b.need(C.len_extra[ls]);
+      const int ds = table_decode<kDistRoot>(b, L.tdist);
       if (ds < 0 || ds >= 30) { st = kInfBadCode; break; }
-      const int dist = kDistBase[ds] + (int)b.need(kDistExtra[ds]);
+      const int dist = C.dist_base[ds] + (int)b.need(C.dist_extra[ds]);
       if (dist > pos) { st = kInfBadCode; break; }
       if (pos + len > isize) { st = kInfOverrun; break; }
-      const uint8_t* src = o + pos - dist;
-      for (int i = 0; i < len; ++i) {  // (overlapping copies repeat the last dist bytes, in order)
-        const uint8_t v = src[i];
-        o[pos + i] = v;
-        crc = crc_byte(crc_tab, crc, v);
-      }
+      match_copy(o, pos, dist, len, isize);
       pos += len;
     }
     if (st == kInfOk && b.past()) st = kInfBadBlock;
   }
   if (st == kInfOk && pos != isize) st = kInfShort;
-  if (st == kInfOk && (crc ^ 0xFFFFFFFFu) != B.crc) st = kInfCrc;
   status[bi] = st;
 }
 

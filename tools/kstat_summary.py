@@ -10,5 +10,5 @@ for d in sys.argv[1:]:
         print("==", f)
         for r in rows:
             name = r["Name"]
-            if any(s in name for s in ("prep", "observe", "apply", "fold", "final", "reduce", "hist")):
+            if any(s in name for s in ("prep", "observe", "apply", "fold", "final", "reduce", "hist", "bgzf", "bam_chain")):
                 print("  %-60s %10.1f us  x%s" % (name[:60], float(r["AverageNs"]) / 1e3, r["Calls"]))
