@@ -521,6 +521,9 @@ struct RecScan {
 // inflate or fails its CRC32, a chain the check rejects, a header it cannot
 // read -- and the caller runs the host form, which reports the file's error
 // as before.
+// the device inflate's form: symbols to HBM, then each block assembled in LDS
+// (bgzf_resolve_kernel), or the bytes written by the decode itself
+constexpr bool kBgzfTokens = true;
 bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n, const std::vector<BgzfBlk>& blks,
                                int64_t m, uint8_t* d_raw, hipStream_t s, std::vector<void*>& tmp, BamHead& BH,
                                SamHeader& H, std::string& hdr, uint64_t** d_rec, int64_t& nr, bool& ok) {
@@ -539,13 +542,27 @@ bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n
       (st = sam_alloc(tmp, &d_status, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK)
     return st;
   if ((st = upload_staged(ctx, d_comp, data, (size_t)n, s)) != BQSR_OK) return st;
-  if (nb > 0)
-    hipLaunchKernelGGL(bgzfk::bgzf_inflate_kernel, dim3((unsigned)((nb + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads)),
-                       dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk, nb, d_raw, d_status);
-  HIP_TRY(hipGetLastError());
-  if (nb > 0)
+  const unsigned g_inf = (unsigned)((nb + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads);
+  if (kBgzfTokens) {  // symbols, then the bytes assembled a block a workgroup in LDS (+ CRC)
+    uint32_t* d_tok;
+    int32_t* d_ntok;
+    if ((st = sam_alloc(tmp, &d_tok, (size_t)std::max<int64_t>(1, m))) != BQSR_OK ||
+        (st = sam_alloc(tmp, &d_ntok, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK)
+      return st;
+    if (nb > 0) {
+      hipLaunchKernelGGL(bgzfk::bgzf_tokens_kernel, dim3(g_inf), dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp,
+                         (const bgzfk::Blk*)d_blk, nb, d_tok, d_ntok, d_status);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(bgzfk::bgzf_resolve_kernel, dim3((unsigned)nb), dim3(bgzfk::kResThreads), 0, s,
+                         (const bgzfk::Blk*)d_blk, (const uint32_t*)d_tok, (const int32_t*)d_ntok, d_raw, d_status);
+    }
+  } else if (nb > 0) {  // the bytes straight from the decode, then the CRC
+    hipLaunchKernelGGL(bgzfk::bgzf_inflate_kernel, dim3(g_inf), dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp,
+                       (const bgzfk::Blk*)d_blk, nb, d_raw, d_status);
+    HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(bgzfk::bgzf_crc_kernel, dim3((unsigned)nb), dim3(bgzfk::kCrcThreads), 0, s,
                        (const bgzfk::Blk*)d_blk, (const uint8_t*)d_raw, d_status);
+  }
   HIP_TRY(hipGetLastError());
   std::vector<int32_t> hs((size_t)std::max<int64_t>(1, nb), 0);
   if (nb > 0) HIP_TRY(hipMemcpyAsync(hs.data(), d_status, (size_t)nb * 4, hipMemcpyDeviceToHost, s));

@@ -78,19 +78,14 @@ struct InfLds {
 };
 static_assert((sizeof(InfLds) / 4) % 2 == 1, "InfLds: an odd number of dwords");
 
-// the length / distance bases and extra bits (§3.2.5), copied to LDS per workgroup
-struct Codes {
-  uint16_t len_base[29];
-  uint8_t len_extra[29];
-  uint16_t dist_base[30];
-  uint8_t dist_extra[30];
-};
-__constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kDistBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
-                                       193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// the length / distance codes' bases and extra bits (RFC 1951 §3.2.5), by
+// arithmetic: each group of four codes doubles the step
+__device__ __forceinline__ int len_extra(int ls) { return (ls < 8 || ls == 28) ? 0 : (ls - 4) >> 2; }
+__device__ __forceinline__ int len_base(int ls, int e) {
+  return ls < 8 ? ls + 3 : ls == 28 ? 258 : ((4 + (ls & 3)) << e) + 3;
+}
+__device__ __forceinline__ int dist_extra(int ds) { return ds < 4 ? 0 : (ds >> 1) - 1; }
+__device__ __forceinline__ int dist_base(int ds, int e) { return ds < 4 ? ds + 1 : ((2 + (ds & 1)) << e) + 1; }
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // LSB-first bit reader over one member's compressed bytes.  The bytes come
@@ -110,6 +105,7 @@ struct Bits {
   int q;             // the next word into buf
   int staged;        // words staged so far
   int64_t endbits;   // the member's last bit + 1, counted from g
+  uint32_t nextw;    // word q, read ahead of its use
   __device__ __attribute__((noinline)) void stage() {
     const uint4* s = g + (staged >> 2);
     uint4 v[8];
@@ -126,13 +122,16 @@ struct Bits {
     }
     staged += 32;
   }
-  // to > 32 bits (a ring half is staged only once its predecessor's words are all taken)
+  // to > 32 bits (a ring half is staged only once its predecessor's words
+  // are all taken); the next word's LDS read is issued here and waited for
+  // at the next refill, off the decode's chain
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
-      if (q >= staged) stage();
-      buf |= (uint64_t)ring[q & 63] << cnt;
-      q++;
+      buf |= (uint64_t)nextw << cnt;
       cnt += 32;
+      q++;
+      if (q >= staged) stage();
+      nextw = ring[q & 63];
     }
   }
   __device__ __forceinline__ uint32_t need(int n) {  // n <= 32 bits
@@ -388,31 +387,26 @@ extern "C" __global__ void __launch_bounds__(kCrcThreads) bgzf_crc_kernel(const 
   }
 }
 
-// A thread per block.  out: the inflated stream; status[b]: kInf* (the CRC
-// is bgzf_crc_kernel's).
-extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(const uint8_t* comp, const Blk* blks,
-                                                                              int64_t n_blk, uint8_t* out,
-                                                                              int32_t* status) {
-  __shared__ InfLds lds[kInfThreads];
-  __shared__ Codes C;
-  for (int i = threadIdx.x; i < 30; i += blockDim.x) {
-    if (i < 29) {
-      C.len_base[i] = kLenBase[i];
-      C.len_extra[i] = kLenExtra[i];
-    }
-    C.dist_base[i] = kDistBase[i];
-    C.dist_extra[i] = kDistExtra[i];
-  }
-  __syncthreads();
+// A thread per block.  kTok false: the block's bytes to out (+ dst).  kTok
+// true: its symbols to tok (+ dst) instead, one a word (a literal byte, or
+// 0x80000000 | (distance - 1) << 9 | length), and their count to ntok.
+// status[b]: kInf* (the CRC is checked after).
+template <bool kTok>
+__device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* blks, int64_t n_blk, uint8_t* out,
+                                               uint32_t* tok, int32_t* ntok, int32_t* status, InfLds* lds) {
   const int64_t bi = (int64_t)blockIdx.x * kInfThreads + threadIdx.x;
   if (bi >= n_blk) return;
   const Blk B = blks[bi];
   InfLds& L = lds[threadIdx.x];
   const uintptr_t a0 = (uintptr_t)(comp + B.src), skip = a0 & 15u;
-  Bits b{(const uint4*)(a0 - skip), L.ring, 0ull, 0, (int)(skip >> 2), 0, 8 * ((int64_t)skip + B.csize)};
+  Bits b{(const uint4*)(a0 - skip), L.ring, 0ull, 0, (int)(skip >> 2), 0, 8 * ((int64_t)skip + B.csize), 0u};
+  b.stage();
+  b.nextw = L.ring[b.q & 63];
   b.refill();
   b.need((int)(skip & 3u) * 8);
   uint8_t* o = out + B.dst;
+  uint32_t* tk = tok + B.dst;
+  int32_t k = 0;  // (tokens written)
   const int32_t isize = B.isize;
   int32_t pos = 0;
   int32_t st = kInfOk;
@@ -427,7 +421,9 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
       if (pos + (int32_t)len > isize) { st = kInfOverrun; break; }
       for (uint32_t i = 0; i < len; ++i) {
         const uint32_t v = b.need(8);
-        o[pos++] = (uint8_t)v;
+        if constexpr (kTok) tk[k++] = v;
+        else o[pos] = (uint8_t)v;
+        pos++;
       }
       if (b.past()) { st = kInfBadBlock; break; }
       continue;
@@ -487,6 +483,11 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
       if (sym < 0) { st = kInfBadCode; break; }
       if (sym < 256) {
         if (pos >= isize) { st = kInfOverrun; break; }
+        if constexpr (kTok) {
+          tk[k++] = (uint32_t)sym;
+          pos++;
+          continue;
+        }
         lit |= (uint64_t)sym << (8 * nlit);
         pos++;
         if (++nlit == 8) {
@@ -504,19 +505,153 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
       if (sym == 256) break;
       const int ls = sym - 257;
       if (ls >= 29) { st = kInfBadCode; break; }
-      const int len = C.len_base[ls] + (int)b.need(C.len_extra[ls]);
+      const int le = len_extra(ls);
+      const int len = len_base(ls, le) + (int)b.need(le);
       const int ds = table_decode<kDistRoot>(b, L.tdist);
       if (ds < 0 || ds >= 30) { st = kInfBadCode; break; }
-      const int dist = C.dist_base[ds] + (int)b.need(C.dist_extra[ds]);
+      const int de = dist_extra(ds);
+      const int dist = dist_base(ds, de) + (int)b.need(de);
       if (dist > pos) { st = kInfBadCode; break; }
       if (pos + len > isize) { st = kInfOverrun; break; }
-      match_copy(o, pos, dist, len, isize);
+      if constexpr (kTok) tk[k++] = 0x80000000u | ((uint32_t)(dist - 1) << 9) | (uint32_t)len;
+      else match_copy(o, pos, dist, len, isize);
       pos += len;
     }
     if (st == kInfOk && b.past()) st = kInfBadBlock;
   }
   if (st == kInfOk && pos != isize) st = kInfShort;
   status[bi] = st;
+  if constexpr (kTok) ntok[bi] = k;
+}
+
+extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(const uint8_t* comp, const Blk* blks,
+                                                                              int64_t n_blk, uint8_t* out,
+                                                                              int32_t* status) {
+  __shared__ InfLds lds[kInfThreads];
+  inflate_blocks<false>(comp, blks, n_blk, out, nullptr, nullptr, status, lds);
+}
+extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(const uint8_t* comp, const Blk* blks,
+                                                                             int64_t n_blk, uint32_t* tok,
+                                                                             int32_t* ntok, int32_t* status) {
+  __shared__ InfLds lds[kInfThreads];
+  inflate_blocks<true>(comp, blks, n_blk, nullptr, tok, ntok, status, lds);
+}
+
+// Pass 2 of the token form: a workgroup per block, its output assembled in
+// LDS (a block inflates to at most 64 KiB) from its tokens 256 at a time --
+// each thread a token, its output offset by a workgroup scan, the literals
+// written at once, then rounds in which every match whose source bytes lie
+// below the first unresolved token's output copies (the first one always
+// can) -- then its CRC32 checked from LDS (bgzf_crc_kernel's chunked form)
+// and the bytes stored to out (+ dst).
+constexpr int kResThreads = 256;
+extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(const Blk* blks, const uint32_t* tok,
+                                                                              const int32_t* ntok, uint8_t* out,
+                                                                              int32_t* status) {
+  __shared__ uint32_t win32[65536 / 4];
+  __shared__ uint32_t tab[8 * 256];
+  __shared__ uint32_t x2n[20];
+  __shared__ int32_t red[kResThreads / 64];
+  uint8_t* win = (uint8_t*)win32;
+  const int64_t bi = blockIdx.x;
+  if (status[bi] != kInfOk) return;  // (uniform over the workgroup)
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  {
+    uint32_t c = (uint32_t)t;
+    for (int k = 0; k < 8; ++k) c = (c & 1u) ? kCrcPoly ^ (c >> 1) : c >> 1;
+    tab[t] = c;
+  }
+  if (t == 0) {
+    x2n[0] = 1u << 23;  // x^8
+    for (int k = 1; k < 20; ++k) x2n[k] = crc_mult(x2n[k - 1], x2n[k - 1]);
+  }
+  const Blk B = blks[bi];
+  const int n = ntok[bi];
+  const uint32_t* T = tok + B.dst;
+  int cur = 0;
+  uint32_t nx = t < n ? T[t] : 0u;
+  for (int g0 = 0; g0 < n; g0 += kResThreads) {
+    const int j = g0 + t;
+    const uint32_t w = nx;
+    nx = j + kResThreads < n ? T[j + kResThreads] : 0u;  // (the next group's, in flight)
+    const bool is_m = j < n && (w >> 31);
+    const int ln = j < n ? (is_m ? (int)(w & 511u) : 1) : 0;
+    // the workgroup's exclusive scan of ln
+    int inc = ln;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (lane >= o) inc += v;
+    }
+    __syncthreads();  // (red: the last group's readers are done)
+    if (lane == 63) red[wv] = inc;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int q = 0; q < kResThreads / 64; ++q) {
+      before += q < wv ? red[q] : 0;
+      total += red[q];
+    }
+    const int p = cur + before + inc - ln;
+    if (j < n && !is_m) win[p] = (uint8_t)w;
+    const int dist = (int)((w >> 9) & 0x7FFFu) + 1;
+    bool pend = is_m;
+    while (true) {
+      // the first unresolved token's output offset: every byte below it is final
+      int f = pend ? p : 0x7FFFFFFF;
+      for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o));
+      __syncthreads();  // (the round's writes; red's readers)
+      if (lane == 0) red[wv] = f;
+      __syncthreads();
+      int F = red[0];
+      for (int q = 1; q < kResThreads / 64; ++q) F = min(F, red[q]);
+      if (F == 0x7FFFFFFF) break;
+      if (pend && p - dist + min(ln, dist) <= F) {
+        for (int i = 0; i < ln; ++i) win[p + i] = win[p - dist + i];  // (forward: a period repeats)
+        pend = false;
+      }
+    }
+    cur += total;
+  }
+  __syncthreads();
+  // CRC32 of the 256-byte chunks, combined
+  for (int k = 1; k < 8; ++k) {
+    tab[k * 256 + t] = (tab[(k - 1) * 256 + t] >> 8) ^ tab[tab[(k - 1) * 256 + t] & 0xFFu];
+    __syncthreads();
+  }
+  const int isize = B.isize, lo = t * kCrcChunk, hi = min(isize, lo + kCrcChunk);
+  uint32_t r = 0;
+  if (lo < hi) {
+    uint32_t crc = 0xFFFFFFFFu;
+    int i = lo;
+    for (; i + 8 <= hi; i += 8) {
+      const uint32_t a = win32[i >> 2] ^ crc, b = win32[(i >> 2) + 1];
+      crc = tab[7 * 256 + (a & 0xFFu)] ^ tab[6 * 256 + ((a >> 8) & 0xFFu)] ^ tab[5 * 256 + ((a >> 16) & 0xFFu)] ^
+            tab[4 * 256 + (a >> 24)] ^ tab[3 * 256 + (b & 0xFFu)] ^ tab[2 * 256 + ((b >> 8) & 0xFFu)] ^
+            tab[1 * 256 + ((b >> 16) & 0xFFu)] ^ tab[b >> 24];
+    }
+    for (; i < hi; ++i) crc = tab[(crc ^ win[i]) & 0xFFu] ^ (crc >> 8);
+    r = crc_mult(crc ^ 0xFFFFFFFFu, crc_x8n(x2n, (uint32_t)(isize - hi)));
+  }
+  for (int o = 32; o > 0; o >>= 1) r ^= __shfl_xor(r, o);
+  if (lane == 0) red[wv] = (int32_t)r;
+  // the bytes out: dwords once the destination is aligned
+  uint8_t* o = out + B.dst;
+  const int head = (int)((4u - ((uintptr_t)o & 3u)) & 3u) < isize ? (int)((4u - ((uintptr_t)o & 3u)) & 3u) : isize;
+  if (t < head) o[t] = win[t];
+  const int nw = (isize - head) >> 2;
+  uint32_t* o32 = (uint32_t*)(o + head);
+  for (int i = t; i < nw; i += kResThreads) {
+    const int q = head + 4 * i;  // (LDS bytes q .. q+3, not dword-aligned unless head is 0)
+    const int s = (q & 3) * 8;
+    const uint32_t v = s ? (win32[q >> 2] >> s) | (win32[(q >> 2) + 1] << (32 - s)) : win32[q >> 2];
+    o32[i] = v;
+  }
+  for (int i = head + 4 * nw + t; i < isize; i += kResThreads) o[i] = win[i];
+  __syncthreads();
+  if (t == 0) {
+    uint32_t c = 0;
+    for (int q = 0; q < kResThreads / 64; ++q) c ^= (uint32_t)red[q];
+    if (c != B.crc) status[bi] = kInfCrc;
+  }
 }
 
 // ---- the records' offsets ----
