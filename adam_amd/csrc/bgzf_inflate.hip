@@ -90,7 +90,9 @@ __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12
 
 // LSB-first bit reader over one member's compressed bytes.  The bytes come
 // through a 256-byte ring in the thread's LDS, staged 128 bytes at a time
-// (eight 16-byte loads, one round trip) from the 16-byte-aligned address at
+// (eight 16-byte loads, one round trip, inline: as a call it cost 10 ms of
+// 36, and loading each half one half ahead, in registers, 18 ms more,
+// profiles/r06t_*) from the 16-byte-aligned address at
 // or below the member's start: a global load per symbol would wait, in the
 // lane's one counter of outstanding memory operations, for every output
 // byte stored before it.  A half that starts before the member's end may
@@ -106,7 +108,7 @@ struct Bits {
   int staged;        // words staged so far
   int64_t endbits;   // the member's last bit + 1, counted from g
   uint32_t nextw;    // word q, read ahead of its use
-  __device__ __attribute__((noinline)) void stage() {
+  __device__ __forceinline__ void stage() {
     const uint4* s = g + (staged >> 2);
     uint4 v[8];
     const bool in = 32ll * staged < endbits;  // (a decode running on past the end reads zeros)
