@@ -52,7 +52,7 @@ class Context:
     # bqsr_context_tune knobs (include/adam_bqsr.h): layout choices of the
     # batches created afterwards, for tests and A/B runs; None = leave as is
     _KNOBS = {"order": 1, "fronts": 2, "key_major": 3, "bgzf": 5}
-    _DEFAULTS = {"order": -1, "fronts": -1, "key_major": 0, "bgzf": 0}
+    _DEFAULTS = {"order": -1, "fronts": -1, "key_major": 0, "bgzf": 1}
 
     def tune(self, **knobs) -> Dict[str, int]:
         """Set layout knobs (order: -1 auto / 0 read / 1 read-group buckets;

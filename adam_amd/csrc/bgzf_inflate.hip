@@ -90,15 +90,14 @@ __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12
 
 // LSB-first bit reader over one member's compressed bytes.  The bytes come
 // through a 256-byte ring in the thread's LDS, staged 128 bytes at a time
-// (eight 16-byte loads, one round trip, inline: as a call it cost 10 ms of
-// 36, and loading each half one half ahead, in registers, 18 ms more,
-// profiles/r06t_*) from the 16-byte-aligned address at
-// or below the member's start: a global load per symbol would wait, in the
-// lane's one counter of outstanding memory operations, for every output
-// byte stored before it.  A half that starts before the member's end may
-// read up to 127 bytes past it (the compressed buffer carries 256 bytes of
-// padding); halves past the end are zeros.  A decode that uses bits past the
-// end fails its checks.
+// from the 16-byte-aligned address at or below the member's start, each half
+// loaded into registers (eight 16-byte loads) a half ahead of its staging:
+// a global load per symbol would wait, in the lane's one counter of
+// outstanding memory operations, behind every symbol stored before it.  (The
+// staging is inline: as a call it cost 10 ms of 36, profiles/r06t_*.)  A half
+// that starts before the member's end may read up to 127 bytes past it (the
+// compressed buffer carries 256 bytes of padding); halves past the end are
+// zeros.  A decode that uses bits past the end fails its checks.
 struct Bits {
   const uint4* g;    // the member's bytes, aligned down to 16
   uint32_t* ring;    // 64 words: word w of the stream at [w & 63]
@@ -108,25 +107,28 @@ struct Bits {
   int staged;        // words staged so far
   int64_t endbits;   // the member's last bit + 1, counted from g
   uint32_t nextw;    // word q, read ahead of its use
-  __device__ __forceinline__ void stage() {
+  uint4 pre[8];      // the half after the staged ones, loaded a half ahead
+  __device__ __forceinline__ void prefetch() {
     const uint4* s = g + (staged >> 2);
-    uint4 v[8];
     const bool in = 32ll * staged < endbits;  // (a decode running on past the end reads zeros)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = in ? s[k] : make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < 8; ++k) pre[k] = in ? s[k] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  // the prefetched half into the ring (over words all taken), the next one's loads issued
+  __device__ __forceinline__ void stage() {
     uint32_t* r = ring + (staged & 63);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      r[4 * k] = v[k].x;
-      r[4 * k + 1] = v[k].y;
-      r[4 * k + 2] = v[k].z;
-      r[4 * k + 3] = v[k].w;
+      r[4 * k] = pre[k].x;
+      r[4 * k + 1] = pre[k].y;
+      r[4 * k + 2] = pre[k].z;
+      r[4 * k + 3] = pre[k].w;
     }
     staged += 32;
+    prefetch();
   }
-  // to > 32 bits (a ring half is staged only once its predecessor's words
-  // are all taken); the next word's LDS read is issued here and waited for
-  // at the next refill, off the decode's chain
+  // to > 32 bits; the next word's LDS read is issued here and waited for at
+  // the next refill, off the decode's chain
   __device__ __forceinline__ void refill() {
     while (cnt <= 32) {
       buf |= (uint64_t)nextw << cnt;
@@ -401,7 +403,8 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
   const Blk B = blks[bi];
   InfLds& L = lds[threadIdx.x];
   const uintptr_t a0 = (uintptr_t)(comp + B.src), skip = a0 & 15u;
-  Bits b{(const uint4*)(a0 - skip), L.ring, 0ull, 0, (int)(skip >> 2), 0, 8 * ((int64_t)skip + B.csize), 0u};
+  Bits b{(const uint4*)(a0 - skip), L.ring, 0ull, 0, (int)(skip >> 2), 0, 8 * ((int64_t)skip + B.csize), 0u, {}};
+  b.prefetch();
   b.stage();
   b.nextw = L.ring[b.q & 63];
   b.refill();
@@ -544,13 +547,15 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(con
 // each thread a token, its output offset by a workgroup scan, the literals
 // written at once, then rounds in which every match whose source bytes lie
 // below the first unresolved token's output copies (the first one always
-// can) -- then its CRC32 checked from LDS (bgzf_crc_kernel's chunked form)
+// can) -- then its CRC32 checked from LDS (bgzf_crc_kernel's chunked form,
+// 260-byte chunks)
 // and the bytes stored to out (+ dst).
 constexpr int kResThreads = 256;
+constexpr int kResChunk = 260;  // kResThreads * kResChunk >= 65536; a 65-dword stride puts the lanes' reads in distinct banks
 extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(const Blk* blks, const uint32_t* tok,
                                                                               const int32_t* ntok, uint8_t* out,
                                                                               int32_t* status) {
-  __shared__ uint32_t win32[65536 / 4];
+  __shared__ uint32_t win32[65536 / 4 + 1];
   __shared__ uint32_t tab[8 * 256];
   __shared__ uint32_t x2n[20];
   __shared__ int32_t red[kResThreads / 64];
@@ -619,7 +624,7 @@ extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(co
     tab[k * 256 + t] = (tab[(k - 1) * 256 + t] >> 8) ^ tab[tab[(k - 1) * 256 + t] & 0xFFu];
     __syncthreads();
   }
-  const int isize = B.isize, lo = t * kCrcChunk, hi = min(isize, lo + kCrcChunk);
+  const int isize = B.isize, lo = t * kResChunk, hi = min(isize, lo + kResChunk);
   uint32_t r = 0;
   if (lo < hi) {
     uint32_t crc = 0xFFFFFFFFu;

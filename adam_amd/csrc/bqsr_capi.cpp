@@ -255,7 +255,7 @@ struct bqsr_context {
   int tune_order = -1;
   int tune_fronts = -1;
   int tune_keymajor = 0;
-  int tune_bgzf = 0;  // BAM ingest: BGZF inflated by host threads (BQSR_TUNE_BGZF), 1 on the device
+  int tune_bgzf = 1;  // BAM ingest: BGZF inflated on the device (BQSR_TUNE_BGZF), 0 by host threads
 };
 
 namespace {

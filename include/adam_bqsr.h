@@ -147,10 +147,12 @@ void bqsr_context_destroy(bqsr_context* ctx);
  *   BQSR_TUNE_FUSED_PREP 0 only: a prep kernel of its own (the form with
  *                        prep inside the observe kernel was measured slower
  *                        and removed; 1 is refused)
- *   BQSR_TUNE_BGZF       0 BAM ingest inflates BGZF on host threads (default),
- *                        1 on the device (a thread per block: correct, but
- *                        3x slower than 16 libdeflate threads; a file it
- *                        cannot take falls back to 0) */
+ *   BQSR_TUNE_BGZF       1 BAM ingest inflates BGZF on the device (default:
+ *                        each block decoded to symbols by a thread, then
+ *                        assembled and CRC-checked in LDS by a workgroup;
+ *                        a file it cannot take -- a block that does not
+ *                        inflate or check, a record chain it cannot prove --
+ *                        falls back to 0), 0 on up to 16 host threads */
 enum { BQSR_TUNE_ORDER = 1, BQSR_TUNE_FRONTS = 2, BQSR_TUNE_KEYMAJOR = 3, BQSR_TUNE_FUSED_PREP = 4, BQSR_TUNE_BGZF = 5 };
 bqsr_status bqsr_context_tune(bqsr_context* ctx, int knob, int64_t value);
 

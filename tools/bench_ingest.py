@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--len", type=int, default=100)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--bam", action="store_true", help="BAM input (BGZF) instead of SAM text")
-    ap.add_argument("--bgzf", type=int, default=0, help="BAM: 0 inflate on host threads (default), 1 on the device")
+    ap.add_argument("--bgzf", type=int, default=1, help="BAM: 1 inflate on the device (default), 0 on host threads")
     a = ap.parse_args()
     import numpy as np
     import torch
