@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--reads", type=int, default=2_000_000)
     ap.add_argument("--len", type=int, default=100)
     ap.add_argument("--bam", action="store_true")
+    ap.add_argument("--bgzf", type=int, default=1, help="BAM: 1 inflate on the device (default), 0 on host threads")
     ap.add_argument("--no-markdup", action="store_true")
     ap.add_argument("--compression", default="snappy")
     ap.add_argument("--part-reads", type=int, default=1 << 19)
@@ -81,8 +82,10 @@ def main():
     t_gen = time.perf_counter() - t0
     log("generated %d bytes in %.1f s" % (len(data), t_gen))
     import torch
+    from adam_amd import bqsr
     from adam_amd import transform as T
     torch.zeros(1, device="cuda")
+    bqsr.Context.get(0).tune(bgzf=a.bgzf)
     work = a.dir or tempfile.mkdtemp(prefix="bench_adam_")
     os.makedirs(work, exist_ok=True)
     src = os.path.join(work, "in.bam" if a.bam else "in.sam")
@@ -117,6 +120,7 @@ def main():
                                                        "" if a.no_markdup else "MarkDuplicates, "),
             "reads": a.reads, "read_len": a.len, "input_bytes": n_bytes, "output_bytes": out_bytes,
             "seconds": dt, "reads_per_s": a.reads / dt, "compression": a.compression,
+            "bgzf": (("device" if a.bgzf else "host threads") if a.bam else None),
             "part_reads": a.part_reads, "partition_bytes": a.partition_bytes, "gen_seconds": t_gen,
             "stats": {k: v for k, v in st.items()}}))
     finally:
