@@ -109,10 +109,17 @@ struct Bits {
   uint32_t nextw;    // word q, read ahead of its use
   uint4 pre[8];      // the half after the staged ones, loaded a half ahead
   __device__ __forceinline__ void prefetch() {
-    const uint4* s = g + (staged >> 2);
+    // (through a global-space pointer: a flat load would also count in the
+    // LDS counter, so every LDS wait of the decode would wait for it)
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    const __attribute__((address_space(1))) u4v* s = (const __attribute__((address_space(1))) u4v*)(g + (staged >> 2));
     const bool in = 32ll * staged < endbits;  // (a decode running on past the end reads zeros)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) pre[k] = in ? s[k] : make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < 8; ++k) {
+      u4v v = {0u, 0u, 0u, 0u};
+      if (in) v = s[k];
+      pre[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
   }
   // the prefetched half into the ring (over words all taken), the next one's loads issued
   __device__ __forceinline__ void stage() {
