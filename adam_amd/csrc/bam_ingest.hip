@@ -544,17 +544,32 @@ bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n
   if ((st = upload_staged(ctx, d_comp, data, (size_t)n, s)) != BQSR_OK) return st;
   const unsigned g_inf = (unsigned)((nb + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads);
   if (kBgzfTokens) {  // symbols, then the bytes assembled a block a workgroup in LDS (+ CRC)
+    // in runs of whole blocks of at most kTokRun output bytes (1 GiB;
+    // ADAM_BQSR_BGZF_RUN overrides it, for the tests), one symbol buffer (4 B
+    // a byte of the run's output at most) reused across runs
+    int64_t kTokRun = int64_t(1) << 30;
+    if (const char* e = getenv("ADAM_BQSR_BGZF_RUN")) kTokRun = std::max<int64_t>(1, atoll(e));
+    int64_t cap = 1;
+    for (int64_t b0 = 0, b1; b0 < nb; b0 = b1) {
+      for (b1 = b0 + 1; b1 < nb && hb[(size_t)b1].dst + hb[(size_t)b1].isize - hb[(size_t)b0].dst <= kTokRun;) ++b1;
+      cap = std::max<int64_t>(cap, hb[(size_t)b1 - 1].dst + hb[(size_t)b1 - 1].isize - hb[(size_t)b0].dst);
+    }
     uint32_t* d_tok;
     int32_t* d_ntok;
-    if ((st = sam_alloc(tmp, &d_tok, (size_t)std::max<int64_t>(1, m))) != BQSR_OK ||
+    if ((st = sam_alloc(tmp, &d_tok, (size_t)cap)) != BQSR_OK ||
         (st = sam_alloc(tmp, &d_ntok, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK)
       return st;
-    if (nb > 0) {
-      hipLaunchKernelGGL(bgzfk::bgzf_tokens_kernel, dim3(g_inf), dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp,
-                         (const bgzfk::Blk*)d_blk, nb, d_tok, d_ntok, d_status);
+    for (int64_t b0 = 0, b1; b0 < nb; b0 = b1) {
+      for (b1 = b0 + 1; b1 < nb && hb[(size_t)b1].dst + hb[(size_t)b1].isize - hb[(size_t)b0].dst <= kTokRun;) ++b1;
+      const int64_t nr_b = b1 - b0, tok0 = hb[(size_t)b0].dst;
+      hipLaunchKernelGGL(bgzfk::bgzf_tokens_kernel, dim3((unsigned)((nr_b + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads)),
+                         dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk + b0, nr_b,
+                         d_tok, tok0, d_ntok + b0, d_status + b0);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(bgzfk::bgzf_resolve_kernel, dim3((unsigned)nb), dim3(bgzfk::kResThreads), 0, s,
-                         (const bgzfk::Blk*)d_blk, (const uint32_t*)d_tok, (const int32_t*)d_ntok, d_raw, d_status);
+      hipLaunchKernelGGL(bgzfk::bgzf_resolve_kernel, dim3((unsigned)nr_b), dim3(bgzfk::kResThreads), 0, s,
+                         (const bgzfk::Blk*)d_blk + b0, (const uint32_t*)d_tok, tok0, (const int32_t*)d_ntok + b0, d_raw,
+                         d_status + b0);
+      HIP_TRY(hipGetLastError());
     }
   } else if (nb > 0) {  // the bytes straight from the decode, then the CRC
     hipLaunchKernelGGL(bgzfk::bgzf_inflate_kernel, dim3(g_inf), dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp,

@@ -399,12 +399,13 @@ extern "C" __global__ void __launch_bounds__(kCrcThreads) bgzf_crc_kernel(const 
 }
 
 // A thread per block.  kTok false: the block's bytes to out (+ dst).  kTok
-// true: its symbols to tok (+ dst) instead, one a word (a literal byte, or
-// 0x80000000 | (distance - 1) << 9 | length), and their count to ntok.
+// true: its symbols to tok (+ dst - tok0) instead, one a word (a literal
+// byte, or 0x80000000 | (distance - 1) << 9 | length), and their count to ntok.
 // status[b]: kInf* (the CRC is checked after).
 template <bool kTok>
 __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* blks, int64_t n_blk, uint8_t* out,
-                                               uint32_t* tok, int32_t* ntok, int32_t* status, InfLds* lds) {
+                                               uint32_t* tok, int64_t tok0, int32_t* ntok, int32_t* status,
+                                               InfLds* lds) {
   const int64_t bi = (int64_t)blockIdx.x * kInfThreads + threadIdx.x;
   if (bi >= n_blk) return;
   const Blk B = blks[bi];
@@ -417,7 +418,7 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
   b.refill();
   b.need((int)(skip & 3u) * 8);
   uint8_t* o = out + B.dst;
-  uint32_t* tk = tok + B.dst;
+  uint32_t* tk = tok + (B.dst - tok0);
   int32_t k = 0;  // (tokens written)
   const int32_t isize = B.isize;
   int32_t pos = 0;
@@ -540,13 +541,13 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(co
                                                                               int64_t n_blk, uint8_t* out,
                                                                               int32_t* status) {
   __shared__ InfLds lds[kInfThreads];
-  inflate_blocks<false>(comp, blks, n_blk, out, nullptr, nullptr, status, lds);
+  inflate_blocks<false>(comp, blks, n_blk, out, nullptr, 0, nullptr, status, lds);
 }
 extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(const uint8_t* comp, const Blk* blks,
-                                                                             int64_t n_blk, uint32_t* tok,
+                                                                             int64_t n_blk, uint32_t* tok, int64_t tok0,
                                                                              int32_t* ntok, int32_t* status) {
   __shared__ InfLds lds[kInfThreads];
-  inflate_blocks<true>(comp, blks, n_blk, nullptr, tok, ntok, status, lds);
+  inflate_blocks<true>(comp, blks, n_blk, nullptr, tok, tok0, ntok, status, lds);
 }
 
 // Pass 2 of the token form: a workgroup per block, its output assembled in
@@ -560,8 +561,8 @@ extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(con
 constexpr int kResThreads = 256;
 constexpr int kResChunk = 260;  // kResThreads * kResChunk >= 65536; a 65-dword stride puts the lanes' reads in distinct banks
 extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(const Blk* blks, const uint32_t* tok,
-                                                                              const int32_t* ntok, uint8_t* out,
-                                                                              int32_t* status) {
+                                                                              int64_t tok0, const int32_t* ntok,
+                                                                              uint8_t* out, int32_t* status) {
   __shared__ uint32_t win32[65536 / 4 + 1];
   __shared__ uint32_t tab[8 * 256];
   __shared__ uint32_t x2n[20];
@@ -581,7 +582,7 @@ extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(co
   }
   const Blk B = blks[bi];
   const int n = ntok[bi];
-  const uint32_t* T = tok + B.dst;
+  const uint32_t* T = tok + (B.dst - tok0);
   int cur = 0;
   uint32_t nx = t < n ? T[t] : 0u;
   for (int g0 = 0; g0 < n; g0 += kResThreads) {

@@ -91,3 +91,13 @@ def test_device_inflate_long_records():
     b = synth.generate(300, (4000,), 1, seed=99)
     data = _reblock(_inflate(sam_to_bam(sam_text(b))), 600, 6, zlib.Z_DEFAULT_STRATEGY)
     assert_same_columns(_columns(data, 1), _columns(data, 0))
+
+
+@pytest.mark.parametrize("run,block", [(150000, 65280), (100000, 20000), (1, 1000)])
+def test_device_inflate_in_runs(raw_bam, monkeypatch, run, block):
+    # the symbol buffer reused over runs of whole blocks (ADAM_BQSR_BGZF_RUN
+    # bytes of output a run; 1: a block a run)
+    data = _reblock(raw_bam, block, 6, zlib.Z_DEFAULT_STRATEGY)
+    want = _columns(data, 0)
+    monkeypatch.setenv("ADAM_BQSR_BGZF_RUN", str(run))
+    assert_same_columns(_columns(data, 1), want)
