@@ -499,6 +499,16 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
         if constexpr (kTok) {
           tk[k++] = (uint32_t)sym;
           pos++;
+          // a second literal in the same step when its code is a root leaf
+          // already in the buffer
+          const uint32_t e = L.tlit[b.buf & ((1u << kLitRoot) - 1u)];
+          const int l2 = (int)((e >> 9) & 15u);
+          if (!(e & 0x8000u) && l2 != 0 && l2 <= b.cnt && (e & 511u) < 256u && pos < isize) {
+            b.buf >>= l2;
+            b.cnt -= l2;
+            tk[k++] = e & 511u;
+            pos++;
+          }
           continue;
         }
         lit |= (uint64_t)sym << (8 * nlit);
