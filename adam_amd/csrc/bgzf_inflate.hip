@@ -539,6 +539,16 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
       if constexpr (kTok) tk[k++] = 0x80000000u | ((uint32_t)(dist - 1) << 9) | (uint32_t)len;
       else match_copy(o, pos, dist, len, isize);
       pos += len;
+      if constexpr (kTok) {  // (and a literal after it, the same way)
+        const uint32_t e = L.tlit[b.buf & ((1u << kLitRoot) - 1u)];
+        const int l2 = (int)((e >> 9) & 15u);
+        if (!(e & 0x8000u) && l2 != 0 && l2 <= b.cnt && (e & 511u) < 256u && pos < isize) {
+          b.buf >>= l2;
+          b.cnt -= l2;
+          tk[k++] = e & 511u;
+          pos++;
+        }
+      }
     }
     if (st == kInfOk && b.past()) st = kInfBadBlock;
   }
