@@ -640,7 +640,17 @@ extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(co
       for (int q = 1; q < kResThreads / 64; ++q) F = min(F, red[q]);
       if (F == 0x7FFFFFFF) break;
       if (pend && p - dist + min(ln, dist) <= F) {
-        for (int i = 0; i < ln; ++i) win[p + i] = win[p - dist + i];  // (forward: a period repeats)
+        int i = 0;
+        if (dist >= 8) {  // 8 bytes a step, their reads in flight together (sources before the step)
+          for (; i + 8 <= ln; i += 8) {
+            uint8_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = win[p - dist + i + q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) win[p + i + q] = v[q];
+          }
+        }
+        for (; i < ln; ++i) win[p + i] = win[p - dist + i];  // (forward: a period repeats)
         pend = false;
       }
     }
