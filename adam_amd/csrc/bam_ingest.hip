@@ -521,9 +521,6 @@ struct RecScan {
 // inflate or fails its CRC32, a chain the check rejects, a header it cannot
 // read -- and the caller runs the host form, which reports the file's error
 // as before.
-// the device inflate's form: symbols to HBM, then each block assembled in LDS
-// (bgzf_resolve_kernel), or the bytes written by the decode itself
-constexpr bool kBgzfTokens = true;
 bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n, const std::vector<BgzfBlk>& blks,
                                int64_t m, uint8_t* d_raw, hipStream_t s, std::vector<void*>& tmp, BamHead& BH,
                                SamHeader& H, std::string& hdr, uint64_t** d_rec, int64_t& nr, bool& ok) {
@@ -542,8 +539,7 @@ bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n
       (st = sam_alloc(tmp, &d_status, (size_t)std::max<int64_t>(1, nb))) != BQSR_OK)
     return st;
   if ((st = upload_staged(ctx, d_comp, data, (size_t)n, s)) != BQSR_OK) return st;
-  const unsigned g_inf = (unsigned)((nb + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads);
-  if (kBgzfTokens) {  // symbols, then the bytes assembled a block a workgroup in LDS (+ CRC)
+  {  // symbols, then the bytes assembled a block a workgroup in LDS (+ CRC)
     // in runs of whole blocks of at most kTokRun output bytes (1 GiB;
     // ADAM_BQSR_BGZF_RUN overrides it, for the tests), one symbol buffer (4 B
     // a byte of the run's output at most) reused across runs
@@ -571,14 +567,7 @@ bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n
                          d_status + b0);
       HIP_TRY(hipGetLastError());
     }
-  } else if (nb > 0) {  // the bytes straight from the decode, then the CRC
-    hipLaunchKernelGGL(bgzfk::bgzf_inflate_kernel, dim3(g_inf), dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp,
-                       (const bgzfk::Blk*)d_blk, nb, d_raw, d_status);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(bgzfk::bgzf_crc_kernel, dim3((unsigned)nb), dim3(bgzfk::kCrcThreads), 0, s,
-                       (const bgzfk::Blk*)d_blk, (const uint8_t*)d_raw, d_status);
   }
-  HIP_TRY(hipGetLastError());
   std::vector<int32_t> hs((size_t)std::max<int64_t>(1, nb), 0);
   if (nb > 0) HIP_TRY(hipMemcpyAsync(hs.data(), d_status, (size_t)nb * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -4,15 +4,16 @@
 // whose BlockGunzipper inflates one BGZF block at a time).
 //
 // A BGZF file is a chain of gzip members of at most 64 KiB inflated each; no
-// DEFLATE back-reference crosses a member, so every block inflates on its own:
-// a thread per block (bgzf_inflate_kernel, kInfThreads blocks a workgroup),
-// its decode tables and a ring its compressed bytes are staged through in the
-// thread's slice of LDS, the output written straight to the block's place in
-// the inflated stream (the host's prefix sum of the blocks' ISIZE).  The
-// CRC32 of each member is a second kernel (bgzf_crc_kernel: a workgroup per
-// member, 256-byte chunks combined in GF(2)).  A block is rejected as the
-// host path rejects it: a code that does not decode, an overrun of ISIZE, a
-// short output, a CRC mismatch.
+// DEFLATE back-reference crosses a member, so every block inflates on its own,
+// in two passes: a thread per block (bgzf_tokens_kernel, kInfThreads blocks a
+// workgroup) decodes it to 32-bit symbols in HBM, its decode tables and a
+// ring its compressed bytes are staged through in the thread's slice of LDS;
+// then a workgroup per block (bgzf_resolve_kernel) assembles its bytes in LDS
+// from the symbols, checks its CRC32 there (256 chunks combined in GF(2)) and
+// stores them at the block's place in the inflated stream (the host's prefix
+// sum of the blocks' ISIZE).  A block is rejected as the host path rejects
+// it: a code that does not decode, an overrun of ISIZE, a short output, a
+// CRC mismatch.
 //
 // The records' offsets (a chain of block_size fields from the first record
 // after the header) are found without walking the chain in order: each block
@@ -26,14 +27,14 @@
 // caller takes the host path, which reports errors as before.
 //
 // Measured (profiles/r06t_bgzf_device_inflate.txt): a thread per block is
-// serial per member, so the kernel's time is one member's decode latency;
-// what set it, in turn: 64 lanes a wavefront diverging (16 now), the
-// canonical bit-by-bit decode (two-level tables now), a global load per bit
-// refill waiting behind the lane's stores (the LDS ring now), the CRC folded
-// in the same kernel (its LDS table pushed the workgroup past two a CU), and
-// byte-wise match copies (batched now).  0.43 GB: 189 ms -> 44 ms, where 16
-// libdeflate threads take 57 ms (78 ms with the transfer).  Its waves now
-// wait on the match copies' L2 round trips.
+// serial per member, so pass 1's time is one member's decode latency; what
+// set it, in turn: 64 lanes a wavefront diverging (16 now), the canonical
+// bit-by-bit decode (two-level tables now), a global load per bit refill
+// waiting behind the lane's stores (the LDS ring now), and -- in the one-pass
+// form that wrote bytes and copied matches from HBM (tools/variants/
+// bgzf_one_pass.diff) -- the matches' L2 round trips (symbols now, the copies
+// in LDS).  0.43 GB: 189 ms -> 22.4 + 5.0 ms, where 16 libdeflate threads
+// take 57 ms.
 //
 // Included by bqsr_capi.cpp before bam_ingest.hip.
 
@@ -261,70 +262,11 @@ __device__ __forceinline__ int table_decode(Bits& b, const uint16_t* t) {
   return (int)(e & 511u);
 }
 
-// A match: len bytes at o + pos repeat the dist bytes before them.  Loads
-// are round trips through L2 (the bytes were stored moments ago by this
-// lane), so the sources of a batch are all loaded before its stores: up to
-// min(dist, 32) bytes a batch for dist >= 8; for dist < 8 the period once
-// (one load of the 8 bytes before), then stores from registers.  Stores are
-// 8 bytes wide; one may run past the match into bytes this lane writes
-// later (never past the block's isize: there the word goes byte by byte).
-__device__ __forceinline__ void store_word(uint8_t* d, uint64_t w, int nb, bool whole) {
-  if (whole) {
-    __builtin_memcpy(d, &w, 8);
-    return;
-  }
-  for (int k = 0; k < nb; ++k) d[k] = (uint8_t)(w >> (8 * k));
-}
-__device__ __forceinline__ void match_copy(uint8_t* o, int pos, int dist, int len, int isize) {
-  uint8_t* d = o + pos;
-  const uint8_t* src = d - dist;
-  const int room = isize - pos;
-  if (dist >= 8) {
-    const int step = dist < 32 ? (dist & ~7) : 32;
-    for (int i = 0; i < len; i += step) {
-      const int nb = min(step, len - i);
-      uint64_t w[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (8 * k < nb) __builtin_memcpy(&w[k], src + i + 8 * k, 8);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (8 * k < nb) store_word(d + i + 8 * k, w[k], min(8, nb - 8 * k), i + 8 * k + 8 <= room);
-    }
-    return;
-  }
-  // the period p (dist bytes), spread over 16 bytes: e0 | e1 << 64 = p p p ...
-  uint64_t v = 0;
-  if (pos >= 8) {
-    uint64_t w;
-    __builtin_memcpy(&w, d - 8, 8);
-    v = w >> (8 * (8 - dist));
-  } else {
-    for (int k = 0; k < dist; ++k) v |= (uint64_t)src[k] << (8 * k);
-  }
-  uint64_t e0 = 0, e1 = 0;
-  for (int k = 0, j = 0; k < 16; ++k) {
-    const uint64_t by = (v >> (8 * j)) & 0xFFull;
-    if (k < 8) e0 |= by << (8 * k); else e1 |= by << (8 * (k - 8));
-    if (++j == dist) j = 0;
-  }
-  const int adv = 8 % dist;  // the phase gained by 8 bytes
-  for (int i = 0, ph = 0; i < len; i += 8) {
-    const uint64_t w = ph == 0 ? e0 : (e0 >> (8 * ph)) | (e1 << (64 - 8 * ph));
-    store_word(d + i, w, min(8, len - i), i + 8 <= room);
-    ph += adv;
-    if (ph >= dist) ph -= dist;
-  }
-}
-
 // ---- the members' CRC32 ----
-// A workgroup per member, a thread per 256-byte chunk of its output: each
-// chunk's CRC32 by slicing-by-8 (tables in LDS), then the chunks' CRCs
+// Each chunk's CRC32 by slicing-by-8 (tables in LDS), then the chunks' CRCs
 // combined in GF(2)[x] mod the CRC polynomial, as zlib's crc32_combine does:
 // crc(A B) = crc(A) * x^(8 |B|) + crc(B), so crc = sum over chunks t of
 // crc_t * x^(8 * (bytes after chunk t)).
-constexpr int kCrcThreads = 256;
-constexpr int kCrcChunk = 256;  // kCrcThreads * kCrcChunk = 65536, a member's most
 constexpr uint32_t kCrcPoly = 0xEDB88320u;
 
 // a * b mod P, bit-reflected (bit 31 is x^0)
@@ -344,68 +286,14 @@ __device__ __forceinline__ uint32_t crc_x8n(const uint32_t* x2n, uint32_t n) {
   return p;
 }
 
-extern "C" __global__ void __launch_bounds__(kCrcThreads) bgzf_crc_kernel(const Blk* blks, const uint8_t* out,
-                                                                           int32_t* status) {
-  __shared__ uint32_t tab[8 * 256];  // [k][v]: the CRC of v followed by k zero bytes
-  __shared__ uint32_t x2n[20];
-  __shared__ uint32_t part[kCrcThreads / 64];
-  const int64_t bi = blockIdx.x;
-  if (status[bi] != kInfOk) return;  // (uniform over the workgroup)
-  const int t = threadIdx.x;
-  {
-    uint32_t c = (uint32_t)t;
-    for (int k = 0; k < 8; ++k) c = (c & 1u) ? kCrcPoly ^ (c >> 1) : c >> 1;
-    tab[t] = c;
-  }
-  if (t == 0) {
-    x2n[0] = 1u << 23;  // x^8
-    for (int k = 1; k < 20; ++k) x2n[k] = crc_mult(x2n[k - 1], x2n[k - 1]);
-  }
-  __syncthreads();
-  for (int k = 1; k < 8; ++k) {
-    tab[k * 256 + t] = (tab[(k - 1) * 256 + t] >> 8) ^ tab[tab[(k - 1) * 256 + t] & 0xFFu];
-    __syncthreads();
-  }
-  const Blk B = blks[bi];
-  const int lo = t * kCrcChunk, hi = min((int)B.isize, lo + kCrcChunk);
-  uint32_t r = 0;
-  if (lo < hi) {
-    const uint8_t* p = out + B.dst + lo;
-    uint32_t crc = 0xFFFFFFFFu;
-    int i = 0;
-    for (; i + 64 <= hi - lo; i += 64) {  // 8 loads in flight, then their CRC steps
-      uint64_t w[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) __builtin_memcpy(&w[k], p + i + 8 * k, 8);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t a = (uint32_t)w[k] ^ crc, b = (uint32_t)(w[k] >> 32);
-        crc = tab[7 * 256 + (a & 0xFFu)] ^ tab[6 * 256 + ((a >> 8) & 0xFFu)] ^ tab[5 * 256 + ((a >> 16) & 0xFFu)] ^
-              tab[4 * 256 + (a >> 24)] ^ tab[3 * 256 + (b & 0xFFu)] ^ tab[2 * 256 + ((b >> 8) & 0xFFu)] ^
-              tab[1 * 256 + ((b >> 16) & 0xFFu)] ^ tab[b >> 24];
-      }
-    }
-    for (; i < hi - lo; ++i) crc = tab[(crc ^ p[i]) & 0xFFu] ^ (crc >> 8);
-    r = crc_mult(crc ^ 0xFFFFFFFFu, crc_x8n(x2n, (uint32_t)(B.isize - hi)));
-  }
-  for (int o = 32; o > 0; o >>= 1) r ^= __shfl_xor(r, o);
-  if ((t & 63) == 0) part[t >> 6] = r;
-  __syncthreads();
-  if (t == 0) {
-    uint32_t c = 0;
-    for (int w = 0; w < kCrcThreads / 64; ++w) c ^= part[w];
-    if (c != B.crc) status[bi] = kInfCrc;
-  }
-}
-
-// A thread per block.  kTok false: the block's bytes to out (+ dst).  kTok
-// true: its symbols to tok (+ dst - tok0) instead, one a word (a literal
-// byte, or 0x80000000 | (distance - 1) << 9 | length), and their count to ntok.
-// status[b]: kInf* (the CRC is checked after).
-template <bool kTok>
-__device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* blks, int64_t n_blk, uint8_t* out,
-                                               uint32_t* tok, int64_t tok0, int32_t* ntok, int32_t* status,
-                                               InfLds* lds) {
+// Pass 1 of the inflate: a thread per block, its symbols to tok (+ dst -
+// tok0), one a word (a literal byte, or 0x80000000 | (distance - 1) << 9 |
+// length), and their count to ntok.  status[b]: kInf* (the CRC is checked by
+// pass 2).
+extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(const uint8_t* comp, const Blk* blks,
+                                                                             int64_t n_blk, uint32_t* tok, int64_t tok0,
+                                                                             int32_t* ntok, int32_t* status) {
+  __shared__ InfLds lds[kInfThreads];
   const int64_t bi = (int64_t)blockIdx.x * kInfThreads + threadIdx.x;
   if (bi >= n_blk) return;
   const Blk B = blks[bi];
@@ -417,7 +305,6 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
   b.nextw = L.ring[b.q & 63];
   b.refill();
   b.need((int)(skip & 3u) * 8);
-  uint8_t* o = out + B.dst;
   uint32_t* tk = tok + (B.dst - tok0);
   int32_t k = 0;  // (tokens written)
   const int32_t isize = B.isize;
@@ -434,8 +321,7 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
       if (pos + (int32_t)len > isize) { st = kInfOverrun; break; }
       for (uint32_t i = 0; i < len; ++i) {
         const uint32_t v = b.need(8);
-        if constexpr (kTok) tk[k++] = v;
-        else o[pos] = (uint8_t)v;
+        tk[k++] = v;
         pos++;
       }
       if (b.past()) { st = kInfBadBlock; break; }
@@ -487,43 +373,25 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
       if (ed < 0 || (ed > 0 && ndist - L.dist.count[0] != 1)) { st = kInfBadBlock; break; }
       if (!table_build<kDistRoot, kDistCap>(L.tdist, L.dist)) { st = kInfBadBlock; break; }
     }
-    // the block's codes; literals gather in a register word (up to 8, stored
-    // as one; flushed before a match, which may read them, and at the block's end)
-    uint64_t lit = 0;
-    int nlit = 0;
+    // the block's codes
     while (true) {
       const int sym = table_decode<kLitRoot>(b, L.tlit);
       if (sym < 0) { st = kInfBadCode; break; }
       if (sym < 256) {
         if (pos >= isize) { st = kInfOverrun; break; }
-        if constexpr (kTok) {
-          tk[k++] = (uint32_t)sym;
-          pos++;
-          // a second literal in the same step when its code is a root leaf
-          // already in the buffer
-          const uint32_t e = L.tlit[b.buf & ((1u << kLitRoot) - 1u)];
-          const int l2 = (int)((e >> 9) & 15u);
-          if (!(e & 0x8000u) && l2 != 0 && l2 <= b.cnt && (e & 511u) < 256u && pos < isize) {
-            b.buf >>= l2;
-            b.cnt -= l2;
-            tk[k++] = e & 511u;
-            pos++;
-          }
-          continue;
-        }
-        lit |= (uint64_t)sym << (8 * nlit);
+        tk[k++] = (uint32_t)sym;
         pos++;
-        if (++nlit == 8) {
-          __builtin_memcpy(o + pos - 8, &lit, 8);
-          lit = 0;
-          nlit = 0;
+        // a second literal in the same step when its code is a root leaf
+        // already in the buffer
+        const uint32_t e = L.tlit[b.buf & ((1u << kLitRoot) - 1u)];
+        const int l2 = (int)((e >> 9) & 15u);
+        if (!(e & 0x8000u) && l2 != 0 && l2 <= b.cnt && (e & 511u) < 256u && pos < isize) {
+          b.buf >>= l2;
+          b.cnt -= l2;
+          tk[k++] = e & 511u;
+          pos++;
         }
         continue;
-      }
-      if (nlit) {
-        store_word(o + pos - nlit, lit, nlit, pos - nlit + 8 <= isize);
-        lit = 0;
-        nlit = 0;
       }
       if (sym == 256) break;
       const int ls = sym - 257;
@@ -536,10 +404,9 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
       const int dist = dist_base(ds, de) + (int)b.need(de);
       if (dist > pos) { st = kInfBadCode; break; }
       if (pos + len > isize) { st = kInfOverrun; break; }
-      if constexpr (kTok) tk[k++] = 0x80000000u | ((uint32_t)(dist - 1) << 9) | (uint32_t)len;
-      else match_copy(o, pos, dist, len, isize);
+      tk[k++] = 0x80000000u | ((uint32_t)(dist - 1) << 9) | (uint32_t)len;
       pos += len;
-      if constexpr (kTok) {  // (and a literal after it, the same way)
+      {  // (and a literal after it, the same way)
         const uint32_t e = L.tlit[b.buf & ((1u << kLitRoot) - 1u)];
         const int l2 = (int)((e >> 9) & 15u);
         if (!(e & 0x8000u) && l2 != 0 && l2 <= b.cnt && (e & 511u) < 256u && pos < isize) {
@@ -554,30 +421,16 @@ __device__ __forceinline__ void inflate_blocks(const uint8_t* comp, const Blk* b
   }
   if (st == kInfOk && pos != isize) st = kInfShort;
   status[bi] = st;
-  if constexpr (kTok) ntok[bi] = k;
+  ntok[bi] = k;
 }
 
-extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_inflate_kernel(const uint8_t* comp, const Blk* blks,
-                                                                              int64_t n_blk, uint8_t* out,
-                                                                              int32_t* status) {
-  __shared__ InfLds lds[kInfThreads];
-  inflate_blocks<false>(comp, blks, n_blk, out, nullptr, 0, nullptr, status, lds);
-}
-extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(const uint8_t* comp, const Blk* blks,
-                                                                             int64_t n_blk, uint32_t* tok, int64_t tok0,
-                                                                             int32_t* ntok, int32_t* status) {
-  __shared__ InfLds lds[kInfThreads];
-  inflate_blocks<true>(comp, blks, n_blk, nullptr, tok, tok0, ntok, status, lds);
-}
-
-// Pass 2 of the token form: a workgroup per block, its output assembled in
+// Pass 2 of the inflate: a workgroup per block, its output assembled in
 // LDS (a block inflates to at most 64 KiB) from its tokens 256 at a time --
 // each thread a token, its output offset by a workgroup scan, the literals
 // written at once, then rounds in which every match whose source bytes lie
 // below the first unresolved token's output copies (the first one always
-// can) -- then its CRC32 checked from LDS (bgzf_crc_kernel's chunked form,
-// 260-byte chunks)
-// and the bytes stored to out (+ dst).
+// can) -- then its CRC32 checked from LDS (260-byte chunks, combined as
+// above) and the bytes stored to out (+ dst).
 constexpr int kResThreads = 256;
 constexpr int kResChunk = 260;  // kResThreads * kResChunk >= 65536; a 65-dword stride puts the lanes' reads in distinct banks
 extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(const Blk* blks, const uint32_t* tok,
