@@ -558,9 +558,16 @@ bqsr_status bam_inflate_device(bqsr_context* ctx, const uint8_t* data, int64_t n
     for (int64_t b0 = 0, b1; b0 < nb; b0 = b1) {
       for (b1 = b0 + 1; b1 < nb && hb[(size_t)b1].dst + hb[(size_t)b1].isize - hb[(size_t)b0].dst <= kTokRun;) ++b1;
       const int64_t nr_b = b1 - b0, tok0 = hb[(size_t)b0].dst;
-      hipLaunchKernelGGL(bgzfk::bgzf_tokens_kernel, dim3((unsigned)((nr_b + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads)),
-                         dim3(bgzfk::kInfThreads), 0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk + b0, nr_b,
-                         d_tok, tok0, d_ntok + b0, d_status + b0);
+      if (nr_b <= (int64_t)ctx->n_cu * 2 * bgzfk::kInfThreads)  // (all in flight at once)
+        hipLaunchKernelGGL(bgzfk::bgzf_tokens_kernel<bgzfk::kInfThreads>,
+                           dim3((unsigned)((nr_b + bgzfk::kInfThreads - 1) / bgzfk::kInfThreads)), dim3(bgzfk::kInfThreads),
+                           0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk + b0, nr_b, d_tok, tok0, d_ntok + b0,
+                           d_status + b0);
+      else
+        hipLaunchKernelGGL(bgzfk::bgzf_tokens_kernel<bgzfk::kInfThreadsDeep>,
+                           dim3((unsigned)((nr_b + bgzfk::kInfThreadsDeep - 1) / bgzfk::kInfThreadsDeep)),
+                           dim3(bgzfk::kInfThreadsDeep), 0, s, (const uint8_t*)d_comp, (const bgzfk::Blk*)d_blk + b0, nr_b,
+                           d_tok, tok0, d_ntok + b0, d_status + b0);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(bgzfk::bgzf_resolve_kernel, dim3((unsigned)nr_b), dim3(bgzfk::kResThreads), 0, s,
                          (const bgzfk::Blk*)d_blk + b0, (const uint32_t*)d_tok, tok0, (const int32_t*)d_ntok + b0, d_raw,

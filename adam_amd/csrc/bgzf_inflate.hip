@@ -48,7 +48,12 @@ struct Blk {          // one BGZF member
   uint32_t crc;       // CRC32 of those bytes (the member's trailer)
 };
 
-constexpr int kInfThreads = 16;  // blocks a workgroup (lanes of one wavefront), a thread per block
+// blocks a workgroup (lanes of one wavefront), a thread per block: 16 while
+// every block of a run is in flight at once (32 a CU, two workgroups' LDS);
+// 12 for longer runs (36 a CU, three workgroups: fewer rounds, at 1 ms more a
+// round, profiles/r06t_*)
+constexpr int kInfThreads = 16;
+constexpr int kInfThreadsDeep = 12;
 constexpr int kLitRoot = 9;      // the decode tables' root index bits
 constexpr int kLitCap = 512;     // and their second-level entries (zlib's bound for 286 codes, root 9: 852 in all)
 constexpr int kDistRoot = 8;
@@ -290,11 +295,12 @@ __device__ __forceinline__ uint32_t crc_x8n(const uint32_t* x2n, uint32_t n) {
 // tok0), one a word (a literal byte, or 0x80000000 | (distance - 1) << 9 |
 // length), and their count to ntok.  status[b]: kInf* (the CRC is checked by
 // pass 2).
-extern "C" __global__ void __launch_bounds__(kInfThreads) bgzf_tokens_kernel(const uint8_t* comp, const Blk* blks,
-                                                                             int64_t n_blk, uint32_t* tok, int64_t tok0,
-                                                                             int32_t* ntok, int32_t* status) {
-  __shared__ InfLds lds[kInfThreads];
-  const int64_t bi = (int64_t)blockIdx.x * kInfThreads + threadIdx.x;
+template <int kThreads>
+__global__ void __launch_bounds__(kThreads) bgzf_tokens_kernel(const uint8_t* comp, const Blk* blks, int64_t n_blk,
+                                                               uint32_t* tok, int64_t tok0, int32_t* ntok,
+                                                               int32_t* status) {
+  __shared__ InfLds lds[kThreads];
+  const int64_t bi = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (bi >= n_blk) return;
   const Blk B = blks[bi];
   InfLds& L = lds[threadIdx.x];

@@ -101,3 +101,11 @@ def test_device_inflate_in_runs(raw_bam, monkeypatch, run, block):
     want = _columns(data, 0)
     monkeypatch.setenv("ADAM_BQSR_BGZF_RUN", str(run))
     assert_same_columns(_columns(data, 1), want)
+
+
+def test_device_inflate_many_blocks(raw_bam):
+    # more blocks than the device holds at once at 16 a workgroup (n_cu * 32):
+    # the 12-a-workgroup decode (bam_ingest.hip)
+    data = _reblock(raw_bam, 250, 6, zlib.Z_DEFAULT_STRATEGY)
+    assert len(raw_bam) // 250 > 256 * 32
+    assert_same_columns(_columns(data, 1), _columns(data, 0))
