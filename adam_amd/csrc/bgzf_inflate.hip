@@ -431,14 +431,14 @@ __global__ void __launch_bounds__(kThreads) bgzf_tokens_kernel(const uint8_t* co
 }
 
 // Pass 2 of the inflate: a workgroup per block, its output assembled in
-// LDS (a block inflates to at most 64 KiB) from its tokens 256 at a time --
+// LDS (a block inflates to at most 64 KiB) from its tokens 512 at a time --
 // each thread a token, its output offset by a workgroup scan, the literals
 // written at once, then rounds in which every match whose source bytes lie
 // below the first unresolved token's output copies (the first one always
-// can) -- then its CRC32 checked from LDS (260-byte chunks, combined as
+// can) -- then its CRC32 checked from LDS (132-byte chunks, combined as
 // above) and the bytes stored to out (+ dst).
-constexpr int kResThreads = 256;
-constexpr int kResChunk = 260;  // kResThreads * kResChunk >= 65536; a 65-dword stride puts the lanes' reads in distinct banks
+constexpr int kResThreads = 512;
+constexpr int kResChunk = 132;  // kResThreads * kResChunk >= 65536; a 33-dword stride puts the lanes' reads in distinct banks
 extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(const Blk* blks, const uint32_t* tok,
                                                                               int64_t tok0, const int32_t* ntok,
                                                                               uint8_t* out, int32_t* status) {
@@ -450,7 +450,7 @@ extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(co
   const int64_t bi = blockIdx.x;
   if (status[bi] != kInfOk) return;  // (uniform over the workgroup)
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  {
+  if (t < 256) {
     uint32_t c = (uint32_t)t;
     for (int k = 0; k < 8; ++k) c = (c & 1u) ? kCrcPoly ^ (c >> 1) : c >> 1;
     tab[t] = c;
@@ -518,7 +518,7 @@ extern "C" __global__ void __launch_bounds__(kResThreads) bgzf_resolve_kernel(co
   __syncthreads();
   // CRC32 of the 256-byte chunks, combined
   for (int k = 1; k < 8; ++k) {
-    tab[k * 256 + t] = (tab[(k - 1) * 256 + t] >> 8) ^ tab[tab[(k - 1) * 256 + t] & 0xFFu];
+    if (t < 256) tab[k * 256 + t] = (tab[(k - 1) * 256 + t] >> 8) ^ tab[tab[(k - 1) * 256 + t] & 0xFFu];
     __syncthreads();
   }
   const int isize = B.isize, lo = t * kResChunk, hi = min(isize, lo + kResChunk);
