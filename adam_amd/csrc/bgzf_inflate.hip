@@ -151,6 +151,13 @@ struct Bits {
       nextw = ring[q & 63];
     }
   }
+  __device__ __forceinline__ uint32_t need_short(int n) {  // n <= 16 bits
+    if (cnt < n) refill();
+    const uint32_t v = (uint32_t)buf & ((1u << n) - 1u);
+    buf >>= n;
+    cnt -= n;
+    return v;
+  }
   __device__ __forceinline__ uint32_t need(int n) {  // n <= 32 bits
     if (cnt < n) refill();
     const uint32_t v = (uint32_t)(buf & ((n == 32) ? 0xFFFFFFFFull : ((1ull << n) - 1ull)));
@@ -403,11 +410,11 @@ __global__ void __launch_bounds__(kThreads) bgzf_tokens_kernel(const uint8_t* co
       const int ls = sym - 257;
       if (ls >= 29) { st = kInfBadCode; break; }
       const int le = len_extra(ls);
-      const int len = len_base(ls, le) + (int)b.need(le);
+      const int len = len_base(ls, le) + (int)b.need_short(le);
       const int ds = table_decode<kDistRoot>(b, L.tdist);
       if (ds < 0 || ds >= 30) { st = kInfBadCode; break; }
       const int de = dist_extra(ds);
-      const int dist = dist_base(ds, de) + (int)b.need(de);
+      const int dist = dist_base(ds, de) + (int)b.need_short(de);
       if (dist > pos) { st = kInfBadCode; break; }
       if (pos + len > isize) { st = kInfOverrun; break; }
       tk[k++] = 0x80000000u | ((uint32_t)(dist - 1) << 9) | (uint32_t)len;
